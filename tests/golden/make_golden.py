@@ -1,0 +1,317 @@
+"""Generate the committed golden fixtures from the REFERENCE implementation.
+
+TEST INFRASTRUCTURE.  Runs only in the survey/build container, where the
+read-only reference is mounted at /root/reference; on any other machine (the
+GPU box) it is a no-op.  Nothing from the reference is copied: the reference
+modules are imported, driven, and only their *outputs* (numbers) are written
+under tests/golden/.
+
+Must run with asserts stripped, exactly like the reference's own entry point
+(`python -OO main.py`, README.md:10): Coach.executeEpisode passes the np.int64
+returned by np.random.choice (Coach.py:81) into InflexionGame.to_next_state,
+whose `assert isinstance(action, int)` (InflexionGame.py:76) only holds under -O.
+
+    PYTHONDONTWRITEBYTECODE=1 python -O tests/golden/make_golden.py [--quick]
+
+Fixtures written (all small, gzip'd JSON or npz):
+  rng_kat.json.gz        numpy legacy MT19937 streams + randint/choice/random_sample
+  symmetry.json.gz       rotate / translate / symmetries() gather tables
+  rules_kat.npz          random playouts: board, turn, action, valid mask, outcome
+  pairwise_kat.npz       numpy f32 pairwise .sum() known answers
+  mcts_<set>.json.gz     Coach.executeEpisode + MCTS traces driven by stubnet
+  nnet_golden.npz        InflexionNNet(manual_seed 0) checksum + (planes -> P, v)
+"""
+import gzip
+import hashlib
+import json
+import os
+import sys
+import time
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _need_reference():
+    if not os.path.isdir(REF):
+        print("make_golden: /root/reference absent - nothing to do")
+        sys.exit(0)
+    if __debug__:
+        print("make_golden: run with `python -O` (see module docstring)")
+        sys.exit(2)
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    sys.path.insert(0, HERE)
+
+
+def _dump(name, obj):
+    path = os.path.join(HERE, name)
+    with gzip.open(path, "wt") as f:
+        json.dump(obj, f, separators=(",", ":"))
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+# --------------------------------------------------------------------------- RNG
+def gen_rng_kat(np):
+    out = []
+    for seed in [0, 1, 7, 42, 12345, 2**31 - 1, 2**32 - 1]:
+        np.random.seed(seed)
+        raw = np.random.randint(0, 2**32, size=1400, dtype=np.uint32).tolist()
+        np.random.seed(seed)
+        ops = []
+        for t in range(600):
+            k = t % 7
+            if k == 0:
+                ops.append(["randint", 0, 6, int(np.random.randint(0, 6))])
+            elif k == 1:
+                ops.append(["randint", 0, 7, int(np.random.randint(0, 7))])
+            elif k == 2:
+                ops.append(["choice3", ["r", "q", "s"].index(np.random.choice(["r", "q", "s"]))])
+            elif k == 3:
+                ops.append(["random_sample", float(np.random.random_sample())])
+            elif k == 4:
+                n = 1 + t % 11
+                ops.append(["choice_n", n, int(np.random.choice(np.arange(n)))])
+            elif k == 5:
+                w = np.random.random_sample(13) if t % 2 else np.zeros(13)
+                w[t % 13] += 1.0
+                p = w / w.sum()
+                ops.append(["choice_p", p.tolist(), int(np.random.choice(13, p=p))])
+            else:
+                p = np.zeros(9, dtype=np.int8)
+                p[t % 9] = 1
+                ops.append(["choice_onehot", t % 9, int(np.random.choice(9, p=p))])
+        out.append({"seed": seed, "raw_u32": raw, "ops": ops})
+    _dump("rng_kat.json.gz", out)
+
+
+# ---------------------------------------------------------------------- symmetry
+def gen_symmetry(np, InflexionGame):
+    g = InflexionGame(7)
+    idx = np.arange(49).reshape(1, 7, 7)
+    idx4 = np.repeat(idx, 4, axis=0)
+    rot = [g.rotate(idx4, k)[0].ravel().tolist() for k in range(6)]
+    tr = {ax: [g.translate(idx4, j, axis=ax)[0].ravel().tolist() for j in range(7)] for ax in "rqs"}
+    sym = [s[0].ravel().tolist() for s in g.symmetries(idx4)]
+    pol = np.arange(343).reshape(7, 7, 7)
+    sym_pol = [s.ravel().tolist() for s in g.symmetries(pol)]
+    _dump("symmetry.json.gz", {"rotate": rot, "translate": tr, "symmetries": sym,
+                               "symmetries_policy": sym_pol})
+
+
+# ------------------------------------------------------------------------- rules
+def gen_rules(np, InflexionGame, GameOutcome):
+    rs = np.random.RandomState(2024)
+    boards, turns, players, actions, valids, outcomes, game_id, max_turns_l = [], [], [], [], [], [], [], []
+    gid = 0
+    for max_turns in [343] * 24 + [100] * 16 + [12] * 16 + [3] * 8:
+        g = InflexionGame(7, max_turns=max_turns)
+        while True:
+            v = g.valid_actions_mask()
+            acts = np.nonzero(v)[0]
+            if len(acts) == 0:
+                break
+            a = int(acts[rs.randint(len(acts))])
+            boards.append(g._board.astype(np.int8).ravel())
+            turns.append(g._curr_turn)
+            players.append(g.player.num)
+            actions.append(a)
+            valids.append(np.packbits(v.astype(np.uint8)))
+            g = g.to_next_state(a)
+            outcomes.append(g.outcome.value)
+            game_id.append(gid)
+            max_turns_l.append(max_turns)
+            if g.outcome != GameOutcome.ONGOING:
+                break
+        gid += 1
+    path = os.path.join(HERE, "rules_kat.npz")
+    np.savez_compressed(path, board=np.array(boards), turn=np.array(turns, np.int32),
+                        player=np.array(players, np.int8), action=np.array(actions, np.int32),
+                        valid_bits=np.array(valids), outcome=np.array(outcomes, np.float64),
+                        game=np.array(game_id, np.int32), max_turns=np.array(max_turns_l, np.int32))
+    print("wrote", path, os.path.getsize(path), "plies", len(actions))
+
+
+# ---------------------------------------------------------------------- pairwise
+def gen_pairwise(np):
+    rs = np.random.RandomState(7)
+    arrs, sums, lens = [], [], []
+    for t in range(600):
+        n = 343 if t < 400 else int(rs.randint(1, 400))
+        a = rs.random_sample(n).astype(np.float32) * (rs.random_sample(n) < 0.4)
+        a = (a * np.float32(rs.random_sample() * 4)).astype(np.float32)
+        buf = np.zeros(400, np.float32)
+        buf[:n] = a
+        arrs.append(buf)
+        lens.append(n)
+        sums.append(a.sum())
+    path = os.path.join(HERE, "pairwise_kat.npz")
+    np.savez_compressed(path, x=np.array(arrs), n=np.array(lens, np.int32), s=np.array(sums, np.float32))
+    print("wrote", path, os.path.getsize(path))
+
+
+# -------------------------------------------------------------------------- MCTS
+def gen_mcts(np, quick):
+    import MCTS as mcts_mod
+    from Coach import Coach
+    from inflexion.InflexionGame import InflexionGame
+    from inflexion.pytorch.NNet import NNetWrapper
+    from utils import dotdict
+    from stubnet import stub_eval
+
+    class StubNNet(NNetWrapper):
+        def __init__(self, game):  # no torch model: the hash evaluator only
+            self.n_actions = game.max_actions
+            self.calls = 0
+
+        def predict(self, board):
+            self.calls += 1
+            return stub_eval(board, self.n_actions)
+
+    class Rec:
+        in_search = False
+        actions = []
+        last = None
+
+    orig_tns = InflexionGame.to_next_state
+
+    def tns(self, action):
+        nxt = orig_tns(self, action)
+        if not Rec.in_search:
+            Rec.actions.append(int(action))
+            Rec.last = nxt
+        return nxt
+
+    InflexionGame.to_next_state = tns
+
+    class RecMCTS(mcts_mod.MCTS):
+        moves = None
+
+        def getActionProb(self, game, temp=1):
+            Rec.in_search = True
+            calls0 = self.nnet.calls
+            probs = super().getActionProb(game, temp)
+            Rec.in_search = False
+            s = game.to_planes().tobytes()
+            counts, qs = [], []
+            for a in range(game.max_actions):
+                if (s, a) in self.Nsa:
+                    counts.append([a, int(self.Nsa[(s, a)])])
+                    q = self.Qsa[(s, a)]
+                    is32 = isinstance(q, np.ndarray)
+                    qs.append([a, float(np.asarray(q).reshape(-1)[0]) if is32 else float(q), int(is32)])
+            self.moves.append({"turn": game._curr_turn, "temp": temp, "counts": counts, "q": qs,
+                               "nodes": len(self.Ps), "exp": self.nnet.calls - calls0,
+                               "pi_sum": float(np.asarray(probs, np.float64).sum()),
+                               "board": game._board.astype(int).ravel().tolist()})
+            return probs
+
+    sets = {
+        "main": dict(max_turns=343, sims=25, cpuct=1, temp_threshold=30, seeds=list(range(8))),
+        "sims100": dict(max_turns=343, sims=100, cpuct=1, temp_threshold=30, seeds=[100, 101]),
+        "short": dict(max_turns=40, sims=25, cpuct=1, temp_threshold=30, seeds=list(range(200, 216))),
+        "pit": dict(max_turns=100, sims=50, cpuct=1.0, temp_threshold=10, seeds=list(range(300, 304))),
+        "deep": dict(max_turns=24, sims=400, cpuct=1, temp_threshold=5, seeds=[400, 401]),
+    }
+    if quick:
+        sets = {"short": sets["short"]}
+    for name, cfg in sets.items():
+        eps = []
+        t0 = time.time()
+        for seed in cfg["seeds"]:
+            game = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
+            nnet = StubNNet(game)
+            args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"],
+                            "tempThreshold": cfg["temp_threshold"]})
+            coach = Coach(game, nnet, args)
+            mcts = RecMCTS(nnet, args)
+            mcts.moves = []
+            Rec.actions = []
+            np.random.seed(seed)
+            examples = coach.executeEpisode((game.restarted(), mcts))
+            final = Rec.last
+            zs = [float(e[2]) for e in examples]
+            rle = []
+            for z in zs:
+                if rle and rle[-1][0] == z:
+                    rle[-1][1] += 1
+                else:
+                    rle.append([z, 1])
+            pol = hashlib.sha256(np.array([e[1] for e in examples], np.float64).tobytes()).hexdigest()
+            brd = hashlib.sha256(np.array([e[0] for e in examples], np.int64).tobytes()).hexdigest()
+            st = np.random.get_state()
+            nxt = np.random.randint(0, 2**32, size=4, dtype=np.uint32).tolist()
+            for m, a in zip(mcts.moves, Rec.actions):
+                m["action"] = a
+            eps.append({"seed": seed, "moves": mcts.moves, "n_moves": len(Rec.actions),
+                        "final_outcome": final.outcome.value, "final_player": final.player.num,
+                        "final_board": final._board.astype(int).ravel().tolist(),
+                        "expansions": nnet.calls, "nodes": len(mcts.Ps),
+                        "z_rle": rle, "n_examples": len(examples), "policy_sha256": pol,
+                        "board_sha256": brd, "rng_pos": int(st[2]), "rng_next": nxt})
+            print(f"  {name} seed {seed}: {len(Rec.actions)} moves, {nnet.calls} expansions, "
+                  f"outcome {final.outcome.name}, {time.time() - t0:.1f}s", flush=True)
+        _dump(f"mcts_{name}.json.gz", {"config": cfg, "episodes": eps})
+    InflexionGame.to_next_state = orig_tns
+
+
+# -------------------------------------------------------------------------- NNet
+def gen_nnet(np, InflexionGame):
+    import torch
+    from inflexion.pytorch.NNet import NNetWrapper
+    torch.manual_seed(0)
+    game = InflexionGame(7, max_turns=343, max_power=6)
+    w = NNetWrapper(game)
+    sd = w.nnet.state_dict()
+    names, sums, shas = [], [], []
+    for k, v in sd.items():
+        names.append(k)
+        sums.append(float(v.double().sum()))
+        shas.append(hashlib.sha256(v.detach().cpu().contiguous().numpy().tobytes()).hexdigest())
+    rs = np.random.RandomState(5)
+    planes = []
+    g = game.restarted()
+    while len(planes) < 64:
+        p = g.to_planes()
+        planes.append(g.random_symmetry(p) if len(planes) % 2 else p)
+        v = np.nonzero(g.valid_actions_mask())[0]
+        g = g.to_next_state(int(v[rs.randint(len(v))]))
+        if g.outcome.value != 0:
+            g = game.restarted()
+    planes = np.array(planes, np.int64)
+    P, V = [], []
+    for p in planes:
+        pi, v = w.predict(p)
+        P.append(pi)
+        V.append(v[0])
+    path = os.path.join(HERE, "nnet_golden.npz")
+    np.savez_compressed(path, planes=planes.astype(np.int16), P=np.array(P, np.float32),
+                        v=np.array(V, np.float32), names=np.array(names), sums=np.array(sums),
+                        sha256=np.array(shas))
+    print("wrote", path, os.path.getsize(path))
+
+
+def main():
+    _need_reference()
+    import numpy as np
+    from inflexion.InflexionGame import InflexionGame
+    from flags import GameOutcome
+    quick = "--quick" in sys.argv
+    only = [a for a in sys.argv[1:] if not a.startswith("--")]
+    jobs = {
+        "rng": lambda: gen_rng_kat(np),
+        "symmetry": lambda: gen_symmetry(np, InflexionGame),
+        "rules": lambda: gen_rules(np, InflexionGame, GameOutcome),
+        "pairwise": lambda: gen_pairwise(np),
+        "nnet": lambda: gen_nnet(np, InflexionGame),
+        "mcts": lambda: gen_mcts(np, quick),
+    }
+    for name, fn in jobs.items():
+        if only and name not in only:
+            continue
+        print("==", name, flush=True)
+        fn()
+
+
+if __name__ == "__main__":
+    main()
