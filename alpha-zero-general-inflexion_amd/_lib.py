@@ -1,0 +1,94 @@
+"""ctypes binding of libazg.so (the C ABI declared in include/azg.h).
+
+The HIP path is the only path: if the library is missing or a call fails, this
+module raises -- there is no CPU fallback.  torch is imported first so that the
+library binds the HIP runtime torch already loaded (same SONAME), which makes
+torch tensors' device pointers and streams directly usable by the engine.
+"""
+import ctypes
+import os
+import subprocess
+
+import torch  # noqa: F401  (load torch's libamdhip64 first)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libazg.so")
+CSRC = os.path.join(HERE, "csrc")
+
+GAME_INFLEXION = 1
+FLAG_GC = 1
+FLAG_RECORD = 2
+
+ERR = {0: "ok", -1: "bad argument", -2: "HIP error", -3: "node pool full", -4: "path too deep",
+       -5: "no valid action", -6: "bad call order"}
+
+
+class AzgError(RuntimeError):
+    pass
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("game_kind", ctypes.c_int32), ("n", ctypes.c_int32), ("max_turns", ctypes.c_int32),
+                ("num_games", ctypes.c_int32), ("sims", ctypes.c_int32), ("temp_threshold", ctypes.c_int32),
+                ("cpuct", ctypes.c_double), ("seed_base", ctypes.c_uint32), ("pad0", ctypes.c_int32),
+                ("first_game", ctypes.c_int64), ("node_capacity", ctypes.c_int32),
+                ("max_depth", ctypes.c_int32), ("max_moves", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+assert ctypes.sizeof(Config) == 64
+
+# (name, restype, argtypes) of every symbol include/azg.h declares
+_VP, _I32, _I64, _U32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32
+SIGNATURES = [
+    ("azg_create", ctypes.c_int, [ctypes.POINTER(Config), _VP, ctypes.POINTER(_VP)]),
+    ("azg_destroy", None, [_VP]),
+    ("azg_last_error", ctypes.c_char_p, []),
+    ("azg_abi_version", ctypes.c_int, []),
+    ("azg_reset", ctypes.c_int, [_VP, _U32, _I64, _VP]),
+    ("azg_sim_begin", ctypes.c_int, [_VP, _VP, _VP]),
+    ("azg_sim_end", ctypes.c_int, [_VP, _VP, _I32, _VP, _VP]),
+    ("azg_stub_eval", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    ("azg_move_end", ctypes.c_int, [_VP, _VP]),
+    ("azg_active_games", ctypes.c_int, [_VP, ctypes.POINTER(_I32), _VP]),
+    ("azg_get_state", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP]),
+    ("azg_set_root", ctypes.c_int, [_VP, _I32, _VP, _I32, _I32, _VP]),
+    ("azg_get_rng", ctypes.c_int, [_VP, _I32, _VP, ctypes.POINTER(_I32), _VP]),
+    ("azg_set_rng", ctypes.c_int, [_VP, _I32, _VP, _I32, _VP]),
+    ("azg_root_counts", ctypes.c_int, [_VP, _I32, _VP, _VP]),
+    ("azg_read_moves", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
+    ("azg_stats", ctypes.c_int, [_VP, _VP, _VP]),
+    ("azg_device_ptrs", ctypes.c_int, [_VP, _VP]),
+]
+
+_lib = None
+
+
+def build(force=False):
+    """Compile libazg.so for gfx950 in-tree (hipcc; no GPU needed)."""
+    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    newest = max(os.path.getmtime(s) for s in srcs)
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
+        subprocess.check_call(["make", "-s", "-C", CSRC])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise AzgError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                           f"g.build()'` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().azg_last_error().decode(errors="replace")
+        raise AzgError(f"libazg: {ERR.get(rc, rc)} ({rc}): {msg}")
+    return rc

@@ -1,0 +1,322 @@
+// azg_capi.cpp -- the C ABI (include/azg.h) over the engine kernels.
+//
+// Owns every device allocation of an engine (one arena per engine, sized once
+// at azg_create for G slots x node_capacity nodes) and forwards each call to a
+// kernel on the caller's stream.  Calls that hand data to the host synchronise
+// that stream; the per-simulation calls never do.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/azg.h"
+#include "azg_engine.h"
+#include "azg_launch.h"
+
+using azg::Dev;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess)                                                           \
+            return fail(AZG_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+int next_pow2(int x) {
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+}  // namespace
+
+struct azg_engine {
+    azg_config cfg;
+    Dev d;
+    int device;
+    std::vector<void*> allocs;
+    int32_t* summary;   // device [2]
+    long long* stats;   // device [8]
+    int32_t* counts1;   // device [A]
+    size_t bytes;
+};
+
+template <typename T>
+static int dalloc(azg_engine* e, T** p, size_t n) {
+    void* q = nullptr;
+    size_t b = n * sizeof(T);
+    if (b == 0) b = 16;
+    HIP_TRY(hipMalloc(&q, b));
+    HIP_TRY(hipMemset(q, 0, b));
+    e->allocs.push_back(q);
+    e->bytes += b;
+    *p = (T*)q;
+    return 0;
+}
+
+#define ALLOC(ptr, n)                          \
+    do {                                       \
+        int _r = dalloc(e, &(ptr), (size_t)(n)); \
+        if (_r) {                              \
+            azg_destroy(e);                    \
+            return _r;                         \
+        }                                      \
+    } while (0)
+
+extern "C" {
+
+const char* azg_last_error(void) { return g_err.c_str(); }
+
+int azg_abi_version(void) { return AZG_ABI_VERSION; }
+
+int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
+    if (!cfg || !out) return fail(AZG_ERR_ARG, "null argument");
+    if (cfg->game_kind != AZG_GAME_INFLEXION) return fail(AZG_ERR_ARG, "only AZG_GAME_INFLEXION is built");
+    if (cfg->n != azg::N) return fail(AZG_ERR_ARG, "this build is specialised for InflexionGame(7)");
+    if (cfg->num_games <= 0 || cfg->sims <= 0 || cfg->max_turns < 0)
+        return fail(AZG_ERR_ARG, "num_games, sims must be > 0 and max_turns >= 0");
+    auto* e = new azg_engine();
+    memset(&e->d, 0, sizeof(Dev));
+    e->cfg = *cfg;
+    e->bytes = 0;
+    HIP_TRY(hipGetDevice(&e->device));
+    Dev& d = e->d;
+    d.G = cfg->num_games;
+    d.M = cfg->node_capacity > 0 ? cfg->node_capacity : 16 * cfg->sims + 128;
+    if (d.M >= (1 << 21)) {
+        delete e;
+        return fail(AZG_ERR_ARG, "node_capacity must be < 2^21");
+    }
+    d.H = next_pow2(2 * d.M < 64 ? 64 : 2 * d.M);
+    d.DMAX = cfg->max_depth > 0 ? cfg->max_depth : 256;
+    d.max_moves = cfg->max_moves > 0 ? cfg->max_moves : cfg->max_turns + 1;
+    d.max_turns = cfg->max_turns;
+    d.sims = cfg->sims;
+    d.temp_threshold = cfg->temp_threshold;
+    d.flags = cfg->flags;
+    d.cpuct_f = (float)cfg->cpuct;
+    const size_t G = (size_t)d.G, GM = G * (size_t)d.M;
+    ALLOC(d.board, G * 64);
+    ALLOC(d.turn, G);
+    ALLOC(d.player, G);
+    ALLOC(d.outcome, G);
+    ALLOC(d.active, G);
+    ALLOC(d.mt, G * azg::MT_N);
+    ALLOC(d.mt_pos, G);
+    ALLOC(d.node_own, GM);
+    ALLOC(d.node_opp, GM);
+    ALLOC(d.node_turn, GM);
+    ALLOC(d.node_cs, GM);
+    ALLOC(d.node_Ns, GM);
+    ALLOC(d.node_P, GM * azg::AP);
+    ALLOC(d.node_N, GM * azg::AP);
+    ALLOC(d.node_Q, GM * azg::AP);
+    ALLOC(d.free_stack, GM);
+    ALLOC(d.free_top, G);
+    ALLOC(d.live, G);
+    ALLOC(d.table, G * (size_t)d.H);
+    ALLOC(d.path, G * (size_t)d.DMAX);
+    ALLOC(d.leaf_kind, G);
+    ALLOC(d.leaf_depth, G);
+    ALLOC(d.leaf_value, G);
+    ALLOC(d.leaf_own, G);
+    ALLOC(d.leaf_opp, G);
+    ALLOC(d.leaf_turn, G);
+    ALLOC(d.leaf_cs, G);
+    ALLOC(d.leaf_slot, G);
+    ALLOC(d.moves, G);
+    ALLOC(d.rec_action, G * (size_t)d.max_moves);
+    ALLOC(d.rec_temp, G * (size_t)d.max_moves);
+    if (cfg->flags & AZG_FLAG_RECORD) ALLOC(d.rec_counts, G * (size_t)d.max_moves * azg::A);
+    ALLOC(d.st_exp, G);
+    ALLOC(d.st_term, G);
+    ALLOC(d.st_fallback, G);
+    ALLOC(d.st_sims, G);
+    ALLOC(d.st_depth, G);
+    ALLOC(d.st_live_max, G);
+    ALLOC(d.err, G);
+    ALLOC(e->summary, 2);
+    ALLOC(e->stats, 8);
+    ALLOC(e->counts1, azg::A);
+    *out = e;
+    int r = azg_reset(e, cfg->seed_base, cfg->first_game, stream);
+    if (r) {
+        azg_destroy(e);
+        *out = nullptr;
+        return r;
+    }
+    return 0;
+}
+
+void azg_destroy(azg_engine* e) {
+    if (!e) return;
+    for (void* p : e->allocs) (void)hipFree(p);
+    delete e;
+}
+
+int azg_reset(azg_engine* e, uint32_t seed_base, int64_t first_game, void* stream) {
+    if (!e) return fail(AZG_ERR_ARG, "null engine");
+    e->cfg.seed_base = seed_base;
+    e->cfg.first_game = first_game;
+    HIP_TRY(azg::launch_reset(e->d, seed_base, (long long)first_game, (hipStream_t)stream));
+    return 0;
+}
+
+int azg_sim_begin(azg_engine* e, float* leaf_planes, void* stream) {
+    if (!e || !leaf_planes) return fail(AZG_ERR_ARG, "null argument");
+    HIP_TRY(azg::launch_select(e->d, leaf_planes, (hipStream_t)stream));
+    return 0;
+}
+
+int azg_sim_end(azg_engine* e, const float* P, int32_t p_stride, const float* v, void* stream) {
+    if (!e || !P || !v || p_stride < azg::A) return fail(AZG_ERR_ARG, "bad P/v");
+    HIP_TRY(azg::launch_expand_backup(e->d, P, p_stride, v, (hipStream_t)stream));
+    return 0;
+}
+
+int azg_stub_eval(azg_engine* e, const float* leaf_planes, float* P, float* v, void* stream) {
+    if (!e || !leaf_planes || !P || !v) return fail(AZG_ERR_ARG, "null argument");
+    HIP_TRY(azg::launch_stub_eval(e->d, leaf_planes, P, v, (hipStream_t)stream));
+    return 0;
+}
+
+int azg_move_end(azg_engine* e, void* stream) {
+    if (!e) return fail(AZG_ERR_ARG, "null engine");
+    HIP_TRY(azg::launch_move_end(e->d, (hipStream_t)stream));
+    return 0;
+}
+
+static const char* err_name(int code) {
+    switch (code) {
+        case AZG_ERR_NODE_POOL: return "node pool or hash table full (raise node_capacity)";
+        case AZG_ERR_PATH: return "search path deeper than max_depth";
+        case AZG_ERR_NO_ACTION: return "no valid action at a searched node";
+        default: return "engine error";
+    }
+}
+
+int azg_active_games(azg_engine* e, int32_t* out, void* stream) {
+    if (!e || !out) return fail(AZG_ERR_ARG, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    int32_t h[2];
+    HIP_TRY(azg::launch_summary(e->d, e->summary, st));
+    HIP_TRY(hipMemcpyAsync(h, e->summary, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *out = h[0];
+    if (h[1]) return fail(h[1], err_name(h[1]));
+    return 0;
+}
+
+int azg_get_state(azg_engine* e, int8_t* boards, int32_t* turns, int32_t* players, int32_t* outcomes,
+                  int32_t* active, void* stream) {
+    if (!e) return fail(AZG_ERR_ARG, "null engine");
+    hipStream_t st = (hipStream_t)stream;
+    const int G = e->d.G, nn = azg::CELLS;
+    if (boards) {
+        std::vector<int8_t> tmp((size_t)G * 64);
+        HIP_TRY(hipMemcpyAsync(tmp.data(), e->d.board, tmp.size(), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        for (int g = 0; g < G; ++g) memcpy(boards + (size_t)g * nn, tmp.data() + (size_t)g * 64, nn);
+    }
+    if (turns) HIP_TRY(hipMemcpyAsync(turns, e->d.turn, G * 4, hipMemcpyDeviceToHost, st));
+    if (players) HIP_TRY(hipMemcpyAsync(players, e->d.player, G * 4, hipMemcpyDeviceToHost, st));
+    if (outcomes) HIP_TRY(hipMemcpyAsync(outcomes, e->d.outcome, G * 4, hipMemcpyDeviceToHost, st));
+    if (active) HIP_TRY(hipMemcpyAsync(active, e->d.active, G * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+int azg_set_root(azg_engine* e, int32_t slot, const int8_t* board, int32_t turn, int32_t player, void* stream) {
+    if (!e || !board || slot < 0 || slot >= e->d.G || (player != 1 && player != -1))
+        return fail(AZG_ERR_ARG, "bad set_root argument");
+    hipStream_t st = (hipStream_t)stream;
+    int8_t b[64] = {0};
+    memcpy(b, board, azg::CELLS);
+    const int32_t ongoing = azg::ONGOING, one = 1, zero = 0;
+    HIP_TRY(hipMemcpyAsync(e->d.board + (size_t)slot * 64, b, 64, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(e->d.turn + slot, &turn, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(e->d.player + slot, &player, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(e->d.outcome + slot, &ongoing, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(e->d.active + slot, &one, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(e->d.moves + slot, &turn, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(e->d.err + slot, &zero, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+int azg_get_rng(azg_engine* e, int32_t slot, uint32_t* mt, int32_t* pos, void* stream) {
+    if (!e || !mt || !pos || slot < 0 || slot >= e->d.G) return fail(AZG_ERR_ARG, "bad get_rng argument");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipMemcpyAsync(mt, e->d.mt + (size_t)slot * azg::MT_N, azg::MT_N * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(pos, e->d.mt_pos + slot, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+int azg_set_rng(azg_engine* e, int32_t slot, const uint32_t* mt, int32_t pos, void* stream) {
+    if (!e || !mt || slot < 0 || slot >= e->d.G || pos < 0 || pos > azg::MT_N)
+        return fail(AZG_ERR_ARG, "bad set_rng argument");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipMemcpyAsync(e->d.mt + (size_t)slot * azg::MT_N, mt, azg::MT_N * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(e->d.mt_pos + slot, &pos, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+int azg_root_counts(azg_engine* e, int32_t slot, int32_t* counts, void* stream) {
+    if (!e || !counts || slot < 0 || slot >= e->d.G) return fail(AZG_ERR_ARG, "bad root_counts argument");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(azg::launch_root_counts(e->d, slot, e->counts1, st));
+    HIP_TRY(hipMemcpyAsync(counts, e->counts1, azg::A * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+int azg_read_moves(azg_engine* e, int32_t* actions, int8_t* temps, int32_t* counts, int32_t* moves,
+                   void* stream) {
+    if (!e) return fail(AZG_ERR_ARG, "null engine");
+    hipStream_t st = (hipStream_t)stream;
+    const size_t G = (size_t)e->d.G, MM = (size_t)e->d.max_moves;
+    if (actions) HIP_TRY(hipMemcpyAsync(actions, e->d.rec_action, G * MM * 4, hipMemcpyDeviceToHost, st));
+    if (temps) HIP_TRY(hipMemcpyAsync(temps, e->d.rec_temp, G * MM, hipMemcpyDeviceToHost, st));
+    if (counts) {
+        if (!e->d.rec_counts) return fail(AZG_ERR_STATE, "engine created without AZG_FLAG_RECORD");
+        HIP_TRY(hipMemcpyAsync(counts, e->d.rec_counts, G * MM * azg::A * 4, hipMemcpyDeviceToHost, st));
+    }
+    if (moves) HIP_TRY(hipMemcpyAsync(moves, e->d.moves, G * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+int azg_stats(azg_engine* e, int64_t* out, void* stream) {
+    if (!e || !out) return fail(AZG_ERR_ARG, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(azg::launch_stats(e->d, e->stats, st));
+    HIP_TRY(hipMemcpyAsync(out, e->stats, 8 * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+int azg_device_ptrs(azg_engine* e, void** out) {
+    if (!e || !out) return fail(AZG_ERR_ARG, "null argument");
+    out[0] = e->d.board;
+    out[1] = e->d.turn;
+    out[2] = e->d.player;
+    out[3] = e->d.outcome;
+    out[4] = e->d.active;
+    out[5] = e->d.rec_action;
+    out[6] = e->d.rec_counts;
+    out[7] = e->d.moves;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,92 @@
+// azg_engine.h -- device-side state of the batched self-play engine.
+//
+// Everything lives in HBM as structure-of-arrays indexed by game slot g (and
+// node id within the slot's pool).  One 64-lane wavefront owns one game slot
+// in every kernel, so no two waves ever touch the same slot's tree: the
+// reference's sequential per-game semantics (MCTS.py) are preserved exactly and
+// no atomics are needed on the tree.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace azg {
+
+constexpr int WAVE = 64;
+constexpr int N = 7;                 // InflexionGame(7) (main.py:34)
+constexpr int CELLS = N * N;         // 49
+constexpr int A = 7 * CELLS;         // 343 = policy_shape (7, 7, 7), InflexionGame.py:47-48
+constexpr int AP = 384;              // per-node action stride, 6 x 64 lanes
+constexpr int AJ = AP / WAVE;        // 6 action chunks per lane
+constexpr int MT_N = 624;
+constexpr int MAX_POWER_AT_SPAWN = 48;   // InflexionGame.py:69
+
+enum Outcome : int { ONGOING = 0, DRAW = 1, WON = 2, LOST = 3 };
+enum LeafKind : int { LEAF_NONE = 0, LEAF_EXPAND = 1, LEAF_TERMINAL = 2 };
+
+// numpy float32 add.reduce pairwise plan: leaves summed with 8 accumulators,
+// combined by an RPN program (op >= 0: push leaf op; op == -1: add top two).
+struct PairwisePlan {
+    int nleaf;
+    int off[16];
+    int len[16];
+    int nops;
+    int8_t ops[32];
+};
+
+struct Dev {
+    int G, M, H, DMAX, max_moves;
+    int max_turns, sims, temp_threshold, flags;
+    float cpuct_f;
+    PairwisePlan pw;
+
+    // per slot
+    int8_t* board;       // [G][64]
+    int32_t* turn;       // [G]
+    int32_t* player;     // [G]  +1 RED, -1 BLUE
+    int32_t* outcome;    // [G]  Outcome w.r.t. player to move
+    int32_t* active;     // [G]
+    uint32_t* mt;        // [G][624]  numpy legacy MT19937 state
+    int32_t* mt_pos;     // [G]
+
+    // node pool [G*M]
+    uint64_t* node_own;
+    uint64_t* node_opp;
+    int32_t* node_turn;  // -1 = free
+    int32_t* node_cs;
+    int32_t* node_Ns;
+    float* node_P;       // [G*M*AP]
+    uint32_t* node_N;    // [G*M*AP]  bit31: Q is f32-typed
+    double* node_Q;      // [G*M*AP]
+    int32_t* free_stack; // [G*M]
+    int32_t* free_top;   // [G]
+    int32_t* live;       // [G] allocated nodes
+    uint64_t* table;     // [G*H] (tag << 32) | (id + 1), 0 = empty
+
+    // search path / leaf
+    int32_t* path;       // [G*DMAX] (node << 10) | action
+    int32_t* leaf_kind;  // [G]
+    int32_t* leaf_depth; // [G]
+    double* leaf_value;  // [G]
+    uint64_t* leaf_own;
+    uint64_t* leaf_opp;
+    int32_t* leaf_turn;
+    int32_t* leaf_cs;
+    int32_t* leaf_slot;
+
+    // per-move record
+    int32_t* moves;      // [G]
+    int32_t* rec_action; // [G*max_moves]
+    int8_t* rec_temp;    // [G*max_moves]
+    int32_t* rec_counts; // [G*max_moves*A] or null
+
+    // per-slot counters (no atomics: one wave per slot)
+    int64_t* st_exp;
+    int64_t* st_term;
+    int64_t* st_fallback;
+    int64_t* st_sims;
+    int32_t* st_depth;
+    int32_t* st_live_max;
+    int32_t* err;        // [G] first error code seen in the slot
+};
+
+}  // namespace azg

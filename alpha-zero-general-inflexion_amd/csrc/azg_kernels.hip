@@ -1,0 +1,877 @@
+// azg_kernels.hip -- CDNA4 (gfx950) kernels of the batched self-play engine.
+//
+// Launch geometry: one 64-thread workgroup (= one wavefront) per game slot.
+// The tree work per simulation is latency-bound pointer chasing over a handful
+// of 1.5-3 KB node rows (~4.8 KB per expansion), so the design
+// goal is: every HBM access is a coalesced 256 B-1.5 KB wave-wide row read,
+// every reduction is an in-register __shfl_xor butterfly, no atomics on the
+// tree (the slot is owned by its wave), and no host synchronisation between
+// kernels (the whole move can be captured in a hipGraph).
+//
+// Numerics restate the reference bit-exactly (oracle/oracle.c is the CPU
+// checker): f32 ops are single-rounded (-ffp-contract=off
+// for this file), math.sqrt is a correctly rounded f64 sqrt, Q values that the
+// reference holds as Python numbers are kept in f64 with a type bit.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "azg_engine.h"
+#include "azg_launch.h"
+
+namespace azg {
+
+// ---------------------------------------------------------------- wave utils
+__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+
+__device__ __forceinline__ int wave_sum(int x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+__device__ __forceinline__ long long wave_sum64(long long x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+__device__ __forceinline__ int wave_max(int x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = max(x, __shfl_xor(x, o));
+    return x;
+}
+
+__device__ __forceinline__ int mod_n(int x) { return ((x % N) + N) % N; }
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ uint64_t key_hash(uint64_t own, uint64_t opp, int turn, int cs) {
+    return mix64(own ^ mix64(opp ^ (((uint64_t)(uint32_t)turn << 1) | (uint64_t)cs)));
+}
+
+__device__ __forceinline__ double outcome_value(int o) {
+    return o == DRAW ? 1e-4 : o == WON ? 1.0 : o == LOST ? -1.0 : 0.0;  // flags.py:32-36
+}
+
+__device__ __forceinline__ int flip_outcome(int o) {  // GameOutcome.opposite, Game.py:49-62
+    return o == WON ? LOST : o == LOST ? WON : o;
+}
+
+// valid_actions_mask (InflexionGame.py:93-100) as a function of the state key.
+__device__ __forceinline__ bool action_valid(int a, uint64_t own, uint64_t opp, int cs) {
+    int m = a / CELLS, c = a - m * CELLS;
+    if (m < 6) return (own >> c) & 1ull;
+    return cs && !(((own | opp) >> c) & 1ull);
+}
+
+// ------------------------------------------------------------ numpy pairwise
+struct PW {
+    int nleaf = 0, nops = 0;
+    int off[16] = {}, len[16] = {}, ops[32] = {};
+};
+constexpr void pw_build(PW& p, int off, int n) {
+    if (n <= 128) {
+        p.ops[p.nops++] = p.nleaf;
+        p.off[p.nleaf] = off;
+        p.len[p.nleaf] = n;
+        p.nleaf++;
+        return;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    pw_build(p, off, n2);
+    pw_build(p, off + n2, n - n2);
+    p.ops[p.nops++] = -1;
+}
+constexpr PW make_pw(int n) {
+    PW p{};
+    pw_build(p, 0, n);
+    return p;
+}
+constexpr PW kPW = make_pw(A);
+static_assert(kPW.nleaf <= 8, "one pass of 8 lanes per leaf");
+
+// float32 add.reduce in numpy's exact association (MCTS.py:96, :107).
+// x: LDS [A]; acc: LDS [64]; leaf: LDS [16].  Returns the sum in every lane.
+__device__ float pairwise_sum(const float* x, float* acc, float* leaf) {
+    const int lane = lane_id();
+    const int l = lane >> 3, j = lane & 7;
+#pragma unroll
+    for (int q = 0; q < kPW.nleaf; ++q) {
+        if (l == q && kPW.len[q] >= 8) {
+            const int off = kPW.off[q], full = kPW.len[q] - kPW.len[q] % 8;
+            float r = x[off + j];
+            for (int i = 8; i < full; i += 8) r = r + x[off + i + j];
+            acc[lane] = r;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPW.nleaf; ++q) {
+        if (lane == q) {
+            const int off = kPW.off[q], len = kPW.len[q];
+            float res;
+            int i;
+            if (len < 8) {
+                res = 0.0f;
+                i = 0;
+            } else {
+                const float* r = acc + q * 8;
+                res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+                i = len - len % 8;
+            }
+            for (; i < len; ++i) res = res + x[off + i];
+            leaf[q] = res;
+        }
+    }
+    __syncthreads();
+    float st[8];
+    int sp = 0;
+#pragma unroll
+    for (int k = 0; k < kPW.nops; ++k) {
+        if (kPW.ops[k] >= 0) {
+            st[sp++] = leaf[kPW.ops[k]];
+        } else {
+            float b = st[--sp];
+            float a = st[--sp];
+            st[sp++] = a + b;
+        }
+    }
+    __syncthreads();
+    return 0.0f + st[0];
+}
+
+// ------------------------------------------------------------------- MT19937
+// numpy RandomState (legacy) stream of one game, staged in LDS for the kernel.
+struct BlockRng {
+    uint32_t* g;   // global [624]
+    int32_t* gpos;
+    uint32_t* s;   // LDS [624]
+    int pos;
+    bool loaded, dirty;
+};
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t nxt, uint32_t far) {
+    uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
+    return far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// In-place sequential twist restated as three wave-parallel phases:
+// i < 227 reads only old words; 227 <= i < 623 reads new[i-227]; i = 623 last.
+__device__ void mt_twist(uint32_t* s) {
+    const int lane = lane_id();
+    for (int b = 0; b < 227; b += WAVE) {
+        int i = b + lane;
+        uint32_t v = 0;
+        if (i < 227) v = mt_mix(s[i], s[i + 1], s[i + 397]);
+        __syncthreads();
+        if (i < 227) s[i] = v;
+        __syncthreads();
+    }
+    for (int b = 227; b < 623; b += WAVE) {
+        int i = b + lane;
+        uint32_t v = 0;
+        if (i < 623) v = mt_mix(s[i], s[i + 1], s[i - 227]);
+        __syncthreads();
+        if (i < 623) s[i] = v;
+        __syncthreads();
+    }
+    if (lane == 0) s[623] = mt_mix(s[623], s[0], s[396]);
+    __syncthreads();
+}
+
+__device__ uint32_t rng_u32(BlockRng& R) {
+    if (!R.loaded) {
+        for (int i = lane_id(); i < MT_N; i += WAVE) R.s[i] = R.g[i];
+        __syncthreads();
+        R.loaded = true;
+    }
+    if (R.pos >= MT_N) {
+        mt_twist(R.s);
+        R.pos = 0;
+        R.dirty = true;
+    }
+    return mt_temper(R.s[R.pos++]);
+}
+
+__device__ int rng_randint(BlockRng& R, int lo, int hi) {  // legacy masked rejection
+    uint32_t rng = (uint32_t)(hi - 1 - lo);
+    if (rng == 0) return lo;
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    for (;;) {
+        uint32_t v = rng_u32(R) & mask;
+        if (v <= rng) return lo + (int)v;
+    }
+}
+
+__device__ double rng_random_sample(BlockRng& R) {
+    uint32_t a = rng_u32(R) >> 5, b = rng_u32(R) >> 6;
+    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+}
+
+__device__ void rng_store(BlockRng& R) {
+    if (R.dirty)
+        for (int i = lane_id(); i < MT_N; i += WAVE) R.g[i] = R.s[i];
+    if (lane_id() == 0) *R.gpos = R.pos;
+}
+
+// ------------------------------------------------------------------- rules
+// One lane per cell (lanes 0..48).  State: cell value, turn, player, outcome.
+struct Pos {
+    int cell, turn, player, outcome;
+};
+
+__device__ __forceinline__ void pos_key(const Pos& p, uint64_t& own, uint64_t& opp, int& cs) {
+    const int lane = lane_id();
+    const bool on = lane < CELLS;
+    own = __ballot(on && p.cell * p.player > 0);
+    opp = __ballot(on && p.cell * p.player < 0);
+    cs = wave_sum(on ? abs(p.cell) : 0) <= MAX_POWER_AT_SPAWN;
+}
+
+// InflexionGame.execute_move (:273-310) + Game.player setter (:49-62).
+__device__ void pos_apply(Pos& p, int a, int max_turns) {
+    const int lane = lane_id();
+    const int m = a / CELLS, c = a - m * CELLS, r = c / N, q = c - (c / N) * N;
+    const int orig = __shfl(p.cell, c);
+    const bool spread = m < 6;
+    if (!spread) {
+        if (lane == c) p.cell = p.player;
+    } else if (lane < CELLS) {
+        const int dr = (m == 0 || m == 4) ? 1 : (m == 1 || m == 5) ? -1 : 0;
+        const int dq = (m == 2 || m == 5) ? 1 : (m == 3 || m == 4) ? -1 : 0;
+        const int power = abs(orig);
+        const int lr = lane / N, lq = lane - (lane / N) * N;
+        const int k = dr != 0 ? mod_n((lr - r) * dr) : mod_n((lq - q) * dq);
+        const bool hit = k >= 1 && k <= power && mod_n(r + k * dr) == lr && mod_n(q + k * dq) == lq;
+        if (hit) {
+            int x = abs(p.cell) + 1;
+            p.cell = (x > 6 ? 0 : x) * p.player;
+        }
+        if (lane == c) p.cell = 0;
+    }
+    const bool on = lane < CELLS;
+    const uint64_t oppb = __ballot(on && p.cell * p.player < 0);
+    const int sum = wave_sum(on ? p.cell : 0);
+    const uint64_t anyb = __ballot(on && p.cell != 0);
+    int out = ONGOING;
+    if (spread && oppb == 0) {
+        out = WON;
+    } else if (p.turn >= max_turns) {
+        const int diff = p.player * sum;
+        out = diff >= 2 ? WON : diff <= -2 ? LOST : DRAW;
+    } else if (anyb == 0) {
+        out = DRAW;
+    }
+    p.turn += 1;
+    p.player = -p.player;
+    p.outcome = flip_outcome(out);
+}
+
+// rotate(k) then translate(shift, axis): source cell of output cell c.
+__device__ __forceinline__ int sym_src(int c, int k, int shift, int axis) {
+    int r = c / N, q = c - (c / N) * N;
+    int tr = r, tq = q;
+    if (axis == 0) tr = r - shift;
+    else if (axis == 1) tq = q - shift;
+    else { tr = r + shift; tq = q - shift; }
+    tr = mod_n(tr);
+    tq = mod_n(tq);
+    const int s = (tr + tq) % N;
+    int rr, qq;
+    switch (k) {
+        case 0: rr = tr; qq = tq; break;
+        case 1: rr = -s; qq = tr; break;
+        case 2: rr = -tq; qq = s; break;
+        case 3: rr = -tr; qq = -tq; break;
+        case 4: rr = s; qq = -tr; break;
+        default: rr = tq; qq = -s; break;
+    }
+    return mod_n(rr) * N + mod_n(qq);
+}
+
+// ------------------------------------------------------------------- tree
+__device__ __forceinline__ size_t node_row(const Dev& E, int g, int id) { return ((size_t)g * E.M + id) * AP; }
+
+// Wave-cooperative open-addressing lookup: 64 consecutive slots per probe.
+// Returns node id or -1 (then *slot = first empty slot in probe order).
+__device__ int table_lookup(const Dev& E, int g, uint64_t own, uint64_t opp, int turn, int cs, int* slot) {
+    const int lane = lane_id();
+    const uint64_t h = key_hash(own, opp, turn, cs);
+    const uint32_t tag = (uint32_t)(h >> 32);
+    const uint64_t* T = E.table + (size_t)g * E.H;
+    const uint32_t hm = (uint32_t)E.H - 1;
+    const uint32_t base = (uint32_t)h & hm;
+    for (int probe = 0; probe < E.H; probe += WAVE) {
+        const uint32_t s = (base + (uint32_t)probe + (uint32_t)lane) & hm;
+        const uint64_t e = T[s];
+        const bool empty = e == 0;
+        int id = -1;
+        bool match = false;
+        if (!empty && (uint32_t)(e >> 32) == tag) {
+            id = (int)(uint32_t)e - 1;
+            const size_t ni = (size_t)g * E.M + id;
+            match = E.node_own[ni] == own && E.node_opp[ni] == opp && E.node_turn[ni] == turn &&
+                    E.node_cs[ni] == cs;
+        }
+        const uint64_t stop = __ballot(match || empty);
+        if (stop) {
+            const int l = __ffsll((unsigned long long)stop) - 1;
+            const int found = __shfl(match ? id : -1, l);
+            *slot = (int)((base + (uint32_t)probe + (uint32_t)l) & hm);
+            return found;
+        }
+    }
+    *slot = -1;
+    return -1;
+}
+
+// PUCT argmax (MCTS.py:114-131): strict '>' scan in action order == max u,
+// ties to the lowest action; NaN never wins.
+__device__ int puct_select(const Dev& E, int g, int id, uint64_t own, uint64_t opp, int cs) {
+    const int lane = lane_id();
+    const size_t row = node_row(E, g, id);
+    const int Ns = E.node_Ns[(size_t)g * E.M + id];
+    const float sq_edge = (float)sqrt((double)Ns);
+    const float sq_new = (float)sqrt((double)Ns + 1e-8);
+    float best = -INFINITY;
+    int besta = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+        const int a = lane + WAVE * j;
+        if (a < A && action_valid(a, own, opp, cs)) {
+            const float cp = E.cpuct_f * E.node_P[row + a];
+            const uint32_t nr = E.node_N[row + a];
+            const int n = (int)(nr & 0x7fffffffu);
+            float u;
+            if (n > 0) {
+                const float t = (cp * sq_edge) / (float)(1 + n);
+                u = (float)E.node_Q[row + a] + t;
+            } else {
+                u = cp * sq_new;
+            }
+            if (u > best) {
+                best = u;
+                besta = a;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float ou = __shfl_xor(best, o);
+        const int oa = __shfl_xor(besta, o);
+        if (ou > best || (ou == best && oa < besta)) {
+            best = ou;
+            besta = oa;
+        }
+    }
+    return besta == 0x7fffffff ? -1 : besta;
+}
+
+__device__ __forceinline__ void set_err(const Dev& E, int g, int code) {
+    if (lane_id() == 0 && E.err[g] == 0) E.err[g] = code;
+}
+
+// --------------------------------------------------------------- kernels
+// sim_begin: MCTS.search down to a leaf (MCTS.py:83-132), writing the leaf's
+// randomly symmetrised planes (MCTS.py:91-92) as f32 into the NN batch.
+__global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__ planes) {
+    __shared__ uint32_t s_mt[MT_N];
+    const int g = blockIdx.x, lane = lane_id();
+    float* out = planes + (size_t)g * 4 * CELLS;
+    if (!E.active[g] || E.err[g]) {
+        for (int i = lane; i < 4 * CELLS; i += WAVE) out[i] = 0.0f;
+        if (lane == 0) E.leaf_kind[g] = LEAF_NONE;
+        return;
+    }
+    Pos p;
+    p.cell = lane < CELLS ? (int)E.board[(size_t)g * 64 + lane] : 0;
+    p.turn = E.turn[g];
+    p.player = E.player[g];
+    p.outcome = E.outcome[g];
+    int depth = 0, kind = LEAF_NONE, slot = -1, cs = 0;
+    uint64_t own = 0, opp = 0;
+    double tval = 0.0;
+    int32_t* path = E.path + (size_t)g * E.DMAX;
+    for (;;) {
+        if (p.outcome != ONGOING) {  // MCTS.py:85-87
+            kind = LEAF_TERMINAL;
+            tval = -outcome_value(p.outcome);
+            break;
+        }
+        pos_key(p, own, opp, cs);
+        const int id = table_lookup(E, g, own, opp, p.turn, cs, &slot);
+        if (id < 0) {
+            if (slot < 0) set_err(E, g, -3);
+            kind = slot < 0 ? LEAF_NONE : LEAF_EXPAND;
+            break;
+        }
+        const int a = puct_select(E, g, id, own, opp, cs);
+        if (a < 0) {
+            set_err(E, g, -5);
+            kind = LEAF_NONE;
+            break;
+        }
+        if (depth >= E.DMAX) {
+            set_err(E, g, -4);
+            kind = LEAF_NONE;
+            break;
+        }
+        if (lane == 0) path[depth] = (id << 10) | a;
+        depth++;
+        pos_apply(p, a, E.max_turns);
+    }
+    if (lane == 0) {
+        E.leaf_kind[g] = kind;
+        E.leaf_depth[g] = depth;
+        E.leaf_value[g] = tval;
+        E.leaf_own[g] = own;
+        E.leaf_opp[g] = opp;
+        E.leaf_turn[g] = p.turn;
+        E.leaf_cs[g] = cs;
+        E.leaf_slot[g] = slot;
+        if (depth > E.st_depth[g]) E.st_depth[g] = depth;
+        E.st_sims[g] += 1;
+    }
+    if (kind != LEAF_EXPAND) {
+        for (int i = lane; i < 4 * CELLS; i += WAVE) out[i] = 0.0f;
+        return;
+    }
+    // random_symmetry: randint(0,6), randint(0,n), choice(['r','q','s'])  (InflexionGame.py:120-121)
+    BlockRng R{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
+    const int k = rng_randint(R, 0, 6);
+    const int shift = rng_randint(R, 0, N);
+    const int axis = rng_randint(R, 0, 3);
+    rng_store(R);
+    if (lane < CELLS) {
+        const int src = sym_src(lane, k, shift, axis);
+        out[lane] = (float)((own >> src) & 1ull);
+        out[CELLS + lane] = (float)((opp >> src) & 1ull);
+        out[2 * CELLS + lane] = (float)p.turn;
+        out[3 * CELLS + lane] = (float)cs;
+    }
+}
+
+// Test evaluator: tests/golden/stubnet.py on the symmetrised planes.
+__global__ __launch_bounds__(WAVE) void stub_eval_kernel(const float* __restrict__ planes, float* __restrict__ P,
+                                                         float* __restrict__ v, int G) {
+    const int g = blockIdx.x, lane = lane_id();
+    const float* in = planes + (size_t)g * 4 * CELLS;
+    const bool on = lane < CELLS;
+    const uint64_t own = __ballot(on && in[lane] != 0.0f);
+    const uint64_t opp = __ballot(on && in[CELLS + lane] != 0.0f);
+    const uint64_t t = (uint64_t)(int64_t)(int)in[2 * CELLS];
+    const uint64_t kk = (uint64_t)(int64_t)(int)in[3 * CELLS];
+    const uint64_t h = mix64(own ^ mix64(opp ^ mix64((t << 1) | kk)));
+    const bool all_zero = (h >> 56) < 4;
+    for (int a = lane; a < A; a += WAVE) {
+        const uint64_t ha = mix64(h ^ ((uint64_t)(a + 1) * 0xD1B54A32D192ED03ull));
+        const float pa = (float)(uint32_t)(ha & 0xFFFFFFu) * 0x1p-24f;
+        P[(size_t)g * A + a] = (all_zero || (ha >> 59) == 0) ? 0.0f : pa;
+    }
+    if (lane == 0) v[g] = (float)((int)((h >> 20) & 2047) - 1024) / 1024.0f;
+}
+
+// sim_end: expand the leaf (MCTS.py:89-112) and back the value up the path
+// (MCTS.py:136-145).  The path holds distinct nodes (turn strictly increases
+// down a path), so lanes update one edge each with no atomics.
+__global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float* __restrict__ Pin, int p_stride,
+                                                             const float* __restrict__ vin) {
+    __shared__ float s_p[AP];
+    __shared__ float s_acc[WAVE];
+    __shared__ float s_leaf[16];
+    const int g = blockIdx.x, lane = lane_id();
+    const int kind = E.leaf_kind[g];
+    if (kind == LEAF_NONE) return;
+    double ret;
+    bool ret_f32;
+    if (kind == LEAF_EXPAND) {
+        const uint64_t own = E.leaf_own[g], opp = E.leaf_opp[g];
+        const int cs = E.leaf_cs[g], turn = E.leaf_turn[g];
+        float pv[AJ];
+        bool vv[AJ];
+#pragma unroll
+        for (int j = 0; j < AJ; ++j) {
+            const int a = lane + WAVE * j;
+            vv[j] = a < A && action_valid(a, own, opp, cs);
+            float x = a < A ? Pin[(size_t)g * p_stride + a] : 0.0f;
+            x = vv[j] ? x : x * 0.0f;  // policies *= valids
+            pv[j] = x;
+            s_p[a] = x;
+        }
+        __syncthreads();
+        const float sum = pairwise_sum(s_p, s_acc, s_leaf);
+        if (sum > 0.0f) {
+#pragma unroll
+            for (int j = 0; j < AJ; ++j) pv[j] = pv[j] / sum;
+        } else {  // MCTS.py:100-107 fallback: policies += valids; policies /= policies.sum()
+            if (lane == 0) E.st_fallback[g] += 1;
+#pragma unroll
+            for (int j = 0; j < AJ; ++j) {
+                pv[j] = (float)((double)pv[j] + (vv[j] ? 1.0 : 0.0));
+                s_p[lane + WAVE * j] = pv[j];
+            }
+            __syncthreads();
+            const float s2 = pairwise_sum(s_p, s_acc, s_leaf);
+#pragma unroll
+            for (int j = 0; j < AJ; ++j) pv[j] = pv[j] / s2;
+        }
+        // allocate a node from the slot's free stack
+        int id = -1;
+        if (lane == 0) {
+            const int top = E.free_top[g];
+            if (top > 0) {
+                id = E.free_stack[(size_t)g * E.M + top - 1];
+                E.free_top[g] = top - 1;
+                const int lv = E.live[g] + 1;
+                E.live[g] = lv;
+                if (lv > E.st_live_max[g]) E.st_live_max[g] = lv;
+            }
+        }
+        id = __shfl(id, 0);
+        if (id < 0) {
+            set_err(E, g, -3);
+            return;
+        }
+        const size_t ni = (size_t)g * E.M + id, row = ni * AP;
+#pragma unroll
+        for (int j = 0; j < AJ; ++j) {
+            const int a = lane + WAVE * j;
+            E.node_P[row + a] = a < A ? pv[j] : 0.0f;
+            E.node_N[row + a] = 0u;
+            E.node_Q[row + a] = 0.0;
+        }
+        if (lane == 0) {
+            E.node_own[ni] = own;
+            E.node_opp[ni] = opp;
+            E.node_turn[ni] = turn;
+            E.node_cs[ni] = cs;
+            E.node_Ns[ni] = 0;
+            const uint64_t h = key_hash(own, opp, turn, cs);
+            E.table[(size_t)g * E.H + E.leaf_slot[g]] = ((h >> 32) << 32) | (uint64_t)(uint32_t)(id + 1);
+            E.st_exp[g] += 1;
+        }
+        ret = -(double)vin[g];  // `return -v`, a float32 array (MCTS.py:112)
+        ret_f32 = true;
+    } else {
+        ret = E.leaf_value[g];  // Python number (MCTS.py:87)
+        ret_f32 = false;
+        if (lane == 0) E.st_term[g] += 1;
+    }
+    const int depth = E.leaf_depth[g];
+    const int32_t* path = E.path + (size_t)g * E.DMAX;
+    for (int d = lane; d < depth; d += WAVE) {
+        const int packed = path[d];
+        const int id = packed >> 10, a = packed & 1023;
+        const double v = ((depth - 1 - d) & 1) ? -ret : ret;
+        const size_t ni = (size_t)g * E.M + id, row = ni * AP + a;
+        const uint32_t nr = E.node_N[row];
+        const int n = (int)(nr & 0x7fffffffu);
+        const bool qf = (nr >> 31) != 0;
+        double q = E.node_Q[row];
+        bool nf;
+        if (n == 0) {
+            q = v;
+            nf = ret_f32;
+        } else if (qf || ret_f32) {  // numpy f32 arithmetic with weak Python scalars
+            const float prod = qf ? (float)n * (float)q : (float)((double)n * q);
+            const float num = prod + (float)v;
+            q = (double)(num / (float)(n + 1));
+            nf = true;
+        } else {  // both Python numbers: double arithmetic
+            q = ((double)n * q + v) / (double)(n + 1);
+            nf = false;
+        }
+        E.node_Q[row] = q;
+        E.node_N[row] = (uint32_t)(n + 1) | (nf ? 0x80000000u : 0u);
+        E.node_Ns[ni] += 1;
+    }
+}
+
+// move_end: MCTS.getActionProb root policy (MCTS.py:48-60), Coach.executeEpisode
+// temperature + np.random.choice + step (Coach.py:68-84), record, node GC.
+__global__ __launch_bounds__(WAVE) void move_end_kernel(Dev E) {
+    __shared__ uint32_t s_mt[MT_N];
+    __shared__ int s_cnt[AP];
+    __shared__ double s_cdf[AP];
+    const int g = blockIdx.x, lane = lane_id();
+    if (!E.active[g] || E.err[g]) return;
+    Pos p;
+    p.cell = lane < CELLS ? (int)E.board[(size_t)g * 64 + lane] : 0;
+    p.turn = E.turn[g];
+    p.player = E.player[g];
+    p.outcome = E.outcome[g];
+    uint64_t own, opp;
+    int cs, slot;
+    pos_key(p, own, opp, cs);
+    const int id = table_lookup(E, g, own, opp, p.turn, cs, &slot);
+    int cnt[AJ];
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+        const int a = lane + WAVE * j;
+        cnt[j] = (id >= 0 && a < A) ? (int)(E.node_N[node_row(E, g, id) + a] & 0x7fffffffu) : 0;
+        s_cnt[a] = cnt[j];
+    }
+    const int m = E.moves[g];
+    const int temp = (m + 1) < E.temp_threshold;  // episodeStep < tempThreshold
+    BlockRng R{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
+    int action = -1;
+    if (temp == 0) {
+        int mx = cnt[0];
+#pragma unroll
+        for (int j = 1; j < AJ; ++j) mx = max(mx, cnt[j]);
+        mx = wave_max(mx);
+        uint64_t tie[AJ];
+        int nb = 0;
+#pragma unroll
+        for (int j = 0; j < AJ; ++j) {
+            const int a = lane + WAVE * j;
+            tie[j] = __ballot(a < A && cnt[j] == mx);
+            nb += __popcll(tie[j]);
+        }
+        int pick = rng_randint(R, 0, nb);  // np.random.choice(bestAs), draws only if nb > 1
+        // pick-th tied action in ascending order (chunk j holds actions 64j..64j+63)
+#pragma unroll
+        for (int j = 0; j < AJ; ++j) {
+            const int c = __popcll(tie[j]);
+            if (action < 0 && pick < c) {
+                uint64_t b = tie[j];
+                for (int k = 0; k < pick; ++k) b &= b - 1ull;
+                action = WAVE * j + __ffsll((unsigned long long)b) - 1;
+            }
+            if (action < 0) pick -= c;
+        }
+        (void)rng_random_sample(R);  // np.random.choice(len(pi), p=one-hot) still draws
+    } else {
+        __syncthreads();
+        if (lane == 0) {  // probs = counts / counts.sum(); cdf = cumsum (sequential f64)
+            long long tot = 0;
+            for (int a = 0; a < A; ++a) tot += s_cnt[a];
+            double acc = 0.0;
+            for (int a = 0; a < A; ++a) {
+                acc += (double)s_cnt[a] / (double)tot;
+                s_cdf[a] = acc;
+            }
+        }
+        __syncthreads();
+        const double last = s_cdf[A - 1];
+        const double u = rng_random_sample(R);
+        int first = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < AJ; ++j) {
+            const int a = lane + WAVE * j;
+            if (a < A && s_cdf[a] / last > u) first = min(first, a);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) first = min(first, __shfl_xor(first, o));
+        action = first == 0x7fffffff ? A : first;
+    }
+    rng_store(R);
+    if (m < E.max_moves) {
+        if (lane == 0) {
+            E.rec_action[(size_t)g * E.max_moves + m] = action;
+            E.rec_temp[(size_t)g * E.max_moves + m] = (int8_t)temp;
+        }
+        if (E.rec_counts) {
+            int32_t* rc = E.rec_counts + ((size_t)g * E.max_moves + m) * A;
+#pragma unroll
+            for (int j = 0; j < AJ; ++j) {
+                const int a = lane + WAVE * j;
+                if (a < A) rc[a] = cnt[j];
+            }
+        }
+    }
+    if (action < 0 || action >= A || !action_valid(action, own, opp, cs)) {
+        set_err(E, g, -5);
+        return;
+    }
+    pos_apply(p, action, E.max_turns);
+    if (lane < CELLS) E.board[(size_t)g * 64 + lane] = (int8_t)p.cell;
+    if (lane == 0) {
+        E.turn[g] = p.turn;
+        E.player[g] = p.player;
+        E.outcome[g] = p.outcome;
+        E.moves[g] = m + 1;
+        if (p.outcome != ONGOING) E.active[g] = 0;
+    }
+    if (!(E.flags & 1)) return;  // AZG_FLAG_GC
+    // Node GC: a search from a root at turn T only reaches keys with turn >= T
+    // (the key contains the turn), so nodes below T are dead; keep all others
+    // (transpositions may still reach them).  Finished game: free everything.
+    const int T = p.outcome != ONGOING ? 0x7fffffff : p.turn;
+    const size_t nb0 = (size_t)g * E.M;
+    int top = 0, live = 0;
+    for (int b = 0; b < E.M; b += WAVE) {
+        const int i = b + lane;
+        bool fr = false;
+        if (i < E.M) {
+            int t = E.node_turn[nb0 + i];
+            if (t >= 0 && t < T) {
+                E.node_turn[nb0 + i] = -1;
+                t = -1;
+            }
+            fr = t < 0;
+        }
+        const uint64_t fb = __ballot(fr);
+        if (fr) E.free_stack[nb0 + top + __popcll(fb & ((1ull << lane) - 1ull))] = i;
+        top += __popcll(fb);
+        live += __popcll(__ballot(i < E.M && !fr));
+    }
+    if (lane == 0) {
+        E.free_top[g] = top;
+        E.live[g] = live;
+    }
+    uint64_t* T64 = E.table + (size_t)g * E.H;
+    for (int s = lane; s < E.H; s += WAVE) T64[s] = 0ull;
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t hm = (uint32_t)E.H - 1;
+    for (int b = 0; b < E.M; b += WAVE) {
+        const int i = b + lane;
+        if (i < E.M && E.node_turn[nb0 + i] >= 0) {
+            const uint64_t h = key_hash(E.node_own[nb0 + i], E.node_opp[nb0 + i], E.node_turn[nb0 + i],
+                                        E.node_cs[nb0 + i]);
+            const unsigned long long ent = ((h >> 32) << 32) | (uint64_t)(uint32_t)(i + 1);
+            uint32_t s = (uint32_t)h & hm;
+            while (atomicCAS((unsigned long long*)&T64[s], 0ull, ent) != 0ull) s = (s + 1) & hm;
+        }
+    }
+}
+
+// Root visit counts of one slot (drop-in MCTS.getActionProb, MCTS.py:48-49).
+__global__ __launch_bounds__(WAVE) void root_counts_kernel(Dev E, int g, int32_t* out) {
+    const int lane = lane_id();
+    Pos p;
+    p.cell = lane < CELLS ? (int)E.board[(size_t)g * 64 + lane] : 0;
+    p.turn = E.turn[g];
+    p.player = E.player[g];
+    p.outcome = E.outcome[g];
+    uint64_t own, opp;
+    int cs, slot;
+    pos_key(p, own, opp, cs);
+    const int id = table_lookup(E, g, own, opp, p.turn, cs, &slot);
+    for (int a = lane; a < A; a += WAVE) out[a] = id >= 0 ? (int)(E.node_N[node_row(E, g, id) + a] & 0x7fffffffu) : 0;
+}
+
+// Fresh games in every slot (Coach.py:110-111): empty board, RED to move,
+// numpy RandomState(seed) per slot, empty tree.
+__global__ __launch_bounds__(WAVE) void reset_kernel(Dev E, uint32_t seed_base, long long first_game) {
+    const int g = blockIdx.x, lane = lane_id();
+    E.board[(size_t)g * 64 + lane] = 0;
+    if (lane == 0) {
+        E.turn[g] = 0;
+        E.player[g] = 1;
+        E.outcome[g] = ONGOING;
+        E.active[g] = 1;
+        E.moves[g] = 0;
+        E.err[g] = 0;
+        E.free_top[g] = E.M;
+        E.live[g] = 0;
+        E.st_exp[g] = E.st_term[g] = E.st_fallback[g] = E.st_sims[g] = 0;
+        E.st_depth[g] = E.st_live_max[g] = 0;
+        E.leaf_kind[g] = LEAF_NONE;
+        // init_genrand (RandomState.seed): sequential recurrence, one lane
+        uint32_t* mt = E.mt + (size_t)g * MT_N;
+        uint32_t x = seed_base + (uint32_t)(first_game + g);
+        mt[0] = x;
+        for (int i = 1; i < MT_N; ++i) {
+            x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
+            mt[i] = x;
+        }
+        E.mt_pos[g] = MT_N;
+    }
+    const size_t nb0 = (size_t)g * E.M;
+    for (int i = lane; i < E.M; i += WAVE) {
+        E.node_turn[nb0 + i] = -1;
+        E.free_stack[nb0 + i] = E.M - 1 - i;
+    }
+    uint64_t* T64 = E.table + (size_t)g * E.H;
+    for (int s = lane; s < E.H; s += WAVE) T64[s] = 0ull;
+}
+
+// [0] active slots, [1] first error code
+__global__ __launch_bounds__(256) void summary_kernel(Dev E, int32_t* out) {
+    int act = 0, err = 0;
+    for (int g = threadIdx.x; g < E.G; g += blockDim.x) {
+        act += E.active[g] && !E.err[g];
+        if (E.err[g] && !err) err = E.err[g];
+    }
+    __shared__ int s_a[256], s_e[256];
+    s_a[threadIdx.x] = act;
+    s_e[threadIdx.x] = err;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int a = 0, e = 0;
+        for (int i = 0; i < (int)blockDim.x; ++i) {
+            a += s_a[i];
+            if (!e) e = s_e[i];
+        }
+        out[0] = a;
+        out[1] = e;
+    }
+}
+
+__global__ __launch_bounds__(256) void stats_kernel(Dev E, long long* out) {
+    if (threadIdx.x != 0) return;
+    long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int g = 0; g < E.G; ++g) {
+        s[0] += E.st_exp[g];
+        s[1] += E.st_term[g];
+        s[2] += E.st_fallback[g];
+        s[3] = s[3] > E.st_depth[g] ? s[3] : E.st_depth[g];
+        s[4] = s[4] > E.st_live_max[g] ? s[4] : E.st_live_max[g];
+        if (!s[5] && E.err[g]) s[5] = E.err[g];
+        s[6] += E.st_sims[g];
+    }
+    for (int i = 0; i < 8; ++i) out[i] = s[i];
+}
+
+// ------------------------------------------------------------- launchers
+hipError_t launch_select(const Dev& E, float* planes, hipStream_t st) {
+    hipLaunchKernelGGL(select_kernel, dim3(E.G), dim3(WAVE), 0, st, E, planes);
+    return hipGetLastError();
+}
+hipError_t launch_stub_eval(const Dev& E, const float* planes, float* P, float* v, hipStream_t st) {
+    hipLaunchKernelGGL(stub_eval_kernel, dim3(E.G), dim3(WAVE), 0, st, planes, P, v, E.G);
+    return hipGetLastError();
+}
+hipError_t launch_expand_backup(const Dev& E, const float* P, int p_stride, const float* v, hipStream_t st) {
+    hipLaunchKernelGGL(expand_backup_kernel, dim3(E.G), dim3(WAVE), 0, st, E, P, p_stride, v);
+    return hipGetLastError();
+}
+hipError_t launch_move_end(const Dev& E, hipStream_t st) {
+    hipLaunchKernelGGL(move_end_kernel, dim3(E.G), dim3(WAVE), 0, st, E);
+    return hipGetLastError();
+}
+hipError_t launch_root_counts(const Dev& E, int g, int32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(root_counts_kernel, dim3(1), dim3(WAVE), 0, st, E, g, out);
+    return hipGetLastError();
+}
+hipError_t launch_reset(const Dev& E, uint32_t seed_base, long long first_game, hipStream_t st) {
+    hipLaunchKernelGGL(reset_kernel, dim3(E.G), dim3(WAVE), 0, st, E, seed_base, first_game);
+    return hipGetLastError();
+}
+hipError_t launch_summary(const Dev& E, int32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(summary_kernel, dim3(1), dim3(256), 0, st, E, out);
+    return hipGetLastError();
+}
+hipError_t launch_stats(const Dev& E, long long* out, hipStream_t st) {
+    hipLaunchKernelGGL(stats_kernel, dim3(1), dim3(256), 0, st, E, out);
+    return hipGetLastError();
+}
+
+}  // namespace azg

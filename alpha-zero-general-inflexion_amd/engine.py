@@ -1,0 +1,174 @@
+"""Batched self-play on one GPU: G concurrent games searched by libazg.so.
+
+Replaces, for G games at once, the reference loop
+
+    for each move:                                    Coach.executeEpisode (Coach.py:41-90)
+        for numMCTSSims:  MCTS.search(game)           MCTS.py:45-46, 62-145
+        pi = root visit counts ** (1/temp)            MCTS.py:48-60
+        action = np.random.choice(len(pi), p=pi)      Coach.py:81
+        game = game.to_next_state(action)             Coach.py:82
+
+One *simulation step* runs one MCTS.search for every live game: the select
+kernel walks each tree to a leaf and writes the leaf's randomly symmetrised
+planes into a [G,4,7,7] f32 batch, the evaluator (the PyTorch-ROCm
+InflexionNNet, or the hash stub used for bit-exact tests) fills P [G,343] and
+v [G], and the expand/backup kernel inserts the leaves and backs the values up.
+Nothing synchronises with the host inside a move.
+
+Game slot i plays the game with global index first_game + i, seeded like
+`np.random.seed(seed_base + first_game + i)`, so results do not depend on how
+games are spread over GPUs.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+
+A = 343
+CELLS = 49
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class SelfPlayEngine:
+    def __init__(self, num_games, *, sims=25, cpuct=1, temp_threshold=30, max_turns=343, seed_base=0,
+                 first_game=0, evaluator="stub", device=None, node_capacity=0, max_depth=0, record=True,
+                 gc=True, max_moves=0):
+        if not torch.cuda.is_available():
+            raise _lib.AzgError("SelfPlayEngine needs a HIP device (no CPU fallback)")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.G = int(num_games)
+        self.sims = int(sims)
+        self.evaluator = evaluator
+        self.L = _lib.lib()
+        with torch.cuda.device(self.device):
+            self.planes = torch.zeros((self.G, 4, 7, 7), dtype=torch.float32, device=self.device)
+            self.P = torch.zeros((self.G, A), dtype=torch.float32, device=self.device)
+            self.v = torch.zeros((self.G,), dtype=torch.float32, device=self.device)
+            cfg = _lib.Config(game_kind=_lib.GAME_INFLEXION, n=7, max_turns=int(max_turns), num_games=self.G,
+                              sims=self.sims, temp_threshold=int(temp_threshold), cpuct=float(cpuct),
+                              seed_base=int(seed_base) & 0xFFFFFFFF, pad0=0, first_game=int(first_game),
+                              node_capacity=int(node_capacity), max_depth=int(max_depth),
+                              max_moves=int(max_moves),
+                              flags=(_lib.FLAG_GC if gc else 0) | (_lib.FLAG_RECORD if record else 0))
+            self.cfg = cfg
+            h = ctypes.c_void_p()
+            check(self.L.azg_create(ctypes.byref(cfg), self._stream(), ctypes.byref(h)))
+            self.h = h
+        self.max_moves = cfg.max_moves if cfg.max_moves > 0 else cfg.max_turns + 1
+        self.record = record
+
+    # ------------------------------------------------------------------ plumbing
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.azg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ the hot path
+    def evaluate(self):
+        """Fill P, v for the current leaf batch (NNetWrapper.predict, batched)."""
+        ev = self.evaluator
+        if isinstance(ev, str):
+            if ev != "stub":
+                raise ValueError(f"unknown evaluator {ev!r}")
+            check(self.L.azg_stub_eval(self.h, _ptr(self.planes), _ptr(self.P), _ptr(self.v), self._stream()))
+            return
+        with torch.no_grad():
+            out_pi, out_v = ev(self.planes)
+            torch.exp(out_pi, out=self.P)  # predict returns exp(log_softmax) (NNet.py:94)
+            self.v.copy_(out_v.reshape(-1))
+
+    def simulate(self):
+        """One MCTS.search for every live game."""
+        s = self._stream()
+        check(self.L.azg_sim_begin(self.h, _ptr(self.planes), s))
+        self.evaluate()
+        check(self.L.azg_sim_end(self.h, _ptr(self.P), A, _ptr(self.v), s))
+
+    def move_end(self):
+        check(self.L.azg_move_end(self.h, self._stream()))
+
+    def move(self):
+        """numMCTSSims simulations + root policy / sample / apply for every live game."""
+        for _ in range(self.sims):
+            self.simulate()
+        self.move_end()
+
+    def active(self):
+        n = ctypes.c_int32()
+        check(self.L.azg_active_games(self.h, ctypes.byref(n), self._stream()))
+        return n.value
+
+    def play(self, max_moves=None):
+        """Play every slot's game to the end (or max_moves moves). Returns moves made."""
+        m = 0
+        while self.active() > 0 and (max_moves is None or m < max_moves):
+            self.move()
+            m += 1
+        return m
+
+    def reset(self, seed_base=None, first_game=None):
+        sb = self.cfg.seed_base if seed_base is None else int(seed_base) & 0xFFFFFFFF
+        fg = self.cfg.first_game if first_game is None else int(first_game)
+        self.cfg.seed_base, self.cfg.first_game = sb, fg
+        check(self.L.azg_reset(self.h, sb, fg, self._stream()))
+
+    # ------------------------------------------------------------------ results
+    def read_moves(self, counts=True):
+        G, MM = self.G, self.max_moves
+        actions = np.zeros((G, MM), np.int32)
+        temps = np.zeros((G, MM), np.int8)
+        moves = np.zeros(G, np.int32)
+        cnt = np.zeros((G, MM, A), np.int32) if (counts and self.record) else None
+        check(self.L.azg_read_moves(self.h, actions.ctypes.data, temps.ctypes.data,
+                                    cnt.ctypes.data if cnt is not None else None, moves.ctypes.data,
+                                    self._stream()))
+        return {"actions": actions, "temps": temps, "counts": cnt, "moves": moves}
+
+    def state(self):
+        G = self.G
+        boards = np.zeros((G, CELLS), np.int8)
+        turns, players, outcomes, active = (np.zeros(G, np.int32) for _ in range(4))
+        check(self.L.azg_get_state(self.h, boards.ctypes.data, turns.ctypes.data, players.ctypes.data,
+                                   outcomes.ctypes.data, active.ctypes.data, self._stream()))
+        return {"boards": boards, "turns": turns, "players": players, "outcomes": outcomes, "active": active}
+
+    def stats(self):
+        s = np.zeros(8, np.int64)
+        check(self.L.azg_stats(self.h, s.ctypes.data, self._stream()))
+        return {"expansions": int(s[0]), "terminal_hits": int(s[1]), "fallbacks": int(s[2]),
+                "max_depth": int(s[3]), "max_live_nodes": int(s[4]), "error": int(s[5]), "sims": int(s[6])}
+
+    # ------------------------------------------------------------------ single-slot access (drop-in MCTS)
+    def set_root(self, slot, board, turn, player):
+        b = np.ascontiguousarray(np.asarray(board).reshape(-1), np.int8)
+        check(self.L.azg_set_root(self.h, int(slot), b.ctypes.data, int(turn), int(player), self._stream()))
+
+    def get_rng(self, slot):
+        mt = np.zeros(624, np.uint32)
+        pos = ctypes.c_int32()
+        check(self.L.azg_get_rng(self.h, int(slot), mt.ctypes.data, ctypes.byref(pos), self._stream()))
+        return mt, pos.value
+
+    def set_rng(self, slot, mt, pos):
+        mt = np.ascontiguousarray(mt, np.uint32)
+        check(self.L.azg_set_rng(self.h, int(slot), mt.ctypes.data, int(pos), self._stream()))
+
+    def root_counts(self, slot):
+        c = np.zeros(A, np.int32)
+        check(self.L.azg_root_counts(self.h, int(slot), c.ctypes.data, self._stream()))
+        return c

@@ -1,0 +1,116 @@
+"""Leaf evaluator: the reference policy/value network on PyTorch-ROCm.
+
+`InflexionNNet` has the reference architecture and parameter names
+(inflexion/pytorch/InflexionNNet.py:12-54) so that `{'state_dict': ...}`
+checkpoints written by NNetWrapper.save_checkpoint (NNet.py:102-111) load
+unchanged, and modules are created in the same order so that
+`torch.manual_seed(s)` gives the same random-init weights.
+
+`NNetWrapper` mirrors the reference wrapper surface (NNet.py:27-120):
+`predict(planes) -> (P f32[A], v f32[1])` batch-1 as the reference does,
+`predict_batch(planes[B,4,n,n]) -> (P [B,A], v [B])` for the engine,
+`save_checkpoint` / `load_checkpoint` with the same file format.  Training
+(`train`) is outside the accelerated hot path and kept on the reference
+algorithm for compatibility.
+"""
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+DEFAULT_ARGS = dict(lr=0.001, dropout=0.3, epochs=10, batch_size=512, num_channels=512)
+
+
+class InflexionNNet(nn.Module):
+    def __init__(self, n=7, depth=4, action_size=343, num_channels=512, dropout=0.3):
+        super().__init__()
+        c = num_channels
+        self.n, self.depth, self.action_size = n, depth, action_size
+        self.num_channels, self.dropout = c, dropout
+        # creation order matters for manual_seed parity: conv1..4, bn1..4, fc1, fc_bn1, fc2, fc_bn2, fc3, fc4
+        for i, (cin, pad) in enumerate([(depth, 1), (c, 1), (c, 0), (c, 0)], start=1):
+            setattr(self, f"conv{i}", nn.Conv2d(cin, c, 3, stride=1, padding=pad))
+        for i in range(1, 5):
+            setattr(self, f"bn{i}", nn.BatchNorm2d(c))
+        self.fc1 = nn.Linear(c * (n - 4) * (n - 4), 1024)
+        self.fc_bn1 = nn.BatchNorm1d(1024)
+        self.fc2 = nn.Linear(1024, 512)
+        self.fc_bn2 = nn.BatchNorm1d(512)
+        self.fc3 = nn.Linear(512, action_size)
+        self.fc4 = nn.Linear(512, 1)
+
+    def forward(self, s):
+        x = s.view(-1, self.depth, self.n, self.n)
+        for i in range(1, 5):
+            x = F.relu(getattr(self, f"bn{i}")(getattr(self, f"conv{i}")(x)))
+        x = x.reshape(x.shape[0], -1)
+        x = F.dropout(F.relu(self.fc_bn1(self.fc1(x))), p=self.dropout, training=self.training)
+        x = F.dropout(F.relu(self.fc_bn2(self.fc2(x))), p=self.dropout, training=self.training)
+        return F.log_softmax(self.fc3(x), dim=1), torch.tanh(self.fc4(x))
+
+
+class NNetWrapper:
+    """Reference NNetWrapper surface (NNet.py:27-120) over InflexionNNet."""
+
+    def __init__(self, game=None, args=None, device=None):
+        a = dict(DEFAULT_ARGS)
+        a.update(args or {})
+        self.args = a
+        if game is not None:
+            depth, bx, by = game.to_planes().shape
+            action_size = game.max_actions
+        else:
+            depth, bx, action_size = 4, 7, 343
+        self.depth, self.board_x, self.board_y, self.action_size = depth, bx, bx, action_size
+        self.nnet = InflexionNNet(bx, depth, action_size, a["num_channels"], a["dropout"])
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+        self.nnet.to(self.device)
+
+    def predict(self, board):
+        """Batch-1 predict (NNet.py:78-94): planes -> (P f32[A], v f32[1])."""
+        x = torch.as_tensor(np.asarray(board).astype(np.float64), dtype=torch.float32, device=self.device)
+        x = x.view(self.depth, self.board_x, self.board_y)
+        self.nnet.eval()
+        with torch.no_grad():
+            pi, v = self.nnet(x)
+        return torch.exp(pi).cpu().numpy()[0], v.cpu().numpy()[0]
+
+    def predict_batch(self, planes):
+        self.nnet.eval()
+        with torch.no_grad():
+            pi, v = self.nnet(planes)
+        return torch.exp(pi), v.view(-1)
+
+    def train(self, examples):
+        """Reference training loop (NNet.py:36-76): Adam, 10 epochs of batches
+        sampled with replacement from numpy's global RNG."""
+        opt = torch.optim.Adam(self.nnet.parameters())
+        bs = self.args["batch_size"]
+        for _ in range(self.args["epochs"]):
+            self.nnet.train()
+            for _ in range(int(len(examples) / bs)):
+                ids = np.random.randint(len(examples), size=bs)
+                boards, pis, vs = list(zip(*[examples[i] for i in ids]))
+                boards = torch.FloatTensor(np.array(boards).astype(np.float64)).to(self.device)
+                tp = torch.FloatTensor(np.array(pis)).to(self.device)
+                tv = torch.FloatTensor(np.array(vs).astype(np.float64)).to(self.device)
+                out_pi, out_v = self.nnet(boards)
+                l_pi = -torch.sum(tp * out_pi) / tp.size()[0]
+                l_v = torch.sum((tv - out_v.view(-1)) ** 2) / tv.size()[0]
+                opt.zero_grad()
+                (l_pi + l_v).backward()
+                opt.step()
+
+    def save_checkpoint(self, folder="checkpoint", filename="checkpoint.pth.tar"):
+        os.makedirs(folder, exist_ok=True)
+        torch.save({"state_dict": self.nnet.state_dict()}, os.path.join(folder, filename))
+
+    def load_checkpoint(self, folder="checkpoint", filename="checkpoint.pth.tar"):
+        path = os.path.join(folder, filename)
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"No model in path {path}")
+        ck = torch.load(path, map_location=self.device, weights_only=True)
+        self.nnet.load_state_dict(ck["state_dict"])

@@ -1,0 +1,123 @@
+/*
+ * azg.h -- C ABI of the MI355X batched self-play engine (libazg.so).
+ *
+ * This is the drop-in boundary for the reference hot path
+ *     Coach.executeEpisode -> MCTS.getActionProb -> MCTS.search
+ * (Coach.py:41-90, MCTS.py:33-145).  The reference exposes it as duck-typed
+ * Python objects; a maintainer binds these entry points with ctypes (see
+ * INTEGRATION.md).  Plain pointers and sizes only; every device pointer is
+ * caller-owned (e.g. a torch tensor's data_ptr()) and every call is ordered on
+ * the HIP stream passed in (torch.cuda.current_stream().cuda_stream).  All
+ * calls return 0 on success or a negative AZG_ERR_* code; azg_last_error()
+ * gives the thread-local message.  One engine per device, one host thread.
+ *
+ * A step of the engine = one simulation for every active game slot:
+ *     azg_sim_begin  -- MCTS.py:83-132  select/descend to a leaf, write its
+ *                       randomly symmetrised planes (InflexionGame.py:115-122)
+ *     <evaluate>     -- NNetWrapper.predict (NNet.py:78-94), batched, or
+ *                       azg_stub_eval (test evaluator)
+ *     azg_sim_end    -- MCTS.py:89-112 expand + MCTS.py:136-145 backup
+ * and after numMCTSSims steps
+ *     azg_move_end   -- MCTS.py:48-60 root policy + Coach.py:68-90 sample,
+ *                       apply, terminal test, record the move.
+ */
+#ifndef AZG_H
+#define AZG_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AZG_ABI_VERSION 1
+
+enum azg_game_kind { AZG_GAME_INFLEXION = 1 };
+
+enum azg_flags {
+    AZG_FLAG_GC = 1,          /* free nodes whose turn < root turn at move end */
+    AZG_FLAG_RECORD = 2,      /* keep per-move root counts (training examples)  */
+};
+
+enum azg_err {
+    AZG_OK = 0,
+    AZG_ERR_ARG = -1,         /* bad argument / config                          */
+    AZG_ERR_HIP = -2,         /* HIP runtime error                              */
+    AZG_ERR_NODE_POOL = -3,   /* a game's node pool is full (raise node_capacity)*/
+    AZG_ERR_PATH = -4,        /* search path deeper than max_depth              */
+    AZG_ERR_NO_ACTION = -5,   /* no valid action (MCTS.py:131 best_act = -1)   */
+    AZG_ERR_STATE = -6,       /* call out of order                               */
+};
+
+typedef struct {
+    int32_t game_kind;        /* AZG_GAME_INFLEXION                               */
+    int32_t n;                /* board side; InflexionGame(n) -- 7                */
+    int32_t max_turns;        /* InflexionGame max_turns (main.py:34: 343)        */
+    int32_t num_games;        /* G concurrent game slots on this device           */
+    int32_t sims;             /* args.numMCTSSims                                 */
+    int32_t temp_threshold;   /* args.tempThreshold                               */
+    double cpuct;             /* args.cpuct                                       */
+    uint32_t seed_base;       /* slot i of game index k is seeded seed_base + k   */
+    int32_t pad0;
+    int64_t first_game;       /* global game index of slot 0 (multi-GPU shards)   */
+    int32_t node_capacity;    /* nodes per game slot, 0 = default                 */
+    int32_t max_depth;        /* search path capacity, 0 = default (256)          */
+    int32_t max_moves;        /* recorded moves per game, 0 = max_turns + 1       */
+    int32_t flags;            /* AZG_FLAG_*                                       */
+} azg_config;
+
+typedef struct azg_engine azg_engine;
+
+/* Engine lifetime.  `stream` is a hipStream_t (may be NULL = default stream). */
+int  azg_create(const azg_config* cfg, void* stream, azg_engine** out);
+void azg_destroy(azg_engine* e);
+const char* azg_last_error(void);
+int  azg_abi_version(void);
+
+/* Start a new generation: every slot gets a fresh game (InflexionGame.restarted,
+ * Game.py:82; Coach.py:110-111 fresh MCTS) seeded with seed_base + first_game + i. */
+int  azg_reset(azg_engine* e, uint32_t seed_base, int64_t first_game, void* stream);
+
+/* One simulation step.  leaf_planes: device f32 [G,4,n,n] written by sim_begin;
+ * P: device f32 [G, p_stride] (probabilities, exp of the net's log_softmax),
+ * v: device f32 [G].  Slots without a leaf to evaluate get zero planes and
+ * ignore P/v. */
+int  azg_sim_begin(azg_engine* e, float* leaf_planes, void* stream);
+int  azg_sim_end(azg_engine* e, const float* P, int32_t p_stride, const float* v, void* stream);
+
+/* Test evaluator (tests/golden/stubnet.py spec): planes -> P, v on device. */
+int  azg_stub_eval(azg_engine* e, const float* leaf_planes, float* P, float* v, void* stream);
+
+/* Root policy, sampling, move application, recording, node GC. */
+int  azg_move_end(azg_engine* e, void* stream);
+
+/* Number of slots whose game is still ongoing (synchronises the stream). */
+int  azg_active_games(azg_engine* e, int32_t* out, void* stream);
+
+/* Host-side state access (synchronise the stream). */
+int  azg_get_state(azg_engine* e, int8_t* boards /*[G,n*n]*/, int32_t* turns, int32_t* players,
+                   int32_t* outcomes, int32_t* active, void* stream);
+int  azg_set_root(azg_engine* e, int32_t slot, const int8_t* board /*[n*n]*/, int32_t turn,
+                  int32_t player, void* stream);
+int  azg_get_rng(azg_engine* e, int32_t slot, uint32_t* mt /*[624]*/, int32_t* pos, void* stream);
+int  azg_set_rng(azg_engine* e, int32_t slot, const uint32_t* mt /*[624]*/, int32_t pos, void* stream);
+int  azg_root_counts(azg_engine* e, int32_t slot, int32_t* counts /*[A]*/, void* stream);
+
+/* Recorded moves: actions [G,max_moves], temps [G,max_moves], counts
+ * [G,max_moves,A] (NULL to skip), moves made [G]. */
+int  azg_read_moves(azg_engine* e, int32_t* actions, int8_t* temps, int32_t* counts,
+                    int32_t* moves, void* stream);
+
+/* Counters: [0] expansions [1] terminal hits [2] fallback expansions
+ * [3] max path depth [4] max live nodes in a slot [5] error code [6] sims run */
+int  azg_stats(azg_engine* e, int64_t* out /*[8]*/, void* stream);
+
+/* Device pointers of the engine state (for zero-copy consumers, e.g. the
+ * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active
+ * [5] record actions [6] record counts [7] moves */
+int  azg_device_ptrs(azg_engine* e, void** out /*[8]*/);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,39 @@
+"""C-ABI boundary checks that need no GPU: the library loads and exports every
+symbol include/azg.h declares, with the declared config layout."""
+import ctypes
+import os
+import re
+
+import azg_amd  # noqa: F401
+from azg_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "azg.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(azg_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    L = _lib.lib()
+    names = _declared()
+    assert len(names) >= 18
+    for n in names:
+        assert hasattr(L, n), n
+    assert sorted(s[0] for s in _lib.SIGNATURES) == names
+
+
+def test_config_layout_and_version():
+    assert ctypes.sizeof(_lib.Config) == 64
+    assert _lib.Config.cpuct.offset == 24 and _lib.Config.first_game.offset == 40
+    assert _lib.lib().azg_abi_version() == 1
+
+
+def test_errors_are_loud_without_device():
+    # a null config must be rejected with a message, never silently ignored
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    assert L.azg_create(None, None, ctypes.byref(h)) == -1
+    assert b"null" in L.azg_last_error()

@@ -1,0 +1,85 @@
+"""GPU parity: libazg.so (HIP) vs the reference, bit-exact on visit counts.
+
+The search is driven by the hash evaluator (tests/golden/stubnet.py) so that
+the comparison is exact: golden traces recorded from the reference
+(Coach.executeEpisode + MCTS) and the C oracle must both be reproduced
+count-for-count, action-for-action, expansion-for-expansion.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def azg():
+    import azg_amd.engine as eng
+    assert torch.cuda.is_available()
+    return eng
+
+
+def _run(eng, seeds, cfg, **kw):
+    assert list(seeds) == list(range(seeds[0], seeds[0] + len(seeds)))
+    e = eng.SelfPlayEngine(len(seeds), sims=cfg["sims"], cpuct=cfg["cpuct"], temp_threshold=cfg["temp_threshold"],
+                           max_turns=cfg["max_turns"], seed_base=0, first_game=seeds[0], evaluator="stub", **kw)
+    e.play()
+    return e, e.read_moves(), e.stats(), e.state()
+
+
+def test_stub_kernel_matches_oracle(azg):
+    rs = np.random.RandomState(11)
+    G = 64
+    planes = np.zeros((G, 4, 7, 7), np.float32)
+    planes[:, 0] = rs.random_sample((G, 7, 7)) < 0.3
+    planes[:, 1] = (rs.random_sample((G, 7, 7)) < 0.3) & (planes[:, 0] == 0)
+    planes[:, 2] = rs.randint(0, 344, size=(G, 1, 1))
+    planes[:, 3] = rs.randint(0, 2, size=(G, 1, 1))
+    e = azg.SelfPlayEngine(G, evaluator="stub")
+    e.planes.copy_(torch.from_numpy(planes))
+    e.evaluate()
+    P = e.P.cpu().numpy()
+    v = e.v.cpu().numpy()
+    for g in range(G):
+        P2, v2 = ol.stub_eval(planes[g].astype(np.int32))
+        assert np.array_equal(P[g].view(np.uint32), P2.view(np.uint32))
+        assert v[g] == v2[0]
+
+
+@pytest.mark.parametrize("name", ["short", "main", "pit", "sims100", "deep"])
+def test_golden_traces_bit_exact(azg, name):
+    data = ol.load_json(f"mcts_{name}.json.gz")
+    cfg, eps = data["config"], data["episodes"]
+    seeds = [ep["seed"] for ep in eps]
+    cap = 16 * cfg["sims"] + 128 if cfg["sims"] < 200 else 8192
+    e, rec, st, state = _run(azg, seeds, cfg, node_capacity=cap, max_depth=512)
+    assert st["error"] == 0
+    exp_total = 0
+    for i, ep in enumerate(eps):
+        assert rec["moves"][i] == ep["n_moves"], f"seed {ep['seed']}"
+        for m, mv in enumerate(ep["moves"]):
+            assert np.array_equal(rec["counts"][i, m], ol.golden_counts(mv)), f"seed {ep['seed']} move {m}"
+            assert rec["actions"][i, m] == mv["action"], f"seed {ep['seed']} move {m}"
+            assert rec["temps"][i, m] == mv["temp"]
+        assert state["boards"][i].tolist() == ep["final_board"]
+        assert state["players"][i] == ep["final_player"]
+        assert ol.OUTCOME_VALUE[int(state["outcomes"][i])] == ep["final_outcome"]
+        exp_total += ep["expansions"]
+        mt, pos = e.get_rng(i)
+        assert pos == ep["rng_pos"]
+    assert st["expansions"] == exp_total
+
+
+def test_random_seeds_vs_oracle(azg):
+    cfg = dict(sims=25, cpuct=1, temp_threshold=30, max_turns=60)
+    seeds = list(range(1000, 1096))
+    e, rec, st, state = _run(azg, seeds, cfg)
+    assert st["error"] == 0
+    for i, s in enumerate(seeds):
+        o = ol.episode(7, cfg["max_turns"], cfg["sims"], cfg["cpuct"], cfg["temp_threshold"], s)
+        m = o["moves"]
+        assert rec["moves"][i] == m
+        assert np.array_equal(rec["actions"][i, :m], o["actions"])
+        assert np.array_equal(rec["counts"][i, :m], o["counts"])

@@ -1,0 +1,44 @@
+"""The leaf network reproduces the reference InflexionNNet (CPU, f32).
+
+Pinned by tests/golden/nnet_golden.npz, generated from the reference NNetWrapper
+under torch.manual_seed(0): per-tensor SHA-256 of the random-init state_dict and
+64 batch-1 predictions (planes -> P, v)."""
+import hashlib
+import os
+
+import numpy as np
+import torch
+
+import azg_amd  # noqa: F401
+from azg_amd.nnet import InflexionNNet, NNetWrapper
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "nnet_golden.npz")
+
+
+def test_state_dict_matches_reference_init():
+    d = dict(np.load(G))
+    torch.manual_seed(0)
+    net = InflexionNNet()
+    sd = net.state_dict()
+    assert list(sd.keys()) == d["names"].tolist()
+    for k, sha in zip(d["names"], d["sha256"]):
+        assert hashlib.sha256(sd[str(k)].contiguous().numpy().tobytes()).hexdigest() == sha, k
+
+
+def test_predict_matches_reference():
+    d = dict(np.load(G))
+    torch.manual_seed(0)
+    w = NNetWrapper(device="cpu")
+    for planes, P, v in zip(d["planes"], d["P"], d["v"]):
+        p2, v2 = w.predict(planes.astype(np.int64))
+        np.testing.assert_allclose(p2, P, rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(v2[0], v, rtol=1e-5, atol=1e-6)
+
+
+def test_batched_matches_batch1():
+    d = dict(np.load(G))
+    torch.manual_seed(0)
+    w = NNetWrapper(device="cpu")
+    P, v = w.predict_batch(torch.from_numpy(d["planes"].astype(np.float32)))
+    np.testing.assert_allclose(P.numpy(), d["P"], rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose(v.numpy(), d["v"], rtol=2e-5, atol=1e-6)
