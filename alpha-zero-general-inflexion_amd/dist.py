@@ -1,0 +1,91 @@
+"""Multi-GPU self-play: one process per GPU, games sharded by global index.
+
+Self-play needs no communication (each game slot is independent and seeded by
+its global index, so results do not depend on the GPU count).  Once per
+iteration -- where the reference's Coach.learn (Coach.py:102-153) collects the
+iteration's examples and trains -- two collectives run over RCCL (backend
+"nccl" on ROCm) on xGMI:
+
+  * gather of every rank's compact move records to the trainer rank
+    (all_gather of per-rank sizes, then one all_gather of padded buffers);
+  * broadcast of the trainer's weights (one flat f32 buffer, ~50 MB).
+
+A compact move record is (moves made, actions, temperatures, root visit
+counts as int16) per game: enough to rebuild every training example
+(Coach.py:74-90) by replaying the actions from the initial position.
+"""
+import ctypes
+
+import torch
+import torch.distributed as dist
+from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+
+from . import _lib
+
+A = 343
+
+
+class _DevArray:
+    """Zero-copy view of an engine-owned device buffer as a torch tensor."""
+
+    def __init__(self, ptr, shape, typestr):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (int(ptr), False),
+                                         "version": 3, "strides": None}
+
+
+def engine_records(engine):
+    """(moves [G] i32, actions [G,MM] i32, counts [G,MM,A] i32 or None) as device tensors (no copy)."""
+    ptrs = (ctypes.c_void_p * 8)()
+    _lib.check(engine.L.azg_device_ptrs(engine.h, ptrs))
+    dev = engine.device
+    G, MM = engine.G, engine.max_moves
+    moves = torch.as_tensor(_DevArray(ptrs[7], (G,), "<i4"), device=dev)
+    actions = torch.as_tensor(_DevArray(ptrs[5], (G, MM), "<i4"), device=dev)
+    counts = None
+    if ptrs[6]:
+        counts = torch.as_tensor(_DevArray(ptrs[6], (G, MM, A), "<i4"), device=dev)
+    return moves, actions, counts
+
+
+def gather_records(engine, dst=0, group=None):
+    """Gather compact move records of all ranks (moves made so far) to `dst`.
+    Returns (moves [W*G], actions [W*G, m], counts [W*G, m, A] int16) on dst, None elsewhere,
+    and the bytes this rank sent."""
+    moves, actions, counts = engine_records(engine)
+    m_local = torch.max(moves).reshape(1).to(torch.int64)
+    m_all = m_local.clone()
+    dist.all_reduce(m_all, op=dist.ReduceOp.MAX, group=group)
+    m = int(m_all.item())
+    ws = dist.get_world_size(group)
+    G = engine.G
+    act = actions[:, :m].contiguous()
+    cnt = counts[:, :m].to(torch.int16).contiguous() if counts is not None else torch.zeros(
+        (G, m, A), dtype=torch.int16, device=engine.device)
+    mv = moves.clone()
+    out_mv = torch.empty((ws * G,), dtype=mv.dtype, device=mv.device)
+    out_act = torch.empty((ws * G, m), dtype=act.dtype, device=act.device)
+    out_cnt = torch.empty((ws * G, m, A), dtype=cnt.dtype, device=cnt.device)
+    dist.all_gather_into_tensor(out_mv, mv, group=group)
+    dist.all_gather_into_tensor(out_act, act, group=group)
+    dist.all_gather_into_tensor(out_cnt, cnt, group=group)
+    sent = mv.numel() * 4 + act.numel() * 4 + cnt.numel() * 2
+    if dist.get_rank(group) == dst:
+        return (out_mv, out_act, out_cnt), sent
+    return None, sent
+
+
+def broadcast_weights(module, src=0, group=None):
+    """Broadcast every parameter and buffer of `module` from `src` as one flat buffer."""
+    tensors = [t for t in list(module.parameters()) + list(module.buffers()) if t.dtype == torch.float32]
+    flat = _flatten_dense_tensors([t.data for t in tensors])
+    dist.broadcast(flat, src=src, group=group)
+    for t, f in zip(tensors, _unflatten_dense_tensors(flat, [t.data for t in tensors])):
+        t.data.copy_(f)
+    return flat.numel() * 4
+
+
+def iteration_sync(engine, module, trainer=0, group=None):
+    """The per-iteration exchange of configs[3]: examples in, weights out."""
+    _, sent = gather_records(engine, dst=trainer, group=group)
+    wb = broadcast_weights(module, src=trainer, group=group)
+    return sent + wb

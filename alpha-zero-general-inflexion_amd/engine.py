@@ -80,24 +80,33 @@ class SelfPlayEngine:
 
     # ------------------------------------------------------------------ the hot path
     def evaluate(self):
-        """Fill P, v for the current leaf batch (NNetWrapper.predict, batched)."""
+        """Evaluate the current leaf batch (NNetWrapper.predict, batched).
+        Returns device tensors (P [G,A] probabilities, v [G]) for sim_end."""
         ev = self.evaluator
         if isinstance(ev, str):
             if ev != "stub":
                 raise ValueError(f"unknown evaluator {ev!r}")
             check(self.L.azg_stub_eval(self.h, _ptr(self.planes), _ptr(self.P), _ptr(self.v), self._stream()))
-            return
+            return self.P, self.v
         with torch.no_grad():
             out_pi, out_v = ev(self.planes)
-            torch.exp(out_pi, out=self.P)  # predict returns exp(log_softmax) (NNet.py:94)
-            self.v.copy_(out_v.reshape(-1))
+            if getattr(ev, "outputs_probs", False):
+                P = out_pi
+            else:  # log_softmax output: predict returns exp(pi) (NNet.py:94)
+                P = torch.exp(out_pi)
+            v = out_v.reshape(-1)
+        if P.dtype != torch.float32 or P.stride(1) != 1 or P.shape != (self.G, A):
+            P = P.float().contiguous()
+        if v.dtype != torch.float32 or not v.is_contiguous():
+            v = v.float().contiguous()
+        return P, v
 
     def simulate(self):
         """One MCTS.search for every live game."""
         s = self._stream()
         check(self.L.azg_sim_begin(self.h, _ptr(self.planes), s))
-        self.evaluate()
-        check(self.L.azg_sim_end(self.h, _ptr(self.P), A, _ptr(self.v), s))
+        P, v = self.evaluate()
+        check(self.L.azg_sim_end(self.h, _ptr(P), P.stride(0), _ptr(v), s))
 
     def move_end(self):
         check(self.L.azg_move_end(self.h, self._stream()))

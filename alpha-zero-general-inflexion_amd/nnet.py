@@ -51,6 +51,72 @@ class InflexionNNet(nn.Module):
         return F.log_softmax(self.fc3(x), dim=1), torch.tanh(self.fc4(x))
 
 
+def _fold_bn(weight, bias, bn):
+    """Eval-mode BatchNorm folded into the preceding conv/linear (f64 math)."""
+    scale = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+    w = weight.double() * scale.reshape(-1, *([1] * (weight.dim() - 1)))
+    b = (bias.double() - bn.running_mean.double()) * scale + bn.bias.double()
+    return w.float(), b.float()
+
+
+class InferenceNet(nn.Module):
+    """Inference form of InflexionNNet for the leaf batches (eval semantics only).
+
+    Every BatchNorm is folded into its conv/linear, activations stay NHWC
+    (channels_last) end to end so the implicit-GEMM convolutions need no layout
+    transposes, fc1's input columns are permuted from NCHW to NHWC flatten
+    order, and the heads return what the engine consumes: P = softmax(fc3)
+    (= exp(log_softmax), NNet.py:94) and v = tanh(fc4).  Same f32 arithmetic
+    class as the reference; results agree with InflexionNNet to ~1e-6 relative
+    (tests/test_nnet_cpu.py)."""
+
+    outputs_probs = True
+
+    def __init__(self, net: InflexionNNet):
+        super().__init__()
+        self.n, self.depth, c = net.n, net.depth, net.num_channels
+        self.pads = []
+        for i in range(1, 5):
+            conv, bn = getattr(net, f"conv{i}"), getattr(net, f"bn{i}")
+            w, b = _fold_bn(conv.weight.detach(), conv.bias.detach(), bn)
+            self.register_buffer(f"w{i}", w.contiguous(memory_format=torch.channels_last))
+            self.register_buffer(f"b{i}", b)
+            self.pads.append(conv.padding[0])
+        s = net.n - 4
+        w1, b1 = _fold_bn(net.fc1.weight.detach(), net.fc1.bias.detach(), net.fc_bn1)
+        w1 = w1.reshape(-1, c, s, s).permute(0, 2, 3, 1).reshape(w1.shape[0], -1)  # (c,h,w) -> (h,w,c)
+        self.register_buffer("fw1", w1.contiguous())
+        self.register_buffer("fb1", b1)
+        w2, b2 = _fold_bn(net.fc2.weight.detach(), net.fc2.bias.detach(), net.fc_bn2)
+        self.register_buffer("fw2", w2.contiguous())
+        self.register_buffer("fb2", b2)
+        self.register_buffer("fw3", net.fc3.weight.detach().clone())
+        self.register_buffer("fb3", net.fc3.bias.detach().clone())
+        self.register_buffer("fw4", net.fc4.weight.detach().clone())
+        self.register_buffer("fb4", net.fc4.bias.detach().clone())
+
+    # optional hook: callable(layer_index, "start"|"stop") used by bench.py to
+    # bracket each convolution with HIP events on the current stream
+    conv_hook = None
+
+    def forward(self, s):
+        x = s.view(-1, self.depth, self.n, self.n).contiguous(memory_format=torch.channels_last)
+        hook = self.conv_hook
+        for i, pad in enumerate(self.pads, start=1):
+            if hook:
+                hook(i, "start")
+            x = F.conv2d(x, getattr(self, f"w{i}"), getattr(self, f"b{i}"), padding=pad)
+            if hook:
+                hook(i, "stop")
+            x = torch.relu_(x)
+        x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten, no copy
+        x = torch.relu_(torch.addmm(self.fb1, x, self.fw1.t()))
+        x = torch.relu_(torch.addmm(self.fb2, x, self.fw2.t()))
+        p = torch.softmax(torch.addmm(self.fb3, x, self.fw3.t()), dim=1)
+        v = torch.tanh(torch.addmm(self.fb4, x, self.fw4.t()))
+        return p, v
+
+
 class NNetWrapper:
     """Reference NNetWrapper surface (NNet.py:27-120) over InflexionNNet."""
 

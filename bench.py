@@ -1,0 +1,264 @@
+"""Self-play throughput of the MI355X engine (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--games G] [--sims S]
+
+One *step* = one move of every concurrent game: numMCTSSims simulations
+(select -> leaf-batched InflexionNNet f32 forward -> expand/backup) followed by
+the root-policy / sample / apply kernel -- the reference's
+Coach.executeEpisode loop body (Coach.py:65-84) for G games at once.
+Default workload (north_star / configs[3] per GPU): 7x7 Inflexion,
+max_turns 343, 4096 games per GPU, 25 sims/move, cpuct 1, tempThreshold 30,
+random-init InflexionNNet (torch.manual_seed(0)), f32.
+
+`value` = node expansions per second over the whole job (new tree nodes = NN
+leaf evaluations, MCTS.py:89-112; terminal hits excluded), all ranks summed.
+Multi-GPU: one process per GPU (torchrun), games sharded by global index, no
+communication inside self-play; each timed region ends with the per-iteration
+RCCL example gather + weight broadcast (configs[3]).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FLOP_PER_LEAF = 404.3e6          # 202,143,744 MAC per leaf
+F32_MFMA_PEAK_TF = 157.3         # MI355X_MICROARCH.md: f32 matrix peak (dense)
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E spec peak
+EXPANSIONS_PER_GAME_REF = 8555   # reference random-init episodes
+CONV_FLOP_PER_LEAF = 2 * 512 * 512 * 9 * (49 + 25 + 9)  # conv2 (7x7 out) + conv3 (5x5) + conv4 (3x3)
+
+
+def tree_bytes_per_sim(A_sel=87.0, d=1.33):
+    """Algorithmic HBM bytes of the tree kernels per simulation:
+    select reads P/N/Q (4+4+8 B) of each valid action at d nodes, board/key
+    traffic, leaf planes write, P/v read, node init of the new leaf, backup RMW."""
+    sel = d * (16.0 * A_sel + 32.0)          # P f32 + N u32 + Q f64 per valid action, + Ns/key
+    table = d * 64.0 + 64.0                  # hash probes (one 64-slot line per lookup)
+    leaf = 4 * 49 * 4 + 343 * 4 + 4          # planes write + P/v read
+    node = 384 * 16 + 32                     # new node row (P, N, Q) + key
+    backup = d * 24.0                        # N, Q, Ns read-modify-write
+    return sel + table + leaf + node + backup
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=4)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
+    p.add_argument("--sims", type=int, default=25)
+    p.add_argument("--max-turns", type=int, default=343)
+    p.add_argument("--evaluator", default="net", choices=["net", "stub"])
+    p.add_argument("--net", default="inference", choices=["inference", "reference"],
+                   help="inference: BN-folded NHWC InferenceNet; reference: InflexionNNet as written")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-moves", type=int, default=40, help="cpu_baseline sample: first moves of one game")
+    return p.parse_args()
+
+
+class Timer:
+    """Accumulates HIP-event durations on the current stream."""
+
+    def __init__(self):
+        self.pairs = []
+
+    def start(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def stop(self, s):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.pairs.append((s, e))
+
+    def total_ms(self):
+        torch.cuda.synchronize()
+        return sum(s.elapsed_time(e) for s, e in self.pairs)
+
+
+def cpu_baseline(args):
+    """Oracle (C restatement of the reference search) + the same f32 network on
+    the host's cores, batch-1 per leaf like NNetWrapper.predict -- the reference
+    CPU path's shape, timed on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as ol
+    from azg_amd.nnet import InflexionNNet
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    net = InflexionNNet().eval()
+
+    def evaluator(planes):
+        with torch.no_grad():
+            pi, v = net(torch.from_numpy(np.array(planes, np.float32)))
+        return torch.exp(pi)[0].numpy(), float(v[0, 0])
+
+    t = time.perf_counter()
+    o = ol.episode(7, args.max_turns, args.sims, 1, 30, 0, evaluator=evaluator, max_moves=args.cpu_moves)
+    # stop after the sample: oracle episode is capped via max_turns below when needed
+    dt = time.perf_counter() - t
+    t2 = time.perf_counter()
+    o2 = ol.episode(7, args.max_turns, args.sims, 1, 30, 0)
+    dt2 = time.perf_counter() - t2
+    return {"value": o["expansions"] / dt, "unit": "node-expansions/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ C MCTS + InflexionNNet f32 batch-1 on CPU, seed 0, max_turns {args.max_turns}, "
+                      f"{o['moves']} moves x {args.sims} sims = {o['expansions']} expansions in {dt:.1f}s",
+            "tree_only_value": o2["expansions"] / dt2,
+            "tree_only_sample": f"same search, hash evaluator, 1 thread: {o2['expansions']} expansions in {dt2:.2f}s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    import azg_amd
+    from azg_amd.engine import SelfPlayEngine
+    from azg_amd.nnet import InflexionNNet, InferenceNet
+    from azg_amd import dist as azg_dist
+
+    torch.manual_seed(0)
+    net = InflexionNNet().cuda().eval()
+    ev = (InferenceNet(net) if args.net == "inference" else net) if args.evaluator == "net" else "stub"
+    G = args.games
+    eng = SelfPlayEngine(G, sims=args.sims, cpuct=1, temp_threshold=30, max_turns=args.max_turns,
+                         seed_base=0, first_game=rank * G, evaluator=ev)
+
+    for _ in range(args.warmup):
+        eng.move()
+    torch.cuda.synchronize()
+    st0 = eng.stats()
+    t_nn, t_sel, t_exp, t_end = Timer(), Timer(), Timer(), Timer()
+    t_conv = {i: Timer() for i in (2, 3, 4)}
+    pending = {}
+
+    def conv_hook(i, what):
+        if i not in t_conv:
+            return
+        if what == "start":
+            pending[i] = t_conv[i].start()
+        else:
+            t_conv[i].stop(pending.pop(i))
+
+    if hasattr(ev, "conv_hook"):
+        ev.conv_hook = conv_hook
+
+    def timed_move():
+        for _ in range(eng.sims):
+            s = t_sel.start()
+            azg_amd._lib.check(eng.L.azg_sim_begin(eng.h, eng.planes.data_ptr(), eng._stream()))
+            t_sel.stop(s)
+            s = t_nn.start()
+            P, v = eng.evaluate()
+            t_nn.stop(s)
+            s = t_exp.start()
+            azg_amd._lib.check(eng.L.azg_sim_end(eng.h, P.data_ptr(), P.stride(0), v.data_ptr(), eng._stream()))
+            t_exp.stop(s)
+        s = t_end.start()
+        eng.move_end()
+        t_end.stop(s)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        timed_move()
+    sync_bytes = 0
+    if world > 1:  # per-iteration exchange: example gather to rank 0 + weight broadcast from rank 0
+        sync_bytes = azg_dist.iteration_sync(eng, net)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st1 = eng.stats()
+    exp = st1["expansions"] - st0["expansions"]
+    sims_run = st1["sims"] - st0["sims"]
+    nn_ms, sel_ms, exp_ms, end_ms = t_nn.total_ms(), t_sel.total_ms(), t_exp.total_ms(), t_end.total_ms()
+    if st1["error"]:
+        raise RuntimeError(f"engine error {st1['error']}")
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([exp, sims_run], dtype=torch.float64, device="cuda")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        exp, sims_run = int(c[0].item()), int(c[1].item())
+
+    if rank == 0:
+        value = exp / elapsed
+        n_forwards = args.steps * args.sims
+        nn_avg = nn_ms / n_forwards / 1e3
+        leaves = G  # the forward is evaluated on the full [G,4,7,7] batch
+        nn_tflops = leaves * FLOP_PER_LEAF / nn_avg / 1e12
+        conv_ms = sum(t.total_ms() for t in t_conv.values())
+        conv_avg = conv_ms / n_forwards / 1e3 if conv_ms > 0 else nn_avg
+        conv_flops = leaves * (CONV_FLOP_PER_LEAF if conv_ms > 0 else FLOP_PER_LEAF)
+        conv_tflops = conv_flops / conv_avg / 1e12
+        tree_s = (sel_ms + exp_ms) / 1e3
+        tree_gbs = (exp / world) * tree_bytes_per_sim() / tree_s / 1e9 if tree_s > 0 else 0.0
+        out = {
+            "metric": "node-expansions/s (7x7 Inflexion self-play, 25 sims/move); games/s in games_per_s",
+            "value": value,
+            "unit": "node-expansions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: fresh self-play games, random-init InflexionNNet (torch.manual_seed(0))"
+                    if args.evaluator == "net" else "synthetic: hash stub evaluator",
+            "config": {"workload": f"7x7 Inflexion self-play, {G} concurrent games/GPU x {args.sims} sims/move, "
+                                   f"max_turns {args.max_turns}, cpuct 1, tempThreshold 30 (configs[3] per GPU)",
+                       "games_per_gpu": G, "sims_per_move": args.sims, "global_games": G * world,
+                       "parallelism": f"games sharded over {world} GPU(s)", "step": "one move of every game"},
+            "games_per_s": value / EXPANSIONS_PER_GAME_REF,
+            "games_per_s_note": "expansions/s / 8555 expansions per random-init game (344 moves, measured on the "
+                                "reference); see DESIGN.md for the measured full-generation rate",
+            "expansions": exp,
+            "simulations": sims_run,
+            "roofline": {"bound": "mfma",
+                         "kernel": "conv2-4 f32 implicit GEMM (igemm_fwd_gtcx35_nhwc_fp32 + bias) per forward",
+                         "achieved": conv_tflops, "peak": F32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                         "frac": conv_tflops / F32_MFMA_PEAK_TF, "traffic": None,
+                         "per_launch": f"{leaves} leaves x {CONV_FLOP_PER_LEAF/1e6:.1f} MFLOP / {conv_avg*1e3:.3f} ms "
+                                       f"(HIP events around conv2+conv3+conv4)",
+                         "forward_tflops": nn_tflops,
+                         "forward_per_launch": f"{leaves} leaves x 404.3 MFLOP / {nn_avg*1e3:.3f} ms (HIP events)"},
+            "roofline_tree": {"bound": "hbm", "kernel": "select_kernel + expand_backup_kernel",
+                              "achieved": tree_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": tree_gbs / HBM_PEAK_GBS, "traffic": None,
+                              "bytes_per_sim": tree_bytes_per_sim(),
+                              "select_ms_per_sim": sel_ms / n_forwards, "expand_ms_per_sim": exp_ms / n_forwards,
+                              "move_end_ms_per_move": end_ms / args.steps},
+            "time_split": {"nn_ms": nn_ms, "select_ms": sel_ms, "expand_backup_ms": exp_ms, "move_end_ms": end_ms,
+                           "wall_ms": elapsed * 1e3},
+            "iteration_sync_bytes": sync_bytes,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -500,6 +500,7 @@ int orc_episode(int n, int max_turns, int sims, double cpuct, int temp_threshold
         moves++;
         if (orc_apply(&g, action) != 0) abort();
         if (g.outcome != ORC_ONGOING) break;
+        if (moves >= max_moves) break; /* bounded sample (cpu_baseline) */
     }
     if (stats) {
         stats[0] = moves; stats[1] = m.expansions; stats[2] = m.n_nodes;

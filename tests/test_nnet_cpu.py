@@ -42,3 +42,24 @@ def test_batched_matches_batch1():
     P, v = w.predict_batch(torch.from_numpy(d["planes"].astype(np.float32)))
     np.testing.assert_allclose(P.numpy(), d["P"], rtol=2e-5, atol=1e-7)
     np.testing.assert_allclose(v.numpy(), d["v"], rtol=2e-5, atol=1e-6)
+
+
+def test_inference_net_matches_reference_net():
+    from azg_amd.nnet import InferenceNet
+    d = dict(np.load(G))
+    torch.manual_seed(0)
+    net = InflexionNNet().eval()
+    # non-trivial BatchNorm statistics so the folding is exercised
+    g = torch.Generator().manual_seed(1)
+    for m in net.modules():
+        if isinstance(m, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)):
+            m.running_mean.normal_(0, 0.1, generator=g)
+            m.running_var.uniform_(0.5, 1.5, generator=g)
+            m.weight.data.uniform_(0.5, 1.5, generator=g)
+            m.bias.data.normal_(0, 0.1, generator=g)
+    x = torch.from_numpy(d["planes"].astype(np.float32))
+    with torch.no_grad():
+        lp, v = net(x)
+        p2, v2 = InferenceNet(net)(x)
+    np.testing.assert_allclose(p2.numpy(), torch.exp(lp).numpy(), rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(v2.numpy(), v.numpy(), rtol=1e-5, atol=1e-6)
