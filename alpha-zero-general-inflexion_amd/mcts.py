@@ -1,0 +1,99 @@
+"""Drop-in MCTS (reference MCTS.py:16-148) whose search runs on the GPU engine.
+
+    mcts = MCTS(nnet, args)                 # args.numMCTSSims, args.cpuct
+    pi = mcts.getActionProb(game, temp)     # same result as the reference, bit for bit
+
+The tree lives in the engine (one game slot, no node GC, so the tree persists
+across calls exactly like the reference's dicts).  The reference draws its
+random symmetries from numpy's *global* RandomState (InflexionGame.py:120-121);
+this class hands that stream to the engine before the simulations and takes it
+back afterwards, so interleaving with the caller's own np.random use
+(Coach.py:81) is preserved draw for draw.  The root policy and the temp-0 tie
+break (MCTS.py:48-60) run here on the host from the engine's root counts.
+
+`nnet` may be a NNetWrapper-like object (its `.nnet` torch module is used on
+the GPU, batched), a torch module returning (log_softmax, tanh), or the string
+"stub" (hash evaluator used by the parity tests).
+"""
+import numpy as np
+import torch
+
+from .engine import SelfPlayEngine
+from .flags import GameOutcome
+
+
+def _evaluator_of(nnet, device):
+    if isinstance(nnet, str):
+        return nnet
+    ev = getattr(nnet, "azg_evaluator", None)
+    if ev is not None:
+        return ev
+    module = getattr(nnet, "nnet", nnet)
+    if isinstance(module, torch.nn.Module):
+        module = module.to(device)
+        module.eval()
+        return module
+    if callable(module):
+        return module
+    raise TypeError("nnet must be a NNetWrapper-like object, a torch module or 'stub'")
+
+
+class MCTS:
+    DEFAULT_NODE_CAPACITY = 32768
+
+    def __init__(self, nnet, args, device=None, node_capacity=None):
+        self.nnet = nnet
+        self.args = args
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.node_capacity = node_capacity or self.DEFAULT_NODE_CAPACITY
+        self._engine = None
+        self._max_turns = None
+
+    def _engine_for(self, game):
+        if self._engine is None or self._max_turns != game._max_turns:
+            if self._engine is not None:
+                self._engine.close()
+            self._engine = SelfPlayEngine(1, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct,
+                                          temp_threshold=1, max_turns=int(game._max_turns),
+                                          evaluator=_evaluator_of(self.nnet, self.device), device=self.device,
+                                          node_capacity=self.node_capacity, max_depth=1024, gc=False,
+                                          record=False)
+            self._max_turns = game._max_turns
+        return self._engine
+
+    def _run(self, game, sims):
+        if game.outcome != GameOutcome.ONGOING:
+            raise ValueError("search from a finished game")
+        eng = self._engine_for(game)
+        state = np.random.get_state()
+        eng.set_rng(0, state[1], state[2])
+        eng.set_root(0, game._board, game._curr_turn, game.player.num)
+        for _ in range(sims):
+            eng.simulate()
+        mt, pos = eng.get_rng(0)
+        np.random.set_state((state[0], mt, pos, state[3], state[4]))
+        return eng
+
+    def search(self, game):
+        """One simulation from `game` (MCTS.py:62-145); updates the tree."""
+        self._run(game, 1)
+
+    def getActionProb(self, game, temp=1):
+        if not (isinstance(temp, (int, float)) and temp >= 0):
+            raise AssertionError("temp must be a number >= 0")
+        eng = self._run(game, int(self.args.numMCTSSims))
+        counts = eng.root_counts(0).astype(np.int64)
+        if temp == 0:
+            best = np.argwhere(counts == np.max(counts)).ravel()
+            pick = np.random.choice(best)
+            probs = np.zeros(len(counts), dtype=np.int8)
+            probs[pick] = 1
+            return probs
+        counts = counts ** (1.0 / temp)
+        return counts / counts.sum()
+
+    def stats(self):
+        return self._engine.stats() if self._engine is not None else {}
+
+    def reset(self):
+        return MCTS(self.nnet, self.args, self.device, self.node_capacity)
