@@ -52,22 +52,28 @@ def gather_records(engine, dst=0, group=None):
     Returns (moves [W*G], actions [W*G, m], counts [W*G, m, A] int16) on dst, None elsewhere,
     and the bytes this rank sent."""
     moves, actions, counts = engine_records(engine)
+    return gather_record_tensors(moves, actions, counts, dst, group)
+
+
+def gather_record_tensors(moves, actions, counts, dst=0, group=None):
+    """gather_records on plain tensors (any device the group's backend serves)."""
     m_local = torch.max(moves).reshape(1).to(torch.int64)
     m_all = m_local.clone()
     dist.all_reduce(m_all, op=dist.ReduceOp.MAX, group=group)
     m = int(m_all.item())
     ws = dist.get_world_size(group)
-    G = engine.G
+    G = moves.shape[0]
     act = actions[:, :m].contiguous()
     cnt = counts[:, :m].to(torch.int16).contiguous() if counts is not None else torch.zeros(
-        (G, m, A), dtype=torch.int16, device=engine.device)
+        (G, m, A), dtype=torch.int16, device=moves.device)
     mv = moves.clone()
     out_mv = torch.empty((ws * G,), dtype=mv.dtype, device=mv.device)
     out_act = torch.empty((ws * G, m), dtype=act.dtype, device=act.device)
     out_cnt = torch.empty((ws * G, m, A), dtype=cnt.dtype, device=cnt.device)
     dist.all_gather_into_tensor(out_mv, mv, group=group)
     dist.all_gather_into_tensor(out_act, act, group=group)
-    dist.all_gather_into_tensor(out_cnt, cnt, group=group)
+    # RCCL/gloo have no int16 type: move the counts as raw bytes
+    dist.all_gather_into_tensor(out_cnt.view(torch.uint8), cnt.view(torch.uint8), group=group)
     sent = mv.numel() * 4 + act.numel() * 4 + cnt.numel() * 2
     if dist.get_rank(group) == dst:
         return (out_mv, out_act, out_cnt), sent

@@ -1,0 +1,70 @@
+"""Multi-process (world size 2, gloo, CPU) tests of the per-iteration exchange:
+move-record gather to the trainer rank and weight broadcast from it."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import azg_amd  # noqa: F401
+        from azg_amd import dist as ad
+        from azg_amd.nnet import InflexionNNet
+        G, MM = 3, 10
+        moves = torch.tensor([4 + rank, 2, 6 - rank], dtype=torch.int32)
+        actions = torch.arange(G * MM, dtype=torch.int32).reshape(G, MM) + 1000 * rank
+        counts = (torch.arange(G * MM * 343, dtype=torch.int32).reshape(G, MM, 343) % 97) + rank
+        out, sent = ad.gather_record_tensors(moves, actions, counts, dst=0)
+        res = {"sent": sent}
+        if rank == 0:
+            mv, act, cnt = out
+            res["moves"] = mv.tolist()
+            res["m"] = act.shape[1]
+            res["act_ok"] = all(torch.equal(act[r * G:(r + 1) * G], (torch.arange(G * MM).reshape(G, MM)
+                                 + 1000 * r)[:, :act.shape[1]].int()) for r in range(world))
+            res["cnt_ok"] = torch.equal(cnt[G:2 * G].long(), ((torch.arange(G * MM * 343).reshape(G, MM, 343) % 97)
+                                        + 1)[:, :act.shape[1]])
+        torch.manual_seed(rank)  # different weights per rank before the broadcast
+        net = InflexionNNet(num_channels=16)
+        nbytes = ad.broadcast_weights(net, src=0)
+        torch.manual_seed(0)
+        ref = InflexionNNet(num_channels=16)
+        res["bcast_ok"] = all(torch.equal(a, b) for a, b in zip(net.state_dict().values(),
+                                                                  ref.state_dict().values()))
+        res["bcast_bytes"] = nbytes
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_and_broadcast_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    r0 = res[0]
+    assert r0["moves"] == [4, 2, 6, 5, 2, 5]
+    assert r0["m"] == 6  # max moves over ranks
+    assert r0["act_ok"] and r0["cnt_ok"]
+    assert res[0]["bcast_ok"] and res[1]["bcast_ok"]
+    assert res[1]["bcast_bytes"] == res[0]["bcast_bytes"] > 0
