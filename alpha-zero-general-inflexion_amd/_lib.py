@@ -58,6 +58,7 @@ SIGNATURES = [
     ("azg_read_moves", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     ("azg_stats", ctypes.c_int, [_VP, _VP, _VP]),
     ("azg_device_ptrs", ctypes.c_int, [_VP, _VP]),
+    ("azg_bias_relu_nhwc", ctypes.c_int, [_VP, _VP, _I64, _I32, _VP]),
 ]
 
 _lib = None

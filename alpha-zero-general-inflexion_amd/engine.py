@@ -113,9 +113,29 @@ class SelfPlayEngine:
 
     def move(self):
         """numMCTSSims simulations + root policy / sample / apply for every live game."""
+        if getattr(self, "_graph", None) is not None:
+            self._graph.replay()
+            return
         for _ in range(self.sims):
             self.simulate()
         self.move_end()
+
+    def capture_move(self):
+        """Record one whole move (sims x [select, network, expand/backup] + move_end)
+        as a HIP graph; later move() calls replay it (no per-kernel host launches).
+        Run at least one eager move first so the network's libraries are initialised.
+        Capturing launches nothing, so the games' state is unchanged."""
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g):
+            for _ in range(self.sims):
+                self.simulate()
+            self.move_end()
+        self._graph = g
+        return g
+
+    def drop_graph(self):
+        self._graph = None
 
     def active(self):
         n = ctypes.c_int32()

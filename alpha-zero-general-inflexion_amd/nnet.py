@@ -51,6 +51,19 @@ class InflexionNNet(nn.Module):
         return F.log_softmax(self.fc3(x), dim=1), torch.tanh(self.fc4(x))
 
 
+def _bias_relu_(x, b):
+    """x = relu(x + b) in place on a channels_last CUDA tensor (libazg, one pass)."""
+    import ctypes
+    from . import _lib
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
+    rows = x.numel() // x.shape[1]
+    rc = _lib.lib().azg_bias_relu_nhwc(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(b.data_ptr()), rows,
+                                       x.shape[1], ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+    _lib.check(rc)
+    return x
+
+
 def _fold_bn(weight, bias, bn):
     """Eval-mode BatchNorm folded into the preceding conv/linear (f64 math)."""
     scale = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
@@ -102,13 +115,18 @@ class InferenceNet(nn.Module):
     def forward(self, s):
         x = s.view(-1, self.depth, self.n, self.n).contiguous(memory_format=torch.channels_last)
         hook = self.conv_hook
+        fused = x.is_cuda
         for i, pad in enumerate(self.pads, start=1):
             if hook:
                 hook(i, "start")
-            x = F.conv2d(x, getattr(self, f"w{i}"), getattr(self, f"b{i}"), padding=pad)
+            b = getattr(self, f"b{i}")
+            x = F.conv2d(x, getattr(self, f"w{i}"), None if fused else b, padding=pad)
             if hook:
                 hook(i, "stop")
-            x = torch.relu_(x)
+            if fused:  # one HIP pass: bias + ReLU in place (azg_nn.hip)
+                x = _bias_relu_(x, b)
+            else:
+                x = torch.relu_(x)
         x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten, no copy
         x = torch.relu_(torch.addmm(self.fb1, x, self.fw1.t()))
         x = torch.relu_(torch.addmm(self.fb2, x, self.fw2.t()))

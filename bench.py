@@ -60,8 +60,22 @@ def parse():
     p.add_argument("--net", default="inference", choices=["inference", "reference"],
                    help="inference: BN-folded NHWC InferenceNet; reference: InflexionNNet as written")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-moves", type=int, default=40, help="cpu_baseline sample: first moves of one game")
-    return p.parse_args()
+    p.add_argument("--cpu-moves", type=int, default=200, help="cpu_baseline sample: first moves of one game")
+    p.add_argument("--full-games", action="store_true",
+                   help="time complete games (restart after warmup, play until every game ends): measured games/s")
+    p.add_argument("--graph", action="store_true",
+                   help="replay each move from a captured HIP graph (roofline fields then come from one extra "
+                        "eager move after the timed region)")
+    p.add_argument("--config", choices=["C2", "C3", "C4"], default=None,
+                   help="BASELINE.json presets: C2 256 games x 25 sims, C3 4096 x 100 sims, C4 4096/GPU x 25 sims")
+    a = p.parse_args()
+    if a.config == "C2":
+        a.games, a.sims = 256, 25
+    elif a.config == "C3":
+        a.games, a.sims = 4096, 100
+    elif a.config == "C4":
+        a.games, a.sims = 4096, 25
+    return a
 
 
 class Timer:
@@ -171,12 +185,33 @@ def main():
         eng.move_end()
         t_end.stop(s)
 
+    step = timed_move
+    if args.graph:
+        hook = getattr(ev, "conv_hook", None)
+        if hook is not None:
+            ev.conv_hook = None  # no event records inside the capture
+        eng.capture_move()
+        if hook is not None:
+            ev.conv_hook = hook
+        step = eng.move
     if world > 1:
         dist.barrier()
+    if args.full_games:
+        eng.reset()
+        torch.cuda.synchronize()
+        st0 = eng.stats()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        timed_move()
+    if args.full_games:
+        args.steps = 0
+        while eng.active() > 0:
+            step()
+            args.steps += 1
+            if rank == 0 and args.steps % 50 == 0:
+                print(f"# {args.steps} moves, {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+    else:
+        for _ in range(args.steps):
+            step()
     sync_bytes = 0
     if world > 1:  # per-iteration exchange: example gather to rank 0 + weight broadcast from rank 0
         sync_bytes = azg_dist.iteration_sync(eng, net)
@@ -187,6 +222,13 @@ def main():
     st1 = eng.stats()
     exp = st1["expansions"] - st0["expansions"]
     sims_run = st1["sims"] - st0["sims"]
+    n_timed = args.steps
+    if args.graph:  # kernel timings from one eager move after the timed region
+        eng.drop_graph()
+        if args.full_games:
+            eng.reset()
+        timed_move()
+        n_timed = 1
     nn_ms, sel_ms, exp_ms, end_ms = t_nn.total_ms(), t_sel.total_ms(), t_exp.total_ms(), t_end.total_ms()
     if st1["error"]:
         raise RuntimeError(f"engine error {st1['error']}")
@@ -201,7 +243,7 @@ def main():
 
     if rank == 0:
         value = exp / elapsed
-        n_forwards = args.steps * args.sims
+        n_forwards = n_timed * args.sims
         nn_avg = nn_ms / n_forwards / 1e3
         leaves = G  # the forward is evaluated on the full [G,4,7,7] batch
         nn_tflops = leaves * FLOP_PER_LEAF / nn_avg / 1e12
@@ -229,9 +271,10 @@ def main():
                                    f"max_turns {args.max_turns}, cpuct 1, tempThreshold 30 (configs[3] per GPU)",
                        "games_per_gpu": G, "sims_per_move": args.sims, "global_games": G * world,
                        "parallelism": f"games sharded over {world} GPU(s)", "step": "one move of every game"},
-            "games_per_s": value / EXPANSIONS_PER_GAME_REF,
-            "games_per_s_note": "expansions/s / 8555 expansions per random-init game (344 moves, measured on the "
-                                "reference); see DESIGN.md for the measured full-generation rate",
+            "games_per_s": (G * world / elapsed) if args.full_games else value / EXPANSIONS_PER_GAME_REF,
+            "games_per_s_note": (f"measured: {G * world} complete games in {elapsed:.1f}s" if args.full_games else
+                                 "expansions/s / 8555 expansions per random-init game (344 moves, measured on the "
+                                 "reference); bench.py --full-games measures it directly"),
             "expansions": exp,
             "simulations": sims_run,
             "roofline": {"bound": "mfma",
@@ -247,7 +290,7 @@ def main():
                               "frac": tree_gbs / HBM_PEAK_GBS, "traffic": None,
                               "bytes_per_sim": tree_bytes_per_sim(),
                               "select_ms_per_sim": sel_ms / n_forwards, "expand_ms_per_sim": exp_ms / n_forwards,
-                              "move_end_ms_per_move": end_ms / args.steps},
+                              "move_end_ms_per_move": end_ms / n_timed},
             "time_split": {"nn_ms": nn_ms, "select_ms": sel_ms, "expand_backup_ms": exp_ms, "move_end_ms": end_ms,
                            "wall_ms": elapsed * 1e3},
             "iteration_sync_bytes": sync_bytes,

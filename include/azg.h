@@ -112,6 +112,12 @@ int  azg_read_moves(azg_engine* e, int32_t* actions, int8_t* temps, int32_t* cou
  * [3] max path depth [4] max live nodes in a slot [5] error code [6] sims run */
 int  azg_stats(azg_engine* e, int64_t* out /*[8]*/, void* stream);
 
+/* Leaf-network epilogue: x[r, c] = max(x[r, c] + bias[c], 0) in place on an NHWC
+ * f32 activation of `rows` pixels x `channels` (multiple of 4, 16-B aligned).
+ * Replaces the BatchNorm + ReLU after each conv of InflexionNNet.forward
+ * (InflexionNNet.py:42-45) once BN is folded into the conv. */
+int  azg_bias_relu_nhwc(float* x, const float* bias, int64_t rows, int32_t channels, void* stream);
+
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active
  * [5] record actions [6] record counts [7] moves */
