@@ -48,6 +48,23 @@ def tree_bytes_per_sim(A_sel=87.0, d=1.33):
     return sel + table + leaf + node + backup
 
 
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_G4096.json")
+
+
+def load_pmc(G):
+    """HBM-side bytes per launch from the committed PMC passes (tools/pmc_summary.py:
+    rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs, FETCH doubled
+    per the gfx950 correction). Only valid for the workload it was measured on."""
+    if G != 4096 or not os.path.exists(PMC_FILE):
+        return None
+    d = json.load(open(PMC_FILE))
+    conv = d["conv2-4 igemm"]["hbm_bytes_sum_over_shapes"]
+    tree = d["select_kernel"]["hbm_bytes_sum_over_shapes"] + d["expand_backup_kernel"]["hbm_bytes_sum_over_shapes"]
+    return {"conv": conv, "tree": tree,
+            "note": f"{os.path.relpath(PMC_FILE, ROOT)}: FETCH_SIZE x2 + WRITE_SIZE per forward (conv2+3+4); "
+                    "counts L2 misses incl. Infinity-Cache hits; algorithmic bytes are ~1.1 GB"}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -295,6 +312,11 @@ def main():
                            "wall_ms": elapsed * 1e3},
             "iteration_sync_bytes": sync_bytes,
         }
+        pmc = load_pmc(G)
+        if pmc:
+            out["roofline"]["traffic"] = pmc["conv"]
+            out["roofline"]["traffic_note"] = pmc["note"]
+            out["roofline_tree"]["traffic"] = pmc["tree"]
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

@@ -1,0 +1,67 @@
+"""HBM traffic per kernel from separate rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+    python tools/pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv> > profiles/x.json
+
+Corrections per MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced streaming read,
+so the read side is doubled (an upper-bound correction for kernels whose reads
+are not all 16-B-per-lane streams).
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def load(path, counter):
+    """{(kernel name, grid size): [counter value per dispatch]}"""
+    per = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") != counter:
+            continue
+        per[(r["Kernel_Name"], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
+    return per
+
+
+def median(xs):
+    xs = sorted(xs)
+    return xs[len(xs) // 2] if xs else 0.0
+
+
+def group(name):
+    if name.startswith("igemm_fwd") and "bt128x128" in name:
+        return "conv2-4 igemm"
+    if name.startswith("igemm_fwd"):
+        return "conv1 igemm"
+    if name.startswith("azg::select"):
+        return "select_kernel"
+    if name.startswith("azg::expand"):
+        return "expand_backup_kernel"
+    if name.startswith("azg::move_end"):
+        return "move_end_kernel"
+    if "bias_relu" in name:
+        return "bias_relu_nhwc"
+    return None
+
+
+def main():
+    fetch = load(sys.argv[1], "FETCH_SIZE")
+    write = load(sys.argv[2], "WRITE_SIZE")
+    out = {}
+    for key in sorted(set(fetch) | set(write), key=lambda k: (k[0], -k[1])):
+        g = group(key[0])
+        if g is None:
+            continue
+        f, w = fetch.get(key, []), write.get(key, [])
+        out.setdefault(g, []).append({
+            "grid": key[1], "dispatches": max(len(f), len(w)),
+            "fetch_kib_raw_median": median(f), "write_kib_median": median(w),
+            "fetch_bytes_corrected": 2 * median(f) * 1024, "write_bytes": median(w) * 1024,
+            "hbm_bytes": 2 * median(f) * 1024 + median(w) * 1024})
+    summary = {g: {"per_shape": v, "hbm_bytes_sum_over_shapes": sum(x["hbm_bytes"] for x in v)}
+               for g, v in out.items()}
+    json.dump(summary, sys.stdout, indent=1)
+
+
+if __name__ == "__main__":
+    main()
