@@ -133,7 +133,102 @@ void orc_game_init(orc_game* g, int n, int max_turns) {
     g->player = 1;
 }
 
+/* ------------------------------------------------------------------- Othello
+ * builder-authored rules (azg_amd/othello.py), restated independently. */
+static const int ODIR[8][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 1}, {1, -1}, {1, 0}, {1, 1}};
+
+int orc_actions(const orc_game* g) { return g->kind == ORC_OTHELLO ? g->n * g->n + 1 : 7 * g->n * g->n; }
+int orc_channels(const orc_game* g) { return g->kind == ORC_OTHELLO ? 2 : 4; }
+
+void orc_othello_init(orc_game* g, int n) {
+    memset(g, 0, sizeof(*g));
+    g->n = n;
+    g->max_turns = 2 * n * n;
+    g->player = 1;
+    g->kind = ORC_OTHELLO;
+    int h = n / 2;
+    g->board[(h - 1) * n + h - 1] = g->board[h * n + h] = -1;
+    g->board[(h - 1) * n + h] = g->board[h * n + h - 1] = 1;
+}
+
+/* flips of a placement by `me` at (r, q): count, and marks them in flip[] when given */
+static int oth_flips(const orc_game* g, int r, int q, int me, uint8_t* flip) {
+    int n = g->n, total = 0;
+    if (g->board[r * n + q] != 0) return 0;
+    for (int d = 0; d < 8; ++d) {
+        int rr = r + ODIR[d][0], qq = q + ODIR[d][1], k = 0;
+        while (rr >= 0 && rr < n && qq >= 0 && qq < n && g->board[rr * n + qq] == -me) {
+            rr += ODIR[d][0];
+            qq += ODIR[d][1];
+            ++k;
+        }
+        if (k > 0 && rr >= 0 && rr < n && qq >= 0 && qq < n && g->board[rr * n + qq] == me) {
+            total += k;
+            if (flip)
+                for (int s = 1; s <= k; ++s) flip[(r + s * ODIR[d][0]) * n + q + s * ODIR[d][1]] = 1;
+        }
+    }
+    return total;
+}
+
+static int oth_has_move(const orc_game* g, int me) {
+    for (int c = 0; c < g->n * g->n; ++c)
+        if (oth_flips(g, c / g->n, c % g->n, me, NULL)) return 1;
+    return 0;
+}
+
+static int oth_valid(const orc_game* g, uint8_t* valid) {
+    int nn = g->n * g->n, cnt = 0;
+    for (int c = 0; c < nn; ++c) {
+        valid[c] = oth_flips(g, c / g->n, c % g->n, g->player, NULL) > 0;
+        cnt += valid[c];
+    }
+    valid[nn] = cnt == 0;
+    return cnt + valid[nn];
+}
+
+static int oth_apply(orc_game* g, int action) {
+    int n = g->n, nn = n * n, me = g->player;
+    if (action < 0 || action > nn) return -1;
+    if (action == nn) {
+        if (oth_has_move(g, me)) return -2;
+    } else {
+        uint8_t flip[ORC_MAXC] = {0};
+        if (!oth_flips(g, action / n, action % n, me, flip)) return -3;
+        g->board[action] = (int8_t)me;
+        for (int c = 0; c < nn; ++c)
+            if (flip[c]) g->board[c] = (int8_t)me;
+    }
+    g->turn += 1;
+    int outcome = ORC_ONGOING;
+    if (!oth_has_move(g, -me) && !oth_has_move(g, me)) {
+        int sum = 0;
+        for (int c = 0; c < nn; ++c) sum += g->board[c];
+        int diff = sum * me;
+        outcome = diff > 0 ? ORC_WON : diff < 0 ? ORC_LOST : ORC_DRAW;
+    }
+    g->player = -me;
+    g->outcome = outcome == ORC_WON ? ORC_LOST : outcome == ORC_LOST ? ORC_WON : outcome;
+    return 0;
+}
+
+void orc_dihedral_gather(int n, int k, int* src) {
+    for (int r = 0; r < n; ++r)
+        for (int q = 0; q < n; ++q) {
+            int i = r, j = (k & 4) ? n - 1 - q : q; /* fliplr after the rotations */
+            int sr, sq;
+            switch (k & 3) {
+                case 0: sr = i; sq = j; break;
+                case 1: sr = j; sq = n - 1 - i; break;
+                case 2: sr = n - 1 - i; sq = n - 1 - j; break;
+                default: sr = n - 1 - j; sq = i; break;
+            }
+            src[r * n + q] = sr * n + sq;
+        }
+}
+
 int orc_valid_mask(const orc_game* g, uint8_t* valid) {
+    if (g->kind == ORC_OTHELLO) return oth_valid(g, valid);
     int nn = g->n * g->n, cnt = 0;
     int can_spawn = total_power(g) <= MAX_POWER_AT_SPAWN;
     for (int m = 0; m < 7; ++m)
@@ -146,6 +241,7 @@ int orc_valid_mask(const orc_game* g, uint8_t* valid) {
 }
 
 int orc_apply(orc_game* g, int action) {
+    if (g->kind == ORC_OTHELLO) return oth_apply(g, action);
     int n = g->n, nn = n * n;
     if (action < 0 || action >= 7 * nn) return -1;
     int m = action / nn, c = action % nn, r = c / n, q = c % n;
@@ -191,6 +287,7 @@ void orc_planes(const orc_game* g, int32_t* planes) {
     for (int c = 0; c < nn; ++c) {
         planes[c] = g->board[c] * g->player > 0;
         planes[nn + c] = g->board[c] * g->player < 0;
+        if (g->kind == ORC_OTHELLO) continue; /* othello.py to_planes: [own, opp] */
         planes[2 * nn + c] = g->turn;
         planes[3 * nn + c] = can_spawn;
     }
@@ -231,16 +328,21 @@ static uint64_t mix64(uint64_t x) {
 }
 
 void orc_stub_eval(const int32_t* planes, int n, float* P, float* v) {
+    orc_stub_eval_c(planes, 4, n, 7 * n * n, P, v);
+}
+
+void orc_stub_eval_c(const int32_t* planes, int channels, int n, int A, float* P, float* v) {
     int nn = n * n;
     uint64_t own = 0, opp = 0;
     for (int c = 0; c < nn; ++c) {
         if (planes[c]) own |= 1ull << c;
         if (planes[nn + c]) opp |= 1ull << c;
     }
-    uint64_t t = (uint64_t)(int64_t)planes[2 * nn], k = (uint64_t)(int64_t)planes[3 * nn];
+    uint64_t t = channels > 2 ? (uint64_t)(int64_t)planes[2 * nn] : 0;
+    uint64_t k = channels > 3 ? (uint64_t)(int64_t)planes[3 * nn] : 0;
     uint64_t h = mix64(own ^ mix64(opp ^ mix64((t << 1) | k)));
     int all_zero = (h >> 56) < 4;
-    for (int a = 0; a < 7 * nn; ++a) {
+    for (int a = 0; a < A; ++a) {
         uint64_t ha = mix64(h ^ ((uint64_t)(a + 1) * 0xD1B54A32D192ED03ull));
         float p = (float)(uint32_t)(ha & 0xFFFFFFu) * 0x1p-24f;
         P[a] = (all_zero || (ha >> 59) == 0) ? 0.0f : p;
@@ -278,7 +380,10 @@ static uint64_t key_hash(uint64_t own, uint64_t opp, int turn, int cs) {
     return mix64(own ^ mix64(opp ^ (((uint64_t)turn << 1) | (uint64_t)cs)));
 }
 
-static void state_key(const orc_game* g, uint64_t* own, uint64_t* opp, int* cs) {
+/* The key is the information in to_planes().tobytes() (MCTS.py:83): Inflexion
+ * (own, opp, turn, can_spawn); Othello (own, opp), with the disc count -- a
+ * function of the planes -- in the turn slot so that nodes can be aged. */
+static void state_key(const orc_game* g, uint64_t* own, uint64_t* opp, int* cs, int* kt) {
     uint64_t o = 0, p = 0;
     for (int c = 0; c < g->n * g->n; ++c) {
         if (g->board[c] * g->player > 0) o |= 1ull << c;
@@ -286,7 +391,13 @@ static void state_key(const orc_game* g, uint64_t* own, uint64_t* opp, int* cs) 
     }
     *own = o;
     *opp = p;
-    *cs = total_power(g) <= MAX_POWER_AT_SPAWN;
+    if (g->kind == ORC_OTHELLO) {
+        *cs = 0;
+        *kt = __builtin_popcountll(o | p);
+    } else {
+        *cs = total_power(g) <= MAX_POWER_AT_SPAWN;
+        *kt = g->turn;
+    }
 }
 
 static int table_find(orc_mcts* m, uint64_t own, uint64_t opp, int turn, int cs, int* slot) {
@@ -319,25 +430,29 @@ static void table_grow(orc_mcts* m) {
 typedef struct { double v; int f32; } pyval; /* value returned by search() */
 
 /* MCTS.py:89-112 */
-static pyval expand(orc_mcts* m, const orc_game* g, uint64_t own, uint64_t opp, int cs, int slot) {
-    int n = g->n, nn = n * n, A = m->A;
+static pyval expand(orc_mcts* m, const orc_game* g, uint64_t own, uint64_t opp, int cs, int kt, int slot) {
+    int n = g->n, nn = n * n, A = m->A, C = orc_channels(g);
     int32_t planes[4 * ORC_MAXC], sym[4 * ORC_MAXC];
     int src[ORC_MAXC];
     orc_planes(g, planes);
-    int k = (int)orc_rng_randint(&m->rng, 0, 6);
-    int shift = (int)orc_rng_randint(&m->rng, 0, n);
-    int axis = (int)orc_rng_randint(&m->rng, 0, 3);
-    orc_sym_gather(n, k, shift, axis, src);
-    for (int ch = 0; ch < 4; ++ch)
+    if (g->kind == ORC_OTHELLO) { /* othello.py random_symmetry: one randint(0, 8) */
+        orc_dihedral_gather(n, (int)orc_rng_randint(&m->rng, 0, 8), src);
+    } else {
+        int k = (int)orc_rng_randint(&m->rng, 0, 6);
+        int shift = (int)orc_rng_randint(&m->rng, 0, n);
+        int axis = (int)orc_rng_randint(&m->rng, 0, 3);
+        orc_sym_gather(n, k, shift, axis, src);
+    }
+    for (int ch = 0; ch < C; ++ch)
         for (int c = 0; c < nn; ++c) sym[ch * nn + c] = planes[ch * nn + src[c]];
 
     float P[ORC_MAXA], v;
     if (m->eval) {
         float fp[4 * ORC_MAXC];
-        for (int i = 0; i < 4 * nn; ++i) fp[i] = (float)sym[i];
+        for (int i = 0; i < C * nn; ++i) fp[i] = (float)sym[i];
         m->eval(fp, P, &v, m->user);
     } else {
-        orc_stub_eval(sym, n, P, &v);
+        orc_stub_eval_c(sym, C, n, A, P, &v);
     }
     uint8_t valid[ORC_MAXA];
     orc_valid_mask(g, valid);
@@ -357,7 +472,7 @@ static pyval expand(orc_mcts* m, const orc_game* g, uint64_t own, uint64_t opp, 
     }
     int id = m->n_nodes++;
     orc_node* nd = &m->nodes[id];
-    nd->own = own; nd->opp = opp; nd->turn = g->turn; nd->can_spawn = cs; nd->Ns = 0;
+    nd->own = own; nd->opp = opp; nd->turn = kt; nd->can_spawn = cs; nd->Ns = 0;
     nd->P = (float*)malloc(sizeof(float) * (size_t)A);
     nd->N = (int32_t*)calloc((size_t)A, sizeof(int32_t));
     nd->Q = (double*)calloc((size_t)A, sizeof(double));
@@ -384,11 +499,11 @@ static pyval search(orc_mcts* m, const orc_game* root) {
             break;
         }
         uint64_t own, opp;
-        int cs, slot;
-        state_key(&g, &own, &opp, &cs);
-        int id = table_find(m, own, opp, g.turn, cs, &slot);
+        int cs, kt, slot;
+        state_key(&g, &own, &opp, &cs, &kt);
+        int id = table_find(m, own, opp, kt, cs, &slot);
         if (id < 0) {
-            ret = expand(m, &g, own, opp, cs, slot);
+            ret = expand(m, &g, own, opp, cs, kt, slot);
             break;
         }
         /* select: MCTS.py:114-131 */
@@ -455,9 +570,24 @@ int orc_episode(int n, int max_turns, int sims, double cpuct, int temp_threshold
                 uint32_t seed, orc_eval_fn eval, void* user,
                 int32_t* actions, int32_t* counts, int8_t* temps, int max_moves,
                 int64_t* stats) {
+    return orc_episode_kind(ORC_INFLEXION, n, max_turns, sims, cpuct, temp_threshold, seed, eval, user,
+                            actions, counts, temps, max_moves, stats);
+}
+
+int orc_episode_kind(int kind, int n, int max_turns, int sims, double cpuct, int temp_threshold,
+                     uint32_t seed, orc_eval_fn eval, void* user,
+                     int32_t* actions, int32_t* counts, int8_t* temps, int max_moves,
+                     int64_t* stats) {
+    orc_game g;
+    if (kind == ORC_OTHELLO) {
+        orc_othello_init(&g, n);
+    } else {
+        orc_game_init(&g, n, max_turns);
+        g.kind = ORC_INFLEXION;
+    }
     orc_mcts m;
     memset(&m, 0, sizeof(m));
-    m.n = n; m.A = 7 * n * n; m.max_turns = max_turns; m.sims = sims;
+    m.n = n; m.A = orc_actions(&g); m.max_turns = max_turns; m.sims = sims;
     m.temp_threshold = temp_threshold;
     m.cpuct_f = (float)cpuct;
     m.eval = eval; m.user = user;
@@ -466,8 +596,6 @@ int orc_episode(int n, int max_turns, int sims, double cpuct, int temp_threshold
     for (int i = 0; i < m.table_cap; ++i) m.table[i] = -1;
     orc_rng_seed(&m.rng, seed);
 
-    orc_game g;
-    orc_game_init(&g, n, max_turns);
     int moves = 0;
     int32_t cnt[ORC_MAXA];
     double pi[ORC_MAXA];
@@ -477,8 +605,9 @@ int orc_episode(int n, int max_turns, int sims, double cpuct, int temp_threshold
         for (int i = 0; i < sims; ++i) search(&m, &g);
         uint64_t own, opp;
         int cs, slot;
-        state_key(&g, &own, &opp, &cs);
-        int id = table_find(&m, own, opp, g.turn, cs, &slot);
+        int kt;
+        state_key(&g, &own, &opp, &cs, &kt);
+        int id = table_find(&m, own, opp, kt, cs, &slot);
         for (int a = 0; a < m.A; ++a) cnt[a] = id >= 0 ? m.nodes[id].N[a] : 0;
         if (temp == 0) { /* MCTS.py:51-56 */
             int mx = cnt[0], nb = 0, best[ORC_MAXA];

@@ -151,13 +151,28 @@ def gen_pairwise(np):
 
 
 # -------------------------------------------------------------------------- MCTS
-def gen_mcts(np, quick):
+def gen_mcts(np, quick, othello=False):
+    """Reference Coach.executeEpisode + MCTS traces.  With othello=True the
+    reference search is driven with this repo's builder-authored OthelloGame
+    plugin (the reference has no Othello): the rules are ours, the search,
+    sampling and example construction are the reference's."""
     import MCTS as mcts_mod
     from Coach import Coach
     from inflexion.InflexionGame import InflexionGame
     from inflexion.pytorch.NNet import NNetWrapper
     from utils import dotdict
     from stubnet import stub_eval
+    GameCls = InflexionGame
+    if othello:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+        import flags as ref_flags
+        import azg_amd  # noqa: F401
+        import azg_amd.flags as own_flags
+        # the reference compares outcomes with ITS enum (MCTS.py:85): the plugin must use it
+        own_flags.GameOutcome = ref_flags.GameOutcome
+        own_flags.PlayerColour = ref_flags.PlayerColour
+        from azg_amd.othello import OthelloGame
+        GameCls = OthelloGame
 
     class StubNNet(NNetWrapper):
         def __init__(self, game):  # no torch model: the hash evaluator only
@@ -173,7 +188,7 @@ def gen_mcts(np, quick):
         actions = []
         last = None
 
-    orig_tns = InflexionGame.to_next_state
+    orig_tns = GameCls.to_next_state
 
     def tns(self, action):
         nxt = orig_tns(self, action)
@@ -182,7 +197,7 @@ def gen_mcts(np, quick):
             Rec.last = nxt
         return nxt
 
-    InflexionGame.to_next_state = tns
+    GameCls.to_next_state = tns
 
     class RecMCTS(mcts_mod.MCTS):
         moves = None
@@ -215,11 +230,17 @@ def gen_mcts(np, quick):
     }
     if quick:
         sets = {"short": sets["short"]}
+    if othello:
+        sets = {
+            "othello6": dict(n=6, sims=25, cpuct=1, temp_threshold=15, seeds=list(range(500, 516))),
+            "othello8": dict(n=8, sims=25, cpuct=1, temp_threshold=30, seeds=list(range(600, 606))),
+            "othello8_s200": dict(n=8, sims=200, cpuct=1, temp_threshold=30, seeds=[700, 701]),
+        }
     for name, cfg in sets.items():
         eps = []
         t0 = time.time()
         for seed in cfg["seeds"]:
-            game = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
+            game = GameCls(cfg["n"]) if othello else InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
             nnet = StubNNet(game)
             args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"],
                             "tempThreshold": cfg["temp_threshold"]})
@@ -252,7 +273,7 @@ def gen_mcts(np, quick):
             print(f"  {name} seed {seed}: {len(Rec.actions)} moves, {nnet.calls} expansions, "
                   f"outcome {final.outcome.name}, {time.time() - t0:.1f}s", flush=True)
         _dump(f"mcts_{name}.json.gz", {"config": cfg, "episodes": eps})
-    InflexionGame.to_next_state = orig_tns
+    GameCls.to_next_state = orig_tns
 
 
 # -------------------------------------------------------------------------- NNet
@@ -305,6 +326,7 @@ def main():
         "pairwise": lambda: gen_pairwise(np),
         "nnet": lambda: gen_nnet(np, InflexionGame),
         "mcts": lambda: gen_mcts(np, quick),
+        "othello": lambda: gen_mcts(np, quick, othello=True),
     }
     for name, fn in jobs.items():
         if only and name not in only:

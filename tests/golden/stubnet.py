@@ -48,8 +48,8 @@ def planes_hash(planes):
     c1 = planes[1].ravel() != 0
     own = sum(1 << int(i) for i in np.nonzero(c0)[0])
     opp = sum(1 << int(i) for i in np.nonzero(c1)[0])
-    t = int(planes[2].ravel()[0])
-    k = int(planes[3].ravel()[0])
+    t = int(planes[2].ravel()[0]) if planes.shape[0] > 2 else 0  # games with 2 planes (Othello): t = k = 0
+    k = int(planes[3].ravel()[0]) if planes.shape[0] > 3 else 0
     return mix(own ^ mix(opp ^ mix(((t << 1) | k) & M64)))
 
 

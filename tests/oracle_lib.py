@@ -52,6 +52,12 @@ def lib():
                                   P(ctypes.c_int32), P(ctypes.c_int32), P(ctypes.c_int8), ctypes.c_int,
                                   P(ctypes.c_int64)]
         L.orc_episode.restype = ctypes.c_int
+        L.orc_episode_kind.argtypes = [ctypes.c_int] + L.orc_episode.argtypes
+        L.orc_episode_kind.restype = ctypes.c_int
+        L.orc_othello_init.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.orc_dihedral_gather.argtypes = [ctypes.c_int, ctypes.c_int, P(ctypes.c_int)]
+        L.orc_stub_eval_c.argtypes = [P(ctypes.c_int32), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      P(ctypes.c_float), P(ctypes.c_float)]
         L.orc_valid_mask.argtypes = [ctypes.c_void_p, P(ctypes.c_uint8)]
         L.orc_valid_mask.restype = ctypes.c_int
         L.orc_apply.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -87,7 +93,11 @@ class Rng:
 
 class OrcGame(ctypes.Structure):
     _fields_ = [("board", ctypes.c_int8 * 64), ("n", ctypes.c_int), ("turn", ctypes.c_int),
-                ("max_turns", ctypes.c_int), ("player", ctypes.c_int), ("outcome", ctypes.c_int)]
+                ("max_turns", ctypes.c_int), ("player", ctypes.c_int), ("outcome", ctypes.c_int),
+                ("kind", ctypes.c_int)]
+
+
+INFLEXION, OTHELLO = 1, 2
 
 
 OUTCOME_VALUE = {0: 0.0, 1: 1e-4, 2: 1.0, 3: -1.0}
@@ -108,9 +118,10 @@ def stub_eval(planes, n=7):
 
 
 def episode(n=7, max_turns=343, sims=25, cpuct=1.0, temp_threshold=30, seed=0, evaluator=None,
-            max_moves=400):
-    """Run one oracle episode.  evaluator(planes f32[4,n,n]) -> (P f32[A], v float)."""
-    A = 7 * n * n
+            max_moves=400, kind=INFLEXION):
+    """Run one oracle episode.  evaluator(planes f32[C,n,n]) -> (P f32[A], v float)."""
+    A = 7 * n * n if kind == INFLEXION else n * n + 1
+    C = 4 if kind == INFLEXION else 2
     actions = np.zeros(max_moves, np.int32)
     counts = np.zeros((max_moves, A), np.int32)
     temps = np.zeros(max_moves, np.int8)
@@ -118,12 +129,12 @@ def episode(n=7, max_turns=343, sims=25, cpuct=1.0, temp_threshold=30, seed=0, e
     cb = EVAL_FN()
     if evaluator is not None:
         def _cb(planes_p, P_p, v_p, _user):
-            planes = np.ctypeslib.as_array(planes_p, shape=(4, n, n))
+            planes = np.ctypeslib.as_array(planes_p, shape=(C, n, n))
             P, v = evaluator(planes)
             np.ctypeslib.as_array(P_p, shape=(A,))[:] = P
             v_p[0] = float(v)
         cb = EVAL_FN(_cb)
-    moves = lib().orc_episode(n, max_turns, sims, float(cpuct), temp_threshold, seed, cb, None,
+    moves = lib().orc_episode_kind(kind, n, max_turns, sims, float(cpuct), temp_threshold, seed, cb, None,
                               ptr(actions, ctypes.c_int32), ptr(counts, ctypes.c_int32),
                               ptr(temps, ctypes.c_int8), max_moves, ptr(stats, ctypes.c_int64))
     m = min(moves, max_moves)
