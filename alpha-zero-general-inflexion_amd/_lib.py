@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(HERE, "libazg.so")
 CSRC = os.path.join(HERE, "csrc")
 
 GAME_INFLEXION = 1
+GAME_OTHELLO = 2
 FLAG_GC = 1
 FLAG_RECORD = 2
 

@@ -25,15 +25,15 @@ from .inflexion import InflexionGame
 N_SYM = 36
 
 
-def _label_players(move_players, label_mode):
-    """Player attached to each of the 36*L examples (Coach.py:77-79)."""
+def _label_players(move_players, label_mode, n_sym=N_SYM):
+    """Player attached to each of the n_sym*L examples (Coach.py:77-79)."""
     L = len(move_players)
-    idx = np.arange(N_SYM * L)
+    idx = np.arange(n_sym * L)
     if label_mode == "per_move":
-        block = idx // N_SYM
+        block = idx // n_sym
     elif label_mode == "reference":
-        # after move m (1-based) the list holds 36 * m * (m + 1) / 2 entries
-        cum = N_SYM * np.arange(1, L + 1) * np.arange(2, L + 2) // 2
+        # after move m (1-based) the list holds n_sym * m * (m + 1) / 2 entries
+        cum = n_sym * np.arange(1, L + 1) * np.arange(2, L + 2) // 2
         block = np.searchsorted(cum, idx, side="right")
     else:
         raise ValueError(f"unknown label_mode {label_mode!r}")
@@ -45,7 +45,8 @@ def build_examples(game, move_planes, move_pis, move_players, final, label_mode=
     for planes, pi in zip(move_planes, move_pis):
         policies += game.symmetries(np.asarray(pi).reshape(game.policy_shape))
         boards += game.symmetries(planes)
-    players = _label_players(move_players, label_mode)
+    n_sym = len(boards) // max(len(move_planes), 1)
+    players = _label_players(move_players, label_mode, n_sym)
     v = final.outcome.value
     return [(b, p.ravel().tolist(), v if pl == final.player.num else -v)
             for b, p, pl in zip(boards, policies, players)]
@@ -81,10 +82,11 @@ class Coach:
     def selfplay_batch(self, num_games, evaluator=None, seed_base=0, first_game=0, return_records=False):
         """Play num_games complete games concurrently on the GPU engine and
         return their examples (same format as executeEpisode)."""
-        from .engine import SelfPlayEngine
+        from .engine import SelfPlayEngine, game_spec
         g0 = self.game
+        name, n, max_turns = game_spec(g0)
         eng = SelfPlayEngine(num_games, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct,
-                             temp_threshold=int(self.args.tempThreshold), max_turns=int(g0._max_turns),
+                             temp_threshold=int(self.args.tempThreshold), max_turns=max_turns, game=name, n=n,
                              seed_base=seed_base, first_game=first_game,
                              evaluator=evaluator if evaluator is not None else self.nnet)
         try:

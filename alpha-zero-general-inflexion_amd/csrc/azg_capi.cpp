@@ -42,6 +42,7 @@ int next_pow2(int x) {
 struct azg_engine {
     azg_config cfg;
     Dev d;
+    azg::GameOps ops;
     int device;
     std::vector<void*> allocs;
     int32_t* summary;   // device [2]
@@ -80,13 +81,16 @@ int azg_abi_version(void) { return AZG_ABI_VERSION; }
 
 int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
     if (!cfg || !out) return fail(AZG_ERR_ARG, "null argument");
-    if (cfg->game_kind != AZG_GAME_INFLEXION) return fail(AZG_ERR_ARG, "only AZG_GAME_INFLEXION is built");
-    if (cfg->n != azg::N) return fail(AZG_ERR_ARG, "this build is specialised for InflexionGame(7)");
+    azg::GameOps ops;
+    if (!azg::game_ops(cfg->game_kind, cfg->n, &ops))
+        return fail(AZG_ERR_ARG, "unsupported game: built for InflexionGame(7), OthelloGame(6), OthelloGame(8)");
     if (cfg->num_games <= 0 || cfg->sims <= 0 || cfg->max_turns < 0)
         return fail(AZG_ERR_ARG, "num_games, sims must be > 0 and max_turns >= 0");
     auto* e = new azg_engine();
     memset(&e->d, 0, sizeof(Dev));
     e->cfg = *cfg;
+    e->ops = ops;
+    const size_t A = (size_t)ops.actions, ROW = (size_t)ops.row;
     e->bytes = 0;
     HIP_TRY(hipGetDevice(&e->device));
     Dev& d = e->d;
@@ -117,9 +121,9 @@ int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
     ALLOC(d.node_turn, GM);
     ALLOC(d.node_cs, GM);
     ALLOC(d.node_Ns, GM);
-    ALLOC(d.node_P, GM * azg::AP);
-    ALLOC(d.node_N, GM * azg::AP);
-    ALLOC(d.node_Q, GM * azg::AP);
+    ALLOC(d.node_P, GM * ROW);
+    ALLOC(d.node_N, GM * ROW);
+    ALLOC(d.node_Q, GM * ROW);
     ALLOC(d.free_stack, GM);
     ALLOC(d.free_top, G);
     ALLOC(d.live, G);
@@ -136,7 +140,7 @@ int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
     ALLOC(d.moves, G);
     ALLOC(d.rec_action, G * (size_t)d.max_moves);
     ALLOC(d.rec_temp, G * (size_t)d.max_moves);
-    if (cfg->flags & AZG_FLAG_RECORD) ALLOC(d.rec_counts, G * (size_t)d.max_moves * azg::A);
+    if (cfg->flags & AZG_FLAG_RECORD) ALLOC(d.rec_counts, G * (size_t)d.max_moves * A);
     ALLOC(d.st_exp, G);
     ALLOC(d.st_term, G);
     ALLOC(d.st_fallback, G);
@@ -146,7 +150,7 @@ int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
     ALLOC(d.err, G);
     ALLOC(e->summary, 2);
     ALLOC(e->stats, 8);
-    ALLOC(e->counts1, azg::A);
+    ALLOC(e->counts1, A);
     *out = e;
     int r = azg_reset(e, cfg->seed_base, cfg->first_game, stream);
     if (r) {
@@ -167,31 +171,31 @@ int azg_reset(azg_engine* e, uint32_t seed_base, int64_t first_game, void* strea
     if (!e) return fail(AZG_ERR_ARG, "null engine");
     e->cfg.seed_base = seed_base;
     e->cfg.first_game = first_game;
-    HIP_TRY(azg::launch_reset(e->d, seed_base, (long long)first_game, (hipStream_t)stream));
+    HIP_TRY(e->ops.reset(e->d, seed_base, (long long)first_game, (hipStream_t)stream));
     return 0;
 }
 
 int azg_sim_begin(azg_engine* e, float* leaf_planes, void* stream) {
     if (!e || !leaf_planes) return fail(AZG_ERR_ARG, "null argument");
-    HIP_TRY(azg::launch_select(e->d, leaf_planes, (hipStream_t)stream));
+    HIP_TRY(e->ops.select(e->d, leaf_planes, (hipStream_t)stream));
     return 0;
 }
 
 int azg_sim_end(azg_engine* e, const float* P, int32_t p_stride, const float* v, void* stream) {
-    if (!e || !P || !v || p_stride < azg::A) return fail(AZG_ERR_ARG, "bad P/v");
-    HIP_TRY(azg::launch_expand_backup(e->d, P, p_stride, v, (hipStream_t)stream));
+    if (!e || !P || !v || p_stride < e->ops.actions) return fail(AZG_ERR_ARG, "bad P/v");
+    HIP_TRY(e->ops.expand_backup(e->d, P, p_stride, v, (hipStream_t)stream));
     return 0;
 }
 
 int azg_stub_eval(azg_engine* e, const float* leaf_planes, float* P, float* v, void* stream) {
     if (!e || !leaf_planes || !P || !v) return fail(AZG_ERR_ARG, "null argument");
-    HIP_TRY(azg::launch_stub_eval(e->d, leaf_planes, P, v, (hipStream_t)stream));
+    HIP_TRY(e->ops.stub_eval(e->d, leaf_planes, P, v, (hipStream_t)stream));
     return 0;
 }
 
 int azg_move_end(azg_engine* e, void* stream) {
     if (!e) return fail(AZG_ERR_ARG, "null engine");
-    HIP_TRY(azg::launch_move_end(e->d, (hipStream_t)stream));
+    HIP_TRY(e->ops.move_end(e->d, (hipStream_t)stream));
     return 0;
 }
 
@@ -220,7 +224,7 @@ int azg_get_state(azg_engine* e, int8_t* boards, int32_t* turns, int32_t* player
                   int32_t* active, void* stream) {
     if (!e) return fail(AZG_ERR_ARG, "null engine");
     hipStream_t st = (hipStream_t)stream;
-    const int G = e->d.G, nn = azg::CELLS;
+    const int G = e->d.G, nn = e->ops.cells;
     if (boards) {
         std::vector<int8_t> tmp((size_t)G * 64);
         HIP_TRY(hipMemcpyAsync(tmp.data(), e->d.board, tmp.size(), hipMemcpyDeviceToHost, st));
@@ -240,7 +244,7 @@ int azg_set_root(azg_engine* e, int32_t slot, const int8_t* board, int32_t turn,
         return fail(AZG_ERR_ARG, "bad set_root argument");
     hipStream_t st = (hipStream_t)stream;
     int8_t b[64] = {0};
-    memcpy(b, board, azg::CELLS);
+    memcpy(b, board, (size_t)e->ops.cells);
     const int32_t ongoing = azg::ONGOING, one = 1, zero = 0;
     HIP_TRY(hipMemcpyAsync(e->d.board + (size_t)slot * 64, b, 64, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(e->d.turn + slot, &turn, 4, hipMemcpyHostToDevice, st));
@@ -275,8 +279,8 @@ int azg_set_rng(azg_engine* e, int32_t slot, const uint32_t* mt, int32_t pos, vo
 int azg_root_counts(azg_engine* e, int32_t slot, int32_t* counts, void* stream) {
     if (!e || !counts || slot < 0 || slot >= e->d.G) return fail(AZG_ERR_ARG, "bad root_counts argument");
     hipStream_t st = (hipStream_t)stream;
-    HIP_TRY(azg::launch_root_counts(e->d, slot, e->counts1, st));
-    HIP_TRY(hipMemcpyAsync(counts, e->counts1, azg::A * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(e->ops.root_counts(e->d, slot, e->counts1, st));
+    HIP_TRY(hipMemcpyAsync(counts, e->counts1, (size_t)e->ops.actions * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return 0;
 }
@@ -290,7 +294,8 @@ int azg_read_moves(azg_engine* e, int32_t* actions, int8_t* temps, int32_t* coun
     if (temps) HIP_TRY(hipMemcpyAsync(temps, e->d.rec_temp, G * MM, hipMemcpyDeviceToHost, st));
     if (counts) {
         if (!e->d.rec_counts) return fail(AZG_ERR_STATE, "engine created without AZG_FLAG_RECORD");
-        HIP_TRY(hipMemcpyAsync(counts, e->d.rec_counts, G * MM * azg::A * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(counts, e->d.rec_counts, G * MM * (size_t)e->ops.actions * 4, hipMemcpyDeviceToHost,
+                               st));
     }
     if (moves) HIP_TRY(hipMemcpyAsync(moves, e->d.moves, G * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));

@@ -12,32 +12,19 @@
 namespace azg {
 
 constexpr int WAVE = 64;
-constexpr int N = 7;                 // InflexionGame(7) (main.py:34)
-constexpr int CELLS = N * N;         // 49
-constexpr int A = 7 * CELLS;         // 343 = policy_shape (7, 7, 7), InflexionGame.py:47-48
-constexpr int AP = 384;              // per-node action stride, 6 x 64 lanes
-constexpr int AJ = AP / WAVE;        // 6 action chunks per lane
 constexpr int MT_N = 624;
 constexpr int MAX_POWER_AT_SPAWN = 48;   // InflexionGame.py:69
 
 enum Outcome : int { ONGOING = 0, DRAW = 1, WON = 2, LOST = 3 };
 enum LeafKind : int { LEAF_NONE = 0, LEAF_EXPAND = 1, LEAF_TERMINAL = 2 };
 
-// numpy float32 add.reduce pairwise plan: leaves summed with 8 accumulators,
-// combined by an RPN program (op >= 0: push leaf op; op == -1: add top two).
-struct PairwisePlan {
-    int nleaf;
-    int off[16];
-    int len[16];
-    int nops;
-    int8_t ops[32];
-};
-
+// Game-specific sizes (cells, actions A, row stride = A rounded up to 64,
+// planes) are compile-time constants of the game traits in azg_kernels.hip;
+// the host sees them through GameOps (azg_launch.h).
 struct Dev {
     int G, M, H, DMAX, max_moves;
     int max_turns, sims, temp_threshold, flags;
     float cpuct_f;
-    PairwisePlan pw;
 
     // per slot
     int8_t* board;       // [G][64]

@@ -2,11 +2,16 @@
 //
 // Launch geometry: one 64-thread workgroup (= one wavefront) per game slot.
 // The tree work per simulation is latency-bound pointer chasing over a handful
-// of 1.5-3 KB node rows (~4.8 KB per expansion), so the design
-// goal is: every HBM access is a coalesced 256 B-1.5 KB wave-wide row read,
-// every reduction is an in-register __shfl_xor butterfly, no atomics on the
-// tree (the slot is owned by its wave), and no host synchronisation between
-// kernels (the whole move can be captured in a hipGraph).
+// of node rows, so the design goal is: every HBM access is a
+// coalesced wave-wide row read, every reduction is an in-register __shfl_xor
+// butterfly or a __ballot, no atomics on the tree (the slot is owned by its
+// wave), and no host synchronisation between kernels (a whole move can be
+// captured in a hipGraph).
+//
+// The search kernels are templates over a game's rules (struct Inflexion,
+// struct Othello<N>): key, valid-action context, move application and the
+// randomly symmetrised NN planes are wave-collective device functions with
+// one lane per board cell.
 //
 // Numerics restate the reference bit-exactly (oracle/oracle.c is the CPU
 // checker): f32 ops are single-rounded (-ffp-contract=off
@@ -29,19 +34,11 @@ __device__ __forceinline__ int wave_sum(int x) {
     return x;
 }
 
-__device__ __forceinline__ long long wave_sum64(long long x) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
-    return x;
-}
-
 __device__ __forceinline__ int wave_max(int x) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) x = max(x, __shfl_xor(x, o));
     return x;
 }
-
-__device__ __forceinline__ int mod_n(int x) { return ((x % N) + N) % N; }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -60,90 +57,6 @@ __device__ __forceinline__ double outcome_value(int o) {
 
 __device__ __forceinline__ int flip_outcome(int o) {  // GameOutcome.opposite, Game.py:49-62
     return o == WON ? LOST : o == LOST ? WON : o;
-}
-
-// valid_actions_mask (InflexionGame.py:93-100) as a function of the state key.
-__device__ __forceinline__ bool action_valid(int a, uint64_t own, uint64_t opp, int cs) {
-    int m = a / CELLS, c = a - m * CELLS;
-    if (m < 6) return (own >> c) & 1ull;
-    return cs && !(((own | opp) >> c) & 1ull);
-}
-
-// ------------------------------------------------------------ numpy pairwise
-struct PW {
-    int nleaf = 0, nops = 0;
-    int off[16] = {}, len[16] = {}, ops[32] = {};
-};
-constexpr void pw_build(PW& p, int off, int n) {
-    if (n <= 128) {
-        p.ops[p.nops++] = p.nleaf;
-        p.off[p.nleaf] = off;
-        p.len[p.nleaf] = n;
-        p.nleaf++;
-        return;
-    }
-    int n2 = n / 2;
-    n2 -= n2 % 8;
-    pw_build(p, off, n2);
-    pw_build(p, off + n2, n - n2);
-    p.ops[p.nops++] = -1;
-}
-constexpr PW make_pw(int n) {
-    PW p{};
-    pw_build(p, 0, n);
-    return p;
-}
-constexpr PW kPW = make_pw(A);
-static_assert(kPW.nleaf <= 8, "one pass of 8 lanes per leaf");
-
-// float32 add.reduce in numpy's exact association (MCTS.py:96, :107).
-// x: LDS [A]; acc: LDS [64]; leaf: LDS [16].  Returns the sum in every lane.
-__device__ float pairwise_sum(const float* x, float* acc, float* leaf) {
-    const int lane = lane_id();
-    const int l = lane >> 3, j = lane & 7;
-#pragma unroll
-    for (int q = 0; q < kPW.nleaf; ++q) {
-        if (l == q && kPW.len[q] >= 8) {
-            const int off = kPW.off[q], full = kPW.len[q] - kPW.len[q] % 8;
-            float r = x[off + j];
-            for (int i = 8; i < full; i += 8) r = r + x[off + i + j];
-            acc[lane] = r;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < kPW.nleaf; ++q) {
-        if (lane == q) {
-            const int off = kPW.off[q], len = kPW.len[q];
-            float res;
-            int i;
-            if (len < 8) {
-                res = 0.0f;
-                i = 0;
-            } else {
-                const float* r = acc + q * 8;
-                res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-                i = len - len % 8;
-            }
-            for (; i < len; ++i) res = res + x[off + i];
-            leaf[q] = res;
-        }
-    }
-    __syncthreads();
-    float st[8];
-    int sp = 0;
-#pragma unroll
-    for (int k = 0; k < kPW.nops; ++k) {
-        if (kPW.ops[k] >= 0) {
-            st[sp++] = leaf[kPW.ops[k]];
-        } else {
-            float b = st[--sp];
-            float a = st[--sp];
-            st[sp++] = a + b;
-        }
-    }
-    __syncthreads();
-    return 0.0f + st[0];
 }
 
 // ------------------------------------------------------------------- MT19937
@@ -229,83 +142,331 @@ __device__ void rng_store(BlockRng& R) {
     if (lane_id() == 0) *R.gpos = R.pos;
 }
 
-// ------------------------------------------------------------------- rules
-// One lane per cell (lanes 0..48).  State: cell value, turn, player, outcome.
+// ------------------------------------------------------------ numpy pairwise
+struct PW {
+    int nleaf = 0, nops = 0;
+    int off[16] = {}, len[16] = {}, ops[32] = {};
+};
+constexpr void pw_build(PW& p, int off, int n) {
+    if (n <= 128) {
+        p.ops[p.nops++] = p.nleaf;
+        p.off[p.nleaf] = off;
+        p.len[p.nleaf] = n;
+        p.nleaf++;
+        return;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    pw_build(p, off, n2);
+    pw_build(p, off + n2, n - n2);
+    p.ops[p.nops++] = -1;
+}
+constexpr PW make_pw(int n) {
+    PW p{};
+    pw_build(p, 0, n);
+    return p;
+}
+
+// float32 add.reduce over NA values in numpy's exact association (MCTS.py:96,
+// :107).  x: LDS [NA]; acc: LDS [64]; leaf: LDS [16].  Sum in every lane.
+template <int NA>
+__device__ float pairwise_sum(const float* x, float* acc, float* leaf) {
+    constexpr PW kPW = make_pw(NA);
+    static_assert(kPW.nleaf <= 8, "one pass of 8 lanes per leaf");
+    const int lane = lane_id();
+    const int l = lane >> 3, j = lane & 7;
+#pragma unroll
+    for (int q = 0; q < kPW.nleaf; ++q) {
+        if (l == q && kPW.len[q] >= 8) {
+            const int off = kPW.off[q], full = kPW.len[q] - kPW.len[q] % 8;
+            float r = x[off + j];
+            for (int i = 8; i < full; i += 8) r = r + x[off + i + j];
+            acc[lane] = r;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPW.nleaf; ++q) {
+        if (lane == q) {
+            const int off = kPW.off[q], len = kPW.len[q];
+            float res;
+            int i;
+            if (len < 8) {
+                res = 0.0f;
+                i = 0;
+            } else {
+                const float* r = acc + q * 8;
+                res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+                i = len - len % 8;
+            }
+            for (; i < len; ++i) res = res + x[off + i];
+            leaf[q] = res;
+        }
+    }
+    __syncthreads();
+    float st[8];
+    int sp = 0;
+#pragma unroll
+    for (int k = 0; k < kPW.nops; ++k) {
+        if (kPW.ops[k] >= 0) {
+            st[sp++] = leaf[kPW.ops[k]];
+        } else {
+            float b = st[--sp];
+            float a = st[--sp];
+            st[sp++] = a + b;
+        }
+    }
+    __syncthreads();
+    return 0.0f + st[0];
+}
+
+// ------------------------------------------------------------------- games
+// One lane per cell (lanes 0..CELLS-1).  Pos: this lane's cell value, and the
+// wave-uniform turn, player to move (+1 RED / -1 BLUE), outcome w.r.t. it.
 struct Pos {
     int cell, turn, player, outcome;
 };
 
-__device__ __forceinline__ void pos_key(const Pos& p, uint64_t& own, uint64_t& opp, int& cs) {
-    const int lane = lane_id();
-    const bool on = lane < CELLS;
-    own = __ballot(on && p.cell * p.player > 0);
-    opp = __ballot(on && p.cell * p.player < 0);
-    cs = wave_sum(on ? abs(p.cell) : 0) <= MAX_POWER_AT_SPAWN;
-}
+// --- InflexionGame(7) (InflexionGame.py) ---------------------------------
+struct Inflexion {
+    static constexpr int N = 7, CELLS = 49, A = 7 * CELLS, AP = 384, AJ = AP / WAVE, PLANES = 4;
+    static constexpr uint64_t FULL = (1ull << CELLS) - 1ull;
+    static __device__ __forceinline__ int mod_n(int x) { return ((x % N) + N) % N; }
 
-// InflexionGame.execute_move (:273-310) + Game.player setter (:49-62).
-__device__ void pos_apply(Pos& p, int a, int max_turns) {
-    const int lane = lane_id();
-    const int m = a / CELLS, c = a - m * CELLS, r = c / N, q = c - (c / N) * N;
-    const int orig = __shfl(p.cell, c);
-    const bool spread = m < 6;
-    if (!spread) {
-        if (lane == c) p.cell = p.player;
-    } else if (lane < CELLS) {
-        const int dr = (m == 0 || m == 4) ? 1 : (m == 1 || m == 5) ? -1 : 0;
-        const int dq = (m == 2 || m == 5) ? 1 : (m == 3 || m == 4) ? -1 : 0;
-        const int power = abs(orig);
-        const int lr = lane / N, lq = lane - (lane / N) * N;
-        const int k = dr != 0 ? mod_n((lr - r) * dr) : mod_n((lq - q) * dq);
-        const bool hit = k >= 1 && k <= power && mod_n(r + k * dr) == lr && mod_n(q + k * dq) == lq;
-        if (hit) {
-            int x = abs(p.cell) + 1;
-            p.cell = (x > 6 ? 0 : x) * p.player;
+    __device__ static int initial_cell(int) { return 0; }
+
+    // key = to_planes() information (InflexionGame.py:84-91): own, opp, turn, can_spawn
+    __device__ static void key(const Pos& p, uint64_t& own, uint64_t& opp, int& kt, int& cs) {
+        const bool on = lane_id() < CELLS;
+        own = __ballot(on && p.cell * p.player > 0);
+        opp = __ballot(on && p.cell * p.player < 0);
+        cs = wave_sum(on ? abs(p.cell) : 0) <= MAX_POWER_AT_SPAWN;
+        kt = p.turn;
+    }
+
+    // valid_actions_mask (InflexionGame.py:93-100) from the key
+    struct VCtx {
+        uint64_t own, spawn;
+    };
+    __device__ static VCtx vctx(uint64_t own, uint64_t opp, int cs) { return {own, cs ? (~(own | opp) & FULL) : 0ull}; }
+    __device__ static bool valid(int a, const VCtx& v) {
+        const int m = a / CELLS, c = a - m * CELLS;
+        return m < 6 ? ((v.own >> c) & 1ull) : ((v.spawn >> c) & 1ull);
+    }
+
+    // execute_move (:273-310) + player setter (Game.py:49-62)
+    __device__ static void apply(Pos& p, int a, int max_turns) {
+        const int lane = lane_id();
+        const int m = a / CELLS, c = a - m * CELLS, r = c / N, q = c - (c / N) * N;
+        const int orig = __shfl(p.cell, c);
+        const bool spread = m < 6;
+        if (!spread) {
+            if (lane == c) p.cell = p.player;
+        } else if (lane < CELLS) {
+            const int dr = (m == 0 || m == 4) ? 1 : (m == 1 || m == 5) ? -1 : 0;
+            const int dq = (m == 2 || m == 5) ? 1 : (m == 3 || m == 4) ? -1 : 0;
+            const int power = abs(orig);
+            const int lr = lane / N, lq = lane - (lane / N) * N;
+            const int k = dr != 0 ? mod_n((lr - r) * dr) : mod_n((lq - q) * dq);
+            const bool hit = k >= 1 && k <= power && mod_n(r + k * dr) == lr && mod_n(q + k * dq) == lq;
+            if (hit) {
+                int x = abs(p.cell) + 1;
+                p.cell = (x > 6 ? 0 : x) * p.player;
+            }
+            if (lane == c) p.cell = 0;
         }
-        if (lane == c) p.cell = 0;
+        const bool on = lane < CELLS;
+        const uint64_t oppb = __ballot(on && p.cell * p.player < 0);
+        const int sum = wave_sum(on ? p.cell : 0);
+        const uint64_t anyb = __ballot(on && p.cell != 0);
+        int out = ONGOING;
+        if (spread && oppb == 0) {
+            out = WON;
+        } else if (p.turn >= max_turns) {
+            const int diff = p.player * sum;
+            out = diff >= 2 ? WON : diff <= -2 ? LOST : DRAW;
+        } else if (anyb == 0) {
+            out = DRAW;
+        }
+        p.turn += 1;
+        p.player = -p.player;
+        p.outcome = flip_outcome(out);
     }
-    const bool on = lane < CELLS;
-    const uint64_t oppb = __ballot(on && p.cell * p.player < 0);
-    const int sum = wave_sum(on ? p.cell : 0);
-    const uint64_t anyb = __ballot(on && p.cell != 0);
-    int out = ONGOING;
-    if (spread && oppb == 0) {
-        out = WON;
-    } else if (p.turn >= max_turns) {
-        const int diff = p.player * sum;
-        out = diff >= 2 ? WON : diff <= -2 ? LOST : DRAW;
-    } else if (anyb == 0) {
-        out = DRAW;
-    }
-    p.turn += 1;
-    p.player = -p.player;
-    p.outcome = flip_outcome(out);
-}
 
-// rotate(k) then translate(shift, axis): source cell of output cell c.
-__device__ __forceinline__ int sym_src(int c, int k, int shift, int axis) {
-    int r = c / N, q = c - (c / N) * N;
-    int tr = r, tq = q;
-    if (axis == 0) tr = r - shift;
-    else if (axis == 1) tq = q - shift;
-    else { tr = r + shift; tq = q - shift; }
-    tr = mod_n(tr);
-    tq = mod_n(tq);
-    const int s = (tr + tq) % N;
-    int rr, qq;
-    switch (k) {
-        case 0: rr = tr; qq = tq; break;
-        case 1: rr = -s; qq = tr; break;
-        case 2: rr = -tq; qq = s; break;
-        case 3: rr = -tr; qq = -tq; break;
-        case 4: rr = s; qq = -tr; break;
-        default: rr = tq; qq = -s; break;
+    // rotate(k) then translate(shift, axis): source cell of output cell c
+    __device__ static int sym_src(int c, int k, int shift, int axis) {
+        int r = c / N, q = c - (c / N) * N;
+        int tr = r, tq = q;
+        if (axis == 0) tr = r - shift;
+        else if (axis == 1) tq = q - shift;
+        else { tr = r + shift; tq = q - shift; }
+        tr = mod_n(tr);
+        tq = mod_n(tq);
+        const int s = (tr + tq) % N;
+        int rr, qq;
+        switch (k) {
+            case 0: rr = tr; qq = tq; break;
+            case 1: rr = -s; qq = tr; break;
+            case 2: rr = -tq; qq = s; break;
+            case 3: rr = -tr; qq = -tq; break;
+            case 4: rr = s; qq = -tr; break;
+            default: rr = tq; qq = -s; break;
+        }
+        return mod_n(rr) * N + mod_n(qq);
     }
-    return mod_n(rr) * N + mod_n(qq);
-}
+
+    // random_symmetry (InflexionGame.py:115-122): randint(0,6), randint(0,n), choice(r,q,s)
+    __device__ static void write_planes(float* out, uint64_t own, uint64_t opp, int kt, int cs, BlockRng& R) {
+        const int k = rng_randint(R, 0, 6);
+        const int shift = rng_randint(R, 0, N);
+        const int axis = rng_randint(R, 0, 3);
+        const int lane = lane_id();
+        if (lane < CELLS) {
+            const int src = sym_src(lane, k, shift, axis);
+            out[lane] = (float)((own >> src) & 1ull);
+            out[CELLS + lane] = (float)((opp >> src) & 1ull);
+            out[2 * CELLS + lane] = (float)kt;
+            out[3 * CELLS + lane] = (float)cs;
+        }
+    }
+};
+
+// --- OthelloGame(n) (azg_amd/othello.py; builder-authored) ----------------
+template <int NB>
+struct Othello {
+    static constexpr int N = NB, CELLS = NB * NB, A = CELLS + 1, AP = ((A + WAVE - 1) / WAVE) * WAVE,
+                         AJ = AP / WAVE, PLANES = 2;
+    static constexpr uint64_t FULL = CELLS == 64 ? ~0ull : (1ull << CELLS) - 1ull;
+
+    static constexpr uint64_t col_mask(int q) {
+        uint64_t m = 0;
+        for (int r = 0; r < N; ++r) m |= 1ull << (r * N + q);
+        return m;
+    }
+    static constexpr uint64_t FIRST = col_mask(0), LAST = col_mask(NB - 1);
+
+    __device__ static int initial_cell(int c) {
+        const int h = N / 2, r = c / N, q = c % N;
+        if ((r == h - 1 && q == h - 1) || (r == h && q == h)) return -1;
+        if ((r == h - 1 && q == h) || (r == h && q == h - 1)) return 1;
+        return 0;
+    }
+
+    // one step of direction d = (dr, dq) in {-1,0,1}^2 \ (0,0) on a bitboard
+    __device__ static __forceinline__ uint64_t step(uint64_t b, int dr, int dq) {
+        if (dq == 1) b &= ~LAST;
+        if (dq == -1) b &= ~FIRST;
+        const int s = dr * N + dq;
+        return (s > 0 ? (b << s) : (b >> (-s))) & FULL;
+    }
+
+    __device__ static uint64_t legal(uint64_t own, uint64_t opp) {
+        const uint64_t empty = ~(own | opp) & FULL;
+        uint64_t moves = 0;
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            const int dr = d / 3 - 1, dq = d % 3 - 1;
+            if (dr == 0 && dq == 0) continue;
+            uint64_t x = step(own, dr, dq) & opp;
+#pragma unroll
+            for (int i = 0; i < N - 3; ++i) x |= step(x, dr, dq) & opp;
+            moves |= step(x, dr, dq) & empty;
+        }
+        return moves;
+    }
+
+    __device__ static uint64_t flips(uint64_t own, uint64_t opp, int c) {
+        uint64_t f = 0;
+        const uint64_t m = 1ull << c;
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            const int dr = d / 3 - 1, dq = d % 3 - 1;
+            if (dr == 0 && dq == 0) continue;
+            uint64_t run = 0, x = step(m, dr, dq);
+            while (x & opp) {
+                run |= x;
+                x = step(x, dr, dq);
+            }
+            if (x & own) f |= run;
+        }
+        return f;
+    }
+
+    // key = to_planes() information: (own, opp); disc count in the turn slot (for node ageing)
+    __device__ static void key(const Pos& p, uint64_t& own, uint64_t& opp, int& kt, int& cs) {
+        const bool on = lane_id() < CELLS;
+        own = __ballot(on && p.cell * p.player > 0);
+        opp = __ballot(on && p.cell * p.player < 0);
+        kt = __popcll(own | opp);
+        cs = 0;
+    }
+
+    struct VCtx {
+        uint64_t legal;
+    };
+    __device__ static VCtx vctx(uint64_t own, uint64_t opp, int) { return {legal(own, opp)}; }
+    __device__ static bool valid(int a, const VCtx& v) {
+        return a < CELLS ? ((v.legal >> a) & 1ull) : (v.legal == 0ull);
+    }
+
+    __device__ static void apply(Pos& p, int a, int) {
+        const int lane = lane_id();
+        const bool on = lane < CELLS;
+        const uint64_t own = __ballot(on && p.cell * p.player > 0);
+        const uint64_t opp = __ballot(on && p.cell * p.player < 0);
+        uint64_t own2 = own, opp2 = opp;
+        if (a < CELLS) {
+            const uint64_t f = flips(own, opp, a);
+            own2 = own | f | (1ull << a);
+            opp2 = opp & ~f;
+            if (on && ((own2 >> lane) & 1ull)) p.cell = p.player;
+        }
+        int out = ONGOING;
+        if (legal(opp2, own2) == 0 && legal(own2, opp2) == 0) {
+            const int diff = __popcll(own2) - __popcll(opp2);
+            out = diff > 0 ? WON : diff < 0 ? LOST : DRAW;
+        }
+        p.turn += 1;
+        p.player = -p.player;
+        p.outcome = flip_outcome(out);
+    }
+
+    // random_symmetry: one randint(0, 8); k&3 rot90s then fliplr if k&4 (othello.py dihedral_source)
+    __device__ static void write_planes(float* out, uint64_t own, uint64_t opp, int, int, BlockRng& R) {
+        const int k = rng_randint(R, 0, 8);
+        const int lane = lane_id();
+        if (lane < CELLS) {
+            const int i = lane / N, j = (k & 4) ? N - 1 - lane % N : lane % N;
+            int sr, sq;
+            switch (k & 3) {
+                case 0: sr = i; sq = j; break;
+                case 1: sr = j; sq = N - 1 - i; break;
+                case 2: sr = N - 1 - i; sq = N - 1 - j; break;
+                default: sr = N - 1 - j; sq = i; break;
+            }
+            const int src = sr * N + sq;
+            out[lane] = (float)((own >> src) & 1ull);
+            out[CELLS + lane] = (float)((opp >> src) & 1ull);
+        }
+    }
+};
 
 // ------------------------------------------------------------------- tree
-__device__ __forceinline__ size_t node_row(const Dev& E, int g, int id) { return ((size_t)g * E.M + id) * AP; }
+template <class R>
+__device__ __forceinline__ size_t node_row(const Dev& E, int g, int id) {
+    return ((size_t)g * E.M + id) * R::AP;
+}
+
+template <class R>
+__device__ __forceinline__ Pos load_root(const Dev& E, int g) {
+    Pos p;
+    const int lane = lane_id();
+    p.cell = lane < R::CELLS ? (int)E.board[(size_t)g * 64 + lane] : 0;
+    p.turn = E.turn[g];
+    p.player = E.player[g];
+    p.outcome = E.outcome[g];
+    return p;
+}
 
 // Wave-cooperative open-addressing lookup: 64 consecutive slots per probe.
 // Returns node id or -1 (then *slot = first empty slot in probe order).
@@ -342,18 +503,19 @@ __device__ int table_lookup(const Dev& E, int g, uint64_t own, uint64_t opp, int
 
 // PUCT argmax (MCTS.py:114-131): strict '>' scan in action order == max u,
 // ties to the lowest action; NaN never wins.
-__device__ int puct_select(const Dev& E, int g, int id, uint64_t own, uint64_t opp, int cs) {
+template <class R>
+__device__ int puct_select(const Dev& E, int g, int id, const typename R::VCtx& vc) {
     const int lane = lane_id();
-    const size_t row = node_row(E, g, id);
+    const size_t row = node_row<R>(E, g, id);
     const int Ns = E.node_Ns[(size_t)g * E.M + id];
     const float sq_edge = (float)sqrt((double)Ns);
     const float sq_new = (float)sqrt((double)Ns + 1e-8);
     float best = -INFINITY;
     int besta = 0x7fffffff;
 #pragma unroll
-    for (int j = 0; j < AJ; ++j) {
+    for (int j = 0; j < R::AJ; ++j) {
         const int a = lane + WAVE * j;
-        if (a < A && action_valid(a, own, opp, cs)) {
+        if (a < R::A && R::valid(a, vc)) {
             const float cp = E.cpuct_f * E.node_P[row + a];
             const uint32_t nr = E.node_N[row + a];
             const int n = (int)(nr & 0x7fffffffu);
@@ -389,21 +551,18 @@ __device__ __forceinline__ void set_err(const Dev& E, int g, int code) {
 // --------------------------------------------------------------- kernels
 // sim_begin: MCTS.search down to a leaf (MCTS.py:83-132), writing the leaf's
 // randomly symmetrised planes (MCTS.py:91-92) as f32 into the NN batch.
+template <class R>
 __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__ planes) {
     __shared__ uint32_t s_mt[MT_N];
     const int g = blockIdx.x, lane = lane_id();
-    float* out = planes + (size_t)g * 4 * CELLS;
+    float* out = planes + (size_t)g * R::PLANES * R::CELLS;
     if (!E.active[g] || E.err[g]) {
-        for (int i = lane; i < 4 * CELLS; i += WAVE) out[i] = 0.0f;
+        for (int i = lane; i < R::PLANES * R::CELLS; i += WAVE) out[i] = 0.0f;
         if (lane == 0) E.leaf_kind[g] = LEAF_NONE;
         return;
     }
-    Pos p;
-    p.cell = lane < CELLS ? (int)E.board[(size_t)g * 64 + lane] : 0;
-    p.turn = E.turn[g];
-    p.player = E.player[g];
-    p.outcome = E.outcome[g];
-    int depth = 0, kind = LEAF_NONE, slot = -1, cs = 0;
+    Pos p = load_root<R>(E, g);
+    int depth = 0, kind = LEAF_NONE, slot = -1, cs = 0, kt = 0;
     uint64_t own = 0, opp = 0;
     double tval = 0.0;
     int32_t* path = E.path + (size_t)g * E.DMAX;
@@ -413,14 +572,14 @@ __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__
             tval = -outcome_value(p.outcome);
             break;
         }
-        pos_key(p, own, opp, cs);
-        const int id = table_lookup(E, g, own, opp, p.turn, cs, &slot);
+        R::key(p, own, opp, kt, cs);
+        const int id = table_lookup(E, g, own, opp, kt, cs, &slot);
         if (id < 0) {
             if (slot < 0) set_err(E, g, -3);
             kind = slot < 0 ? LEAF_NONE : LEAF_EXPAND;
             break;
         }
-        const int a = puct_select(E, g, id, own, opp, cs);
+        const int a = puct_select<R>(E, g, id, R::vctx(own, opp, cs));
         if (a < 0) {
             set_err(E, g, -5);
             kind = LEAF_NONE;
@@ -433,7 +592,7 @@ __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__
         }
         if (lane == 0) path[depth] = (id << 10) | a;
         depth++;
-        pos_apply(p, a, E.max_turns);
+        R::apply(p, a, E.max_turns);
     }
     if (lane == 0) {
         E.leaf_kind[g] = kind;
@@ -441,57 +600,49 @@ __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__
         E.leaf_value[g] = tval;
         E.leaf_own[g] = own;
         E.leaf_opp[g] = opp;
-        E.leaf_turn[g] = p.turn;
+        E.leaf_turn[g] = kt;
         E.leaf_cs[g] = cs;
         E.leaf_slot[g] = slot;
         if (depth > E.st_depth[g]) E.st_depth[g] = depth;
         E.st_sims[g] += 1;
     }
     if (kind != LEAF_EXPAND) {
-        for (int i = lane; i < 4 * CELLS; i += WAVE) out[i] = 0.0f;
+        for (int i = lane; i < R::PLANES * R::CELLS; i += WAVE) out[i] = 0.0f;
         return;
     }
-    // random_symmetry: randint(0,6), randint(0,n), choice(['r','q','s'])  (InflexionGame.py:120-121)
-    BlockRng R{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
-    const int k = rng_randint(R, 0, 6);
-    const int shift = rng_randint(R, 0, N);
-    const int axis = rng_randint(R, 0, 3);
-    rng_store(R);
-    if (lane < CELLS) {
-        const int src = sym_src(lane, k, shift, axis);
-        out[lane] = (float)((own >> src) & 1ull);
-        out[CELLS + lane] = (float)((opp >> src) & 1ull);
-        out[2 * CELLS + lane] = (float)p.turn;
-        out[3 * CELLS + lane] = (float)cs;
-    }
+    BlockRng rg{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
+    R::write_planes(out, own, opp, kt, cs, rg);
+    rng_store(rg);
 }
 
 // Test evaluator: tests/golden/stubnet.py on the symmetrised planes.
+template <class R>
 __global__ __launch_bounds__(WAVE) void stub_eval_kernel(const float* __restrict__ planes, float* __restrict__ P,
-                                                         float* __restrict__ v, int G) {
+                                                         float* __restrict__ v) {
     const int g = blockIdx.x, lane = lane_id();
-    const float* in = planes + (size_t)g * 4 * CELLS;
-    const bool on = lane < CELLS;
+    const float* in = planes + (size_t)g * R::PLANES * R::CELLS;
+    const bool on = lane < R::CELLS;
     const uint64_t own = __ballot(on && in[lane] != 0.0f);
-    const uint64_t opp = __ballot(on && in[CELLS + lane] != 0.0f);
-    const uint64_t t = (uint64_t)(int64_t)(int)in[2 * CELLS];
-    const uint64_t kk = (uint64_t)(int64_t)(int)in[3 * CELLS];
+    const uint64_t opp = __ballot(on && in[R::CELLS + lane] != 0.0f);
+    const uint64_t t = R::PLANES > 2 ? (uint64_t)(int64_t)(int)in[2 * R::CELLS] : 0ull;
+    const uint64_t kk = R::PLANES > 3 ? (uint64_t)(int64_t)(int)in[3 * R::CELLS] : 0ull;
     const uint64_t h = mix64(own ^ mix64(opp ^ mix64((t << 1) | kk)));
     const bool all_zero = (h >> 56) < 4;
-    for (int a = lane; a < A; a += WAVE) {
+    for (int a = lane; a < R::A; a += WAVE) {
         const uint64_t ha = mix64(h ^ ((uint64_t)(a + 1) * 0xD1B54A32D192ED03ull));
         const float pa = (float)(uint32_t)(ha & 0xFFFFFFu) * 0x1p-24f;
-        P[(size_t)g * A + a] = (all_zero || (ha >> 59) == 0) ? 0.0f : pa;
+        P[(size_t)g * R::A + a] = (all_zero || (ha >> 59) == 0) ? 0.0f : pa;
     }
     if (lane == 0) v[g] = (float)((int)((h >> 20) & 2047) - 1024) / 1024.0f;
 }
 
 // sim_end: expand the leaf (MCTS.py:89-112) and back the value up the path
-// (MCTS.py:136-145).  The path holds distinct nodes (turn strictly increases
-// down a path), so lanes update one edge each with no atomics.
+// (MCTS.py:136-145).  The path holds distinct nodes, so lanes update one edge
+// each with no atomics.
+template <class R>
 __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float* __restrict__ Pin, int p_stride,
                                                              const float* __restrict__ vin) {
-    __shared__ float s_p[AP];
+    __shared__ float s_p[R::AP];
     __shared__ float s_acc[WAVE];
     __shared__ float s_leaf[16];
     const int g = blockIdx.x, lane = lane_id();
@@ -501,36 +652,36 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
     bool ret_f32;
     if (kind == LEAF_EXPAND) {
         const uint64_t own = E.leaf_own[g], opp = E.leaf_opp[g];
-        const int cs = E.leaf_cs[g], turn = E.leaf_turn[g];
-        float pv[AJ];
-        bool vv[AJ];
+        const int cs = E.leaf_cs[g], kt = E.leaf_turn[g];
+        const typename R::VCtx vc = R::vctx(own, opp, cs);
+        float pv[R::AJ];
+        bool vv[R::AJ];
 #pragma unroll
-        for (int j = 0; j < AJ; ++j) {
+        for (int j = 0; j < R::AJ; ++j) {
             const int a = lane + WAVE * j;
-            vv[j] = a < A && action_valid(a, own, opp, cs);
-            float x = a < A ? Pin[(size_t)g * p_stride + a] : 0.0f;
+            vv[j] = a < R::A && R::valid(a, vc);
+            float x = a < R::A ? Pin[(size_t)g * p_stride + a] : 0.0f;
             x = vv[j] ? x : x * 0.0f;  // policies *= valids
             pv[j] = x;
             s_p[a] = x;
         }
         __syncthreads();
-        const float sum = pairwise_sum(s_p, s_acc, s_leaf);
+        const float sum = pairwise_sum<R::A>(s_p, s_acc, s_leaf);
         if (sum > 0.0f) {
 #pragma unroll
-            for (int j = 0; j < AJ; ++j) pv[j] = pv[j] / sum;
+            for (int j = 0; j < R::AJ; ++j) pv[j] = pv[j] / sum;
         } else {  // MCTS.py:100-107 fallback: policies += valids; policies /= policies.sum()
             if (lane == 0) E.st_fallback[g] += 1;
 #pragma unroll
-            for (int j = 0; j < AJ; ++j) {
+            for (int j = 0; j < R::AJ; ++j) {
                 pv[j] = (float)((double)pv[j] + (vv[j] ? 1.0 : 0.0));
                 s_p[lane + WAVE * j] = pv[j];
             }
             __syncthreads();
-            const float s2 = pairwise_sum(s_p, s_acc, s_leaf);
+            const float s2 = pairwise_sum<R::A>(s_p, s_acc, s_leaf);
 #pragma unroll
-            for (int j = 0; j < AJ; ++j) pv[j] = pv[j] / s2;
+            for (int j = 0; j < R::AJ; ++j) pv[j] = pv[j] / s2;
         }
-        // allocate a node from the slot's free stack
         int id = -1;
         if (lane == 0) {
             const int top = E.free_top[g];
@@ -547,21 +698,21 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
             set_err(E, g, -3);
             return;
         }
-        const size_t ni = (size_t)g * E.M + id, row = ni * AP;
+        const size_t ni = (size_t)g * E.M + id, row = ni * R::AP;
 #pragma unroll
-        for (int j = 0; j < AJ; ++j) {
+        for (int j = 0; j < R::AJ; ++j) {
             const int a = lane + WAVE * j;
-            E.node_P[row + a] = a < A ? pv[j] : 0.0f;
+            E.node_P[row + a] = a < R::A ? pv[j] : 0.0f;
             E.node_N[row + a] = 0u;
             E.node_Q[row + a] = 0.0;
         }
         if (lane == 0) {
             E.node_own[ni] = own;
             E.node_opp[ni] = opp;
-            E.node_turn[ni] = turn;
+            E.node_turn[ni] = kt;
             E.node_cs[ni] = cs;
             E.node_Ns[ni] = 0;
-            const uint64_t h = key_hash(own, opp, turn, cs);
+            const uint64_t h = key_hash(own, opp, kt, cs);
             E.table[(size_t)g * E.H + E.leaf_slot[g]] = ((h >> 32) << 32) | (uint64_t)(uint32_t)(id + 1);
             E.st_exp[g] += 1;
         }
@@ -578,7 +729,7 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
         const int packed = path[d];
         const int id = packed >> 10, a = packed & 1023;
         const double v = ((depth - 1 - d) & 1) ? -ret : ret;
-        const size_t ni = (size_t)g * E.M + id, row = ni * AP + a;
+        const size_t ni = (size_t)g * E.M + id, row = ni * R::AP + a;
         const uint32_t nr = E.node_N[row];
         const int n = (int)(nr & 0x7fffffffu);
         const bool qf = (nr >> 31) != 0;
@@ -604,49 +755,45 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
 
 // move_end: MCTS.getActionProb root policy (MCTS.py:48-60), Coach.executeEpisode
 // temperature + np.random.choice + step (Coach.py:68-84), record, node GC.
+template <class R>
 __global__ __launch_bounds__(WAVE) void move_end_kernel(Dev E) {
     __shared__ uint32_t s_mt[MT_N];
-    __shared__ int s_cnt[AP];
-    __shared__ double s_cdf[AP];
+    __shared__ int s_cnt[R::AP];
+    __shared__ double s_cdf[R::AP];
     const int g = blockIdx.x, lane = lane_id();
     if (!E.active[g] || E.err[g]) return;
-    Pos p;
-    p.cell = lane < CELLS ? (int)E.board[(size_t)g * 64 + lane] : 0;
-    p.turn = E.turn[g];
-    p.player = E.player[g];
-    p.outcome = E.outcome[g];
+    Pos p = load_root<R>(E, g);
     uint64_t own, opp;
-    int cs, slot;
-    pos_key(p, own, opp, cs);
-    const int id = table_lookup(E, g, own, opp, p.turn, cs, &slot);
-    int cnt[AJ];
+    int cs, kt, slot;
+    R::key(p, own, opp, kt, cs);
+    const int id = table_lookup(E, g, own, opp, kt, cs, &slot);
+    int cnt[R::AJ];
 #pragma unroll
-    for (int j = 0; j < AJ; ++j) {
+    for (int j = 0; j < R::AJ; ++j) {
         const int a = lane + WAVE * j;
-        cnt[j] = (id >= 0 && a < A) ? (int)(E.node_N[node_row(E, g, id) + a] & 0x7fffffffu) : 0;
+        cnt[j] = (id >= 0 && a < R::A) ? (int)(E.node_N[node_row<R>(E, g, id) + a] & 0x7fffffffu) : 0;
         s_cnt[a] = cnt[j];
     }
     const int m = E.moves[g];
     const int temp = (m + 1) < E.temp_threshold;  // episodeStep < tempThreshold
-    BlockRng R{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
+    BlockRng rg{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
     int action = -1;
     if (temp == 0) {
         int mx = cnt[0];
 #pragma unroll
-        for (int j = 1; j < AJ; ++j) mx = max(mx, cnt[j]);
+        for (int j = 1; j < R::AJ; ++j) mx = max(mx, cnt[j]);
         mx = wave_max(mx);
-        uint64_t tie[AJ];
+        uint64_t tie[R::AJ];
         int nb = 0;
 #pragma unroll
-        for (int j = 0; j < AJ; ++j) {
+        for (int j = 0; j < R::AJ; ++j) {
             const int a = lane + WAVE * j;
-            tie[j] = __ballot(a < A && cnt[j] == mx);
+            tie[j] = __ballot(a < R::A && cnt[j] == mx);
             nb += __popcll(tie[j]);
         }
-        int pick = rng_randint(R, 0, nb);  // np.random.choice(bestAs), draws only if nb > 1
-        // pick-th tied action in ascending order (chunk j holds actions 64j..64j+63)
+        int pick = rng_randint(rg, 0, nb);  // np.random.choice(bestAs), draws only if nb > 1
 #pragma unroll
-        for (int j = 0; j < AJ; ++j) {
+        for (int j = 0; j < R::AJ; ++j) {
             const int c = __popcll(tie[j]);
             if (action < 0 && pick < c) {
                 uint64_t b = tie[j];
@@ -655,52 +802,52 @@ __global__ __launch_bounds__(WAVE) void move_end_kernel(Dev E) {
             }
             if (action < 0) pick -= c;
         }
-        (void)rng_random_sample(R);  // np.random.choice(len(pi), p=one-hot) still draws
+        (void)rng_random_sample(rg);  // np.random.choice(len(pi), p=one-hot) still draws
     } else {
         __syncthreads();
         if (lane == 0) {  // probs = counts / counts.sum(); cdf = cumsum (sequential f64)
             long long tot = 0;
-            for (int a = 0; a < A; ++a) tot += s_cnt[a];
+            for (int a = 0; a < R::A; ++a) tot += s_cnt[a];
             double acc = 0.0;
-            for (int a = 0; a < A; ++a) {
+            for (int a = 0; a < R::A; ++a) {
                 acc += (double)s_cnt[a] / (double)tot;
                 s_cdf[a] = acc;
             }
         }
         __syncthreads();
-        const double last = s_cdf[A - 1];
-        const double u = rng_random_sample(R);
+        const double last = s_cdf[R::A - 1];
+        const double u = rng_random_sample(rg);
         int first = 0x7fffffff;
 #pragma unroll
-        for (int j = 0; j < AJ; ++j) {
+        for (int j = 0; j < R::AJ; ++j) {
             const int a = lane + WAVE * j;
-            if (a < A && s_cdf[a] / last > u) first = min(first, a);
+            if (a < R::A && s_cdf[a] / last > u) first = min(first, a);
         }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) first = min(first, __shfl_xor(first, o));
-        action = first == 0x7fffffff ? A : first;
+        action = first == 0x7fffffff ? R::A : first;
     }
-    rng_store(R);
+    rng_store(rg);
     if (m < E.max_moves) {
         if (lane == 0) {
             E.rec_action[(size_t)g * E.max_moves + m] = action;
             E.rec_temp[(size_t)g * E.max_moves + m] = (int8_t)temp;
         }
         if (E.rec_counts) {
-            int32_t* rc = E.rec_counts + ((size_t)g * E.max_moves + m) * A;
+            int32_t* rc = E.rec_counts + ((size_t)g * E.max_moves + m) * R::A;
 #pragma unroll
-            for (int j = 0; j < AJ; ++j) {
+            for (int j = 0; j < R::AJ; ++j) {
                 const int a = lane + WAVE * j;
-                if (a < A) rc[a] = cnt[j];
+                if (a < R::A) rc[a] = cnt[j];
             }
         }
     }
-    if (action < 0 || action >= A || !action_valid(action, own, opp, cs)) {
+    if (action < 0 || action >= R::A || !R::valid(action, R::vctx(own, opp, cs))) {
         set_err(E, g, -5);
         return;
     }
-    pos_apply(p, action, E.max_turns);
-    if (lane < CELLS) E.board[(size_t)g * 64 + lane] = (int8_t)p.cell;
+    R::apply(p, action, E.max_turns);
+    if (lane < R::CELLS) E.board[(size_t)g * 64 + lane] = (int8_t)p.cell;
     if (lane == 0) {
         E.turn[g] = p.turn;
         E.player[g] = p.player;
@@ -709,10 +856,14 @@ __global__ __launch_bounds__(WAVE) void move_end_kernel(Dev E) {
         if (p.outcome != ONGOING) E.active[g] = 0;
     }
     if (!(E.flags & 1)) return;  // AZG_FLAG_GC
-    // Node GC: a search from a root at turn T only reaches keys with turn >= T
-    // (the key contains the turn), so nodes below T are dead; keep all others
+    // Node GC: a search from a root whose key-turn is T only reaches key-turns
+    // >= T (Inflexion: the turn, in the key; Othello: the disc count, which
+    // never decreases), so nodes below T are dead; keep all others
     // (transpositions may still reach them).  Finished game: free everything.
-    const int T = p.outcome != ONGOING ? 0x7fffffff : p.turn;
+    uint64_t o2, p2;
+    int cs2, T;
+    R::key(p, o2, p2, T, cs2);
+    if (p.outcome != ONGOING) T = 0x7fffffff;
     const size_t nb0 = (size_t)g * E.M;
     int top = 0, live = 0;
     for (int b = 0; b < E.M; b += WAVE) {
@@ -753,25 +904,24 @@ __global__ __launch_bounds__(WAVE) void move_end_kernel(Dev E) {
 }
 
 // Root visit counts of one slot (drop-in MCTS.getActionProb, MCTS.py:48-49).
+template <class R>
 __global__ __launch_bounds__(WAVE) void root_counts_kernel(Dev E, int g, int32_t* out) {
     const int lane = lane_id();
-    Pos p;
-    p.cell = lane < CELLS ? (int)E.board[(size_t)g * 64 + lane] : 0;
-    p.turn = E.turn[g];
-    p.player = E.player[g];
-    p.outcome = E.outcome[g];
+    Pos p = load_root<R>(E, g);
     uint64_t own, opp;
-    int cs, slot;
-    pos_key(p, own, opp, cs);
-    const int id = table_lookup(E, g, own, opp, p.turn, cs, &slot);
-    for (int a = lane; a < A; a += WAVE) out[a] = id >= 0 ? (int)(E.node_N[node_row(E, g, id) + a] & 0x7fffffffu) : 0;
+    int cs, kt, slot;
+    R::key(p, own, opp, kt, cs);
+    const int id = table_lookup(E, g, own, opp, kt, cs, &slot);
+    for (int a = lane; a < R::A; a += WAVE)
+        out[a] = id >= 0 ? (int)(E.node_N[node_row<R>(E, g, id) + a] & 0x7fffffffu) : 0;
 }
 
-// Fresh games in every slot (Coach.py:110-111): empty board, RED to move,
+// Fresh games in every slot (Coach.py:110-111): initial board, RED to move,
 // numpy RandomState(seed) per slot, empty tree.
+template <class R>
 __global__ __launch_bounds__(WAVE) void reset_kernel(Dev E, uint32_t seed_base, long long first_game) {
     const int g = blockIdx.x, lane = lane_id();
-    E.board[(size_t)g * 64 + lane] = 0;
+    E.board[(size_t)g * 64 + lane] = lane < R::CELLS ? (int8_t)R::initial_cell(lane) : (int8_t)0;
     if (lane == 0) {
         E.turn[g] = 0;
         E.player[g] = 1;
@@ -826,45 +976,94 @@ __global__ __launch_bounds__(256) void summary_kernel(Dev E, int32_t* out) {
 }
 
 __global__ __launch_bounds__(256) void stats_kernel(Dev E, long long* out) {
-    if (threadIdx.x != 0) return;
-    long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int g = 0; g < E.G; ++g) {
-        s[0] += E.st_exp[g];
-        s[1] += E.st_term[g];
-        s[2] += E.st_fallback[g];
-        s[3] = s[3] > E.st_depth[g] ? s[3] : E.st_depth[g];
-        s[4] = s[4] > E.st_live_max[g] ? s[4] : E.st_live_max[g];
-        if (!s[5] && E.err[g]) s[5] = E.err[g];
-        s[6] += E.st_sims[g];
+    __shared__ long long s[256][8];
+    long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int g = threadIdx.x; g < E.G; g += blockDim.x) {
+        v[0] += E.st_exp[g];
+        v[1] += E.st_term[g];
+        v[2] += E.st_fallback[g];
+        v[3] = max(v[3], (long long)E.st_depth[g]);
+        v[4] = max(v[4], (long long)E.st_live_max[g]);
+        if (!v[5] && E.err[g]) v[5] = E.err[g];
+        v[6] += E.st_sims[g];
     }
-    for (int i = 0; i < 8; ++i) out[i] = s[i];
+    for (int i = 0; i < 8; ++i) s[threadIdx.x][i] = v[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int t = 1; t < (int)blockDim.x; ++t) {
+            v[0] += s[t][0];
+            v[1] += s[t][1];
+            v[2] += s[t][2];
+            v[3] = max(v[3], s[t][3]);
+            v[4] = max(v[4], s[t][4]);
+            if (!v[5]) v[5] = s[t][5];
+            v[6] += s[t][6];
+        }
+        for (int i = 0; i < 8; ++i) out[i] = v[i];
+    }
 }
 
 // ------------------------------------------------------------- launchers
-hipError_t launch_select(const Dev& E, float* planes, hipStream_t st) {
-    hipLaunchKernelGGL(select_kernel, dim3(E.G), dim3(WAVE), 0, st, E, planes);
-    return hipGetLastError();
+template <class R>
+struct Impl {
+    static hipError_t select(const Dev& E, float* planes, hipStream_t st) {
+        hipLaunchKernelGGL(select_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, planes);
+        return hipGetLastError();
+    }
+    static hipError_t stub_eval(const Dev& E, const float* planes, float* P, float* v, hipStream_t st) {
+        hipLaunchKernelGGL(stub_eval_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, planes, P, v);
+        return hipGetLastError();
+    }
+    static hipError_t expand_backup(const Dev& E, const float* P, int p_stride, const float* v, hipStream_t st) {
+        hipLaunchKernelGGL(expand_backup_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, P, p_stride, v);
+        return hipGetLastError();
+    }
+    static hipError_t move_end(const Dev& E, hipStream_t st) {
+        hipLaunchKernelGGL(move_end_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E);
+        return hipGetLastError();
+    }
+    static hipError_t root_counts(const Dev& E, int g, int32_t* out, hipStream_t st) {
+        hipLaunchKernelGGL(root_counts_kernel<R>, dim3(1), dim3(WAVE), 0, st, E, g, out);
+        return hipGetLastError();
+    }
+    static hipError_t reset(const Dev& E, uint32_t seed_base, long long first_game, hipStream_t st) {
+        hipLaunchKernelGGL(reset_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, seed_base, first_game);
+        return hipGetLastError();
+    }
+};
+
+template <class R>
+static GameOps make_ops() {
+    GameOps o;
+    o.cells = R::CELLS;
+    o.actions = R::A;
+    o.row = R::AP;
+    o.planes = R::PLANES;
+    o.select = &Impl<R>::select;
+    o.stub_eval = &Impl<R>::stub_eval;
+    o.expand_backup = &Impl<R>::expand_backup;
+    o.move_end = &Impl<R>::move_end;
+    o.root_counts = &Impl<R>::root_counts;
+    o.reset = &Impl<R>::reset;
+    return o;
 }
-hipError_t launch_stub_eval(const Dev& E, const float* planes, float* P, float* v, hipStream_t st) {
-    hipLaunchKernelGGL(stub_eval_kernel, dim3(E.G), dim3(WAVE), 0, st, planes, P, v, E.G);
-    return hipGetLastError();
+
+bool game_ops(int kind, int n, GameOps* out) {
+    if (kind == 1 && n == 7) {
+        *out = make_ops<Inflexion>();
+        return true;
+    }
+    if (kind == 2 && n == 6) {
+        *out = make_ops<Othello<6>>();
+        return true;
+    }
+    if (kind == 2 && n == 8) {
+        *out = make_ops<Othello<8>>();
+        return true;
+    }
+    return false;
 }
-hipError_t launch_expand_backup(const Dev& E, const float* P, int p_stride, const float* v, hipStream_t st) {
-    hipLaunchKernelGGL(expand_backup_kernel, dim3(E.G), dim3(WAVE), 0, st, E, P, p_stride, v);
-    return hipGetLastError();
-}
-hipError_t launch_move_end(const Dev& E, hipStream_t st) {
-    hipLaunchKernelGGL(move_end_kernel, dim3(E.G), dim3(WAVE), 0, st, E);
-    return hipGetLastError();
-}
-hipError_t launch_root_counts(const Dev& E, int g, int32_t* out, hipStream_t st) {
-    hipLaunchKernelGGL(root_counts_kernel, dim3(1), dim3(WAVE), 0, st, E, g, out);
-    return hipGetLastError();
-}
-hipError_t launch_reset(const Dev& E, uint32_t seed_base, long long first_game, hipStream_t st) {
-    hipLaunchKernelGGL(reset_kernel, dim3(E.G), dim3(WAVE), 0, st, E, seed_base, first_game);
-    return hipGetLastError();
-}
+
 hipError_t launch_summary(const Dev& E, int32_t* out, hipStream_t st) {
     hipLaunchKernelGGL(summary_kernel, dim3(1), dim3(256), 0, st, E, out);
     return hipGetLastError();

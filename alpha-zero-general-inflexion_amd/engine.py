@@ -27,8 +27,18 @@ import torch
 from . import _lib
 from ._lib import check
 
-A = 343
+A = 343  # InflexionGame(7) actions (the default game)
 CELLS = 49
+
+# game -> (kind code, planes per cell, actions(n))
+GAMES = {"inflexion": (_lib.GAME_INFLEXION, 4, lambda n: 7 * n * n),
+         "othello": (_lib.GAME_OTHELLO, 2, lambda n: n * n + 1)}
+
+
+def game_spec(game):
+    """(name, n, max_turns) of a Game plugin instance (duck-typed)."""
+    name = "othello" if "othello" in type(game).__name__.lower() else "inflexion"
+    return name, int(game._n), int(getattr(game, "_max_turns", 0) or 0)
 
 
 def _ptr(t):
@@ -38,19 +48,26 @@ def _ptr(t):
 class SelfPlayEngine:
     def __init__(self, num_games, *, sims=25, cpuct=1, temp_threshold=30, max_turns=343, seed_base=0,
                  first_game=0, evaluator="stub", device=None, node_capacity=0, max_depth=0, record=True,
-                 gc=True, max_moves=0):
+                 gc=True, max_moves=0, game="inflexion", n=None):
         if not torch.cuda.is_available():
             raise _lib.AzgError("SelfPlayEngine needs a HIP device (no CPU fallback)")
+        if game not in GAMES:
+            raise ValueError(f"unknown game {game!r}")
+        kind, nplanes, actions = GAMES[game]
+        n = int(n) if n is not None else (7 if game == "inflexion" else 8)
+        self.game, self.n, self.A, self.cells, self.nplanes = game, n, actions(n), n * n, nplanes
+        if game == "othello" and max_turns == 343:
+            max_turns = 2 * n * n  # no turn limit in Othello; bounds the move records
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.G = int(num_games)
         self.sims = int(sims)
         self.evaluator = evaluator
         self.L = _lib.lib()
         with torch.cuda.device(self.device):
-            self.planes = torch.zeros((self.G, 4, 7, 7), dtype=torch.float32, device=self.device)
-            self.P = torch.zeros((self.G, A), dtype=torch.float32, device=self.device)
+            self.planes = torch.zeros((self.G, nplanes, n, n), dtype=torch.float32, device=self.device)
+            self.P = torch.zeros((self.G, self.A), dtype=torch.float32, device=self.device)
             self.v = torch.zeros((self.G,), dtype=torch.float32, device=self.device)
-            cfg = _lib.Config(game_kind=_lib.GAME_INFLEXION, n=7, max_turns=int(max_turns), num_games=self.G,
+            cfg = _lib.Config(game_kind=kind, n=n, max_turns=int(max_turns), num_games=self.G,
                               sims=self.sims, temp_threshold=int(temp_threshold), cpuct=float(cpuct),
                               seed_base=int(seed_base) & 0xFFFFFFFF, pad0=0, first_game=int(first_game),
                               node_capacity=int(node_capacity), max_depth=int(max_depth),
@@ -95,7 +112,7 @@ class SelfPlayEngine:
             else:  # log_softmax output: predict returns exp(pi) (NNet.py:94)
                 P = torch.exp(out_pi)
             v = out_v.reshape(-1)
-        if P.dtype != torch.float32 or P.stride(1) != 1 or P.shape != (self.G, A):
+        if P.dtype != torch.float32 or P.stride(1) != 1 or P.shape != (self.G, self.A):
             P = P.float().contiguous()
         if v.dtype != torch.float32 or not v.is_contiguous():
             v = v.float().contiguous()
@@ -162,7 +179,7 @@ class SelfPlayEngine:
         actions = np.zeros((G, MM), np.int32)
         temps = np.zeros((G, MM), np.int8)
         moves = np.zeros(G, np.int32)
-        cnt = np.zeros((G, MM, A), np.int32) if (counts and self.record) else None
+        cnt = np.zeros((G, MM, self.A), np.int32) if (counts and self.record) else None
         check(self.L.azg_read_moves(self.h, actions.ctypes.data, temps.ctypes.data,
                                     cnt.ctypes.data if cnt is not None else None, moves.ctypes.data,
                                     self._stream()))
@@ -170,7 +187,7 @@ class SelfPlayEngine:
 
     def state(self):
         G = self.G
-        boards = np.zeros((G, CELLS), np.int8)
+        boards = np.zeros((G, self.cells), np.int8)
         turns, players, outcomes, active = (np.zeros(G, np.int32) for _ in range(4))
         check(self.L.azg_get_state(self.h, boards.ctypes.data, turns.ctypes.data, players.ctypes.data,
                                    outcomes.ctypes.data, active.ctypes.data, self._stream()))
@@ -198,6 +215,6 @@ class SelfPlayEngine:
         check(self.L.azg_set_rng(self.h, int(slot), mt.ctypes.data, int(pos), self._stream()))
 
     def root_counts(self, slot):
-        c = np.zeros(A, np.int32)
+        c = np.zeros(self.A, np.int32)
         check(self.L.azg_root_counts(self.h, int(slot), c.ctypes.data, self._stream()))
         return c

@@ -18,7 +18,7 @@ the GPU, batched), a torch module returning (log_softmax, tanh), or the string
 import numpy as np
 import torch
 
-from .engine import SelfPlayEngine
+from .engine import SelfPlayEngine, game_spec
 from .flags import GameOutcome
 
 
@@ -50,15 +50,17 @@ class MCTS:
         self._max_turns = None
 
     def _engine_for(self, game):
-        if self._engine is None or self._max_turns != game._max_turns:
+        spec = game_spec(game)
+        if self._engine is None or self._max_turns != spec:
             if self._engine is not None:
                 self._engine.close()
+            name, n, max_turns = spec
             self._engine = SelfPlayEngine(1, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct,
-                                          temp_threshold=1, max_turns=int(game._max_turns),
+                                          temp_threshold=1, max_turns=max_turns, game=name, n=n,
                                           evaluator=_evaluator_of(self.nnet, self.device), device=self.device,
                                           node_capacity=self.node_capacity, max_depth=1024, gc=False,
                                           record=False)
-            self._max_turns = game._max_turns
+            self._max_turns = spec
         return self._engine
 
     def _run(self, game, sims):

@@ -83,3 +83,50 @@ def test_random_seeds_vs_oracle(azg):
         assert rec["moves"][i] == m
         assert np.array_equal(rec["actions"][i, :m], o["actions"])
         assert np.array_equal(rec["counts"][i, :m], o["counts"])
+
+
+@pytest.mark.parametrize("name", ["othello6", "othello8", "othello8_s200"])
+def test_othello_golden_traces_bit_exact(azg, name):
+    """Othello (builder-authored plugin) searched on the GPU vs the reference
+    MCTS/Coach driven with the same plugin: bit-exact counts and actions."""
+    data = ol.load_json(f"mcts_{name}.json.gz")
+    cfg, eps = data["config"], data["episodes"]
+    n, A = cfg["n"], cfg["n"] * cfg["n"] + 1
+    seeds = [ep["seed"] for ep in eps]
+    e = azg.SelfPlayEngine(len(seeds), sims=cfg["sims"], cpuct=cfg["cpuct"], temp_threshold=cfg["temp_threshold"],
+                           game="othello", n=n, first_game=seeds[0], evaluator="stub",
+                           node_capacity=16 * cfg["sims"] + 128)
+    e.play()
+    rec, st, state = e.read_moves(), e.stats(), e.state()
+    assert st["error"] == 0
+    for i, ep in enumerate(eps):
+        assert rec["moves"][i] == ep["n_moves"], ep["seed"]
+        for m, mv in enumerate(ep["moves"]):
+            assert np.array_equal(rec["counts"][i, m], ol.golden_counts(mv, A)), (ep["seed"], m)
+            assert rec["actions"][i, m] == mv["action"]
+        assert state["boards"][i].tolist() == ep["final_board"]
+        assert ol.OUTCOME_VALUE[int(state["outcomes"][i])] == ep["final_outcome"]
+    assert st["expansions"] == sum(ep["expansions"] for ep in eps)
+
+
+def test_othello_dropin_matches_reference():
+    import hashlib
+    import azg_amd  # noqa: F401
+    from azg_amd.coach import Coach
+    from azg_amd.mcts import MCTS
+    from azg_amd.othello import OthelloGame
+
+    class Args(dict):
+        __getattr__ = dict.__getitem__
+
+    data = ol.load_json("mcts_othello6.json.gz")
+    cfg = data["config"]
+    args = Args(numMCTSSims=cfg["sims"], cpuct=cfg["cpuct"], tempThreshold=cfg["temp_threshold"])
+    for ep in data["episodes"][:4]:
+        game = OthelloGame(cfg["n"])
+        np.random.seed(ep["seed"])
+        ex = Coach(game, "stub", args).executeEpisode((game.restarted(), MCTS("stub", args)))
+        assert len(ex) == ep["n_examples"]
+        pol = hashlib.sha256(np.array([e[1] for e in ex], np.float64).tobytes()).hexdigest()
+        brd = hashlib.sha256(np.array([e[0] for e in ex], np.int64).tobytes()).hexdigest()
+        assert pol == ep["policy_sha256"] and brd == ep["board_sha256"]

@@ -120,3 +120,17 @@ def test_oracle_othello_episodes_match_reference_search(name):
         assert got["expansions"] == ep["expansions"] and got["nodes"] == ep["nodes"]
         assert got["rng_pos"] == ep["rng_pos"] and got["rng_next"] == ep["rng_next"]
         assert ol.OUTCOME_VALUE[got["final_outcome"]] == ep["final_outcome"]
+
+
+def test_othello_examples_from_records_match_reference():
+    import hashlib
+    import oracle_lib as ol
+    from azg_amd.coach import examples_from_record
+    data = ol.load_json("mcts_othello6.json.gz")
+    cfg = data["config"]
+    for ep in data["episodes"][:6]:
+        o = ol.episode(cfg["n"], 0, cfg["sims"], cfg["cpuct"], cfg["temp_threshold"], ep["seed"], kind=ol.OTHELLO)
+        ex = examples_from_record(OthelloGame(cfg["n"]), o["actions"], o["temps"], o["counts"], o["moves"])
+        assert len(ex) == ep["n_examples"]
+        assert hashlib.sha256(np.array([e[1] for e in ex], np.float64).tobytes()).hexdigest() == ep["policy_sha256"]
+        assert hashlib.sha256(np.array([e[0] for e in ex], np.int64).tobytes()).hexdigest() == ep["board_sha256"]
