@@ -1,20 +1,23 @@
 """Self-play throughput of the MI355X engine (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--games G] [--sims S]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1..C5] [--games G] [--sims S]
 
 One *step* = one move of every concurrent game: numMCTSSims simulations
-(select -> leaf-batched InflexionNNet f32 forward -> expand/backup) followed by
-the root-policy / sample / apply kernel -- the reference's
-Coach.executeEpisode loop body (Coach.py:65-84) for G games at once.
-Default workload (north_star / configs[3] per GPU): 7x7 Inflexion,
-max_turns 343, 4096 games per GPU, 25 sims/move, cpuct 1, tempThreshold 30,
-random-init InflexionNNet (torch.manual_seed(0)), f32.
+(select -> leaf-batched network f32 forward -> expand/backup) followed by the
+root-policy / sample / apply kernel -- the reference's Coach.executeEpisode
+loop body (Coach.py:65-84) for G games at once.
 
-`value` = node expansions per second over the whole job (new tree nodes = NN
-leaf evaluations, MCTS.py:89-112; terminal hits excluded), all ranks summed.
-Multi-GPU: one process per GPU (torchrun), games sharded by global index, no
-communication inside self-play; each timed region ends with the per-iteration
-RCCL example gather + weight broadcast (configs[3]).
+Default workload (north_star target, configs[3] per GPU): 7x7 Inflexion,
+max_turns 343, 4096 games per GPU, 25 sims/move, cpuct 1, tempThreshold 30,
+random-init InflexionNNet (torch.manual_seed(0)), f32.  Presets: C1 6x6
+Othello (1 game, 25 sims), C2 Inflexion 256 games x 25, C3 4096 x 100,
+C4 4096/GPU x 25, C5 8x8 Othello 4096/GPU x 200.
+
+`value` = node expansions per second over the whole job (new tree nodes =
+network leaf evaluations, MCTS.py:89-112; terminal hits excluded), all ranks
+summed.  Multi-GPU: one process per GPU (torchrun), games sharded by global
+index, no communication inside self-play; each timed region ends with the
+per-iteration RCCL example gather + weight broadcast (configs[3]).
 """
 import argparse
 import json
@@ -29,33 +32,47 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-FLOP_PER_LEAF = 404.3e6          # 202,143,744 MAC per leaf
 F32_MFMA_PEAK_TF = 157.3         # MI355X_MICROARCH.md: f32 matrix peak (dense)
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E spec peak
-EXPANSIONS_PER_GAME_REF = 8555   # reference random-init episodes
-CONV_FLOP_PER_LEAF = 2 * 512 * 512 * 9 * (49 + 25 + 9)  # conv2 (7x7 out) + conv3 (5x5) + conv4 (3x3)
+EXPANSIONS_PER_GAME_REF = 8555   # reference random-init Inflexion episodes
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_G4096.json")
+
+PRESETS = {
+    "C1": dict(game="othello", n=6, games=1, sims=25),
+    "C2": dict(game="inflexion", n=7, games=256, sims=25),
+    "C3": dict(game="inflexion", n=7, games=4096, sims=100),
+    "C4": dict(game="inflexion", n=7, games=4096, sims=25),
+    "C5": dict(game="othello", n=8, games=4096, sims=200),
+}
 
 
-def tree_bytes_per_sim(A_sel=87.0, d=1.33):
+def net_flops(n, depth, A, c=512):
+    """FLOPs per leaf of InflexionNNet(n, depth, A, c): (whole forward, conv2+conv3+conv4).
+    Inflexion 7x7: 404.3 M / 391.6 M."""
+    conv1 = 2 * depth * c * 9 * n * n
+    conv234 = 2 * c * c * 9 * (n * n + (n - 2) ** 2 + (n - 4) ** 2)
+    fc = 2 * (c * (n - 4) ** 2 * 1024 + 1024 * 512 + 512 * A + 512)
+    return conv1 + conv234 + fc, conv234
+
+
+def tree_bytes_per_sim(row, valid=87.0, d=1.33):
     """Algorithmic HBM bytes of the tree kernels per simulation:
-    select reads P/N/Q (4+4+8 B) of each valid action at d nodes, board/key
-    traffic, leaf planes write, P/v read, node init of the new leaf, backup RMW."""
-    sel = d * (16.0 * A_sel + 32.0)          # P f32 + N u32 + Q f64 per valid action, + Ns/key
-    table = d * 64.0 + 64.0                  # hash probes (one 64-slot line per lookup)
-    leaf = 4 * 49 * 4 + 343 * 4 + 4          # planes write + P/v read
-    node = 384 * 16 + 32                     # new node row (P, N, Q) + key
-    backup = d * 24.0                        # N, Q, Ns read-modify-write
+    select reads P/N/Q (4+4+8 B) of each valid action at d nodes + hash lines,
+    the leaf writes its planes and reads P/v, the new node row (P, N, Q) is
+    initialised, backup read-modify-writes N, Q, Ns."""
+    sel = d * (16.0 * valid + 32.0)
+    table = d * 64.0 + 64.0
+    leaf = 4 * 49 * 4 + 343 * 4 + 4
+    node = row * 16 + 32
+    backup = d * 24.0
     return sel + table + leaf + node + backup
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_G4096.json")
-
-
-def load_pmc(G):
+def load_pmc(G, game):
     """HBM-side bytes per launch from the committed PMC passes (tools/pmc_summary.py:
     rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs, FETCH doubled
-    per the gfx950 correction). Only valid for the workload it was measured on."""
-    if G != 4096 or not os.path.exists(PMC_FILE):
+    per the gfx950 correction).  Only valid for the workload it was measured on."""
+    if G != 4096 or game != "inflexion" or not os.path.exists(PMC_FILE):
         return None
     d = json.load(open(PMC_FILE))
     conv = d["conv2-4 igemm"]["hbm_bytes_sum_over_shapes"]
@@ -70,6 +87,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=4)
     p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--config", choices=sorted(PRESETS), default=None, help="BASELINE.json configs")
+    p.add_argument("--game", choices=["inflexion", "othello"], default="inflexion")
+    p.add_argument("--n", type=int, default=None)
     p.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
     p.add_argument("--sims", type=int, default=25)
     p.add_argument("--max-turns", type=int, default=343)
@@ -83,15 +103,12 @@ def parse():
     p.add_argument("--graph", action="store_true",
                    help="replay each move from a captured HIP graph (roofline fields then come from one extra "
                         "eager move after the timed region)")
-    p.add_argument("--config", choices=["C2", "C3", "C4"], default=None,
-                   help="BASELINE.json presets: C2 256 games x 25 sims, C3 4096 x 100 sims, C4 4096/GPU x 25 sims")
     a = p.parse_args()
-    if a.config == "C2":
-        a.games, a.sims = 256, 25
-    elif a.config == "C3":
-        a.games, a.sims = 4096, 100
-    elif a.config == "C4":
-        a.games, a.sims = 4096, 25
+    if a.config:
+        for k, v in PRESETS[a.config].items():
+            setattr(a, k, v)
+    if a.n is None:
+        a.n = 7 if a.game == "inflexion" else 8
     return a
 
 
@@ -116,17 +133,18 @@ class Timer:
         return sum(s.elapsed_time(e) for s, e in self.pairs)
 
 
-def cpu_baseline(args):
+def cpu_baseline(args, depth, A):
     """Oracle (C restatement of the reference search) + the same f32 network on
-    the host's cores, batch-1 per leaf like NNetWrapper.predict -- the reference
-    CPU path's shape, timed on a bounded sample."""
+    the host's cores, batch-1 per leaf like NNetWrapper.predict -- the
+    reference CPU path's shape -- timed on a bounded sample of the workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as ol
     from azg_amd.nnet import InflexionNNet
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     torch.manual_seed(0)
-    net = InflexionNNet().eval()
+    net = InflexionNNet(n=args.n, depth=depth, action_size=A).eval()
+    kind = ol.OTHELLO if args.game == "othello" else ol.INFLEXION
 
     def evaluator(planes):
         with torch.no_grad():
@@ -134,15 +152,16 @@ def cpu_baseline(args):
         return torch.exp(pi)[0].numpy(), float(v[0, 0])
 
     t = time.perf_counter()
-    o = ol.episode(7, args.max_turns, args.sims, 1, 30, 0, evaluator=evaluator, max_moves=args.cpu_moves)
-    # stop after the sample: oracle episode is capped via max_turns below when needed
+    o = ol.episode(args.n, args.max_turns, args.sims, 1, 30, 0, evaluator=evaluator, max_moves=args.cpu_moves,
+                   kind=kind)
     dt = time.perf_counter() - t
     t2 = time.perf_counter()
-    o2 = ol.episode(7, args.max_turns, args.sims, 1, 30, 0)
+    o2 = ol.episode(args.n, args.max_turns, args.sims, 1, 30, 0, kind=kind)
     dt2 = time.perf_counter() - t2
     return {"value": o["expansions"] / dt, "unit": "node-expansions/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ C MCTS + InflexionNNet f32 batch-1 on CPU, seed 0, max_turns {args.max_turns}, "
-                      f"{o['moves']} moves x {args.sims} sims = {o['expansions']} expansions in {dt:.1f}s",
+            "sample": f"oracle/ C MCTS + InflexionNNet f32 batch-1 on CPU ({threads} threads), {args.game} "
+                      f"{args.n}x{args.n}, seed 0, {o['moves']} moves x {args.sims} sims = {o['expansions']} "
+                      f"expansions in {dt:.1f}s",
             "tree_only_value": o2["expansions"] / dt2,
             "tree_only_sample": f"same search, hash evaluator, 1 thread: {o2['expansions']} expansions in {dt2:.2f}s"}
 
@@ -157,16 +176,19 @@ def main():
     torch.cuda.set_device(local)
 
     import azg_amd
-    from azg_amd.engine import SelfPlayEngine
+    from azg_amd.engine import GAMES, SelfPlayEngine
     from azg_amd.nnet import InflexionNNet, InferenceNet
     from azg_amd import dist as azg_dist
 
+    _, depth, actions = GAMES[args.game]
+    A = actions(args.n)
+    flop_leaf, conv_flop_leaf = net_flops(args.n, depth, A)
     torch.manual_seed(0)
-    net = InflexionNNet().cuda().eval()
+    net = InflexionNNet(n=args.n, depth=depth, action_size=A).cuda().eval()
     ev = (InferenceNet(net) if args.net == "inference" else net) if args.evaluator == "net" else "stub"
     G = args.games
     eng = SelfPlayEngine(G, sims=args.sims, cpuct=1, temp_threshold=30, max_turns=args.max_turns,
-                         seed_base=0, first_game=rank * G, evaluator=ev)
+                         seed_base=0, first_game=rank * G, evaluator=ev, game=args.game, n=args.n)
 
     for _ in range(args.warmup):
         eng.move()
@@ -260,65 +282,70 @@ def main():
 
     if rank == 0:
         value = exp / elapsed
-        n_forwards = n_timed * args.sims
+        n_forwards = max(n_timed * args.sims, 1)
         nn_avg = nn_ms / n_forwards / 1e3
-        leaves = G  # the forward is evaluated on the full [G,4,7,7] batch
-        nn_tflops = leaves * FLOP_PER_LEAF / nn_avg / 1e12
+        leaves = G  # the forward is evaluated on the full [G, planes, n, n] batch
+        nn_tflops = leaves * flop_leaf / nn_avg / 1e12 if nn_avg > 0 else 0.0
         conv_ms = sum(t.total_ms() for t in t_conv.values())
         conv_avg = conv_ms / n_forwards / 1e3 if conv_ms > 0 else nn_avg
-        conv_flops = leaves * (CONV_FLOP_PER_LEAF if conv_ms > 0 else FLOP_PER_LEAF)
-        conv_tflops = conv_flops / conv_avg / 1e12
+        conv_flops = leaves * (conv_flop_leaf if conv_ms > 0 else flop_leaf)
+        conv_tflops = conv_flops / conv_avg / 1e12 if conv_avg > 0 else 0.0
         tree_s = (sel_ms + exp_ms) / 1e3
-        tree_gbs = (exp / world) * tree_bytes_per_sim() / tree_s / 1e9 if tree_s > 0 else 0.0
+        row = ((A + 63) // 64) * 64  # node row stride (actions rounded up to 64 lanes)
+        tree_gbs = (exp / world) * tree_bytes_per_sim(row) / tree_s / 1e9 if tree_s > 0 else 0.0
+        gname = f"{args.n}x{args.n} {'Inflexion' if args.game == 'inflexion' else 'Othello'}"
         out = {
-            "metric": "node-expansions/s (7x7 Inflexion self-play, 25 sims/move); games/s in games_per_s",
+            "metric": f"node-expansions/s ({gname} self-play, {args.sims} sims/move); games/s in games_per_s",
             "value": value,
             "unit": "node-expansions/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": elapsed / max(args.steps, 1) * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: fresh self-play games, random-init InflexionNNet (torch.manual_seed(0))"
-                    if args.evaluator == "net" else "synthetic: hash stub evaluator",
-            "config": {"workload": f"7x7 Inflexion self-play, {G} concurrent games/GPU x {args.sims} sims/move, "
-                                   f"max_turns {args.max_turns}, cpuct 1, tempThreshold 30 (configs[3] per GPU)",
+            "data": f"synthetic: fresh self-play games, random-init InflexionNNet-architecture net "
+                    f"(torch.manual_seed(0))" if args.evaluator == "net" else "synthetic: hash stub evaluator",
+            "config": {"workload": f"{gname} self-play, {G} concurrent games/GPU x {args.sims} sims/move"
+                                   + (f", max_turns {args.max_turns}" if args.game == "inflexion" else "")
+                                   + f", cpuct 1, tempThreshold 30 ({args.config or 'configs[3] per GPU'})",
                        "games_per_gpu": G, "sims_per_move": args.sims, "global_games": G * world,
                        "parallelism": f"games sharded over {world} GPU(s)", "step": "one move of every game"},
-            "games_per_s": (G * world / elapsed) if args.full_games else value / EXPANSIONS_PER_GAME_REF,
+            "games_per_s": (G * world / elapsed) if args.full_games else (
+                value / EXPANSIONS_PER_GAME_REF if args.game == "inflexion" else None),
             "games_per_s_note": (f"measured: {G * world} complete games in {elapsed:.1f}s" if args.full_games else
                                  "expansions/s / 8555 expansions per random-init game (344 moves, measured on the "
                                  "reference); bench.py --full-games measures it directly"),
             "expansions": exp,
             "simulations": sims_run,
             "roofline": {"bound": "mfma",
-                         "kernel": "conv2-4 f32 implicit GEMM (igemm_fwd_gtcx35_nhwc_fp32 + bias) per forward",
+                         "kernel": "conv2-4 f32 implicit GEMM (MIOpen igemm_fwd_gtcx35_nhwc_fp32) per forward",
                          "achieved": conv_tflops, "peak": F32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                          "frac": conv_tflops / F32_MFMA_PEAK_TF, "traffic": None,
-                         "per_launch": f"{leaves} leaves x {CONV_FLOP_PER_LEAF/1e6:.1f} MFLOP / {conv_avg*1e3:.3f} ms "
+                         "per_launch": f"{leaves} leaves x {conv_flop_leaf / 1e6:.1f} MFLOP / {conv_avg * 1e3:.3f} ms "
                                        f"(HIP events around conv2+conv3+conv4)",
                          "forward_tflops": nn_tflops,
-                         "forward_per_launch": f"{leaves} leaves x 404.3 MFLOP / {nn_avg*1e3:.3f} ms (HIP events)"},
+                         "forward_per_launch": f"{leaves} leaves x {flop_leaf / 1e6:.1f} MFLOP / "
+                                               f"{nn_avg * 1e3:.3f} ms (HIP events)"},
             "roofline_tree": {"bound": "hbm", "kernel": "select_kernel + expand_backup_kernel",
                               "achieved": tree_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": tree_gbs / HBM_PEAK_GBS, "traffic": None,
-                              "bytes_per_sim": tree_bytes_per_sim(),
+                              "bytes_per_sim": tree_bytes_per_sim(row),
                               "select_ms_per_sim": sel_ms / n_forwards, "expand_ms_per_sim": exp_ms / n_forwards,
-                              "move_end_ms_per_move": end_ms / n_timed},
+                              "move_end_ms_per_move": end_ms / max(n_timed, 1)},
             "time_split": {"nn_ms": nn_ms, "select_ms": sel_ms, "expand_backup_ms": exp_ms, "move_end_ms": end_ms,
-                           "wall_ms": elapsed * 1e3},
+                           "wall_ms": elapsed * 1e3, "graph": bool(args.graph)},
             "iteration_sync_bytes": sync_bytes,
         }
-        pmc = load_pmc(G)
+        pmc = load_pmc(G, args.game)
         if pmc:
             out["roofline"]["traffic"] = pmc["conv"]
             out["roofline"]["traffic_note"] = pmc["note"]
             out["roofline_tree"]["traffic"] = pmc["tree"]
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args)
+            out["cpu_baseline"] = cpu_baseline(args, depth, A)
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:
