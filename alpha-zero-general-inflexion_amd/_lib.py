@@ -60,6 +60,8 @@ SIGNATURES = [
     ("azg_stats", ctypes.c_int, [_VP, _VP, _VP]),
     ("azg_device_ptrs", ctypes.c_int, [_VP, _VP]),
     ("azg_bias_relu_nhwc", ctypes.c_int, [_VP, _VP, _I64, _I32, _VP]),
+    ("azg_conv3x3_bias_relu_nhwc", ctypes.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
+    ("azg_conv3x3_variant", ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
 ]
 
 _lib = None

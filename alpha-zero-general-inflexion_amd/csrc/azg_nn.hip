@@ -1,9 +1,22 @@
-// azg_nn.hip -- epilogue kernels for the leaf network (NHWC activations).
+// azg_nn.hip -- leaf-network kernels (NHWC activations, f32).
 //
-// The implicit-GEMM convolutions run without a bias; this kernel applies the
-// BatchNorm-folded bias and the ReLU in ONE read-modify-write pass over the
-// NHWC output (instead of a bias pass plus a ReLU pass).  HBM-bound: 8 bytes
-// moved per element, float4 per lane, grid-stride over >= 8 waves per CU.
+//  * bias_relu_nhwc: the BatchNorm-folded bias + ReLU in ONE read-modify-write
+//    pass over an NHWC activation (HBM-bound, float4 per lane, grid-stride).
+//  * conv3x3 implicit GEMM on f32 MFMA with the bias + ReLU fused into the
+//    epilogue (conv2-4 + bn2-4 + relu of InflexionNNet.forward):
+//        y[m, n] = relu(bias[n] + sum_k A[m, k] * W[k, n]),
+//        m = output pixel (b, oy, ox), k = tap * C + c, tap = dy * 3 + dx,
+//        A[m, k] = x[b, oy + dy - pad, ox + dx - pad, c] (0 outside the image),
+//    W pre-transposed to [9*C][N] (k-major).  Per 256-thread workgroup a
+//    128 (pixels) x BN (channels) tile, K in steps of BK; the 4 waves form a
+//    2x2 grid, each owning 64 x BN/2 as (BN/64) x 2 v_mfma_f32_32x32x2_f32
+//    accumulators.  A is gathered with zero padding (unconditional loads from
+//    a zero page), transposed into a k-major LDS image (conflict-free fragment
+//    reads) through registers; B (a plain row copy) goes global -> LDS by
+//    global_load_lds.  Both are double-buffered: stage k+1's loads are issued
+//    before stage k's MFMAs.  The channel tiles of one pixel tile get block ids
+//    that are equal mod 8 (one XCD under round-robin dispatch) so the gathered
+//    pixels are re-read from that XCD's L2 -- a speed choice only.
 #include <hip/hip_runtime.h>
 
 #include "../../include/azg.h"
@@ -22,7 +35,180 @@ __global__ __launch_bounds__(256) void bias_relu_nhwc_kernel(float4* __restrict_
         x[i] = v;
     }
 }
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+constexpr int CBM = 128;
+
+// Zero page for the padding taps: every A load is unconditional (a select
+// between a load and 0 makes hipcc wait for the load right after issuing it).
+__device__ __attribute__((aligned(16))) float g_zero_page[64];
+
+template <int BN, int BK, int MINB>
+__global__ __launch_bounds__(256, MINB) void conv3x3_bias_relu_kernel(
+    const float* __restrict__ x, const float* __restrict__ wt, const float* __restrict__ bias,
+    float* __restrict__ y, int M, int HWo, int Wo, int Hi, int Wi, int pad, int C, int N) {
+    constexpr int STAGE = BK * (CBM + BN);
+    constexpr int TN = BN / 64;              // 32-col MFMA tiles per wave (wave covers BN/2 columns)
+    constexpr int AV = BK / 8;               // float4 of A per thread per stage (2 threads per pixel)
+    constexpr int BI = BK * BN / 256 / 4;    // global_load_lds (1 KB each) per wave per stage
+    constexpr int BROWS = 256 / BN;          // B rows per global_load_lds
+    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int ntn = N / BN;
+    const int grp = blockIdx.x / (8 * ntn), rr = blockIdx.x % (8 * ntn);
+    const int mt = grp * 8 + (rr & 7), nt = rr >> 3;
+    const int m0 = mt * CBM, n0 = nt * BN;
+    if (m0 >= M) return;  // grid rounded up to whole XCD groups
+
+    // A staging: pixel ap (0..127), channel half ah (BK/2 channels each)
+    const int ap = tid >> 1, ah = tid & 1;
+    const int am = m0 + ap;
+    const bool a_ok = am < M;
+    const int amc = a_ok ? am : 0;
+    const int bimg = amc / HWo, rem = amc - bimg * HWo, oy = rem / Wo, ox = rem - (rem / Wo) * Wo;
+    const float* xb = x + (size_t)bimg * Hi * Wi * C + (BK / 2) * ah;
+    // B staging: wave-instruction i of wave w fills rows [(w*BI + i) * BROWS, +BROWS) of [BK][BN]
+    const int brow = (lane * 4) / BN, bcol = (lane * 4) % BN;
+    const float* wb = wt + (size_t)brow * N + n0 + bcol;
+
+    float4 ra[AV];
+    auto load_b = [&](int ks, int buf) {
+        float* Bs = smem + buf * STAGE + BK * CBM;
+        const float* src = wb + (size_t)ks * BK * N;
+#pragma unroll
+        for (int i = 0; i < BI; ++i) {
+            const int r0 = (wid * BI + i) * BROWS;
+            __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)r0 * N), (void*)(Bs + r0 * BN), 16, 0, 0);
+        }
+    };
+    auto load_a = [&](int ks) {
+        const int k0 = ks * BK, tap = k0 / C, c0 = k0 - tap * C;
+        const int dy = tap / 3, dx = tap - (tap / 3) * 3;
+        const int iy = oy + dy - pad, ix = ox + dx - pad;
+        const bool ok = a_ok && iy >= 0 && iy < Hi && ix >= 0 && ix < Wi;
+        const float4* src = ok ? (const float4*)(xb + ((size_t)iy * Wi + ix) * C + c0) : (const float4*)g_zero_page;
+#pragma unroll
+        for (int i = 0; i < AV; ++i) ra[i] = src[i];
+    };
+    auto store_a = [&](int buf) {
+        float* As = smem + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < AV; ++i) {
+            const int k = (BK / 2) * ah + 4 * i;
+            As[(k + 0) * CBM + ap] = ra[i].x;
+            As[(k + 1) * CBM + ap] = ra[i].y;
+            As[(k + 2) * CBM + ap] = ra[i].z;
+            As[(k + 3) * CBM + ap] = ra[i].w;
+        }
+    };
+
+    f32x16 acc[2][TN];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+    const int wm = (wid >> 1) * 64, wn = (wid & 1) * (BN / 2);
+    const int li = lane & 31, lk = lane >> 5;
+    const int nks = 9 * C / BK;
+    load_b(0, 0);
+    load_a(0);
+    store_a(0);
+    __syncthreads();
+    for (int ks = 0; ks < nks; ++ks) {
+        const int cur = ks & 1;
+        // unconditional (the last iteration reloads its own stage into the idle buffer):
+        // guarded loads/stores let hipcc merge the guards and hoist the LDS writes
+        const int nx = ks + 1 < nks ? ks + 1 : ks;
+        load_b(nx, cur ^ 1);  // retired by the barrier's vmcnt(0) below
+        load_a(nx);
+        __builtin_amdgcn_sched_barrier(0);  // the next stage's loads go out before this stage's MFMAs
+        const float* As = smem + cur * STAGE + wm + li + lk * CBM;
+        const float* Bs = smem + cur * STAGE + BK * CBM + wn + li + lk * BN;
+        // fragments of k-step kk+1 are read while the MFMAs of kk run
+        float a[2], b[TN];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = As[32 * i];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = Bs[32 * j];
+#pragma unroll
+        for (int kk = 0; kk < BK / 2; ++kk) {
+            float na[2] = {0.f, 0.f}, nb[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) nb[j] = 0.f;
+            if (kk + 1 < BK / 2) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) na[i] = As[(2 * kk + 2) * CBM + 32 * i];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) nb[j] = Bs[(2 * kk + 2) * BN + 32 * j];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) a[i] = na[i];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) b[j] = nb[j];
+        }
+        store_a(cur ^ 1);
+        __syncthreads();
+    }
+    // epilogue: C/D map col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn + 32 * j + li;
+        const float bn = bias[n];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+                if (m < M) y[(size_t)m * N + n] = fmaxf(acc[i][j][r] + bn, 0.0f);
+            }
+        }
+    }
+}
+
+template <int BN, int BK, int MINB>
+int launch_conv(const float* x, const float* wt, const float* bias, float* y, int batch, int h_in, int pad, int c_in,
+                int c_out, hipStream_t st) {
+    const int h_out = h_in + 2 * pad - 2;
+    if (c_in % BK || c_out % BN) return AZG_ERR_ARG;
+    const int M = batch * h_out * h_out;
+    const int ntn = c_out / BN;
+    const int mtiles = (M + CBM - 1) / CBM, groups = (mtiles + 7) / 8;
+    hipLaunchKernelGGL((conv3x3_bias_relu_kernel<BN, BK, MINB>), dim3(groups * 8 * ntn), dim3(256), 0, st, x, wt,
+                       bias, y, M, h_out * h_out, h_out, h_in, h_in, pad, c_in, c_out);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
 }  // namespace
+
+extern "C" int azg_conv3x3_variant(int variant, const float* x, const float* wt, const float* bias, float* y,
+                                   int32_t batch, int32_t h_in, int32_t pad, int32_t c_in, int32_t c_out,
+                                   void* stream) {
+    const int h_out = h_in + 2 * pad - 2;
+    if (!x || !wt || !bias || !y || batch <= 0 || h_out <= 0 || ((uintptr_t)x & 15) || ((uintptr_t)wt & 15))
+        return AZG_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    switch (variant) {
+        case 0: return launch_conv<128, 32, 2>(x, wt, bias, y, batch, h_in, pad, c_in, c_out, st);
+        case 1: return launch_conv<128, 16, 3>(x, wt, bias, y, batch, h_in, pad, c_in, c_out, st);
+        case 2: return launch_conv<256, 16, 2>(x, wt, bias, y, batch, h_in, pad, c_in, c_out, st);
+        case 3: return launch_conv<256, 32, 1>(x, wt, bias, y, batch, h_in, pad, c_in, c_out, st);
+        default: return AZG_ERR_ARG;
+    }
+}
+
+extern "C" int azg_conv3x3_bias_relu_nhwc(const float* x, const float* wt, const float* bias, float* y,
+                                          int32_t batch, int32_t h_in, int32_t pad, int32_t c_in, int32_t c_out,
+                                          void* stream) {
+    // variant 1 (BN 128, BK 16, 3+ blocks per CU) measured fastest on conv2-4 at 4096 leaves
+    // (profiles/r01_conv_probe.json)
+    return azg_conv3x3_variant(1, x, wt, bias, y, batch, h_in, pad, c_in, c_out, stream);
+}
 
 extern "C" int azg_bias_relu_nhwc(float* x, const float* bias, int64_t rows, int32_t channels, void* stream) {
     if (!x || !bias || rows < 0 || channels <= 0 || channels % 4 || ((uintptr_t)x & 15) || ((uintptr_t)bias & 15))

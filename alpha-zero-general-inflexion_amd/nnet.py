@@ -64,6 +64,24 @@ def _bias_relu_(x, b):
     return x
 
 
+def _azg_conv3x3(x, wt, b, pad):
+    """relu(conv3x3(x) + b) on a channels_last CUDA tensor by libazg's f32-MFMA
+    implicit GEMM (azg_nn.hip); returns a channels_last tensor."""
+    import ctypes
+    from . import _lib
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
+    B, C, H, _ = x.shape
+    N = wt.shape[1]
+    Ho = H + 2 * pad - 2
+    y = torch.empty((B, N, Ho, Ho), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+    s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _lib.check(_lib.lib().azg_conv3x3_bias_relu_nhwc(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wt.data_ptr()),
+                                                     ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(y.data_ptr()),
+                                                     B, H, pad, C, N, s))
+    return y
+
+
 def _fold_bn(weight, bias, bn):
     """Eval-mode BatchNorm folded into the preceding conv/linear (f64 math)."""
     scale = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
@@ -85,16 +103,24 @@ class InferenceNet(nn.Module):
 
     outputs_probs = True
 
-    def __init__(self, net: InflexionNNet):
+    def __init__(self, net: InflexionNNet, conv="miopen"):
+        """conv: "miopen" (MIOpen implicit GEMM + one fused bias/ReLU pass) or
+        "azg" (libazg's f32-MFMA implicit GEMM with the bias/ReLU in its
+        epilogue) for conv2-4; measured side by side in profiles/r01_conv_probe.json."""
         super().__init__()
+        if conv not in ("miopen", "azg"):
+            raise ValueError(f"unknown conv implementation {conv!r}")
+        self.conv_impl = conv
         self.n, self.depth, c = net.n, net.depth, net.num_channels
         self.pads = []
         for i in range(1, 5):
-            conv, bn = getattr(net, f"conv{i}"), getattr(net, f"bn{i}")
-            w, b = _fold_bn(conv.weight.detach(), conv.bias.detach(), bn)
+            conv_i, bn = getattr(net, f"conv{i}"), getattr(net, f"bn{i}")
+            w, b = _fold_bn(conv_i.weight.detach(), conv_i.bias.detach(), bn)
             self.register_buffer(f"w{i}", w.contiguous(memory_format=torch.channels_last))
             self.register_buffer(f"b{i}", b)
-            self.pads.append(conv.padding[0])
+            # [9*Cin, Cout] k-major copy for the libazg implicit GEMM (k = (dy*3+dx)*Cin + c)
+            self.register_buffer(f"wt{i}", w.permute(2, 3, 1, 0).reshape(-1, w.shape[0]).contiguous())
+            self.pads.append(conv_i.padding[0])
         s = net.n - 4
         w1, b1 = _fold_bn(net.fc1.weight.detach(), net.fc1.bias.detach(), net.fc_bn1)
         w1 = w1.reshape(-1, c, s, s).permute(0, 2, 3, 1).reshape(w1.shape[0], -1)  # (c,h,w) -> (h,w,c)
@@ -120,6 +146,11 @@ class InferenceNet(nn.Module):
             if hook:
                 hook(i, "start")
             b = getattr(self, f"b{i}")
+            if fused and self.conv_impl == "azg" and i > 1:  # bias + ReLU inside the conv's epilogue
+                x = _azg_conv3x3(x, getattr(self, f"wt{i}"), b, pad)
+                if hook:
+                    hook(i, "stop")
+                continue
             x = F.conv2d(x, getattr(self, f"w{i}"), None if fused else b, padding=pad)
             if hook:
                 hook(i, "stop")

@@ -94,6 +94,8 @@ def parse():
     p.add_argument("--sims", type=int, default=25)
     p.add_argument("--max-turns", type=int, default=343)
     p.add_argument("--evaluator", default="net", choices=["net", "stub"])
+    p.add_argument("--conv", default="miopen", choices=["miopen", "azg"],
+                   help="conv2-4 implementation of the inference net (MIOpen igemm or libazg f32-MFMA implicit GEMM)")
     p.add_argument("--net", default="inference", choices=["inference", "reference"],
                    help="inference: BN-folded NHWC InferenceNet; reference: InflexionNNet as written")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -185,7 +187,7 @@ def main():
     flop_leaf, conv_flop_leaf = net_flops(args.n, depth, A)
     torch.manual_seed(0)
     net = InflexionNNet(n=args.n, depth=depth, action_size=A).cuda().eval()
-    ev = (InferenceNet(net) if args.net == "inference" else net) if args.evaluator == "net" else "stub"
+    ev = (InferenceNet(net, conv=args.conv) if args.net == "inference" else net) if args.evaluator == "net" else "stub"
     G = args.games
     eng = SelfPlayEngine(G, sims=args.sims, cpuct=1, temp_threshold=30, max_turns=args.max_turns,
                          seed_base=0, first_game=rank * G, evaluator=ev, game=args.game, n=args.n)
@@ -321,7 +323,9 @@ def main():
             "expansions": exp,
             "simulations": sims_run,
             "roofline": {"bound": "mfma",
-                         "kernel": "conv2-4 f32 implicit GEMM (MIOpen igemm_fwd_gtcx35_nhwc_fp32) per forward",
+                         "kernel": ("conv2-4 f32 implicit GEMM (MIOpen igemm_fwd_gtcx35_nhwc_fp32) per forward"
+                                    if args.conv == "miopen" else
+                                    "conv2-4 f32-MFMA implicit GEMM + bias/ReLU epilogue (libazg conv3x3) per forward"),
                          "achieved": conv_tflops, "peak": F32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                          "frac": conv_tflops / F32_MFMA_PEAK_TF, "traffic": None,
                          "per_launch": f"{leaves} leaves x {conv_flop_leaf / 1e6:.1f} MFLOP / {conv_avg * 1e3:.3f} ms "

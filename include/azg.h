@@ -118,6 +118,18 @@ int  azg_stats(azg_engine* e, int64_t* out /*[8]*/, void* stream);
  * (InflexionNNet.py:42-45) once BN is folded into the conv. */
 int  azg_bias_relu_nhwc(float* x, const float* bias, int64_t rows, int32_t channels, void* stream);
 
+/* Leaf-network 3x3 convolution, stride 1, as an f32-MFMA implicit GEMM with the
+ * folded-BN bias and ReLU fused (conv2-4 + bn2-4 + relu of InflexionNNet.forward,
+ * InflexionNNet.py:43-45): x NHWC [batch, h_in, h_in, c_in], wt [9*c_in, c_out]
+ * (k = (dy*3+dx)*c_in + c), y NHWC [batch, h_out, h_out, c_out] with
+ * h_out = h_in + 2*pad - 2; c_in % 32 == 0, c_out % 128 == 0. */
+int  azg_conv3x3_bias_relu_nhwc(const float* x, const float* wt, const float* bias, float* y, int32_t batch,
+                                int32_t h_in, int32_t pad, int32_t c_in, int32_t c_out, void* stream);
+/* Tuning hook: the same convolution with an explicit tile variant (0..3:
+ * BNxBK 128x32, 128x16, 256x16, 256x32). */
+int  azg_conv3x3_variant(int variant, const float* x, const float* wt, const float* bias, float* y, int32_t batch,
+                         int32_t h_in, int32_t pad, int32_t c_in, int32_t c_out, void* stream);
+
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active
  * [5] record actions [6] record counts [7] moves */

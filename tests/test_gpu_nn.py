@@ -19,14 +19,15 @@ def test_bias_relu_kernel():
     assert torch.equal(got, want)
 
 
-def test_inference_net_vs_reference_gpu():
+@pytest.mark.parametrize("conv", ["miopen", "azg"])
+def test_inference_net_vs_reference_gpu(conv):
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
     d = dict(np.load(ol.os.path.join(ol.GOLDEN, "nnet_golden.npz")))
     torch.manual_seed(0)
     net = InflexionNNet().eval()
     x = torch.from_numpy(d["planes"].astype(np.float32))
-    fast = InferenceNet(net.cuda()).cuda()
+    fast = InferenceNet(net.cuda(), conv=conv).cuda()
     with torch.no_grad():
         p, v = fast(x.cuda())
     np.testing.assert_allclose(p.cpu().numpy(), d["P"], rtol=1e-5, atol=1e-7)
@@ -51,3 +52,19 @@ def test_graph_replay_matches_eager():
     assert np.array_equal(ra["counts"][:, :4], rb["counts"][:, :4])
     assert np.array_equal(ra["actions"][:, :4], rb["actions"][:, :4])
     assert a.stats()["expansions"] == b.stats()["expansions"]
+
+
+@pytest.mark.parametrize("B,H,pad", [(1, 7, 1), (37, 7, 1), (300, 7, 0), (129, 5, 0), (64, 8, 1), (64, 6, 0)])
+def test_azg_conv3x3_matches_torch(B, H, pad):
+    """libazg implicit-GEMM conv (+bias, ReLU) vs torch conv2d on ragged batch sizes."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import _azg_conv3x3
+    torch.manual_seed(1)
+    C = N = 512
+    w = torch.randn(N, C, 3, 3, device="cuda") * 0.02
+    b = torch.randn(N, device="cuda") * 0.1
+    wt = w.permute(2, 3, 1, 0).reshape(9 * C, N).contiguous()
+    x = torch.relu(torch.randn(B, C, H, H, device="cuda")).contiguous(memory_format=torch.channels_last)
+    want = torch.relu(torch.nn.functional.conv2d(x, w, b, padding=pad))
+    got = _azg_conv3x3(x, wt, b, pad)
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)

@@ -130,3 +130,18 @@ def test_othello_dropin_matches_reference():
         pol = hashlib.sha256(np.array([e[1] for e in ex], np.float64).tobytes()).hexdigest()
         brd = hashlib.sha256(np.array([e[0] for e in ex], np.int64).tobytes()).hexdigest()
         assert pol == ep["policy_sha256"] and brd == ep["board_sha256"]
+
+
+def test_engine_records_zero_copy_view(azg):
+    """dist.engine_records (the tensors the RCCL example gather sends) alias the
+    engine's own move records."""
+    from azg_amd import dist as ad
+    e = azg.SelfPlayEngine(8, sims=4, evaluator="stub", max_turns=30)
+    for _ in range(3):
+        e.move()
+    moves, actions, counts = ad.engine_records(e)
+    rec = e.read_moves()
+    assert moves.device.type == "cuda" and moves.dtype == torch.int32
+    assert np.array_equal(moves.cpu().numpy(), rec["moves"])
+    assert np.array_equal(actions.cpu().numpy(), rec["actions"])
+    assert np.array_equal(counts.cpu().numpy(), rec["counts"])
