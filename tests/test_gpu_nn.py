@@ -68,3 +68,27 @@ def test_azg_conv3x3_matches_torch(B, H, pad):
     want = torch.relu(torch.nn.functional.conv2d(x, w, b, padding=pad))
     got = _azg_conv3x3(x, wt, b, pad)
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("B,H,pad", [(37, 7, 1), (129, 5, 0), (3, 6, 1)])
+def test_azg_conv3x3_variants(variant, B, H, pad):
+    """Every libazg conv tile variant (incl. the LDS-DMA ring) on ragged pixel counts."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    torch.manual_seed(2)
+    C = N = 512
+    w = torch.randn(N, C, 3, 3, device="cuda") * 0.02
+    b = torch.randn(N, device="cuda") * 0.1
+    wt = w.permute(2, 3, 1, 0).reshape(9 * C, N).contiguous()
+    x = torch.relu(torch.randn(B, H, H, C, device="cuda"))
+    want = torch.relu(torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w, b, padding=pad)).permute(0, 2, 3, 1)
+    Ho = H + 2 * pad - 2
+    y = torch.full((B, Ho, Ho, N), float("nan"), device="cuda")
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(_lib.lib().azg_conv3x3_variant(variant, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wt.data_ptr()),
+                                              ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(y.data_ptr()),
+                                              B, H, pad, C, N, s))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(y, want, rtol=1e-4, atol=1e-4)
