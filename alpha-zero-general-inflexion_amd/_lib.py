@@ -19,6 +19,9 @@ GAME_INFLEXION = 1
 GAME_OTHELLO = 2
 FLAG_GC = 1
 FLAG_RECORD = 2
+FLAG_ARENA = 4
+OPPONENT_RANDOM = 1
+OPPONENT_GREEDY = 2
 
 ERR = {0: "ok", -1: "bad argument", -2: "HIP error", -3: "node pool full", -4: "path too deep",
        -5: "no valid action", -6: "bad call order"}
@@ -62,6 +65,11 @@ SIGNATURES = [
     ("azg_bias_relu_nhwc", ctypes.c_int, [_VP, _VP, _I64, _I32, _VP]),
     ("azg_conv3x3_bias_relu_nhwc", ctypes.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
     ("azg_conv3x3_variant", ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
+    ("azg_game_info", ctypes.c_int, [_I32, _I32, _VP]),
+    ("azg_set_arena", ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    ("azg_opponent_move", ctypes.c_int, [_VP, _I32, _VP]),
+    ("azg_examples", ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _I32, _I32, _I64, _VP, _VP,
+                                    _VP, ctypes.POINTER(_I64), _VP]),
 ]
 
 _lib = None

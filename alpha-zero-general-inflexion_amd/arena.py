@@ -1,0 +1,82 @@
+"""Batched Arena: MCTSPlayer against a baseline player, all games at once on the GPU.
+
+The reference pits the trained net every pitInterval iterations (Coach.py:158-165):
+Arena(MCTSPlayer(MCTS(nnet)), RandomPlayer() | GreedyPlayer(), game).playGames(
+arenaCompare) runs each game in a spawn-Pool process (Arena.py:125), one
+MCTS.search at a time.  Here every game is a slot of one SelfPlayEngine in
+arena mode:
+
+  * slot i < num//2 + 1 starts with RED to move, the others with BLUE
+    (Arena.playGames: `(player1, player2) if i <= subtotal else (player2,
+    player1)`, Arena.py:126-129); the MCTS player always plays RED
+    (self.player = {RED: player1, BLUE: player2}, Arena.py:35);
+  * the MCTS side searches numMCTSSims simulations with temp = 0 and plays the
+    argmax of the one-hot policy (MCTSPlayer.play, InflexionPlayers.py:86-88),
+    keeping its tree for the whole game (MCTSPlayer.reset per game);
+  * the baseline's move is computed on the GPU (opponent_kernel): RandomPlayer
+    draws np.random.choice over the valid actions from the slot's numpy stream,
+    GreedyPlayer takes the best piece_count_diff after the move, ties to the
+    larger action (InflexionPlayers.py:24-77);
+  * results are read from RED's perspective (Arena.py:71-88).
+
+Each slot has its own numpy stream seeded by its game index (the reference's
+Pool workers draw from unseeded per-process streams, so its arena results are
+not reproducible run to run).
+"""
+import numpy as np
+
+from .engine import SelfPlayEngine, game_spec
+from .flags import GameOutcome
+
+_OUT = {0: GameOutcome.ONGOING, 1: GameOutcome.DRAW, 2: GameOutcome.WON, 3: GameOutcome.LOST}
+
+
+class BatchedArena:
+    def __init__(self, game, nnet, args, opponent="random", evaluator=None, seed_base=0, first_game=0):
+        if opponent not in ("random", "greedy"):
+            raise ValueError(f"unknown opponent {opponent!r}")
+        self.game, self.nnet, self.args, self.opponent = game, nnet, args, opponent
+        if evaluator is None:
+            from .nnet import InferenceNet, NNetWrapper
+            evaluator = InferenceNet(nnet.nnet) if isinstance(nnet, NNetWrapper) else nnet
+        self.evaluator = evaluator
+        self.seed_base, self.first_game = seed_base, first_game
+        self.last_engine_state = None
+
+    def playGames(self, num, verbose=False):
+        """Arena.playGames (Arena.py:90-142): (MCTS player wins, baseline wins, draws)."""
+        if not (isinstance(num, int) and num >= 2):
+            raise AssertionError("num must be an int >= 2")
+        name, n, max_turns = game_spec(self.game)
+        eng = SelfPlayEngine(num, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct, temp_threshold=0,
+                             max_turns=max_turns, game=name, n=n, seed_base=self.seed_base,
+                             first_game=self.first_game, evaluator=self.evaluator, record=False, arena=True)
+        try:
+            subtotal = num // 2
+            first = np.where(np.arange(num) <= subtotal, 1, -1).astype(np.int32)
+            eng.set_arena(np.ones(num, np.int32), first)
+            while eng.active() > 0:
+                eng.move()  # searches in the slots where the MCTS player (RED) is to move
+                eng.opponent_move(self.opponent)
+            st = eng.state()
+            self.last_moves = eng.read_moves(counts=False)
+            err = eng.stats()["error"]
+        finally:
+            eng.close()
+        if err:
+            raise RuntimeError(f"arena engine error {err}")
+        self.last_engine_state = st
+        one = two = draws = 0
+        for g in range(num):
+            out = _OUT[int(st["outcomes"][g])]
+            if int(st["players"][g]) != 1:  # game.player = RED: the setter flips the outcome
+                out = out.opposite()
+            if out == GameOutcome.WON:
+                one += 1
+            elif out == GameOutcome.LOST:
+                two += 1
+            elif out == GameOutcome.DRAW:
+                draws += 1
+            else:
+                raise ValueError(f"Unexpected game status: {out}")
+        return one, two, draws

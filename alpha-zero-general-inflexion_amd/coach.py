@@ -15,14 +15,24 @@ action = np.random.choice(len(pi), p=pi), step; returns
 
 `selfplay_batch` plays many games at once on the batched engine (per-game
 numpy streams seeded by global game index) and builds the same examples from
-the engine's move records.
+the engine's move records on the host; `selfplay_examples` builds them on the
+GPU (examples.py) and `learn` runs the reference's iteration loop
+(Coach.py:92-165) with self-play, examples and training all on the device.
 """
+import logging
+import os
+import pickle
+import random
+from collections import deque
+
 import numpy as np
+import torch
 
 from .flags import GameOutcome, PlayerColour
 from .inflexion import InflexionGame
 
 N_SYM = 36
+log = logging.getLogger(__name__)
 
 
 def _label_players(move_players, label_mode, n_sym=N_SYM):
@@ -79,16 +89,28 @@ class Coach:
             if game.outcome != GameOutcome.ONGOING:
                 return build_examples(game, planes, pis, players, game, self.label_mode)
 
+    def _engine(self, num_games, evaluator, seed_base, first_game):
+        from .engine import SelfPlayEngine, game_spec
+        name, n, max_turns = game_spec(self.game)
+        return SelfPlayEngine(num_games, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct,
+                              temp_threshold=int(self.args.tempThreshold), max_turns=max_turns, game=name, n=n,
+                              seed_base=seed_base, first_game=first_game,
+                              evaluator=evaluator if evaluator is not None else self.evaluator())
+
+    def evaluator(self):
+        """The leaf evaluator for the engine: an NNetWrapper's current weights as
+        the inference form (BN folded, NHWC; nnet.InferenceNet), else self.nnet
+        itself (a module, or "stub")."""
+        from .nnet import InferenceNet, NNetWrapper
+        if isinstance(self.nnet, NNetWrapper):
+            return InferenceNet(self.nnet.nnet)
+        return self.nnet
+
     def selfplay_batch(self, num_games, evaluator=None, seed_base=0, first_game=0, return_records=False):
         """Play num_games complete games concurrently on the GPU engine and
         return their examples (same format as executeEpisode)."""
-        from .engine import SelfPlayEngine, game_spec
         g0 = self.game
-        name, n, max_turns = game_spec(g0)
-        eng = SelfPlayEngine(num_games, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct,
-                             temp_threshold=int(self.args.tempThreshold), max_turns=max_turns, game=name, n=n,
-                             seed_base=seed_base, first_game=first_game,
-                             evaluator=evaluator if evaluator is not None else self.nnet)
+        eng = self._engine(num_games, evaluator, seed_base, first_game)
         try:
             eng.play()
             rec = eng.read_moves()
@@ -99,6 +121,127 @@ class Coach:
             examples += examples_from_record(g0, rec["actions"][i], rec["temps"][i], rec["counts"][i],
                                              int(rec["moves"][i]), self.label_mode)
         return (examples, rec) if return_records else examples
+
+    # ---------------------------------------------------------------- learn loop
+    def selfplay_examples(self, num_games, evaluator=None, seed_base=0, first_game=0, maxlen=None):
+        """One iteration's self-play (Coach.py:106-112) as num_games concurrent
+        games; the examples (last maxlen, default args.maxlenOfQueue) are built on
+        the GPU and returned as a device ExampleSet."""
+        from .examples import engine_examples
+        maxlen = int(self.args.maxlenOfQueue if maxlen is None else maxlen)
+        eng = self._engine(num_games, evaluator, seed_base, first_game)
+        try:
+            eng.play()
+            return engine_examples(eng, int(self.args.tempThreshold), self.label_mode, maxlen)
+        finally:
+            eng.close()
+
+    def _selfplay_iteration(self, i, group):
+        """Self-play of iteration i over all ranks; examples land on the trainer (rank 0)."""
+        import torch.distributed as dist
+        from .dist import broadcast_weights, gather_records
+        from .engine import game_spec
+        from .examples import examples_from_records
+        eps = int(self.args.numEps)
+        if group is None and not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+            return self.selfplay_examples(eps, first_game=(i - 1) * eps)
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        broadcast_weights(self.nnet.nnet, src=0, group=group)
+        eng = self._engine(eps, None, 0, ((i - 1) * world + rank) * eps)
+        try:
+            eng.play()
+            rec, _ = gather_records(eng, dst=0, group=group)
+        finally:
+            eng.close()
+        if rank != 0:
+            return None
+        name, n, max_turns = game_spec(self.game)
+        mv, act, cnt = rec
+        return examples_from_records(name, n, max_turns, int(self.args.tempThreshold), mv, act, cnt,
+                                     self.label_mode, int(self.args.maxlenOfQueue))
+
+    def learn(self, group=None, pit=True):
+        """Coach.learn (Coach.py:92-165): per iteration, numEps self-play games
+        (on every rank when torch.distributed is initialised: the engine plays
+        numEps games per rank, records are gathered to rank 0 and the weights
+        broadcast back), the example history window, the examples file, training
+        (NNetWrapper.train_examples), temp.pth.tar and, every pitInterval
+        iterations, the arena against the baselines."""
+        import torch.distributed as dist
+        from .examples import ExampleSet
+        distributed = group is not None or (dist.is_available() and dist.is_initialized()
+                                            and dist.get_world_size() > 1)
+        trainer = not distributed or dist.get_rank(group) == 0
+        pit_interval = 5
+        for i in range(1, int(self.args.numIters) + 1):
+            log.info("Starting Iter #%d ...", i)
+            if not self.skipFirstSelfPlay or i > 1:
+                ex = self._selfplay_iteration(i, group)
+                if trainer:
+                    self.trainExamplesHistory.append(ex)
+            if not trainer:
+                continue
+            if len(self.trainExamplesHistory) > int(self.args.numItersForTrainExamplesHistory):
+                log.warning("Removing the oldest entry in trainExamples. len(trainExamplesHistory) = %d",
+                            len(self.trainExamplesHistory))
+                self.trainExamplesHistory.pop(0)
+            if self.args.get("saveExamples", True):
+                self.saveTrainExamples(i - 1)
+            train = ExampleSet.cat(self.trainExamplesHistory)
+            perm = list(range(len(train)))
+            random.shuffle(perm)  # shuffle(trainExamples), Coach.py:149
+            self.last_losses = self.nnet.train_examples(
+                train.index(torch.as_tensor(perm, dtype=torch.long, device=train.vs.device)))
+            self.nnet.save_checkpoint(folder=self.args.checkpoint, filename="temp.pth.tar")
+            if pit and i % pit_interval == 0:
+                self.pit_baselines()
+        if distributed:
+            from .dist import broadcast_weights
+            broadcast_weights(self.nnet.nnet, src=0, group=group)
+
+    def pit_baselines(self):
+        """Coach.py:158-165: the new net's MCTSPlayer against RandomPlayer and
+        GreedyPlayer, args.arenaCompare games each (batched on the GPU)."""
+        from .arena import BatchedArena
+        res = {}
+        for opp in ("random", "greedy"):
+            arena = BatchedArena(self.game, self.nnet, self.args, opponent=opp)
+            p1, p2, draws = arena.playGames(int(self.args.arenaCompare))
+            log.info("NEW/%s WINS : %d / %d ; DRAWS : %d", opp, p1, p2, draws)
+            res[opp] = (p1, p2, draws)
+        self.last_pit = res
+        return res
+
+    # ---------------------------------------------------------------- example files
+    def getCheckpointFile(self, iteration):
+        return "checkpoint_" + str(iteration) + ".pth.tar"
+
+    def saveTrainExamples(self, iteration):
+        """Coach.py:170-176: the history as a pickled list of deques of
+        (board, pi, z) tuples in checkpoint_{iteration}.pth.tar.examples."""
+        folder = self.args.checkpoint
+        os.makedirs(folder, exist_ok=True)
+        filename = os.path.join(folder, self.getCheckpointFile(iteration) + ".examples")
+        hist = [deque(h.to_list() if hasattr(h, "to_list") else h, maxlen=int(self.args.maxlenOfQueue))
+                for h in self.trainExamplesHistory]
+        with open(filename, "wb+") as f:
+            pickle.Pickler(f).dump(hist)
+
+    def loadTrainExamples(self, device=None):
+        """Coach.py:178-193 for a file this Coach (or the reference) wrote: the
+        history comes back as device ExampleSets; self-play of iteration 1 is
+        skipped.  A missing file raises FileNotFoundError (the reference asks on
+        stdin)."""
+        from .examples import ExampleSet
+        model_file = os.path.join(self.args.load_folder_file[0], self.args.load_folder_file[1])
+        examples_file = model_file + ".examples"
+        if not os.path.isfile(examples_file):
+            raise FileNotFoundError(f'File "{examples_file}" with trainExamples not found')
+        with open(examples_file, "rb") as f:
+            hist = pickle.Unpickler(f).load()
+        dev = device or self.nnet.device
+        self.trainExamplesHistory = [ExampleSet.from_list(list(h), dev) for h in hist if len(h)]
+        self.skipFirstSelfPlay = True
 
 
 def examples_from_record(template, actions, temps, counts, moves, label_mode="reference"):

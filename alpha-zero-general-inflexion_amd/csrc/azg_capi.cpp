@@ -114,6 +114,7 @@ int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
     ALLOC(d.player, G);
     ALLOC(d.outcome, G);
     ALLOC(d.active, G);
+    ALLOC(d.searcher, G);
     ALLOC(d.mt, G * azg::MT_N);
     ALLOC(d.mt_pos, G);
     ALLOC(d.node_own, GM);
@@ -322,6 +323,107 @@ int azg_device_ptrs(azg_engine* e, void** out) {
     out[6] = e->d.rec_counts;
     out[7] = e->d.moves;
     return 0;
+}
+
+int azg_set_arena(azg_engine* e, const int32_t* searcher, const int32_t* first_player, void* stream) {
+    if (!e || !searcher || !first_player) return fail(AZG_ERR_ARG, "null argument");
+    if (!(e->cfg.flags & AZG_FLAG_ARENA)) return fail(AZG_ERR_STATE, "engine created without AZG_FLAG_ARENA");
+    const size_t G = (size_t)e->d.G;
+    for (size_t g = 0; g < G; ++g)
+        if ((searcher[g] != 1 && searcher[g] != -1) || (first_player[g] != 1 && first_player[g] != -1))
+            return fail(AZG_ERR_ARG, "searcher / first_player must be +1 (RED) or -1 (BLUE)");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipMemcpyAsync(e->d.searcher, searcher, G * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(e->d.player, first_player, G * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+int azg_opponent_move(azg_engine* e, int32_t kind, void* stream) {
+    if (!e) return fail(AZG_ERR_ARG, "null engine");
+    if (kind != AZG_OPPONENT_RANDOM && kind != AZG_OPPONENT_GREEDY) return fail(AZG_ERR_ARG, "unknown opponent");
+    HIP_TRY(e->ops.opponent(e->d, kind, (hipStream_t)stream));
+    return 0;
+}
+
+int azg_game_info(int32_t game_kind, int32_t n, int32_t* out) {
+    azg::GameOps ops;
+    if (!out || !azg::game_ops(game_kind, n, &ops)) return fail(AZG_ERR_ARG, "unsupported game kind / size");
+    out[0] = ops.cells;
+    out[1] = ops.actions;
+    out[2] = ops.planes;
+    out[3] = ops.nsym;
+    return 0;
+}
+
+int azg_examples(int32_t game_kind, int32_t n, int32_t max_turns, int32_t temp_threshold, int32_t num_games,
+                 int32_t max_moves, const int32_t* moves, const int32_t* actions, const void* counts,
+                 int32_t counts_bytes, int32_t label_mode, int64_t maxlen, float* planes, float* pis, float* vs,
+                 int64_t* count, void* stream) {
+    azg::GameOps ops;
+    if (!azg::game_ops(game_kind, n, &ops)) return fail(AZG_ERR_ARG, "unsupported game kind / size");
+    if (num_games < 0 || max_moves <= 0 || max_moves > 65535 || !moves || !actions || !counts || !count ||
+        (counts_bytes != 2 && counts_bytes != 4) || (label_mode != 0 && label_mode != 1) || maxlen < 0 ||
+        (maxlen > 0 && (!planes || !pis || !vs)))
+        return fail(AZG_ERR_ARG, "bad azg_examples argument");
+    *count = 0;
+    if (num_games == 0 || maxlen == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const size_t G = (size_t)num_games, MM = (size_t)max_moves;
+    azg::ExampleArgs X{};
+    X.G = num_games;
+    X.MM = max_moves;
+    X.max_turns = max_turns;
+    X.temp_threshold = temp_threshold;
+    X.label_mode = label_mode;
+    X.moves = moves;
+    X.actions = actions;
+    X.counts16 = counts_bytes == 2 ? (const int16_t*)counts : nullptr;
+    X.counts32 = counts_bytes == 4 ? (const int32_t*)counts : nullptr;
+    X.planes = planes;
+    X.pis = pis;
+    X.vs = vs;
+    // one scratch block: keys [G*MM] | base [G] | status [G] | zplayer [G] | zval [G]
+    const size_t bytes = G * MM * sizeof(azg::MoveKey) + G * 8 + G * 4 * 3;
+    char* scratch = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&scratch, bytes, st));
+    X.keys = (azg::MoveKey*)scratch;
+    long long* base = (long long*)(scratch + G * MM * sizeof(azg::MoveKey));
+    X.base = base;
+    X.status = (int32_t*)(base + G);
+    X.zplayer = X.status + G;
+    X.zval = (float*)(X.zplayer + G);
+    int rc = 0;
+    std::vector<int32_t> status(G);
+    std::vector<long long> hbase(G);
+    long long total = 0;
+    hipError_t he = ops.replay(X, st);
+    if (he == hipSuccess) he = hipMemcpyAsync(status.data(), X.status, G * 4, hipMemcpyDeviceToHost, st);
+    if (he == hipSuccess) he = hipStreamSynchronize(st);
+    if (he != hipSuccess) {
+        rc = fail(AZG_ERR_HIP, std::string("examples replay: ") + hipGetErrorString(he));
+    } else {
+        for (size_t g = 0; g < G && !rc; ++g) {
+            if (status[g] < 0) rc = fail(AZG_ERR_ARG, "move record " + std::to_string(g) + " is not a legal game");
+            hbase[g] = total;
+            total += (long long)ops.nsym * (status[g] > 0 ? status[g] : 0);
+        }
+    }
+    if (!rc) {
+        // deque(maxlen) keeps the last maxlen examples (Coach.py:107)
+        X.skip = total > maxlen ? total - maxlen : 0;
+        int g0 = 0;
+        while (g0 < (int)G && hbase[g0] + (long long)ops.nsym * (status[g0] > 0 ? status[g0] : 0) <= X.skip) ++g0;
+        X.g0 = g0;
+        he = hipMemcpyAsync(base, hbase.data(), G * 8, hipMemcpyHostToDevice, st);
+        if (he == hipSuccess) he = ops.emit(X, st);
+        if (he == hipSuccess) he = hipStreamSynchronize(st);  // hbase must outlive the copy
+        if (he != hipSuccess) rc = fail(AZG_ERR_HIP, std::string("examples emit: ") + hipGetErrorString(he));
+        else *count = total - X.skip;
+    }
+    hipError_t fe = hipFreeAsync(scratch, st);
+    if (!rc && fe != hipSuccess) rc = fail(AZG_ERR_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(fe));
+    return rc;
 }
 
 }  // extern "C"

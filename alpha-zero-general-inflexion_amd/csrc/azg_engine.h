@@ -32,6 +32,7 @@ struct Dev {
     int32_t* player;     // [G]  +1 RED, -1 BLUE
     int32_t* outcome;    // [G]  Outcome w.r.t. player to move
     int32_t* active;     // [G]
+    int32_t* searcher;   // [G]  colour the search plays (arena), 0 = both (self-play)
     uint32_t* mt;        // [G][624]  numpy legacy MT19937 state
     int32_t* mt_pos;     // [G]
 

@@ -329,6 +329,24 @@ struct Inflexion {
             out[3 * CELLS + lane] = (float)cs;
         }
     }
+
+    // symmetries() (InflexionGame.py:102-113), form s: identity, rotate(s) for
+    // s = 1..5, then translate(rotate(k), j, 'r') for k = 1..5, j = 1..n-1
+    static constexpr int NSYM = 6 + 5 * (N - 1);
+    __device__ static int form_src(int s, int c) {
+        if (s < 6) return sym_src(c, s, 0, 0);
+        return sym_src(c, 1 + (s - 6) / (N - 1), 1 + (s - 6) % (N - 1), 0);
+    }
+    // the policy plane (7, n, n) moves its cells; the move kinds stay put
+    __device__ static int form_action_src(int s, int a) {
+        const int m = a / CELLS;
+        return m * CELLS + form_src(s, a - m * CELLS);
+    }
+    // to_planes() value of plane pl at (source) cell src (InflexionGame.py:84-91)
+    __device__ static float plane(int pl, int src, uint64_t own, uint64_t opp, int kt, int cs) {
+        return pl == 0 ? (float)((own >> src) & 1ull)
+                       : pl == 1 ? (float)((opp >> src) & 1ull) : pl == 2 ? (float)kt : (float)cs;
+    }
 };
 
 // --- OthelloGame(n) (azg_amd/othello.py; builder-authored) ----------------
@@ -436,18 +454,29 @@ struct Othello {
         const int k = rng_randint(R, 0, 8);
         const int lane = lane_id();
         if (lane < CELLS) {
-            const int i = lane / N, j = (k & 4) ? N - 1 - lane % N : lane % N;
-            int sr, sq;
-            switch (k & 3) {
-                case 0: sr = i; sq = j; break;
-                case 1: sr = j; sq = N - 1 - i; break;
-                case 2: sr = N - 1 - i; sq = N - 1 - j; break;
-                default: sr = N - 1 - j; sq = i; break;
-            }
-            const int src = sr * N + sq;
+            const int src = form_src(k, lane);
             out[lane] = (float)((own >> src) & 1ull);
             out[CELLS + lane] = (float)((opp >> src) & 1ull);
         }
+    }
+
+    // symmetries(): the 8 dihedral forms k (k & 3 rot90s, then fliplr if k & 4);
+    // source cell of output cell c
+    static constexpr int NSYM = 8;
+    __device__ static int form_src(int k, int c) {
+        const int i = c / N, j = (k & 4) ? N - 1 - c % N : c % N;
+        int sr, sq;
+        switch (k & 3) {
+            case 0: sr = i; sq = j; break;
+            case 1: sr = j; sq = N - 1 - i; break;
+            case 2: sr = N - 1 - i; sq = N - 1 - j; break;
+            default: sr = N - 1 - j; sq = i; break;
+        }
+        return sr * N + sq;
+    }
+    __device__ static int form_action_src(int k, int a) { return a < CELLS ? form_src(k, a) : a; }  // pass stays
+    __device__ static float plane(int pl, int src, uint64_t own, uint64_t opp, int, int) {
+        return pl == 0 ? (float)((own >> src) & 1ull) : (float)((opp >> src) & 1ull);
     }
 };
 
@@ -544,6 +573,11 @@ __device__ int puct_select(const Dev& E, int g, int id, const typename R::VCtx& 
     return besta == 0x7fffffff ? -1 : besta;
 }
 
+// arena slots search only on their own colour's turns (searcher 0 = self-play)
+__device__ __forceinline__ bool searching(const Dev& E, int g) {
+    return E.searcher[g] == 0 || E.searcher[g] == E.player[g];
+}
+
 __device__ __forceinline__ void set_err(const Dev& E, int g, int code) {
     if (lane_id() == 0 && E.err[g] == 0) E.err[g] = code;
 }
@@ -556,7 +590,7 @@ __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__
     __shared__ uint32_t s_mt[MT_N];
     const int g = blockIdx.x, lane = lane_id();
     float* out = planes + (size_t)g * R::PLANES * R::CELLS;
-    if (!E.active[g] || E.err[g]) {
+    if (!E.active[g] || E.err[g] || !searching(E, g)) {
         for (int i = lane; i < R::PLANES * R::CELLS; i += WAVE) out[i] = 0.0f;
         if (lane == 0) E.leaf_kind[g] = LEAF_NONE;
         return;
@@ -755,97 +789,12 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
 
 // move_end: MCTS.getActionProb root policy (MCTS.py:48-60), Coach.executeEpisode
 // temperature + np.random.choice + step (Coach.py:68-84), record, node GC.
+// Game.to_next_state for slot g's root (Coach.py:82 / Arena.py:69): apply the
+// action, store the new root, and (AZG_FLAG_GC) free the nodes no later
+// search can reach and rebuild the slot's hash table.
 template <class R>
-__global__ __launch_bounds__(WAVE) void move_end_kernel(Dev E) {
-    __shared__ uint32_t s_mt[MT_N];
-    __shared__ int s_cnt[R::AP];
-    __shared__ double s_cdf[R::AP];
-    const int g = blockIdx.x, lane = lane_id();
-    if (!E.active[g] || E.err[g]) return;
-    Pos p = load_root<R>(E, g);
-    uint64_t own, opp;
-    int cs, kt, slot;
-    R::key(p, own, opp, kt, cs);
-    const int id = table_lookup(E, g, own, opp, kt, cs, &slot);
-    int cnt[R::AJ];
-#pragma unroll
-    for (int j = 0; j < R::AJ; ++j) {
-        const int a = lane + WAVE * j;
-        cnt[j] = (id >= 0 && a < R::A) ? (int)(E.node_N[node_row<R>(E, g, id) + a] & 0x7fffffffu) : 0;
-        s_cnt[a] = cnt[j];
-    }
-    const int m = E.moves[g];
-    const int temp = (m + 1) < E.temp_threshold;  // episodeStep < tempThreshold
-    BlockRng rg{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
-    int action = -1;
-    if (temp == 0) {
-        int mx = cnt[0];
-#pragma unroll
-        for (int j = 1; j < R::AJ; ++j) mx = max(mx, cnt[j]);
-        mx = wave_max(mx);
-        uint64_t tie[R::AJ];
-        int nb = 0;
-#pragma unroll
-        for (int j = 0; j < R::AJ; ++j) {
-            const int a = lane + WAVE * j;
-            tie[j] = __ballot(a < R::A && cnt[j] == mx);
-            nb += __popcll(tie[j]);
-        }
-        int pick = rng_randint(rg, 0, nb);  // np.random.choice(bestAs), draws only if nb > 1
-#pragma unroll
-        for (int j = 0; j < R::AJ; ++j) {
-            const int c = __popcll(tie[j]);
-            if (action < 0 && pick < c) {
-                uint64_t b = tie[j];
-                for (int k = 0; k < pick; ++k) b &= b - 1ull;
-                action = WAVE * j + __ffsll((unsigned long long)b) - 1;
-            }
-            if (action < 0) pick -= c;
-        }
-        (void)rng_random_sample(rg);  // np.random.choice(len(pi), p=one-hot) still draws
-    } else {
-        __syncthreads();
-        if (lane == 0) {  // probs = counts / counts.sum(); cdf = cumsum (sequential f64)
-            long long tot = 0;
-            for (int a = 0; a < R::A; ++a) tot += s_cnt[a];
-            double acc = 0.0;
-            for (int a = 0; a < R::A; ++a) {
-                acc += (double)s_cnt[a] / (double)tot;
-                s_cdf[a] = acc;
-            }
-        }
-        __syncthreads();
-        const double last = s_cdf[R::A - 1];
-        const double u = rng_random_sample(rg);
-        int first = 0x7fffffff;
-#pragma unroll
-        for (int j = 0; j < R::AJ; ++j) {
-            const int a = lane + WAVE * j;
-            if (a < R::A && s_cdf[a] / last > u) first = min(first, a);
-        }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) first = min(first, __shfl_xor(first, o));
-        action = first == 0x7fffffff ? R::A : first;
-    }
-    rng_store(rg);
-    if (m < E.max_moves) {
-        if (lane == 0) {
-            E.rec_action[(size_t)g * E.max_moves + m] = action;
-            E.rec_temp[(size_t)g * E.max_moves + m] = (int8_t)temp;
-        }
-        if (E.rec_counts) {
-            int32_t* rc = E.rec_counts + ((size_t)g * E.max_moves + m) * R::A;
-#pragma unroll
-            for (int j = 0; j < R::AJ; ++j) {
-                const int a = lane + WAVE * j;
-                if (a < R::A) rc[a] = cnt[j];
-            }
-        }
-    }
-    if (action < 0 || action >= R::A || !R::valid(action, R::vctx(own, opp, cs))) {
-        set_err(E, g, -5);
-        return;
-    }
+__device__ void commit_move(const Dev& E, int g, Pos p, int action, int m) {
+    const int lane = lane_id();
     R::apply(p, action, E.max_turns);
     if (lane < R::CELLS) E.board[(size_t)g * 64 + lane] = (int8_t)p.cell;
     if (lane == 0) {
@@ -903,6 +852,169 @@ __global__ __launch_bounds__(WAVE) void move_end_kernel(Dev E) {
     }
 }
 
+template <class R>
+__global__ __launch_bounds__(WAVE) void move_end_kernel(Dev E) {
+    __shared__ uint32_t s_mt[MT_N];
+    __shared__ int s_cnt[R::AP];
+    __shared__ double s_cdf[R::AP];
+    const int g = blockIdx.x, lane = lane_id();
+    if (!E.active[g] || E.err[g] || !searching(E, g)) return;
+    Pos p = load_root<R>(E, g);
+    uint64_t own, opp;
+    int cs, kt, slot;
+    R::key(p, own, opp, kt, cs);
+    const int id = table_lookup(E, g, own, opp, kt, cs, &slot);
+    int cnt[R::AJ];
+#pragma unroll
+    for (int j = 0; j < R::AJ; ++j) {
+        const int a = lane + WAVE * j;
+        cnt[j] = (id >= 0 && a < R::A) ? (int)(E.node_N[node_row<R>(E, g, id) + a] & 0x7fffffffu) : 0;
+        s_cnt[a] = cnt[j];
+    }
+    const int m = E.moves[g];
+    const int temp = (m + 1) < E.temp_threshold;  // episodeStep < tempThreshold
+    BlockRng rg{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
+    int action = -1;
+    if (temp == 0) {
+        int mx = cnt[0];
+#pragma unroll
+        for (int j = 1; j < R::AJ; ++j) mx = max(mx, cnt[j]);
+        mx = wave_max(mx);
+        uint64_t tie[R::AJ];
+        int nb = 0;
+#pragma unroll
+        for (int j = 0; j < R::AJ; ++j) {
+            const int a = lane + WAVE * j;
+            tie[j] = __ballot(a < R::A && cnt[j] == mx);
+            nb += __popcll(tie[j]);
+        }
+        int pick = rng_randint(rg, 0, nb);  // np.random.choice(bestAs), draws only if nb > 1
+#pragma unroll
+        for (int j = 0; j < R::AJ; ++j) {
+            const int c = __popcll(tie[j]);
+            if (action < 0 && pick < c) {
+                uint64_t b = tie[j];
+                for (int k = 0; k < pick; ++k) b &= b - 1ull;
+                action = WAVE * j + __ffsll((unsigned long long)b) - 1;
+            }
+            if (action < 0) pick -= c;
+        }
+        // Coach.py:81 np.random.choice(len(pi), p=one-hot) still draws; the arena's
+        // MCTSPlayer takes the argmax instead (InflexionPlayers.py:88)
+        if (!(E.flags & 4)) (void)rng_random_sample(rg);
+    } else {
+        __syncthreads();
+        if (lane == 0) {  // probs = counts / counts.sum(); cdf = cumsum (sequential f64)
+            long long tot = 0;
+            for (int a = 0; a < R::A; ++a) tot += s_cnt[a];
+            double acc = 0.0;
+            for (int a = 0; a < R::A; ++a) {
+                acc += (double)s_cnt[a] / (double)tot;
+                s_cdf[a] = acc;
+            }
+        }
+        __syncthreads();
+        const double last = s_cdf[R::A - 1];
+        const double u = rng_random_sample(rg);
+        int first = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < R::AJ; ++j) {
+            const int a = lane + WAVE * j;
+            if (a < R::A && s_cdf[a] / last > u) first = min(first, a);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) first = min(first, __shfl_xor(first, o));
+        action = first == 0x7fffffff ? R::A : first;
+    }
+    rng_store(rg);
+    if (m < E.max_moves) {
+        if (lane == 0) {
+            E.rec_action[(size_t)g * E.max_moves + m] = action;
+            E.rec_temp[(size_t)g * E.max_moves + m] = (int8_t)temp;
+        }
+        if (E.rec_counts) {
+            int32_t* rc = E.rec_counts + ((size_t)g * E.max_moves + m) * R::A;
+#pragma unroll
+            for (int j = 0; j < R::AJ; ++j) {
+                const int a = lane + WAVE * j;
+                if (a < R::A) rc[a] = cnt[j];
+            }
+        }
+    }
+    if (action < 0 || action >= R::A || !R::valid(action, R::vctx(own, opp, cs))) {
+        set_err(E, g, -5);
+        return;
+    }
+    commit_move<R>(E, g, p, action, m);
+}
+
+// The arena's baseline players (InflexionPlayers.py:24-77) for the slots whose
+// colour to move is not the searcher's: RandomPlayer = np.random.choice over
+// the valid actions (the slot's numpy stream); GreedyPlayer = the valid action
+// whose next state has the best piece_count_diff for the mover, ties to the
+// larger action (candidates.sort(reverse=True)).
+template <class R>
+__global__ __launch_bounds__(WAVE) void opponent_kernel(Dev E, int kind) {
+    __shared__ uint32_t s_mt[MT_N];
+    const int g = blockIdx.x, lane = lane_id();
+    if (!E.active[g] || E.err[g] || E.searcher[g] == 0 || searching(E, g)) return;
+    Pos p = load_root<R>(E, g);
+    uint64_t own, opp;
+    int cs, kt;
+    R::key(p, own, opp, kt, cs);
+    const typename R::VCtx vc = R::vctx(own, opp, cs);
+    uint64_t vb[R::AJ];
+    int nv = 0;
+#pragma unroll
+    for (int j = 0; j < R::AJ; ++j) {
+        const int a = lane + WAVE * j;
+        vb[j] = __ballot(a < R::A && R::valid(a, vc));
+        nv += __popcll(vb[j]);
+    }
+    if (nv == 0) {
+        set_err(E, g, -5);
+        return;
+    }
+    int action = -1;
+    if (kind == 1) {
+        BlockRng rg{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
+        int pick = rng_randint(rg, 0, nv);
+        rng_store(rg);
+#pragma unroll
+        for (int j = 0; j < R::AJ; ++j) {
+            const int c = __popcll(vb[j]);
+            if (action < 0 && pick < c) {
+                uint64_t b = vb[j];
+                for (int k = 0; k < pick; ++k) b &= b - 1ull;
+                action = WAVE * j + __ffsll((unsigned long long)b) - 1;
+            }
+            if (action < 0) pick -= c;
+        }
+    } else {
+        int best = -0x7fffffff;
+        const bool on = lane < R::CELLS;
+        for (int j = 0; j < R::AJ; ++j) {
+            for (uint64_t b = vb[j]; b; b &= b - 1ull) {
+                const int a = WAVE * j + __ffsll((unsigned long long)b) - 1;
+                Pos q = p;
+                R::apply(q, a, E.max_turns);
+                const int sc = __popcll(__ballot(on && q.cell * p.player > 0)) -
+                               __popcll(__ballot(on && q.cell * p.player < 0));
+                if (sc >= best) {
+                    best = sc;
+                    action = a;
+                }
+            }
+        }
+    }
+    const int m = E.moves[g];
+    if (m < E.max_moves && lane == 0) {
+        E.rec_action[(size_t)g * E.max_moves + m] = action;
+        E.rec_temp[(size_t)g * E.max_moves + m] = 0;
+    }
+    commit_move<R>(E, g, p, action, m);
+}
+
 // Root visit counts of one slot (drop-in MCTS.getActionProb, MCTS.py:48-49).
 template <class R>
 __global__ __launch_bounds__(WAVE) void root_counts_kernel(Dev E, int g, int32_t* out) {
@@ -925,6 +1037,7 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Dev E, uint32_t seed_base, 
     if (lane == 0) {
         E.turn[g] = 0;
         E.player[g] = 1;
+        E.searcher[g] = 0;
         E.outcome[g] = ONGOING;
         E.active[g] = 1;
         E.moves[g] = 0;
@@ -1003,9 +1116,140 @@ __global__ __launch_bounds__(256) void stats_kernel(Dev E, long long* out) {
     }
 }
 
+// ------------------------------------------------------ training examples
+// Coach.executeEpisode's example list (Coach.py:74-90) rebuilt from compact
+// move records (moves, actions, root counts): replay_kernel re-plays every
+// game from the initial position (one wave per game), keeping each move's
+// root key and player and the final outcome; emit_kernel then writes the
+// game.symmetries() forms of each move's planes and policy with its label.
+
+// per-game status: > 0 finished game of that many moves, 0 unfinished/empty, -1 bad record
+template <class R>
+__global__ __launch_bounds__(WAVE) void replay_kernel(ExampleArgs X) {
+    const int g = blockIdx.x, lane = lane_id();
+    Pos p;
+    p.cell = lane < R::CELLS ? R::initial_cell(lane) : 0;
+    p.turn = 0;
+    p.player = 1;
+    p.outcome = ONGOING;
+    const int L = X.moves[g];
+    int status = (L < 0 || L > X.MM) ? -1 : L;
+    for (int m = 0; m < L && status > 0; ++m) {
+        if (p.outcome != ONGOING) {  // record runs past the end of the game
+            status = -1;
+            break;
+        }
+        uint64_t own, opp;
+        int kt, cs;
+        R::key(p, own, opp, kt, cs);
+        const int a = X.actions[(size_t)g * X.MM + m];
+        if (a < 0 || a >= R::A || !R::valid(a, R::vctx(own, opp, cs))) {
+            status = -1;
+            break;
+        }
+        if (lane == 0) X.keys[(size_t)g * X.MM + m] = MoveKey{own, opp, kt, cs | (p.player > 0 ? 2 : 0)};
+        R::apply(p, a, X.max_turns);
+    }
+    if (status > 0 && p.outcome == ONGOING) status = 0;
+    if (lane == 0) {
+        X.status[g] = status;
+        X.zval[g] = (float)outcome_value(p.outcome);  // result.value (flags.py:32-36)
+        X.zplayer[g] = p.player;                      // game.player after the last move
+    }
+}
+
+// Coach.py:79 player list: after move m (0-based) it holds S (m+1)(m+2)/2
+// entries, so example el of the game is labelled with the player of move mb,
+// the first with S (mb+1)(mb+2)/2 > el
+__device__ __forceinline__ int label_move(long long el, int S) {
+    int mb = (int)((sqrt(8.0 * (double)el / S + 1.0) - 1.0) * 0.5);
+    while ((long long)S * (mb + 1) * (mb + 2) / 2 <= el) ++mb;
+    while (mb > 0 && (long long)S * mb * (mb + 1) / 2 > el) --mb;
+    return mb;
+}
+
+// one 256-thread block per (game g >= g0, move m); writes the move's R::NSYM examples
+// that fall inside the kept window [skip, skip + maxlen)
+template <class R>
+__global__ __launch_bounds__(256) void emit_kernel(ExampleArgs X) {
+    __shared__ float s_pi[R::AP];
+    __shared__ long long s_part[4];
+    const int g = X.g0 + blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
+    const int L = X.status[g];
+    if (L <= 0 || m >= L) return;
+    const long long e0 = X.base[g] + (long long)R::NSYM * m;
+    if (e0 + R::NSYM <= X.skip) return;
+    const size_t row = (size_t)g * X.MM + m;
+    const int temp = (m + 1) < X.temp_threshold;  // episodeStep < tempThreshold (Coach.py:68)
+    const int action = X.actions[row];
+    long long part = 0;
+    for (int a = tid; a < R::A; a += 256) {
+        const int c = X.counts16 ? (int)X.counts16[row * R::A + a] : X.counts32[row * R::A + a];
+        s_pi[a] = (float)c;  // exact: counts < 2^24
+        part += c;
+    }
+    if (temp) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+        if ((tid & 63) == 0) s_part[tid >> 6] = part;
+    }
+    __syncthreads();
+    // getActionProb (MCTS.py:51-60): counts / counts.sum() in f64, or the one-hot
+    // of the sampled action; the trainer reads it as f32 (NNet.py:55)
+    if (temp) {
+        const double tot = (double)(s_part[0] + s_part[1] + s_part[2] + s_part[3]);
+        float v[(R::A + 255) / 256];
+#pragma unroll
+        for (int i = 0; i < (R::A + 255) / 256; ++i) {
+            const int a = tid + 256 * i;
+            if (a < R::A) v[i] = (float)((double)s_pi[a] / tot);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < (R::A + 255) / 256; ++i) {
+            const int a = tid + 256 * i;
+            if (a < R::A) s_pi[a] = v[i];
+        }
+    } else {
+        for (int a = tid; a < R::A; a += 256) s_pi[a] = a == action ? 1.0f : 0.0f;
+    }
+    __syncthreads();
+    const MoveKey k = X.keys[row];
+    const int cs = k.cp & 1;
+    const float zv = X.zval[g];
+    const int zp = X.zplayer[g];
+    for (int s = 0; s < R::NSYM; ++s) {
+        const long long e = e0 + s;
+        if (e < X.skip) continue;
+        const long long o = e - X.skip;
+        float* pl = X.planes + o * (R::PLANES * R::CELLS);
+        for (int t = tid; t < R::PLANES * R::CELLS; t += 256) {
+            const int q = t / R::CELLS, c = t - q * R::CELLS;
+            pl[t] = R::plane(q, R::form_src(s, c), k.own, k.opp, k.kt, cs);
+        }
+        float* pi = X.pis + o * R::A;
+        for (int a = tid; a < R::A; a += 256) pi[a] = s_pi[R::form_action_src(s, a)];
+        if (tid == 0) {
+            const long long el = (long long)R::NSYM * m + s;
+            const int mb = X.label_mode == 0 ? label_move(el, R::NSYM) : m;
+            const int player = (X.keys[(size_t)g * X.MM + mb].cp & 2) ? 1 : -1;
+            X.vs[o] = player == zp ? zv : -zv;
+        }
+    }
+}
+
 // ------------------------------------------------------------- launchers
 template <class R>
 struct Impl {
+    static hipError_t replay(const ExampleArgs& X, hipStream_t st) {
+        hipLaunchKernelGGL(replay_kernel<R>, dim3(X.G), dim3(WAVE), 0, st, X);
+        return hipGetLastError();
+    }
+    static hipError_t emit(const ExampleArgs& X, hipStream_t st) {
+        if (X.G - X.g0 <= 0) return hipSuccess;
+        hipLaunchKernelGGL(emit_kernel<R>, dim3(X.G - X.g0, X.MM), dim3(256), 0, st, X);
+        return hipGetLastError();
+    }
     static hipError_t select(const Dev& E, float* planes, hipStream_t st) {
         hipLaunchKernelGGL(select_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, planes);
         return hipGetLastError();
@@ -1020,6 +1264,10 @@ struct Impl {
     }
     static hipError_t move_end(const Dev& E, hipStream_t st) {
         hipLaunchKernelGGL(move_end_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E);
+        return hipGetLastError();
+    }
+    static hipError_t opponent(const Dev& E, int kind, hipStream_t st) {
+        hipLaunchKernelGGL(opponent_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, kind);
         return hipGetLastError();
     }
     static hipError_t root_counts(const Dev& E, int g, int32_t* out, hipStream_t st) {
@@ -1039,12 +1287,16 @@ static GameOps make_ops() {
     o.actions = R::A;
     o.row = R::AP;
     o.planes = R::PLANES;
+    o.nsym = R::NSYM;
     o.select = &Impl<R>::select;
     o.stub_eval = &Impl<R>::stub_eval;
     o.expand_backup = &Impl<R>::expand_backup;
     o.move_end = &Impl<R>::move_end;
     o.root_counts = &Impl<R>::root_counts;
     o.reset = &Impl<R>::reset;
+    o.opponent = &Impl<R>::opponent;
+    o.replay = &Impl<R>::replay;
+    o.emit = &Impl<R>::emit;
     return o;
 }
 

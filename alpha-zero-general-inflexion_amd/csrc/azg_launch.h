@@ -10,17 +10,46 @@
 
 namespace azg {
 
+// root key + player of one recorded move (examples pipeline)
+struct MoveKey {
+    uint64_t own, opp;
+    int32_t kt;  // turn (Inflexion) / disc count (Othello)
+    int32_t cp;  // bit0 can_spawn, bit1 player to move is RED (+1)
+};
+
+// arguments of the replay / emit kernels (azg_examples)
+struct ExampleArgs {
+    int G, MM, max_turns, temp_threshold, label_mode, g0;
+    const int32_t* moves;     // [G]
+    const int32_t* actions;   // [G*MM]
+    const int16_t* counts16;  // [G*MM*A] (one of the two)
+    const int32_t* counts32;
+    MoveKey* keys;            // [G*MM] scratch
+    int32_t* status;          // [G]
+    float* zval;              // [G]
+    int32_t* zplayer;         // [G]
+    const long long* base;    // [G] first example index of each game
+    long long skip;           // examples before the kept window
+    float* planes;            // [maxlen, PLANES*CELLS]
+    float* pis;               // [maxlen, A]
+    float* vs;                // [maxlen]
+};
+
 struct GameOps {
     int cells;    // board cells (lanes in use)
     int actions;  // A = max_actions
     int row;      // per-node action stride (A rounded up to 64)
     int planes;   // NN input planes per cell
+    int nsym;     // forms in game.symmetries()
     hipError_t (*select)(const Dev&, float* planes, hipStream_t);
     hipError_t (*stub_eval)(const Dev&, const float* planes, float* P, float* v, hipStream_t);
     hipError_t (*expand_backup)(const Dev&, const float* P, int p_stride, const float* v, hipStream_t);
     hipError_t (*move_end)(const Dev&, hipStream_t);
     hipError_t (*root_counts)(const Dev&, int g, int32_t* out, hipStream_t);
     hipError_t (*reset)(const Dev&, uint32_t seed_base, long long first_game, hipStream_t);
+    hipError_t (*opponent)(const Dev&, int kind, hipStream_t);
+    hipError_t (*replay)(const ExampleArgs&, hipStream_t);
+    hipError_t (*emit)(const ExampleArgs&, hipStream_t);
 };
 
 // kind: AZG_GAME_INFLEXION (n = 7) or AZG_GAME_OTHELLO (n = 6, 8)

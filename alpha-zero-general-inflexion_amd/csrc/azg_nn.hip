@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256, MINB) void conv3x3_bias_relu_kernel(
 // [16 k][128 n] read with the same k permutation.  Per wave and stage: 2 A + 2 B
 // global_load_lds (16 B/lane); stage ks+2 is issued right after the barrier
 // that publishes stage ks, so two stages are always in flight.
-constexpr int R_BK = 16, R_BN = 128, R_ASTAGE = CBM * R_BK, R_STAGE = R_ASTAGE + R_BK * R_BN, R_NBUF = 3;
+constexpr int R_BK = 16, R_BN = 128, R_ASTAGE = CBM * R_BK, R_STAGE = R_ASTAGE + R_BK * R_BN;  // 3 ring slots
 
 __global__ __launch_bounds__(256, 3) void conv3x3_ring_kernel(const float* __restrict__ x, const float* __restrict__ wt,
                                                               const float* __restrict__ bias, float* __restrict__ y,

@@ -10,9 +10,10 @@ iteration's examples and trains -- two collectives run over RCCL (backend
     (all_gather of per-rank sizes, then one all_gather of padded buffers);
   * broadcast of the trainer's weights (one flat f32 buffer, ~50 MB).
 
-A compact move record is (moves made, actions, temperatures, root visit
-counts as int16) per game: enough to rebuild every training example
-(Coach.py:74-90) by replaying the actions from the initial position.
+A compact move record is (moves made, actions, root visit counts as int16 --
+int32 if any count exceeds 32767) per game: enough to rebuild every training
+example (Coach.py:74-90) by replaying the actions from the initial position
+(examples.examples_from_records; temperatures follow from tempThreshold).
 """
 import ctypes
 
@@ -21,8 +22,6 @@ import torch.distributed as dist
 from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
 
 from . import _lib
-
-A = 343
 
 
 class _DevArray:
@@ -43,38 +42,42 @@ def engine_records(engine):
     actions = torch.as_tensor(_DevArray(ptrs[5], (G, MM), "<i4"), device=dev)
     counts = None
     if ptrs[6]:
-        counts = torch.as_tensor(_DevArray(ptrs[6], (G, MM, A), "<i4"), device=dev)
+        counts = torch.as_tensor(_DevArray(ptrs[6], (G, MM, engine.A), "<i4"), device=dev)
     return moves, actions, counts
 
 
 def gather_records(engine, dst=0, group=None):
     """Gather compact move records of all ranks (moves made so far) to `dst`.
-    Returns (moves [W*G], actions [W*G, m], counts [W*G, m, A] int16) on dst, None elsewhere,
-    and the bytes this rank sent."""
+    Returns (moves [W*G], actions [W*G, m], counts [W*G, m, A] int16/int32) on dst, None
+    elsewhere, and the bytes this rank sent."""
     moves, actions, counts = engine_records(engine)
-    return gather_record_tensors(moves, actions, counts, dst, group)
+    return gather_record_tensors(moves, actions, counts, dst, group, actions_per_move=engine.A)
 
 
-def gather_record_tensors(moves, actions, counts, dst=0, group=None):
+def gather_record_tensors(moves, actions, counts, dst=0, group=None, actions_per_move=343):
     """gather_records on plain tensors (any device the group's backend serves)."""
-    m_local = torch.max(moves).reshape(1).to(torch.int64)
+    A = counts.shape[2] if counts is not None else int(actions_per_move)
+    m_local = torch.stack([torch.max(moves).to(torch.int64),
+                           (counts.max() if counts is not None and counts.numel() else moves.new_zeros(())).to(
+                               torch.int64)])
     m_all = m_local.clone()
     dist.all_reduce(m_all, op=dist.ReduceOp.MAX, group=group)
-    m = int(m_all.item())
+    m, cmax = (int(x) for x in m_all.tolist())
+    ctype = torch.int16 if cmax <= 32767 else torch.int32
     ws = dist.get_world_size(group)
     G = moves.shape[0]
     act = actions[:, :m].contiguous()
-    cnt = counts[:, :m].to(torch.int16).contiguous() if counts is not None else torch.zeros(
-        (G, m, A), dtype=torch.int16, device=moves.device)
+    cnt = counts[:, :m].to(ctype).contiguous() if counts is not None else torch.zeros(
+        (G, m, A), dtype=ctype, device=moves.device)
     mv = moves.clone()
     out_mv = torch.empty((ws * G,), dtype=mv.dtype, device=mv.device)
     out_act = torch.empty((ws * G, m), dtype=act.dtype, device=act.device)
     out_cnt = torch.empty((ws * G, m, A), dtype=cnt.dtype, device=cnt.device)
     dist.all_gather_into_tensor(out_mv, mv, group=group)
     dist.all_gather_into_tensor(out_act, act, group=group)
-    # RCCL/gloo have no int16 type: move the counts as raw bytes
+    # moved as raw bytes (RCCL/gloo have no int16 type)
     dist.all_gather_into_tensor(out_cnt.view(torch.uint8), cnt.view(torch.uint8), group=group)
-    sent = mv.numel() * 4 + act.numel() * 4 + cnt.numel() * 2
+    sent = mv.numel() * 4 + act.numel() * 4 + cnt.numel() * cnt.element_size()
     if dist.get_rank(group) == dst:
         return (out_mv, out_act, out_cnt), sent
     return None, sent

@@ -48,7 +48,7 @@ def _ptr(t):
 class SelfPlayEngine:
     def __init__(self, num_games, *, sims=25, cpuct=1, temp_threshold=30, max_turns=343, seed_base=0,
                  first_game=0, evaluator="stub", device=None, node_capacity=0, max_depth=0, record=True,
-                 gc=True, max_moves=0, game="inflexion", n=None):
+                 gc=True, max_moves=0, game="inflexion", n=None, arena=False):
         if not torch.cuda.is_available():
             raise _lib.AzgError("SelfPlayEngine needs a HIP device (no CPU fallback)")
         if game not in GAMES:
@@ -72,7 +72,8 @@ class SelfPlayEngine:
                               seed_base=int(seed_base) & 0xFFFFFFFF, pad0=0, first_game=int(first_game),
                               node_capacity=int(node_capacity), max_depth=int(max_depth),
                               max_moves=int(max_moves),
-                              flags=(_lib.FLAG_GC if gc else 0) | (_lib.FLAG_RECORD if record else 0))
+                              flags=(_lib.FLAG_GC if gc else 0) | (_lib.FLAG_RECORD if record else 0)
+                              | (_lib.FLAG_ARENA if arena else 0))
             self.cfg = cfg
             h = ctypes.c_void_p()
             check(self.L.azg_create(ctypes.byref(cfg), self._stream(), ctypes.byref(h)))
@@ -172,6 +173,20 @@ class SelfPlayEngine:
         fg = self.cfg.first_game if first_game is None else int(first_game)
         self.cfg.seed_base, self.cfg.first_game = sb, fg
         check(self.L.azg_reset(self.h, sb, fg, self._stream()))
+
+    # ------------------------------------------------------------------ arena
+    def set_arena(self, searcher, first_player):
+        """Per slot: colour the search plays and colour to move first (+1 RED / -1 BLUE)."""
+        s = np.ascontiguousarray(searcher, np.int32)
+        f = np.ascontiguousarray(first_player, np.int32)
+        if s.shape != (self.G,) or f.shape != (self.G,):
+            raise ValueError("searcher / first_player need one entry per slot")
+        check(self.L.azg_set_arena(self.h, s.ctypes.data, f.ctypes.data, self._stream()))
+
+    def opponent_move(self, kind):
+        """The baseline player's move in every slot where it is to move."""
+        code = {"random": _lib.OPPONENT_RANDOM, "greedy": _lib.OPPONENT_GREEDY}[kind]
+        check(self.L.azg_opponent_move(self.h, code, self._stream()))
 
     # ------------------------------------------------------------------ results
     def read_moves(self, counts=True):

@@ -219,6 +219,37 @@ class NNetWrapper:
                 (l_pi + l_v).backward()
                 opt.step()
 
+    def train_examples(self, ex):
+        """NNet.py:36-76 on an ExampleSet already resident on the device: the same
+        Adam, epochs and batch draws (np.random.randint on numpy's global stream,
+        so the sampled batches are the reference's), with the batch gathered on
+        the GPU instead of converted from Python lists.  Returns per-batch
+        (l_pi, l_v) as a device tensor [batches, 2] (one host sync at the end)."""
+        opt = torch.optim.Adam(self.nnet.parameters())
+        bs = self.args["batch_size"]
+        E = len(ex)
+        nb = int(E / bs)
+        losses = torch.zeros((self.args["epochs"] * nb, 2), dtype=torch.float32, device=self.device)
+        planes = ex.planes.to(self.device)
+        pis = ex.pis.to(self.device)
+        vs = ex.vs.to(self.device)
+        k = 0
+        for _ in range(self.args["epochs"]):
+            self.nnet.train()
+            for _ in range(nb):
+                ids = torch.from_numpy(np.random.randint(E, size=bs)).to(self.device)
+                out_pi, out_v = self.nnet(planes[ids])
+                tp, tv = pis[ids], vs[ids]
+                l_pi = -torch.sum(tp * out_pi) / tp.size()[0]
+                l_v = torch.sum((tv - out_v.view(-1)) ** 2) / tv.size()[0]
+                opt.zero_grad()
+                (l_pi + l_v).backward()
+                opt.step()
+                losses[k, 0] = l_pi.detach()
+                losses[k, 1] = l_v.detach()
+                k += 1
+        return losses
+
     def save_checkpoint(self, folder="checkpoint", filename="checkpoint.pth.tar"):
         os.makedirs(folder, exist_ok=True)
         torch.save({"state_dict": self.nnet.state_dict()}, os.path.join(folder, filename))

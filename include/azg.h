@@ -32,12 +32,17 @@ extern "C" {
 
 #define AZG_ABI_VERSION 1
 
-enum azg_game_kind { AZG_GAME_INFLEXION = 1 };
+enum azg_game_kind { AZG_GAME_INFLEXION = 1, AZG_GAME_OTHELLO = 2 };
 
 enum azg_flags {
     AZG_FLAG_GC = 1,          /* free nodes whose turn < root turn at move end */
     AZG_FLAG_RECORD = 2,      /* keep per-move root counts (training examples)  */
+    AZG_FLAG_ARENA = 4,       /* arena play: the searcher takes the argmax of the
+                                 one-hot policy (MCTSPlayer, InflexionPlayers.py:88),
+                                 no sampling draw (Coach.py:81)                   */
 };
+
+enum azg_opponent { AZG_OPPONENT_RANDOM = 1, AZG_OPPONENT_GREEDY = 2 };
 
 enum azg_err {
     AZG_OK = 0,
@@ -50,8 +55,8 @@ enum azg_err {
 };
 
 typedef struct {
-    int32_t game_kind;        /* AZG_GAME_INFLEXION                               */
-    int32_t n;                /* board side; InflexionGame(n) -- 7                */
+    int32_t game_kind;        /* AZG_GAME_INFLEXION / AZG_GAME_OTHELLO            */
+    int32_t n;                /* board side: InflexionGame 7, OthelloGame 6 or 8  */
     int32_t max_turns;        /* InflexionGame max_turns (main.py:34: 343)        */
     int32_t num_games;        /* G concurrent game slots on this device           */
     int32_t sims;             /* args.numMCTSSims                                 */
@@ -134,6 +139,43 @@ int  azg_conv3x3_variant(int variant, const float* x, const float* wt, const flo
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active
  * [5] record actions [6] record counts [7] moves */
 int  azg_device_ptrs(azg_engine* e, void** out /*[8]*/);
+
+/* Batched Arena (Arena.py:38-142 with MCTSPlayer vs a baseline player,
+ * Coach.py:158-165).  After azg_reset, azg_set_arena gives every slot the
+ * colour the search plays (searcher[g] = +1 RED / -1 BLUE) and the colour to
+ * move first (first_player[g], Arena.playGame's game.player = player1).  The
+ * engine then searches (sim_begin / sim_end / move_end, with temp_threshold 0)
+ * only in slots where the searcher is to move, and azg_opponent_move plays the
+ * baseline's move (AZG_OPPONENT_RANDOM: RandomPlayer, np.random.choice of the
+ * valid actions on the slot's stream; AZG_OPPONENT_GREEDY: GreedyPlayer,
+ * InflexionPlayers.py:61-74) in the others.  Needs AZG_FLAG_ARENA. */
+int  azg_set_arena(azg_engine* e, const int32_t* searcher /*[G] host*/, const int32_t* first_player /*[G] host*/,
+                   void* stream);
+int  azg_opponent_move(azg_engine* e, int32_t kind, void* stream);
+
+/* Sizes of a supported game: out[0] cells, [1] actions (max_actions), [2] NN
+ * input planes, [3] forms returned by game.symmetries(). */
+int  azg_game_info(int32_t game_kind, int32_t n, int32_t* out /*[4]*/);
+
+/* Training examples from compact move records -- Coach.executeEpisode's
+ * example list (Coach.py:74-90) with game.symmetries() (InflexionGame.py:102-113)
+ * for every finished game, in the reference's order (game, move, symmetry form),
+ * keeping the LAST maxlen like the per-iteration deque(maxlen=maxlenOfQueue)
+ * (Coach.py:107).  Records (device): moves [G], actions [G,max_moves], root visit
+ * counts [G,max_moves,A] as int16 (counts_bytes 2) or int32 (4) -- what
+ * azg_read_moves / the rank gather hold.  Each game is replayed from the initial
+ * position; a record that is not a legal game fails with AZG_ERR_ARG; unfinished
+ * games (moves < max_moves cap) contribute nothing.  Outputs (device, f32, as the
+ * trainer reads them, NNet.py:54-56): planes [maxlen, planes, n, n], pis
+ * [maxlen, A] (counts / sum in f64 for temp 1, one-hot of the played action for
+ * temp 0), vs [maxlen] (+-outcome value).  label_mode 0 labels as Coach.py:79
+ * does (player list grown by the cumulative example count), 1 labels each
+ * example with its own move's player.  *count = examples written.  Synchronises
+ * the stream. */
+int  azg_examples(int32_t game_kind, int32_t n, int32_t max_turns, int32_t temp_threshold, int32_t num_games,
+                  int32_t max_moves, const int32_t* moves, const int32_t* actions, const void* counts,
+                  int32_t counts_bytes, int32_t label_mode, int64_t maxlen, float* planes, float* pis,
+                  float* vs, int64_t* count, void* stream);
 
 #ifdef __cplusplus
 }

@@ -19,6 +19,7 @@ Fixtures written (all small, gzip'd JSON or npz):
   rules_kat.npz          random playouts: board, turn, action, valid mask, outcome
   pairwise_kat.npz       numpy f32 pairwise .sum() known answers
   mcts_<set>.json.gz     Coach.executeEpisode + MCTS traces driven by stubnet
+  arena_<set>.json.gz    Arena.playGame MCTSPlayer(stubnet) vs Random/Greedy players
   nnet_golden.npz        InflexionNNet(manual_seed 0) checksum + (planes -> P, v)
 """
 import gzip
@@ -276,6 +277,66 @@ def gen_mcts(np, quick, othello=False):
     GameCls.to_next_state = orig_tns
 
 
+# -------------------------------------------------------------------------- Arena
+def gen_arena(np):
+    """Reference Arena.playGame (Arena.py:38-88) between MCTSPlayer (stub
+    evaluator) and RandomPlayer / GreedyPlayer, one game per seed: game i of a
+    set is seeded np.random.seed(seed_base + i) and gets the colour order
+    Arena.playGames gives index i (Arena.py:126-129).  Records every move
+    played and the result counters."""
+    import MCTS as mcts_mod
+    from Arena import Arena
+    from flags import PlayerColour
+    from inflexion.InflexionGame import InflexionGame
+    from inflexion.InflexionPlayers import GreedyPlayer, MCTSPlayer, RandomPlayer
+    from inflexion.pytorch.NNet import NNetWrapper
+    from utils import dotdict
+    from stubnet import stub_eval
+
+    class StubNNet(NNetWrapper):
+        def __init__(self, game):
+            self.n_actions = game.max_actions
+
+        def predict(self, board):
+            return stub_eval(board, self.n_actions)
+
+    played = []
+    wrapped = {}
+    for cls in (MCTSPlayer, RandomPlayer, GreedyPlayer):
+        orig = cls.play
+        wrapped[cls] = orig
+
+        def play(self, game, _orig=orig):
+            a = _orig(self, game)
+            played.append(int(a))
+            return a
+        cls.play = play
+    sets = {
+        "arena_random": dict(opponent="random", max_turns=100, sims=25, cpuct=1, num=8, seed_base=800),
+        "arena_greedy": dict(opponent="greedy", max_turns=100, sims=25, cpuct=1, num=8, seed_base=900),
+    }
+    red, blue = list(PlayerColour)
+    for name, cfg in sets.items():
+        game = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
+        args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"]})
+        opp = RandomPlayer() if cfg["opponent"] == "random" else GreedyPlayer()
+        arena = Arena(MCTSPlayer(mcts_mod.MCTS(StubNNet(game), args)), opp, game)
+        games = []
+        t0 = time.time()
+        for i in range(cfg["num"]):
+            p1, p2 = (red, blue) if i <= cfg["num"] // 2 else (blue, red)
+            np.random.seed(cfg["seed_base"] + i)
+            played.clear()
+            wins, draws = arena.playGame(p1, p2)
+            games.append({"first": p1.num, "actions": list(played), "red_wins": wins[red],
+                          "blue_wins": wins[blue], "draws": draws})
+            print(f"  {name} game {i}: {len(played)} moves, red {wins[red]} blue {wins[blue]} draw {draws}, "
+                  f"{time.time() - t0:.1f}s", flush=True)
+        _dump(f"{name}.json.gz", {"config": cfg, "games": games})
+    for cls, orig in wrapped.items():
+        cls.play = orig
+
+
 # -------------------------------------------------------------------------- NNet
 def gen_nnet(np, InflexionGame):
     import torch
@@ -327,6 +388,7 @@ def main():
         "nnet": lambda: gen_nnet(np, InflexionGame),
         "mcts": lambda: gen_mcts(np, quick),
         "othello": lambda: gen_mcts(np, quick, othello=True),
+        "arena": lambda: gen_arena(np),
     }
     for name, fn in jobs.items():
         if only and name not in only:

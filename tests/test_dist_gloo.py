@@ -46,6 +46,13 @@ def _worker(rank, world, port, q):
         res["bcast_ok"] = all(torch.equal(a, b) for a, b in zip(net.state_dict().values(),
                                                                   ref.state_dict().values()))
         res["bcast_bytes"] = nbytes
+        # a root count above int16: the gather switches to int32 on every rank
+        big = counts.clone()
+        big[0, 0, 0] = 40000 if rank == 1 else 7
+        out2, sent2 = ad.gather_record_tensors(moves, actions, big, dst=0)
+        res["sent2"] = sent2
+        if rank == 0:
+            res["big_ok"] = out2[2].dtype == torch.int32 and int(out2[2][G, 0, 0]) == 40000
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -68,3 +75,4 @@ def test_gather_and_broadcast_world2():
     assert r0["act_ok"] and r0["cnt_ok"]
     assert res[0]["bcast_ok"] and res[1]["bcast_ok"]
     assert res[1]["bcast_bytes"] == res[0]["bcast_bytes"] > 0
+    assert r0["big_ok"] and res[1]["sent2"] > res[1]["sent"]
