@@ -333,6 +333,7 @@ struct Inflexion {
     // symmetries() (InflexionGame.py:102-113), form s: identity, rotate(s) for
     // s = 1..5, then translate(rotate(k), j, 'r') for k = 1..5, j = 1..n-1
     static constexpr int NSYM = 6 + 5 * (N - 1);
+    static constexpr int SYM_ACTIONS = A;  // every action is a (move kind, cell)
     __device__ static int form_src(int s, int c) {
         if (s < 6) return sym_src(c, s, 0, 0);
         return sym_src(c, 1 + (s - 6) / (N - 1), 1 + (s - 6) % (N - 1), 0);
@@ -463,6 +464,7 @@ struct Othello {
     // symmetries(): the 8 dihedral forms k (k & 3 rot90s, then fliplr if k & 4);
     // source cell of output cell c
     static constexpr int NSYM = 8;
+    static constexpr int SYM_ACTIONS = CELLS;  // the pass action is not moved
     __device__ static int form_src(int k, int c) {
         const int i = c / N, j = (k & 4) ? N - 1 - c % N : c % N;
         int sr, sq;
@@ -1174,6 +1176,7 @@ template <class R>
 __global__ __launch_bounds__(256) void emit_kernel(ExampleArgs X) {
     __shared__ float s_pi[R::AP];
     __shared__ long long s_part[4];
+    __shared__ uint8_t s_src[R::NSYM * R::CELLS];
     const int g = X.g0 + blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
     const int L = X.status[g];
     if (L <= 0 || m >= L) return;
@@ -1218,23 +1221,33 @@ __global__ __launch_bounds__(256) void emit_kernel(ExampleArgs X) {
     const int cs = k.cp & 1;
     const float zv = X.zval[g];
     const int zp = X.zplayer[g];
-    for (int s = 0; s < R::NSYM; ++s) {
-        const long long e = e0 + s;
-        if (e < X.skip) continue;
-        const long long o = e - X.skip;
-        float* pl = X.planes + o * (R::PLANES * R::CELLS);
-        for (int t = tid; t < R::PLANES * R::CELLS; t += 256) {
-            const int q = t / R::CELLS, c = t - q * R::CELLS;
-            pl[t] = R::plane(q, R::form_src(s, c), k.own, k.opp, k.kt, cs);
-        }
-        float* pi = X.pis + o * R::A;
-        for (int a = tid; a < R::A; a += 256) pi[a] = s_pi[R::form_action_src(s, a)];
-        if (tid == 0) {
-            const long long el = (long long)R::NSYM * m + s;
-            const int mb = X.label_mode == 0 ? label_move(el, R::NSYM) : m;
-            const int player = (X.keys[(size_t)g * X.MM + mb].cp & 2) ? 1 : -1;
-            X.vs[o] = player == zp ? zv : -zv;
-        }
+    // the move's examples e0 + s (s = s_lo..NSYM-1 inside the window) are
+    // consecutive rows of planes / pis / vs: write them as three flat,
+    // fully coalesced ranges, gathering through an LDS table of symmetry sources
+    const int s_lo = e0 < X.skip ? (int)(X.skip - e0) : 0;
+    const long long o0 = e0 + s_lo - X.skip;
+    for (int t = tid; t < (R::NSYM - s_lo) * R::CELLS; t += 256) {
+        const int s = s_lo + t / R::CELLS;
+        s_src[t] = (uint8_t)R::form_src(s, t - (t / R::CELLS) * R::CELLS);
+    }
+    __syncthreads();
+    constexpr int PC = R::PLANES * R::CELLS;
+    float* pl = X.planes + o0 * PC;
+    for (int t = tid; t < (R::NSYM - s_lo) * PC; t += 256) {
+        const int j = t / PC, r = t - j * PC, q = r / R::CELLS, c = r - q * R::CELLS;
+        pl[t] = R::plane(q, s_src[j * R::CELLS + c], k.own, k.opp, k.kt, cs);
+    }
+    float* pi = X.pis + o0 * R::A;
+    for (int t = tid; t < (R::NSYM - s_lo) * R::A; t += 256) {
+        const int j = t / R::A, a = t - j * R::A;
+        const int mv = a / R::CELLS, c = a - mv * R::CELLS;
+        pi[t] = s_pi[a < R::SYM_ACTIONS ? mv * R::CELLS + s_src[j * R::CELLS + c] : a];
+    }
+    for (int j = tid; j < R::NSYM - s_lo; j += 256) {
+        const long long el = (long long)R::NSYM * m + s_lo + j;
+        const int mb = X.label_mode == 0 ? label_move(el, R::NSYM) : m;
+        const int player = (X.keys[(size_t)g * X.MM + mb].cp & 2) ? 1 : -1;
+        X.vs[o0 + j] = player == zp ? zv : -zv;
     }
 }
 
