@@ -104,13 +104,15 @@ class InferenceNet(nn.Module):
     outputs_probs = True
 
     def __init__(self, net: InflexionNNet, conv="miopen"):
-        """conv: "miopen" (MIOpen implicit GEMM + one fused bias/ReLU pass) or
-        "azg" (libazg's f32-MFMA implicit GEMM with the bias/ReLU in its
-        epilogue) for conv2-4; measured side by side in profiles/r01_conv_probe.json."""
+        """conv: "miopen" (MIOpen implicit GEMM + one fused bias/ReLU pass), "azg"
+        (libazg's f32-MFMA implicit GEMM with the bias/ReLU in its epilogue) or
+        "auto" (per layer and input shape, whichever measured faster on first use)
+        for conv2-4; measured side by side in profiles/r01_conv_probe*.json."""
         super().__init__()
-        if conv not in ("miopen", "azg"):
+        if conv not in ("miopen", "azg", "auto"):
             raise ValueError(f"unknown conv implementation {conv!r}")
         self.conv_impl = conv
+        self._choices = {}
         self.n, self.depth, c = net.n, net.depth, net.num_channels
         self.pads = []
         for i in range(1, 5):
@@ -138,26 +140,59 @@ class InferenceNet(nn.Module):
     # bracket each convolution with HIP events on the current stream
     conv_hook = None
 
+    def _conv_miopen(self, x, i, pad):
+        # MIOpen conv without bias, then one HIP pass: bias + ReLU in place (azg_nn.hip)
+        x = F.conv2d(x, getattr(self, f"w{i}"), None, padding=pad)
+        return _bias_relu_(x, getattr(self, f"b{i}"))
+
+    def _conv_azg(self, x, i, pad):
+        # bias + ReLU inside the libazg conv's epilogue
+        return _azg_conv3x3(x, getattr(self, f"wt{i}"), getattr(self, f"b{i}"), pad)
+
+    def _pick(self, x, i, pad):
+        """conv="auto": time both implementations once per (layer, input shape) and
+        keep the faster (like cudnn.benchmark).  Never inside a graph capture: an
+        unmeasured shape there takes MIOpen."""
+        key = (i, tuple(x.shape))
+        choice = self._choices.get(key)
+        if choice is not None:
+            return choice
+        if torch.cuda.is_current_stream_capturing():
+            return "miopen"
+        best = None
+        for name, fn in (("miopen", self._conv_miopen), ("azg", self._conv_azg)):
+            for _ in range(2):
+                fn(x, i, pad)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(3):
+                fn(x, i, pad)
+            ev[1].record()
+            ev[1].synchronize()
+            ms = ev[0].elapsed_time(ev[1])
+            if best is None or ms < best[1]:
+                best = (name, ms)
+        self._choices[key] = best[0]
+        return best[0]
+
     def forward(self, s):
         x = s.view(-1, self.depth, self.n, self.n).contiguous(memory_format=torch.channels_last)
         hook = self.conv_hook
         fused = x.is_cuda
         for i, pad in enumerate(self.pads, start=1):
+            impl = self.conv_impl if i > 1 else "miopen"
+            if fused and impl == "auto":
+                impl = self._pick(x, i, pad)
             if hook:
                 hook(i, "start")
-            b = getattr(self, f"b{i}")
-            if fused and self.conv_impl == "azg" and i > 1:  # bias + ReLU inside the conv's epilogue
-                x = _azg_conv3x3(x, getattr(self, f"wt{i}"), b, pad)
-                if hook:
-                    hook(i, "stop")
-                continue
-            x = F.conv2d(x, getattr(self, f"w{i}"), None if fused else b, padding=pad)
+            if not fused:
+                x = torch.relu_(F.conv2d(x, getattr(self, f"w{i}"), getattr(self, f"b{i}"), padding=pad))
+            elif impl == "azg":
+                x = self._conv_azg(x, i, pad)
+            else:
+                x = self._conv_miopen(x, i, pad)
             if hook:
                 hook(i, "stop")
-            if fused:  # one HIP pass: bias + ReLU in place (azg_nn.hip)
-                x = _bias_relu_(x, b)
-            else:
-                x = torch.relu_(x)
         x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten, no copy
         x = torch.relu_(torch.addmm(self.fb1, x, self.fw1.t()))
         x = torch.relu_(torch.addmm(self.fb2, x, self.fw2.t()))

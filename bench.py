@@ -94,8 +94,9 @@ def parse():
     p.add_argument("--sims", type=int, default=25)
     p.add_argument("--max-turns", type=int, default=343)
     p.add_argument("--evaluator", default="net", choices=["net", "stub"])
-    p.add_argument("--conv", default="miopen", choices=["miopen", "azg"],
-                   help="conv2-4 implementation of the inference net (MIOpen igemm or libazg f32-MFMA implicit GEMM)")
+    p.add_argument("--conv", default="miopen", choices=["auto", "miopen", "azg"],
+                   help="conv2-4 implementation of the inference net (MIOpen igemm + bias/ReLU pass, libazg f32-MFMA "
+                        "implicit GEMM with fused epilogue, or auto: per layer, the faster one measured at first use)")
     p.add_argument("--net", default="inference", choices=["inference", "reference"],
                    help="inference: BN-folded NHWC InferenceNet; reference: InflexionNNet as written")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -292,6 +293,15 @@ def main():
         conv_avg = conv_ms / n_forwards / 1e3 if conv_ms > 0 else nn_avg
         conv_flops = leaves * (conv_flop_leaf if conv_ms > 0 else flop_leaf)
         conv_tflops = conv_flops / conv_avg / 1e12 if conv_avg > 0 else 0.0
+        impls = {}
+        if hasattr(ev, "_choices") or getattr(ev, "conv_impl", None):
+            for i in (2, 3, 4):
+                impls[i] = (next((v for (li, _), v in ev._choices.items() if li == i), "miopen")
+                            if ev.conv_impl == "auto" else ev.conv_impl)
+        names = {"miopen": "MIOpen igemm_fwd_gtcx35_nhwc_fp32 + libazg bias/ReLU pass",
+                 "azg": "libazg f32-MFMA implicit GEMM (LDS-DMA ring) + fused bias/ReLU"}
+        conv_kernel_desc = ("conv2-4 per forward: " + "; ".join(f"conv{i} {names[m]}" for i, m in impls.items())
+                            if impls else "whole forward (no conv hook)")
         tree_s = (sel_ms + exp_ms) / 1e3
         row = ((A + 63) // 64) * 64  # node row stride (actions rounded up to 64 lanes)
         tree_gbs = (exp / world) * tree_bytes_per_sim(row) / tree_s / 1e9 if tree_s > 0 else 0.0
@@ -323,9 +333,7 @@ def main():
             "expansions": exp,
             "simulations": sims_run,
             "roofline": {"bound": "mfma",
-                         "kernel": ("conv2-4 f32 implicit GEMM (MIOpen igemm_fwd_gtcx35_nhwc_fp32) per forward"
-                                    if args.conv == "miopen" else
-                                    "conv2-4 f32-MFMA implicit GEMM + bias/ReLU epilogue (libazg conv3x3) per forward"),
+                         "kernel": conv_kernel_desc,
                          "achieved": conv_tflops, "peak": F32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                          "frac": conv_tflops / F32_MFMA_PEAK_TF, "traffic": None,
                          "per_launch": f"{leaves} leaves x {conv_flop_leaf / 1e6:.1f} MFLOP / {conv_avg * 1e3:.3f} ms "

@@ -127,11 +127,14 @@ int  azg_bias_relu_nhwc(float* x, const float* bias, int64_t rows, int32_t chann
  * folded-BN bias and ReLU fused (conv2-4 + bn2-4 + relu of InflexionNNet.forward,
  * InflexionNNet.py:43-45): x NHWC [batch, h_in, h_in, c_in], wt [9*c_in, c_out]
  * (k = (dy*3+dx)*c_in + c), y NHWC [batch, h_out, h_out, c_out] with
- * h_out = h_in + 2*pad - 2; c_in % 32 == 0, c_out % 128 == 0. */
+ * h_out = h_in + 2*pad - 2; c_in % 32 == 0, c_out % 128 == 0.  May allocate a
+ * split-K workspace on first use of a shape (not inside a graph capture). */
 int  azg_conv3x3_bias_relu_nhwc(const float* x, const float* wt, const float* bias, float* y, int32_t batch,
                                 int32_t h_in, int32_t pad, int32_t c_in, int32_t c_out, void* stream);
-/* Tuning hook: the same convolution with an explicit tile variant (0..3:
- * BNxBK 128x32, 128x16, 256x16, 256x32). */
+/* Tuning hook: the same convolution with an explicit variant: 0..3 register-
+ * staged A with BNxBK 128x32, 128x16, 256x16, 256x32; 4 LDS-DMA 3-slot ring
+ * (128x128x16, split-K tail; the default); 5 the ring with next-stage operand
+ * reads overlapping the current stage's MFMAs. */
 int  azg_conv3x3_variant(int variant, const float* x, const float* wt, const float* bias, float* y, int32_t batch,
                          int32_t h_in, int32_t pad, int32_t c_in, int32_t c_out, void* stream);
 

@@ -19,7 +19,7 @@ def test_bias_relu_kernel():
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("conv", ["miopen", "azg"])
+@pytest.mark.parametrize("conv", ["miopen", "azg", "auto"])
 def test_inference_net_vs_reference_gpu(conv):
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
@@ -70,7 +70,7 @@ def test_azg_conv3x3_matches_torch(B, H, pad):
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("B,H,pad", [(37, 7, 1), (129, 5, 0), (3, 6, 1)])
 def test_azg_conv3x3_variants(variant, B, H, pad):
     """Every libazg conv tile variant (incl. the LDS-DMA ring) on ragged pixel counts."""
