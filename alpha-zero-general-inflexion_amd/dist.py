@@ -84,13 +84,25 @@ def gather_record_tensors(moves, actions, counts, dst=0, group=None, actions_per
 
 
 def broadcast_weights(module, src=0, group=None):
-    """Broadcast every parameter and buffer of `module` from `src` as one flat buffer."""
-    tensors = [t for t in list(module.parameters()) + list(module.buffers()) if t.dtype == torch.float32]
-    flat = _flatten_dense_tensors([t.data for t in tensors])
+    """Broadcast every parameter and buffer of `module` from `src`: the f32 ones as
+    one flat buffer, the rest (BatchNorm's num_batches_tracked) as one int64 buffer."""
+    tensors = list(module.parameters()) + list(module.buffers())
+    f32 = [t for t in tensors if t.dtype == torch.float32]
+    rest = [t for t in tensors if t.dtype != torch.float32]
+    flat = _flatten_dense_tensors([t.data for t in f32])
     dist.broadcast(flat, src=src, group=group)
-    for t, f in zip(tensors, _unflatten_dense_tensors(flat, [t.data for t in tensors])):
+    for t, f in zip(f32, _unflatten_dense_tensors(flat, [t.data for t in f32])):
         t.data.copy_(f)
-    return flat.numel() * 4
+    nbytes = flat.numel() * 4
+    if rest:
+        ints = torch.cat([t.data.reshape(-1).to(torch.int64) for t in rest])
+        dist.broadcast(ints, src=src, group=group)
+        off = 0
+        for t in rest:
+            t.data.copy_(ints[off:off + t.numel()].reshape(t.shape).to(t.dtype))
+            off += t.numel()
+        nbytes += ints.numel() * 8
+    return nbytes
 
 
 def iteration_sync(engine, module, trainer=0, group=None):

@@ -1,0 +1,95 @@
+"""Two ranks on one GPU (gloo over device tensors): the per-iteration exchange
+of the self-play shards (dist.py) and Coach.learn's multi-rank iteration.
+
+RCCL refuses two ranks on one device, so this rehearses the N > 1 code path with
+gloo; the data moved and the results are the same, only the transport differs.
+Each rank plays games [rank*G, (rank+1)*G), so the gathered examples must equal
+one rank-free engine playing all 2G games."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class Args(dict):
+    __getattr__ = dict.__getitem__
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import azg_amd  # noqa: F401
+        from azg_amd import dist as ad
+        from azg_amd.coach import Coach
+        from azg_amd.engine import SelfPlayEngine
+        from azg_amd.examples import examples_from_records
+        from azg_amd.inflexion import InflexionGame
+        torch.cuda.set_device(0)
+        G = 6
+        eng = SelfPlayEngine(G, sims=6, max_turns=20, seed_base=3, first_game=rank * G)
+        eng.play()
+        rec, sent = ad.gather_records(eng, dst=0)
+        res = {"sent": sent}
+        if rank == 0:
+            mv, act, cnt = rec
+            ex = examples_from_records("inflexion", 7, 20, 30, mv, act, cnt, maxlen=10**9)
+            # numpy, not tensors: torch's queue shares tensor storage by fd with a process that exits
+            res["examples"] = (ex.planes.cpu().numpy(), ex.pis.cpu().numpy(), ex.vs.cpu().numpy())
+        eng.close()
+        # Coach.learn's self-play over both ranks: rank 0 trains, weights go back out
+        game = InflexionGame(7, max_turns=10, max_power=6)
+        from azg_amd.nnet import NNetWrapper
+        torch.manual_seed(rank)  # different weights until the broadcast
+        nnet = NNetWrapper(game, dict(epochs=1, batch_size=32, num_channels=8), device="cuda")
+        args = Args(numIters=2, numEps=4, tempThreshold=5, maxlenOfQueue=10**6, numMCTSSims=3, cpuct=1,
+                    arenaCompare=2, checkpoint="/tmp/azg_dist_ckpt_%d" % rank, numItersForTrainExamplesHistory=5,
+                    saveExamples=False)
+        c = Coach(game, nnet, args)
+        c.learn(pit=False)
+        res["hist"] = [len(h) for h in c.trainExamplesHistory]
+        res["w"] = {k: v.cpu().numpy() for k, v in nnet.nnet.state_dict().items()}
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_gather_and_learn():
+    import azg_amd  # noqa: F401
+    from azg_amd.engine import SelfPlayEngine
+    from azg_amd.examples import engine_examples
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # the gathered shards = one engine over all 12 games
+    eng = SelfPlayEngine(12, sims=6, max_turns=20, seed_base=3)
+    eng.play()
+    ref = engine_examples(eng, 30, maxlen=10**9)
+    planes, pis, vs = res[0]["examples"]
+    assert (planes == ref.planes.cpu().numpy()).all() and (pis == ref.pis.cpu().numpy()).all()
+    assert (vs == ref.vs.cpu().numpy()).all()
+    # learn: rank 0 holds 2 iterations of 2 x 4 games' examples; the final broadcast
+    # leaves both ranks with rank 0's trained weights
+    assert len(res[0]["hist"]) == 2 and all(n > 0 for n in res[0]["hist"]) and res[1]["hist"] == []
+    for k in res[0]["w"]:
+        assert (res[0]["w"][k] == res[1]["w"][k]).all(), k
