@@ -60,14 +60,30 @@ __device__ __forceinline__ int flip_outcome(int o) {  // GameOutcome.opposite, G
 }
 
 // ------------------------------------------------------------------- MT19937
-// numpy RandomState (legacy) stream of one game, staged in LDS for the kernel.
+// numpy RandomState (legacy) stream of one game.  A kernel draws a handful of
+// words, so the 64 words from the current position are prefetched into one
+// register per lane (one coalesced 256-B load, issued as early as the kernel
+// knows the slot) and served by __shfl; only a draw past them or past the end
+// of the state (the twist) stages the whole 2.5 KB state in LDS.
 struct BlockRng {
     uint32_t* g;   // global [624]
     int32_t* gpos;
     uint32_t* s;   // LDS [624]
     int pos;
     bool loaded, dirty;
+    int pre_base;  // position of lane 0's prefetched word (-1: none)
+    uint32_t pre;  // this lane's prefetched word g[pre_base + lane]
 };
+
+__device__ __forceinline__ BlockRng rng_open(uint32_t* g, int32_t* gpos, uint32_t* s) {
+    BlockRng r{g, gpos, s, *gpos, false, false, -1, 0u};
+    const int i = r.pos + (int)threadIdx.x;
+    if (r.pos < MT_N) {
+        r.pre_base = r.pos;
+        r.pre = i < MT_N ? g[i] : 0u;
+    }
+    return r;
+}
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= y >> 11;
@@ -107,6 +123,8 @@ __device__ void mt_twist(uint32_t* s) {
 }
 
 __device__ uint32_t rng_u32(BlockRng& R) {
+    if (!R.loaded && R.pre_base >= 0 && R.pos < MT_N && R.pos - R.pre_base < WAVE)
+        return mt_temper(__shfl(R.pre, R.pos++ - R.pre_base));
     if (!R.loaded) {
         for (int i = lane_id(); i < MT_N; i += WAVE) R.s[i] = R.g[i];
         __syncthreads();
@@ -597,6 +615,8 @@ __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__
         if (lane == 0) E.leaf_kind[g] = LEAF_NONE;
         return;
     }
+    // the slot's next random words, fetched while the tree is walked
+    BlockRng rg = rng_open(E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt);
     Pos p = load_root<R>(E, g);
     int depth = 0, kind = LEAF_NONE, slot = -1, cs = 0, kt = 0;
     uint64_t own = 0, opp = 0;
@@ -646,7 +666,6 @@ __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__
         for (int i = lane; i < R::PLANES * R::CELLS; i += WAVE) out[i] = 0.0f;
         return;
     }
-    BlockRng rg{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
     R::write_planes(out, own, opp, kt, cs, rg);
     rng_store(rg);
 }
@@ -875,7 +894,7 @@ __global__ __launch_bounds__(WAVE) void move_end_kernel(Dev E) {
     }
     const int m = E.moves[g];
     const int temp = (m + 1) < E.temp_threshold;  // episodeStep < tempThreshold
-    BlockRng rg{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
+    BlockRng rg = rng_open(E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt);
     int action = -1;
     if (temp == 0) {
         int mx = cnt[0];
@@ -979,7 +998,7 @@ __global__ __launch_bounds__(WAVE) void opponent_kernel(Dev E, int kind) {
     }
     int action = -1;
     if (kind == 1) {
-        BlockRng rg{E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt, E.mt_pos[g], false, false};
+        BlockRng rg = rng_open(E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt);
         int pick = rng_randint(rg, 0, nv);
         rng_store(rg);
 #pragma unroll
