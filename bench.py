@@ -55,17 +55,18 @@ def net_flops(n, depth, A, c=512):
     return conv1 + conv234 + fc, conv234
 
 
-def tree_bytes_per_sim(row, valid=87.0, d=1.33):
-    """Algorithmic HBM bytes of the tree kernels per simulation:
-    select reads P/N/Q (4+4+8 B) of each valid action at d nodes + hash lines,
-    the leaf writes its planes and reads P/v, the new node row (P, N, Q) is
-    initialised, backup read-modify-writes N, Q, Ns."""
-    sel = d * (16.0 * valid + 32.0)
-    table = d * 64.0 + 64.0
-    leaf = 4 * 49 * 4 + 343 * 4 + 4
-    node = row * 16 + 32
-    backup = d * 24.0
-    return sel + table + leaf + node + backup
+# mean valid actions per visited node (87 for 7x7 Inflexion; legal
+# moves of random-play Othello positions for the builder's plugin)
+VALID_ACTIONS = {("inflexion", 7): 87.0, ("othello", 6): 6.0, ("othello", 8): 9.0}
+
+
+def tree_bytes_per_exp(A, planes_bytes, valid=87.0, d=1.33):
+    """Algorithmic HBM bytes of the tree kernels per expansion, SURVEY 8(d)(1):
+    B_exp = sum_sel(12 A_i + 8) + 80 d + (24 + 12 A_leaf) + planes + P/v + 24 d
+    (select reads P f32 / N i32 / Q f32 of each valid action at d nodes, board
+    read + write per descent step, hash insert + node init, planes write, P/v
+    read, backup read-modify-write).  4.77 KB for 7x7 Inflexion."""
+    return d * (12.0 * valid + 8.0) + 80.0 * d + (24.0 + 12.0 * valid) + planes_bytes + (A + 1) * 4.0 + 24.0 * d
 
 
 def load_pmc(G, game):
@@ -303,8 +304,8 @@ def main():
         conv_kernel_desc = ("conv2-4 per forward: " + "; ".join(f"conv{i} {names[m]}" for i, m in impls.items())
                             if impls else "whole forward (no conv hook)")
         tree_s = (sel_ms + exp_ms) / 1e3
-        row = ((A + 63) // 64) * 64  # node row stride (actions rounded up to 64 lanes)
-        tree_gbs = (exp / world) * tree_bytes_per_sim(row) / tree_s / 1e9 if tree_s > 0 else 0.0
+        b_exp = tree_bytes_per_exp(A, depth * args.n * args.n * 4, VALID_ACTIONS.get((args.game, args.n), 87.0))
+        tree_gbs = (exp / world) * b_exp / tree_s / 1e9 if tree_s > 0 else 0.0
         gname = f"{args.n}x{args.n} {'Inflexion' if args.game == 'inflexion' else 'Othello'}"
         out = {
             "metric": f"node-expansions/s ({gname} self-play, {args.sims} sims/move); games/s in games_per_s",
@@ -344,7 +345,7 @@ def main():
             "roofline_tree": {"bound": "hbm", "kernel": "select_kernel + expand_backup_kernel",
                               "achieved": tree_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": tree_gbs / HBM_PEAK_GBS, "traffic": None,
-                              "bytes_per_sim": tree_bytes_per_sim(row),
+                              "bytes_per_expansion": b_exp,
                               "select_ms_per_sim": sel_ms / n_forwards, "expand_ms_per_sim": exp_ms / n_forwards,
                               "move_end_ms_per_move": end_ms / max(n_timed, 1)},
             "time_split": {"nn_ms": nn_ms, "select_ms": sel_ms, "expand_backup_ms": exp_ms, "move_end_ms": end_ms,
