@@ -115,6 +115,7 @@ int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
     ALLOC(d.outcome, G);
     ALLOC(d.active, G);
     ALLOC(d.searcher, G);
+    ALLOC(d.root_id, G);
     ALLOC(d.mt, G * azg::MT_N);
     ALLOC(d.mt_pos, G);
     ALLOC(d.node_own, GM);
@@ -254,6 +255,7 @@ int azg_set_root(azg_engine* e, int32_t slot, const int8_t* board, int32_t turn,
     HIP_TRY(hipMemcpyAsync(e->d.active + slot, &one, 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(e->d.moves + slot, &turn, 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(e->d.err + slot, &zero, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(e->d.root_id + slot, 0xff, 4, st));  // -1: look the new root up
     HIP_TRY(hipStreamSynchronize(st));
     return 0;
 }

@@ -33,6 +33,7 @@ struct Dev {
     int32_t* outcome;    // [G]  Outcome w.r.t. player to move
     int32_t* active;     // [G]
     int32_t* searcher;   // [G]  colour the search plays (arena), 0 = both (self-play)
+    int32_t* root_id;    // [G]  node id of the root during a move, -1 = look it up
     uint32_t* mt;        // [G][624]  numpy legacy MT19937 state
     int32_t* mt_pos;     // [G]
 

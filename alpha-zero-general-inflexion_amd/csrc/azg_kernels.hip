@@ -567,11 +567,14 @@ __device__ int puct_select(const Dev& E, int g, int id, const typename R::VCtx& 
         if (a < R::A && R::valid(a, vc)) {
             const float cp = E.cpuct_f * E.node_P[row + a];
             const uint32_t nr = E.node_N[row + a];
+            // Q loaded with P and N (not after N says the edge exists): one dependent
+            // round trip less per level; the value is used only where N > 0
+            const double qv = E.node_Q[row + a];
             const int n = (int)(nr & 0x7fffffffu);
             float u;
             if (n > 0) {
                 const float t = (cp * sq_edge) / (float)(1 + n);
-                u = (float)E.node_Q[row + a] + t;
+                u = (float)qv + t;
             } else {
                 u = cp * sq_new;
             }
@@ -617,6 +620,7 @@ __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__
     }
     // the slot's next random words, fetched while the tree is walked
     BlockRng rg = rng_open(E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt);
+    const int root_id = E.root_id[g];
     Pos p = load_root<R>(E, g);
     int depth = 0, kind = LEAF_NONE, slot = -1, cs = 0, kt = 0;
     uint64_t own = 0, opp = 0;
@@ -629,7 +633,13 @@ __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__
             break;
         }
         R::key(p, own, opp, kt, cs);
-        const int id = table_lookup(E, g, own, opp, kt, cs, &slot);
+        // the root's node id is cached for the rest of the move (ids are stable;
+        // commit_move / set_root invalidate it): one hash probe less per simulation
+        int id = depth == 0 ? root_id : -1;
+        if (id < 0) {
+            id = table_lookup(E, g, own, opp, kt, cs, &slot);
+            if (depth == 0 && id >= 0 && lane == 0) E.root_id[g] = id;
+        }
         if (id < 0) {
             if (slot < 0) set_err(E, g, -3);
             kind = slot < 0 ? LEAF_NONE : LEAF_EXPAND;
@@ -761,6 +771,7 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
             E.node_N[row + a] = 0u;  // Q is read only where N > 0: no init (3 KB less per expansion)
         }
         if (lane == 0) {
+            if (E.leaf_depth[g] == 0) E.root_id[g] = id;
             E.node_own[ni] = own;
             E.node_opp[ni] = opp;
             E.node_turn[ni] = kt;
@@ -822,6 +833,7 @@ __device__ void commit_move(const Dev& E, int g, Pos p, int action, int m) {
         E.player[g] = p.player;
         E.outcome[g] = p.outcome;
         E.moves[g] = m + 1;
+        E.root_id[g] = -1;  // the next search looks the new root up (and caches it)
         if (p.outcome != ONGOING) E.active[g] = 0;
     }
     if (!(E.flags & 1)) return;  // AZG_FLAG_GC
@@ -1058,6 +1070,7 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Dev E, uint32_t seed_base, 
         E.turn[g] = 0;
         E.player[g] = 1;
         E.searcher[g] = 0;
+        E.root_id[g] = -1;
         E.outcome[g] = ONGOING;
         E.active[g] = 1;
         E.moves[g] = 0;
