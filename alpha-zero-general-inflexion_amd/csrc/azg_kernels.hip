@@ -713,6 +713,20 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
     const int g = blockIdx.x, lane = lane_id();
     const int kind = E.leaf_kind[g];
     if (kind == LEAF_NONE) return;
+    // Everything the backup reads (path entry, edge N and Q; one level per lane) and
+    // the free-stack top are fetched up front, so they travel with the leaf's P
+    // row instead of after the expansion (the path's edges are never the new node).
+    const int depth = E.leaf_depth[g];
+    const int32_t* path = E.path + (size_t)g * E.DMAX;
+    const int packed0 = lane < depth ? path[lane] : 0;
+    const int top0 = kind == LEAF_EXPAND ? E.free_top[g] : 0;
+    uint32_t nr0 = 0u;
+    double q0 = 0.0;
+    if (lane < depth) {
+        const size_t erow = ((size_t)g * E.M + (packed0 >> 10)) * R::AP + (packed0 & 1023);
+        nr0 = E.node_N[erow];
+        q0 = E.node_Q[erow];  // used only where N > 0
+    }
     double ret;
     bool ret_f32;
     if (kind == LEAF_EXPAND) {
@@ -749,7 +763,7 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
         }
         int id = -1;
         if (lane == 0) {
-            const int top = E.free_top[g];
+            const int top = top0;
             if (top > 0) {
                 id = E.free_stack[(size_t)g * E.M + top - 1];
                 E.free_top[g] = top - 1;
@@ -771,7 +785,7 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
             E.node_N[row + a] = 0u;  // Q is read only where N > 0: no init (3 KB less per expansion)
         }
         if (lane == 0) {
-            if (E.leaf_depth[g] == 0) E.root_id[g] = id;
+            if (depth == 0) E.root_id[g] = id;
             E.node_own[ni] = own;
             E.node_opp[ni] = opp;
             E.node_turn[ni] = kt;
@@ -788,19 +802,17 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
         ret_f32 = false;
         if (lane == 0) E.st_term[g] += 1;
     }
-    const int depth = E.leaf_depth[g];
-    const int32_t* path = E.path + (size_t)g * E.DMAX;
     for (int d = lane; d < depth; d += WAVE) {
-        const int packed = path[d];
+        const int packed = d < WAVE ? packed0 : path[d];
         const int id = packed >> 10, a = packed & 1023;
         const double v = ((depth - 1 - d) & 1) ? -ret : ret;
         const size_t ni = (size_t)g * E.M + id, row = ni * R::AP + a;
-        const uint32_t nr = E.node_N[row];
+        const uint32_t nr = d < WAVE ? nr0 : E.node_N[row];
         const int n = (int)(nr & 0x7fffffffu);
         const bool qf = (nr >> 31) != 0;
-        double q = n > 0 ? E.node_Q[row] : 0.0;  // an edge's first backup defines Q
+        double q = d < WAVE ? q0 : E.node_Q[row];
         bool nf;
-        if (n == 0) {
+        if (n == 0) {  // an edge's first backup defines Q
             q = v;
             nf = ret_f32;
         } else if (qf || ret_f32) {  // numpy f32 arithmetic with weak Python scalars
