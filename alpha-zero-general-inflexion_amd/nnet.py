@@ -82,6 +82,15 @@ def _azg_conv3x3(x, wt, b, pad):
     return y
 
 
+def _winograd_u(w):
+    """Winograd F(2x2,3x3) weights U[e = 4a + b][c][k] = (G g_kc G^T)[a][b], formed in
+    f64 and rounded once (G has entries 1/2)."""
+    G = torch.tensor([[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]],
+                     dtype=torch.float64, device=w.device)
+    u = torch.einsum("ar,kcrs,bs->abck", G, w.double(), G)
+    return u.reshape(16, w.shape[1], w.shape[0]).float().contiguous()
+
+
 def _fold_bn(weight, bias, bn):
     """Eval-mode BatchNorm folded into the preceding conv/linear (f64 math)."""
     scale = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
@@ -103,16 +112,20 @@ class InferenceNet(nn.Module):
 
     outputs_probs = True
 
-    def __init__(self, net: InflexionNNet, conv="miopen"):
-        """conv: "miopen" (MIOpen implicit GEMM + one fused bias/ReLU pass), "azg"
-        (libazg's f32-MFMA implicit GEMM with the bias/ReLU in its epilogue) or
-        "auto" (per layer and input shape, whichever measured faster on first use)
-        for conv2-4; measured side by side in profiles/r01_conv_probe*.json."""
+    def __init__(self, net: InflexionNNet, conv="winograd"):
+        """conv (conv2-4): "winograd" (default; Winograd F(2x2,3x3): libazg input /
+        output transforms around 16 f32 GEMMs, bias + ReLU in the output transform,
+        1.6x fewer multiply-adds), "miopen" (MIOpen implicit GEMM + one fused
+        bias/ReLU pass), "azg" (libazg's f32-MFMA implicit GEMM with the bias/ReLU
+        in its epilogue) or "auto" (per layer and input shape, whichever measured
+        faster on first use).  All within the 1e-5 tolerance of the reference
+        network (tests/test_gpu_nn.py); measured side by side in DESIGN.md 4.1."""
         super().__init__()
-        if conv not in ("miopen", "azg", "auto"):
+        if conv not in ("miopen", "azg", "auto", "winograd"):
             raise ValueError(f"unknown conv implementation {conv!r}")
         self.conv_impl = conv
         self._choices = {}
+        self._ws = None  # Winograd V / M workspace, grown to the largest layer seen
         self.n, self.depth, c = net.n, net.depth, net.num_channels
         self.pads = []
         for i in range(1, 5):
@@ -122,6 +135,8 @@ class InferenceNet(nn.Module):
             self.register_buffer(f"b{i}", b)
             # [9*Cin, Cout] k-major copy for the libazg implicit GEMM (k = (dy*3+dx)*Cin + c)
             self.register_buffer(f"wt{i}", w.permute(2, 3, 1, 0).reshape(-1, w.shape[0]).contiguous())
+            if i > 1 and conv in ("winograd", "auto"):
+                self.register_buffer(f"u{i}", _winograd_u(w))
             self.pads.append(conv_i.padding[0])
         s = net.n - 4
         w1, b1 = _fold_bn(net.fc1.weight.detach(), net.fc1.bias.detach(), net.fc_bn1)
@@ -149,6 +164,34 @@ class InferenceNet(nn.Module):
         # bias + ReLU inside the libazg conv's epilogue
         return _azg_conv3x3(x, getattr(self, f"wt{i}"), getattr(self, f"b{i}"), pad)
 
+    def _conv_winograd(self, x, i, pad):
+        """Winograd F(2x2,3x3): libazg input transform, 16 f32 GEMMs (torch.bmm ->
+        hipBLASLt), libazg output transform with bias + ReLU (azg_winograd.hip)."""
+        import ctypes
+        from . import _lib
+        if not x.is_contiguous(memory_format=torch.channels_last):
+            x = x.contiguous(memory_format=torch.channels_last)
+        B, C, H, _ = x.shape
+        U = getattr(self, f"u{i}")
+        K = U.shape[2]
+        Ho = H + 2 * pad - 2
+        t = (Ho + 1) // 2
+        T = B * t * t
+        need = 16 * T * max(C, K)
+        if self._ws is None or self._ws[0].numel() < need:
+            self._ws = (torch.empty(need, device=x.device), torch.empty(need, device=x.device))
+        V = self._ws[0][:16 * T * C].view(16, T, C)
+        M = self._ws[1][:16 * T * K].view(16, T, K)
+        s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+        L = _lib.lib()
+        _lib.check(L.azg_winograd_in_nhwc(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(V.data_ptr()),
+                                          B, H, pad, C, s))
+        torch.bmm(V, U, out=M)
+        y = torch.empty((B, K, Ho, Ho), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+        _lib.check(L.azg_winograd_out_nhwc(ctypes.c_void_p(M.data_ptr()), ctypes.c_void_p(getattr(self, f"b{i}").data_ptr()),
+                                           ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, s))
+        return y
+
     def _pick(self, x, i, pad):
         """conv="auto": time both implementations once per (layer, input shape) and
         keep the faster (like cudnn.benchmark).  Never inside a graph capture: an
@@ -160,7 +203,7 @@ class InferenceNet(nn.Module):
         if torch.cuda.is_current_stream_capturing():
             return "miopen"
         best = None
-        for name, fn in (("miopen", self._conv_miopen), ("azg", self._conv_azg)):
+        for name, fn in (("miopen", self._conv_miopen), ("azg", self._conv_azg), ("winograd", self._conv_winograd)):
             for _ in range(2):
                 fn(x, i, pad)
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -189,6 +232,8 @@ class InferenceNet(nn.Module):
                 x = torch.relu_(F.conv2d(x, getattr(self, f"w{i}"), getattr(self, f"b{i}"), padding=pad))
             elif impl == "azg":
                 x = self._conv_azg(x, i, pad)
+            elif impl == "winograd":
+                x = self._conv_winograd(x, i, pad)
             else:
                 x = self._conv_miopen(x, i, pad)
             if hook:

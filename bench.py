@@ -36,6 +36,7 @@ F32_MFMA_PEAK_TF = 157.3         # MI355X_MICROARCH.md: f32 matrix peak (dense)
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E spec peak
 EXPANSIONS_PER_GAME_REF = 8555   # reference random-init Inflexion episodes
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_G4096.json")
+PMC_FILE_WINOGRAD = os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd.json")
 
 PRESETS = {
     "C1": dict(game="othello", n=6, games=1, sims=25),
@@ -55,6 +56,12 @@ def net_flops(n, depth, A, c=512):
     return conv1 + conv234 + fc, conv234
 
 
+def winograd_flops(n, c=512):
+    """GEMM FLOPs per leaf of conv2-4 as Winograd F(2x2,3x3): 16 x 2 C K per 2x2
+    output tile, ceil(h_out/2)^2 tiles (7x7: 243.3 M vs 391.6 M direct)."""
+    return sum(16 * 2 * c * c * ((h + 1) // 2) ** 2 for h in (n, n - 2, n - 4))
+
+
 # mean valid actions per visited node (SURVEY 8(d): 87 for 7x7 Inflexion; legal
 # moves of random-play Othello positions for the builder's plugin)
 VALID_ACTIONS = {("inflexion", 7): 87.0, ("othello", 6): 6.0, ("othello", 8): 9.0}
@@ -69,18 +76,29 @@ def tree_bytes_per_exp(A, planes_bytes, valid=87.0, d=1.33):
     return d * (12.0 * valid + 8.0) + 80.0 * d + (24.0 + 12.0 * valid) + planes_bytes + (A + 1) * 4.0 + 24.0 * d
 
 
-def load_pmc(G, game):
+def load_pmc(G, game, impl):
     """HBM-side bytes per launch from the committed PMC passes (tools/pmc_summary.py:
     rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs, FETCH doubled
-    per the gfx950 correction).  Only valid for the workload it was measured on."""
-    if G != 4096 or game != "inflexion" or not os.path.exists(PMC_FILE):
+    per the gfx950 correction).  Only valid for the workload and convolution
+    implementation it was measured on."""
+    path = {"miopen": PMC_FILE, "winograd": PMC_FILE_WINOGRAD}.get(impl)
+    if G != 4096 or game != "inflexion" or not path or not os.path.exists(path):
         return None
-    d = json.load(open(PMC_FILE))
-    conv = d["conv2-4 igemm"]["hbm_bytes_sum_over_shapes"]
-    tree = d["select_kernel"]["hbm_bytes_sum_over_shapes"] + d["expand_backup_kernel"]["hbm_bytes_sum_over_shapes"]
+    d = json.load(open(path))
+    def tot(k):
+        if k not in d:
+            return 0.0
+        return d[k].get("hbm_bytes_per_forward") or d[k]["hbm_bytes_sum_over_shapes"]
+    if impl == "winograd":
+        conv = tot("winograd_in") + tot("winograd_out") + tot("gemm (hipBLASLt)")
+        what = "winograd_in + the 16-GEMM batches + winograd_out (and the FC GEMMs, ~1%)"
+    else:
+        conv = tot("conv2-4 igemm")
+        what = "conv2+3+4 igemm"
+    tree = tot("select_kernel") + tot("expand_backup_kernel")
     return {"conv": conv, "tree": tree,
-            "note": f"{os.path.relpath(PMC_FILE, ROOT)}: FETCH_SIZE x2 + WRITE_SIZE per forward (conv2+3+4); "
-                    "counts L2 misses incl. Infinity-Cache hits; algorithmic bytes are ~1.1 GB"}
+            "note": f"{os.path.relpath(path, ROOT)}: FETCH_SIZE x2 + WRITE_SIZE per forward ({what}); "
+                    "counts L2 misses incl. Infinity-Cache hits"}
 
 
 def parse():
@@ -95,7 +113,7 @@ def parse():
     p.add_argument("--sims", type=int, default=25)
     p.add_argument("--max-turns", type=int, default=343)
     p.add_argument("--evaluator", default="net", choices=["net", "stub"])
-    p.add_argument("--conv", default="miopen", choices=["auto", "miopen", "azg"],
+    p.add_argument("--conv", default="winograd", choices=["auto", "miopen", "azg", "winograd"],
                    help="conv2-4 implementation of the inference net (MIOpen igemm + bias/ReLU pass, libazg f32-MFMA "
                         "implicit GEMM with fused epilogue, or auto: per layer, the faster one measured at first use)")
     p.add_argument("--net", default="inference", choices=["inference", "reference"],
@@ -289,18 +307,25 @@ def main():
         n_forwards = max(n_timed * args.sims, 1)
         nn_avg = nn_ms / n_forwards / 1e3
         leaves = G  # the forward is evaluated on the full [G, planes, n, n] batch
-        nn_tflops = leaves * flop_leaf / nn_avg / 1e12 if nn_avg > 0 else 0.0
+        nn_tflops = None  # set below, from the FLOPs the chosen convolution performs
         conv_ms = sum(t.total_ms() for t in t_conv.values())
         conv_avg = conv_ms / n_forwards / 1e3 if conv_ms > 0 else nn_avg
-        conv_flops = leaves * (conv_flop_leaf if conv_ms > 0 else flop_leaf)
+        impl = getattr(ev, "conv_impl", None) if not isinstance(ev, str) else None
+        # algorithmic FLOPs of conv2-4 as computed: the Winograd path does fewer
+        algo_conv_leaf = winograd_flops(args.n) if impl == "winograd" else conv_flop_leaf
+        conv_flops = leaves * (algo_conv_leaf if conv_ms > 0 else flop_leaf)
         conv_tflops = conv_flops / conv_avg / 1e12 if conv_avg > 0 else 0.0
+        direct_tflops = leaves * conv_flop_leaf / conv_avg / 1e12 if conv_ms > 0 and conv_avg > 0 else None
+        algo_fwd_leaf = flop_leaf - conv_flop_leaf + algo_conv_leaf
+        nn_tflops = leaves * algo_fwd_leaf / nn_avg / 1e12 if nn_avg > 0 else 0.0
         impls = {}
         if hasattr(ev, "_choices") or getattr(ev, "conv_impl", None):
             for i in (2, 3, 4):
                 impls[i] = (next((v for (li, _), v in ev._choices.items() if li == i), "miopen")
                             if ev.conv_impl == "auto" else ev.conv_impl)
         names = {"miopen": "MIOpen igemm_fwd_gtcx35_nhwc_fp32 + libazg bias/ReLU pass",
-                 "azg": "libazg f32-MFMA implicit GEMM (LDS-DMA ring) + fused bias/ReLU"}
+                 "azg": "libazg f32-MFMA implicit GEMM (LDS-DMA ring) + fused bias/ReLU",
+                 "winograd": "Winograd F(2x2,3x3): libazg transforms + 16 f32 GEMMs (hipBLASLt), bias/ReLU fused"}
         conv_kernel_desc = ("conv2-4 per forward: " + "; ".join(f"conv{i} {names[m]}" for i, m in impls.items())
                             if impls else "whole forward (no conv hook)")
         tree_s = (sel_ms + exp_ms) / 1e3
@@ -337,10 +362,11 @@ def main():
                          "kernel": conv_kernel_desc,
                          "achieved": conv_tflops, "peak": F32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                          "frac": conv_tflops / F32_MFMA_PEAK_TF, "traffic": None,
-                         "per_launch": f"{leaves} leaves x {conv_flop_leaf / 1e6:.1f} MFLOP / {conv_avg * 1e3:.3f} ms "
+                         "direct_conv_equivalent_tflops": direct_tflops,
+                         "per_launch": f"{leaves} leaves x {algo_conv_leaf / 1e6:.1f} MFLOP / {conv_avg * 1e3:.3f} ms "
                                        f"(HIP events around conv2+conv3+conv4)",
                          "forward_tflops": nn_tflops,
-                         "forward_per_launch": f"{leaves} leaves x {flop_leaf / 1e6:.1f} MFLOP / "
+                         "forward_per_launch": f"{leaves} leaves x {algo_fwd_leaf / 1e6:.1f} MFLOP / "
                                                f"{nn_avg * 1e3:.3f} ms (HIP events)"},
             "roofline_tree": {"bound": "hbm", "kernel": "select_kernel + expand_backup_kernel",
                               "achieved": tree_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -352,7 +378,7 @@ def main():
                            "wall_ms": elapsed * 1e3, "graph": bool(args.graph)},
             "iteration_sync_bytes": sync_bytes,
         }
-        pmc = load_pmc(G, args.game)
+        pmc = load_pmc(G, args.game, impl)
         if pmc:
             out["roofline"]["traffic"] = pmc["conv"]
             out["roofline"]["traffic_note"] = pmc["note"]

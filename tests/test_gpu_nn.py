@@ -19,7 +19,7 @@ def test_bias_relu_kernel():
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("conv", ["miopen", "azg", "auto"])
+@pytest.mark.parametrize("conv", ["miopen", "azg", "auto", "winograd"])
 def test_inference_net_vs_reference_gpu(conv):
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
@@ -92,3 +92,22 @@ def test_azg_conv3x3_variants(variant, B, H, pad):
                                               B, H, pad, C, N, s))
     torch.cuda.synchronize()
     torch.testing.assert_close(y, want, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,H,pad", [(1, 7, 1), (37, 7, 1), (300, 7, 0), (129, 5, 0), (64, 8, 1), (5, 6, 0)])
+def test_winograd_conv3x3_matches_torch(B, H, pad):
+    """Winograd F(2x2,3x3) layer (libazg transforms + f32 bmm) vs torch conv2d + bias + ReLU."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    torch.manual_seed(3)
+    net = InflexionNNet(n=max(H, 5)).eval()
+    fast = InferenceNet(net, conv="winograd").cuda()
+    C = N = 512
+    w = torch.randn(N, C, 3, 3) * 0.02
+    from azg_amd.nnet import _winograd_u
+    fast.u2 = _winograd_u(w).cuda()
+    fast.b2 = (torch.randn(N) * 0.1).cuda()
+    x = torch.relu(torch.randn(B, C, H, H, device="cuda")).contiguous(memory_format=torch.channels_last)
+    want = torch.relu(torch.nn.functional.conv2d(x, w.cuda(), fast.b2, padding=pad))
+    got = fast._conv_winograd(x, 2, pad)
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)

@@ -33,14 +33,20 @@ def group(name):
         return "conv2-4 igemm"
     if name.startswith("igemm_fwd"):
         return "conv1 igemm"
-    if name.startswith("azg::select"):
+    if "azg::select_kernel" in name:
         return "select_kernel"
-    if name.startswith("azg::expand"):
+    if "azg::expand_backup_kernel" in name:
         return "expand_backup_kernel"
-    if name.startswith("azg::move_end"):
+    if "azg::move_end_kernel" in name:
         return "move_end_kernel"
     if "bias_relu" in name:
         return "bias_relu_nhwc"
+    if "winograd_in" in name:
+        return "winograd_in"
+    if "winograd_out" in name:
+        return "winograd_out"
+    if name.startswith("Cijk_"):
+        return "gemm (hipBLASLt)"
     return None
 
 
@@ -58,8 +64,24 @@ def main():
             "fetch_kib_raw_median": median(f), "write_kib_median": median(w),
             "fetch_bytes_corrected": 2 * median(f) * 1024, "write_bytes": median(w) * 1024,
             "hbm_bytes": 2 * median(f) * 1024 + median(w) * 1024})
-    summary = {g: {"per_shape": v, "hbm_bytes_sum_over_shapes": sum(x["hbm_bytes"] for x in v)}
-               for g, v in out.items()}
+    # per leaf forward = per simulation: totals over all dispatches / select_kernel dispatches
+    # (robust where several layers share one kernel name and grid, e.g. the three GEMM batches)
+    tot = defaultdict(lambda: [0.0, 0.0, 0])
+    for key in set(fetch) | set(write):
+        g = group(key[0])
+        if g is None:
+            continue
+        tot[g][0] += 2 * sum(fetch.get(key, [])) * 1024
+        tot[g][1] += sum(write.get(key, [])) * 1024
+        tot[g][2] += max(len(fetch.get(key, [])), len(write.get(key, [])))
+    n_fwd = tot["select_kernel"][2] if "select_kernel" in tot else 0
+    summary = {}
+    for g, v in out.items():
+        f, w, n = tot[g]
+        summary[g] = {"per_shape": v, "hbm_bytes_sum_over_shapes": sum(x["hbm_bytes"] for x in v),
+                      "dispatches": n, "fetch_bytes_corrected_total": f, "write_bytes_total": w,
+                      "hbm_bytes_per_forward": (f + w) / n_fwd if n_fwd else None}
+    summary["_forwards"] = n_fwd
     json.dump(summary, sys.stdout, indent=1)
 
 

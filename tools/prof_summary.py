@@ -7,7 +7,7 @@ import sys
 
 
 def short(name):
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     return n if len(n) < 70 else n[:67] + "..."
 
 
