@@ -25,12 +25,22 @@ namespace {
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 __device__ __forceinline__ float4 f4sub(float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
 
+// Work item of a thread: block ids are dealt round-robin to the 8 XCDs, so the
+// block -> work mapping gives each XCD one contiguous eighth of the work:
+// neighbouring tiles, which share input halo pixels, then hit the same L2.
+__device__ __forceinline__ long long xcd_item() {
+    const unsigned per = gridDim.x / 8;  // the grid is a multiple of 8 blocks
+    const unsigned vb = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    return (long long)vb * blockDim.x + threadIdx.x;
+}
+
 // tile index t = (b * tiles + ty) * tiles + tx
 __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restrict__ x, float4* __restrict__ V,
                                                           int H, int pad, int C4, int tiles, long long T) {
     const long long n = T * C4;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (long long)gridDim.x * blockDim.x) {
+    {
+        const long long i = xcd_item();
+        if (i >= n) return;
         const int c4 = (int)(i % C4);
         const long long t = i / C4;
         const int tx = (int)(t % tiles);
@@ -74,8 +84,9 @@ __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restr
                                                            float4* __restrict__ y, int Ho, int K4, int tiles,
                                                            long long T, int relu) {
     const long long n = T * K4;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (long long)gridDim.x * blockDim.x) {
+    {
+        const long long i = xcd_item();
+        if (i >= n) return;
         const int k4 = (int)(i % K4);
         const long long t = i / K4;
         const int tx = (int)(t % tiles);
@@ -117,17 +128,18 @@ __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restr
     }
 }
 
+// one thread per work item, rounded up to whole groups of 8 blocks (xcd_item)
 unsigned grid_for(long long n) {
-    long long blocks = (n + 255) / 256;
-    if (blocks > (1ll << 30)) blocks = 1ll << 30;  // grid-stride beyond
-    return (unsigned)(blocks > 0 ? blocks : 1);
+    const long long blocks = (n + 255) / 256;
+    return (unsigned)(((blocks + 7) / 8) * 8);
 }
 }  // namespace
 
 extern "C" int azg_winograd_in_nhwc(const float* x, float* V, int32_t batch, int32_t h_in, int32_t pad, int32_t c,
                                     void* stream) {
     const int h_out = h_in + 2 * pad - 2;
-    if (!x || !V || batch <= 0 || h_out <= 0 || c <= 0 || c % 4 || ((uintptr_t)x & 15) || ((uintptr_t)V & 15))
+    if (!x || !V || batch <= 0 || h_out <= 0 || c <= 0 || c % 4 || ((uintptr_t)x & 15) || ((uintptr_t)V & 15) ||
+        (long long)batch * ((h_out + 1) / 2) * ((h_out + 1) / 2) * (c / 4) > (1ll << 38))
         return AZG_ERR_ARG;
     const int tiles = (h_out + 1) / 2;
     const long long T = (long long)batch * tiles * tiles;
@@ -139,7 +151,8 @@ extern "C" int azg_winograd_in_nhwc(const float* x, float* V, int32_t batch, int
 extern "C" int azg_winograd_out_nhwc(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out,
                                      int32_t k, int32_t relu, void* stream) {
     if (!M || !bias || !y || batch <= 0 || h_out <= 0 || k <= 0 || k % 4 || ((uintptr_t)M & 15) ||
-        ((uintptr_t)bias & 15) || ((uintptr_t)y & 15))
+        ((uintptr_t)bias & 15) || ((uintptr_t)y & 15) ||
+        (long long)batch * ((h_out + 1) / 2) * ((h_out + 1) / 2) * (k / 4) > (1ll << 38))
         return AZG_ERR_ARG;
     const int tiles = (h_out + 1) / 2;
     const long long T = (long long)batch * tiles * tiles;
