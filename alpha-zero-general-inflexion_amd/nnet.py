@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 DEFAULT_ARGS = dict(lr=0.001, dropout=0.3, epochs=10, batch_size=512, num_channels=512)
+WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C1: 1 game)
 
 
 class InflexionNNet(nn.Module):
@@ -224,6 +225,8 @@ class InferenceNet(nn.Module):
         fused = x.is_cuda
         for i, pad in enumerate(self.pads, start=1):
             impl = self.conv_impl if i > 1 else "miopen"
+            if impl == "winograd" and x.shape[0] < WINOGRAD_MIN_BATCH:
+                impl = "miopen"  # a few leaves: the 16 small GEMMs lose to one direct conv
             if fused and impl == "auto":
                 impl = self._pick(x, i, pad)
             if hook:
