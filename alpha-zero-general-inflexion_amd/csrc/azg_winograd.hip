@@ -35,7 +35,10 @@ __device__ __forceinline__ long long xcd_item() {
 }
 
 // tile index t = (b * tiles + ty) * tiles + tx
-__global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restrict__ x, float4* __restrict__ V,
+// in_bias != null: x is the previous layer's raw output and relu(x + in_bias)
+// is applied on load (that layer's bias + ReLU fused here; padding stays 0)
+__global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restrict__ x,
+                                                          const float4* __restrict__ in_bias, float4* __restrict__ V,
                                                           int H, int pad, int C4, int tiles, long long T) {
     const long long n = T * C4;
     {
@@ -47,6 +50,7 @@ __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restri
         const long long r = t / tiles;
         const int ty = (int)(r % tiles);
         const long long b = r / tiles;
+        const float4 ib = in_bias ? in_bias[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
         float4 d[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -54,8 +58,18 @@ __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restri
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
                 const int ix = 2 * tx - pad + v;
-                d[u][v] = (iy >= 0 && iy < H && ix >= 0 && ix < H) ? x[((b * H + iy) * H + ix) * C4 + c4]
-                                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+                float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (iy >= 0 && iy < H && ix >= 0 && ix < H) {
+                    z = x[((b * H + iy) * H + ix) * C4 + c4];
+                    if (in_bias) {
+                        z = f4add(z, ib);
+                        z.x = fmaxf(z.x, 0.f);
+                        z.y = fmaxf(z.y, 0.f);
+                        z.z = fmaxf(z.z, 0.f);
+                        z.w = fmaxf(z.w, 0.f);
+                    }
+                }
+                d[u][v] = z;
             }
         }
         // B^T d: rows (d0 - d2, d1 + d2, d2 - d1, d1 - d3)
@@ -135,16 +149,17 @@ unsigned grid_for(long long n) {
 }
 }  // namespace
 
-extern "C" int azg_winograd_in_nhwc(const float* x, float* V, int32_t batch, int32_t h_in, int32_t pad, int32_t c,
-                                    void* stream) {
+extern "C" int azg_winograd_in_nhwc(const float* x, const float* in_bias, float* V, int32_t batch, int32_t h_in,
+                                    int32_t pad, int32_t c, void* stream) {
     const int h_out = h_in + 2 * pad - 2;
     if (!x || !V || batch <= 0 || h_out <= 0 || c <= 0 || c % 4 || ((uintptr_t)x & 15) || ((uintptr_t)V & 15) ||
+        ((uintptr_t)in_bias & 15) ||
         (long long)batch * ((h_out + 1) / 2) * ((h_out + 1) / 2) * (c / 4) > (1ll << 38))
         return AZG_ERR_ARG;
     const int tiles = (h_out + 1) / 2;
     const long long T = (long long)batch * tiles * tiles;
     hipLaunchKernelGGL(winograd_in_kernel, dim3(grid_for(T * (c / 4))), dim3(256), 0, (hipStream_t)stream,
-                       (const float4*)x, (float4*)V, h_in, pad, c / 4, tiles, T);
+                       (const float4*)x, (const float4*)in_bias, (float4*)V, h_in, pad, c / 4, tiles, T);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 

@@ -165,7 +165,7 @@ class InferenceNet(nn.Module):
         # bias + ReLU inside the libazg conv's epilogue
         return _azg_conv3x3(x, getattr(self, f"wt{i}"), getattr(self, f"b{i}"), pad)
 
-    def _conv_winograd(self, x, i, pad):
+    def _conv_winograd(self, x, i, pad, in_bias=None):
         """Winograd F(2x2,3x3): libazg input transform, 16 f32 GEMMs (torch.bmm ->
         hipBLASLt), libazg output transform with bias + ReLU (azg_winograd.hip)."""
         import ctypes
@@ -185,7 +185,8 @@ class InferenceNet(nn.Module):
         M = self._ws[1][:16 * T * K].view(16, T, K)
         s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
         L = _lib.lib()
-        _lib.check(L.azg_winograd_in_nhwc(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(V.data_ptr()),
+        ib = ctypes.c_void_p(in_bias.data_ptr()) if in_bias is not None else None
+        _lib.check(L.azg_winograd_in_nhwc(ctypes.c_void_p(x.data_ptr()), ib, ctypes.c_void_p(V.data_ptr()),
                                           B, H, pad, C, s))
         torch.bmm(V, U, out=M)
         y = torch.empty((B, K, Ho, Ho), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
@@ -223,10 +224,15 @@ class InferenceNet(nn.Module):
         x = s.view(-1, self.depth, self.n, self.n).contiguous(memory_format=torch.channels_last)
         hook = self.conv_hook
         fused = x.is_cuda
-        for i, pad in enumerate(self.pads, start=1):
+        impls = []
+        for i in range(1, 5):
             impl = self.conv_impl if i > 1 else "miopen"
             if impl == "winograd" and x.shape[0] < WINOGRAD_MIN_BATCH:
                 impl = "miopen"  # a few leaves: the 16 small GEMMs lose to one direct conv
+            impls.append(impl)
+        pending = None  # bias of the previous conv, to be applied (with ReLU) by this one's input transform
+        for i, pad in enumerate(self.pads, start=1):
+            impl = impls[i - 1]
             if fused and impl == "auto":
                 impl = self._pick(x, i, pad)
             if hook:
@@ -236,7 +242,12 @@ class InferenceNet(nn.Module):
             elif impl == "azg":
                 x = self._conv_azg(x, i, pad)
             elif impl == "winograd":
-                x = self._conv_winograd(x, i, pad)
+                x = self._conv_winograd(x, i, pad, in_bias=pending)
+                pending = None
+            elif i == 1 and impls[1] == "winograd":
+                # conv1's bias + ReLU ride in conv2's Winograd input transform (no separate pass)
+                x = F.conv2d(x, self.w1, None, padding=pad)
+                pending = self.b1
             else:
                 x = self._conv_miopen(x, i, pad)
             if hook:
