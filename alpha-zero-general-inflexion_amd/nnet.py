@@ -83,13 +83,25 @@ def _azg_conv3x3(x, wt, b, pad):
     return y
 
 
-def _winograd_u(w):
-    """Winograd F(2x2,3x3) weights U[e = 4a + b][c][k] = (G g_kc G^T)[a][b], formed in
-    f64 and rounded once (G has entries 1/2)."""
-    G = torch.tensor([[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]],
-                     dtype=torch.float64, device=w.device)
+# Winograd F(m x m, 3x3) weight transforms G [n][3], n = m + 2 (azg_winograd.hip holds B^T, A^T)
+WINOGRAD_G = {2: [[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]],
+              3: [[0.5, 0.0, 0.0], [-0.5, -0.5, -0.5], [-1 / 6, 1 / 6, -1 / 6], [1 / 6, 1 / 3, 2 / 3],
+                  [0.0, 0.0, 1.0]]}
+
+
+def winograd_tile(h_out):
+    """Output tile m (2 or 3) with the fewest GEMM multiply-adds (m+2)^2 ceil(h/m)^2
+    for an h_out x h_out output: 3 for 7x7 (225 vs 256), 5x5, 3x3; 2 for 4x4, 2x2."""
+    return min((2, 3), key=lambda m: ((m + 2) * ((h_out + m - 1) // m)) ** 2)
+
+
+def _winograd_u(w, m=2):
+    """Winograd F(m x m,3x3) weights U[e = n a + b][c][k] = (G g_kc G^T)[a][b], formed in
+    f64 and rounded once (G has entries 1/2, 1/3, 1/6)."""
+    G = torch.tensor(WINOGRAD_G[m], dtype=torch.float64, device=w.device)
+    n = m + 2
     u = torch.einsum("ar,kcrs,bs->abck", G, w.double(), G)
-    return u.reshape(16, w.shape[1], w.shape[0]).float().contiguous()
+    return u.reshape(n * n, w.shape[1], w.shape[0]).float().contiguous()
 
 
 def _fold_bn(weight, bias, bn):
@@ -127,18 +139,23 @@ class InferenceNet(nn.Module):
         self.conv_impl = conv
         self._choices = {}
         self._ws = None  # Winograd V / M workspace, grown to the largest layer seen
+        self.tiles = {}  # Winograd output tile per conv layer
         self.n, self.depth, c = net.n, net.depth, net.num_channels
         self.pads = []
+        h = net.n  # input side of conv i
         for i in range(1, 5):
             conv_i, bn = getattr(net, f"conv{i}"), getattr(net, f"bn{i}")
+            h_out = h + 2 * conv_i.padding[0] - 2
             w, b = _fold_bn(conv_i.weight.detach(), conv_i.bias.detach(), bn)
             self.register_buffer(f"w{i}", w.contiguous(memory_format=torch.channels_last))
             self.register_buffer(f"b{i}", b)
             # [9*Cin, Cout] k-major copy for the libazg implicit GEMM (k = (dy*3+dx)*Cin + c)
             self.register_buffer(f"wt{i}", w.permute(2, 3, 1, 0).reshape(-1, w.shape[0]).contiguous())
             if i > 1 and conv in ("winograd", "auto"):
-                self.register_buffer(f"u{i}", _winograd_u(w))
+                self.tiles[i] = winograd_tile(h_out)
+                self.register_buffer(f"u{i}", _winograd_u(w, self.tiles[i]))
             self.pads.append(conv_i.padding[0])
+            h = h_out
         s = net.n - 4
         w1, b1 = _fold_bn(net.fc1.weight.detach(), net.fc1.bias.detach(), net.fc_bn1)
         w1 = w1.reshape(-1, c, s, s).permute(0, 2, 3, 1).reshape(w1.shape[0], -1)  # (c,h,w) -> (h,w,c)
@@ -174,24 +191,26 @@ class InferenceNet(nn.Module):
             x = x.contiguous(memory_format=torch.channels_last)
         B, C, H, _ = x.shape
         U = getattr(self, f"u{i}")
+        m = self.tiles[i]
+        nn2 = (m + 2) ** 2
         K = U.shape[2]
         Ho = H + 2 * pad - 2
-        t = (Ho + 1) // 2
+        t = (Ho + m - 1) // m
         T = B * t * t
-        need = 16 * T * max(C, K)
+        need = nn2 * T * max(C, K)
         if self._ws is None or self._ws[0].numel() < need:
             self._ws = (torch.empty(need, device=x.device), torch.empty(need, device=x.device))
-        V = self._ws[0][:16 * T * C].view(16, T, C)
-        M = self._ws[1][:16 * T * K].view(16, T, K)
+        V = self._ws[0][:nn2 * T * C].view(nn2, T, C)
+        M = self._ws[1][:nn2 * T * K].view(nn2, T, K)
         s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
         L = _lib.lib()
         ib = ctypes.c_void_p(in_bias.data_ptr()) if in_bias is not None else None
         _lib.check(L.azg_winograd_in_nhwc(ctypes.c_void_p(x.data_ptr()), ib, ctypes.c_void_p(V.data_ptr()),
-                                          B, H, pad, C, s))
+                                          B, H, pad, C, m, s))
         torch.bmm(V, U, out=M)
         y = torch.empty((B, K, Ho, Ho), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
         _lib.check(L.azg_winograd_out_nhwc(ctypes.c_void_p(M.data_ptr()), ctypes.c_void_p(getattr(self, f"b{i}").data_ptr()),
-                                           ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, s))
+                                           ctypes.c_void_p(y.data_ptr()), B, Ho, K, m, 1, s))
         return y
 
     def _pick(self, x, i, pad):

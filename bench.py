@@ -56,10 +56,10 @@ def net_flops(n, depth, A, c=512):
     return conv1 + conv234 + fc, conv234
 
 
-def winograd_flops(n, c=512):
-    """GEMM FLOPs per leaf of conv2-4 as Winograd F(2x2,3x3): 16 x 2 C K per 2x2
-    output tile, ceil(h_out/2)^2 tiles (7x7: 243.3 M vs 391.6 M direct)."""
-    return sum(16 * 2 * c * c * ((h + 1) // 2) ** 2 for h in (n, n - 2, n - 4))
+def winograd_flops(n, c=512, tiles=(3, 3, 3)):
+    """GEMM FLOPs per leaf of conv2-4 as Winograd F(m x m,3x3) (m per layer, nnet.winograd_tile):
+    (m+2)^2 x 2 C K per m x m output tile, ceil(h_out/m)^2 tiles (7x7 board: 183.5 M vs 391.6 M direct)."""
+    return sum((m + 2) ** 2 * 2 * c * c * ((h + m - 1) // m) ** 2 for h, m in zip((n, n - 2, n - 4), tiles))
 
 
 # mean valid actions per visited node (SURVEY 8(d): 87 for 7x7 Inflexion; legal
@@ -312,7 +312,8 @@ def main():
         conv_avg = conv_ms / n_forwards / 1e3 if conv_ms > 0 else nn_avg
         impl = getattr(ev, "conv_impl", None) if not isinstance(ev, str) else None
         # algorithmic FLOPs of conv2-4 as computed: the Winograd path does fewer
-        algo_conv_leaf = winograd_flops(args.n) if impl == "winograd" else conv_flop_leaf
+        algo_conv_leaf = (winograd_flops(args.n, tiles=tuple(ev.tiles[i] for i in (2, 3, 4)))
+                          if impl == "winograd" else conv_flop_leaf)
         conv_flops = leaves * (algo_conv_leaf if conv_ms > 0 else flop_leaf)
         conv_tflops = conv_flops / conv_avg / 1e12 if conv_avg > 0 else 0.0
         direct_tflops = leaves * conv_flop_leaf / conv_avg / 1e12 if conv_ms > 0 and conv_avg > 0 else None

@@ -138,21 +138,21 @@ int  azg_conv3x3_bias_relu_nhwc(const float* x, const float* wt, const float* bi
 int  azg_conv3x3_variant(int variant, const float* x, const float* wt, const float* bias, float* y, int32_t batch,
                          int32_t h_in, int32_t pad, int32_t c_in, int32_t c_out, void* stream);
 
-/* Leaf-network 3x3 convolution as Winograd F(2x2,3x3) (azg_winograd.hip): the
- * same layer as azg_conv3x3_bias_relu_nhwc in three steps, with T = batch * t * t
- * tiles, t = ceil(h_out / 2):
+/* Leaf-network 3x3 convolution as Winograd F(m x m, 3x3), m = 2 or 3
+ * (azg_winograd.hip): the same layer as azg_conv3x3_bias_relu_nhwc in three steps,
+ * with n = m + 2, T = batch * t * t tiles, t = ceil(h_out / m):
  *   azg_winograd_in_nhwc : x NHWC [batch, h_in, h_in, c] (zero padding `pad`) ->
- *                          V [16][T][c] (B^T d B per tile and channel); with
+ *                          V [n*n][T][c] (B^T d B per tile and channel); with
  *                          in_bias != NULL, relu(x + in_bias[c]) is transformed
  *                          (the previous layer's bias + ReLU fused);
- *   (caller)             : M[e] = V[e] x U[e] for e = 0..15, U [16][c][k] = G g G^T;
- *   azg_winograd_out_nhwc: M [16][T][k] -> y NHWC [batch, h_out, h_out, k] =
+ *   (caller)             : M[e] = V[e] x U[e] for e < n*n, U [n*n][c][k] = G g G^T;
+ *   azg_winograd_out_nhwc: M [n*n][T][k] -> y NHWC [batch, h_out, h_out, k] =
  *                          A^T M A + bias, ReLU if relu != 0.
  * c % 4 == 0, k % 4 == 0, 16-B aligned pointers. */
 int  azg_winograd_in_nhwc(const float* x, const float* in_bias, float* V, int32_t batch, int32_t h_in, int32_t pad,
-                          int32_t c, void* stream);
+                          int32_t c, int32_t m, void* stream);
 int  azg_winograd_out_nhwc(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,
-                           int32_t relu, void* stream);
+                           int32_t m, int32_t relu, void* stream);
 
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active

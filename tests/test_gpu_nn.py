@@ -94,9 +94,10 @@ def test_azg_conv3x3_variants(variant, B, H, pad):
     torch.testing.assert_close(y, want, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("m", [2, 3])
 @pytest.mark.parametrize("B,H,pad", [(1, 7, 1), (37, 7, 1), (300, 7, 0), (129, 5, 0), (64, 8, 1), (5, 6, 0)])
-def test_winograd_conv3x3_matches_torch(B, H, pad):
-    """Winograd F(2x2,3x3) layer (libazg transforms + f32 bmm) vs torch conv2d + bias + ReLU."""
+def test_winograd_conv3x3_matches_torch(B, H, pad, m):
+    """Winograd F(m x m,3x3) layer (libazg transforms + f32 bmm) vs torch conv2d + bias + ReLU."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
     torch.manual_seed(3)
@@ -105,9 +106,12 @@ def test_winograd_conv3x3_matches_torch(B, H, pad):
     C = N = 512
     w = torch.randn(N, C, 3, 3) * 0.02
     from azg_amd.nnet import _winograd_u
-    fast.u2 = _winograd_u(w).cuda()
-    fast.b2 = (torch.randn(N) * 0.1).cuda()
+    layer = 2
+    fast.tiles[layer] = m
+    setattr(fast, f"u{layer}", _winograd_u(w, m).cuda())
+    b = (torch.randn(N) * 0.1).cuda()
+    setattr(fast, f"b{layer}", b)
     x = torch.relu(torch.randn(B, C, H, H, device="cuda")).contiguous(memory_format=torch.channels_last)
-    want = torch.relu(torch.nn.functional.conv2d(x, w.cuda(), fast.b2, padding=pad))
-    got = fast._conv_winograd(x, 2, pad)
+    want = torch.relu(torch.nn.functional.conv2d(x, w.cuda(), b, padding=pad))
+    got = fast._conv_winograd(x, layer, pad)
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
