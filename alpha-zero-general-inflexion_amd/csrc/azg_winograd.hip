@@ -174,6 +174,113 @@ __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restr
     }
 }
 
+// Layer i's output transform fused with layer i+1's input transform (pad 0
+// between them, as conv2->conv3->conv4): one wave per (image, 64 channels),
+// each lane owning one channel.  The lane's h x h output plane of layer i
+// (bias + ReLU applied) is staged in LDS -- only that lane reads it back, so
+// no barrier -- and the next layer's tiles are transformed from it: layer i's
+// NHWC activation never goes to HBM.
+template <int MI, int MO>
+__global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restrict__ Min, const float* __restrict__ bias,
+                                                          float* __restrict__ Vout, int h, int C, long long Ti,
+                                                          long long To) {
+    using WI = WinoT<MI>;
+    using WO = WinoT<MO>;
+    constexpr int NI = WI::N, NO = WO::N;
+    extern __shared__ float ys_raw[];  // [h * h][64]
+    float(*ys)[64] = reinterpret_cast<float(*)[64]>(ys_raw);
+    const int lane = threadIdx.x;
+    const int cblocks = C / 64;
+    const long long b = blockIdx.x / cblocks;
+    const int c = (blockIdx.x % cblocks) * 64 + lane;
+    const int ti = (h + MI - 1) / MI, to = (h - 2 + MO - 1) / MO;  // tiles per side: layer i, layer i+1
+    const float bc = bias[c];
+    for (int ty = 0; ty < ti; ++ty)
+        for (int tx = 0; tx < ti; ++tx) {
+            const long long t = (b * ti + ty) * ti + tx;
+            float mm[NI][NI];
+#pragma unroll
+            for (int e = 0; e < NI * NI; ++e) mm[e / NI][e % NI] = Min[((long long)e * Ti + t) * C + c];
+            float sr[MI][NI];
+#pragma unroll
+            for (int v = 0; v < NI; ++v)
+#pragma unroll
+                for (int a = 0; a < MI; ++a) {
+                    float acc = 0.f;
+                    bool first = true;
+#pragma unroll
+                    for (int u = 0; u < NI; ++u) {
+                        if (WI::AT[a][u] == 0.f) continue;
+                        const float term = WI::AT[a][u] == 1.f ? mm[u][v] : WI::AT[a][u] * mm[u][v];
+                        acc = first ? term : acc + term;
+                        first = false;
+                    }
+                    sr[a][v] = acc;
+                }
+#pragma unroll
+            for (int a = 0; a < MI; ++a)
+#pragma unroll
+                for (int q = 0; q < MI; ++q) {
+                    const int oy = MI * ty + a, ox = MI * tx + q;
+                    if (oy < h && ox < h) {
+                        float acc = 0.f;
+                        bool first = true;
+#pragma unroll
+                        for (int v = 0; v < NI; ++v) {
+                            if (WI::AT[q][v] == 0.f) continue;
+                            const float term = WI::AT[q][v] == 1.f ? sr[a][v] : WI::AT[q][v] * sr[a][v];
+                            acc = first ? term : acc + term;
+                            first = false;
+                        }
+                        ys[oy * h + ox][lane] = fmaxf(acc + bc, 0.f);
+                    }
+                }
+        }
+    for (int ty = 0; ty < to; ++ty)
+        for (int tx = 0; tx < to; ++tx) {
+            const long long t = (b * to + ty) * to + tx;
+            float d[NO][NO];
+#pragma unroll
+            for (int u = 0; u < NO; ++u)
+#pragma unroll
+                for (int v = 0; v < NO; ++v) {
+                    const int iy = MO * ty + u, ix = MO * tx + v;
+                    d[u][v] = (iy < h && ix < h) ? ys[iy * h + ix][lane] : 0.f;
+                }
+            float sr[NO][NO];
+#pragma unroll
+            for (int v = 0; v < NO; ++v)
+#pragma unroll
+                for (int a = 0; a < NO; ++a) {
+                    float acc = 0.f;
+                    bool first = true;
+#pragma unroll
+                    for (int u = 0; u < NO; ++u) {
+                        if (WO::BT[a][u] == 0.f) continue;
+                        const float term = WO::BT[a][u] == 1.f ? d[u][v] : WO::BT[a][u] * d[u][v];
+                        acc = first ? term : acc + term;
+                        first = false;
+                    }
+                    sr[a][v] = acc;
+                }
+#pragma unroll
+            for (int a = 0; a < NO; ++a)
+#pragma unroll
+                for (int bb = 0; bb < NO; ++bb) {
+                    float acc = 0.f;
+                    bool first = true;
+#pragma unroll
+                    for (int v = 0; v < NO; ++v) {
+                        if (WO::BT[bb][v] == 0.f) continue;
+                        const float term = WO::BT[bb][v] == 1.f ? sr[a][v] : WO::BT[bb][v] * sr[a][v];
+                        acc = first ? term : acc + term;
+                        first = false;
+                    }
+                    Vout[((long long)(a * NO + bb) * To + t) * C + c] = acc;
+                }
+        }
+}
+
 // one thread per work item, rounded up to whole groups of 8 blocks (xcd_item)
 unsigned grid_for(long long n) {
     const long long blocks = (n + 255) / 256;
@@ -213,5 +320,26 @@ extern "C" int azg_winograd_out_nhwc(const float* M, const float* bias, float* y
     else
         hipLaunchKernelGGL(winograd_out_kernel<3>, dim3(grid_for(T * (k / 4))), dim3(256), 0, (hipStream_t)stream,
                            (const float4*)M, (const float4*)bias, (float4*)y, h_out, k / 4, tiles, T, relu);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, float* V, int32_t batch, int32_t h, int32_t c,
+                                     int32_t m_in, int32_t m_out, void* stream) {
+    if (!M || !bias || !V || batch <= 0 || h < 3 || h > 9 || c <= 0 || c % 64 || (m_in != 2 && m_in != 3) ||
+        (m_out != 2 && m_out != 3))
+        return AZG_ERR_ARG;
+    const int ti = (h + m_in - 1) / m_in, to = (h - 2 + m_out - 1) / m_out;
+    const long long Ti = (long long)batch * ti * ti, To = (long long)batch * to * to;
+    const dim3 grid((unsigned)(batch * (c / 64)));
+    const size_t lds = (size_t)h * h * 64 * sizeof(float);
+    hipStream_t st = (hipStream_t)stream;
+    if (m_in == 2 && m_out == 2)
+        hipLaunchKernelGGL((winograd_mid_kernel<2, 2>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
+    else if (m_in == 2)
+        hipLaunchKernelGGL((winograd_mid_kernel<2, 3>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
+    else if (m_out == 2)
+        hipLaunchKernelGGL((winograd_mid_kernel<3, 2>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
+    else
+        hipLaunchKernelGGL((winograd_mid_kernel<3, 3>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }

@@ -140,6 +140,7 @@ class InferenceNet(nn.Module):
         self._choices = {}
         self._ws = None  # Winograd V / M workspace, grown to the largest layer seen
         self.tiles = {}  # Winograd output tile per conv layer
+        self.fuse_transforms = True  # conv2->3->4: output + next input transform in one pass
         self.n, self.depth, c = net.n, net.depth, net.num_channels
         self.pads = []
         h = net.n  # input side of conv i
@@ -182,14 +183,22 @@ class InferenceNet(nn.Module):
         # bias + ReLU inside the libazg conv's epilogue
         return _azg_conv3x3(x, getattr(self, f"wt{i}"), getattr(self, f"b{i}"), pad)
 
-    def _conv_winograd(self, x, i, pad, in_bias=None):
-        """Winograd F(2x2,3x3): libazg input transform, 16 f32 GEMMs (torch.bmm ->
-        hipBLASLt), libazg output transform with bias + ReLU (azg_winograd.hip)."""
+    def _conv_winograd(self, x, i, pad, in_bias=None, carried=False, B=None, H=None, fuse_next=False):
+        """Winograd F(m x m,3x3) layer i: libazg input transform (or, with carried=True,
+        the V the previous layer's fused transform left in the workspace), the n^2 f32
+        GEMMs (torch.bmm -> hipBLASLt), then either the output transform with bias + ReLU
+        (returns the NHWC activation) or, with fuse_next, the fused output / next-input
+        transform writing layer i+1's V (returns None) (azg_winograd.hip)."""
         import ctypes
         from . import _lib
-        if not x.is_contiguous(memory_format=torch.channels_last):
-            x = x.contiguous(memory_format=torch.channels_last)
-        B, C, H, _ = x.shape
+        if not carried:
+            if not x.is_contiguous(memory_format=torch.channels_last):
+                x = x.contiguous(memory_format=torch.channels_last)
+            B, C, H, _ = x.shape
+            dev = x.device
+        else:
+            C = getattr(self, f"u{i}").shape[1]
+            dev = self._ws[0].device
         U = getattr(self, f"u{i}")
         m = self.tiles[i]
         nn2 = (m + 2) ** 2
@@ -198,19 +207,31 @@ class InferenceNet(nn.Module):
         t = (Ho + m - 1) // m
         T = B * t * t
         need = nn2 * T * max(C, K)
+        if fuse_next:
+            m2 = self.tiles[i + 1]
+            t2 = (Ho - 2 + m2 - 1) // m2
+            need = max(need, (m2 + 2) ** 2 * B * t2 * t2 * K)
         if self._ws is None or self._ws[0].numel() < need:
-            self._ws = (torch.empty(need, device=x.device), torch.empty(need, device=x.device))
+            if carried:
+                raise RuntimeError("Winograd workspace too small for a carried layer")
+            self._ws = (torch.empty(need, device=dev), torch.empty(need, device=dev))
         V = self._ws[0][:nn2 * T * C].view(nn2, T, C)
         M = self._ws[1][:nn2 * T * K].view(nn2, T, K)
-        s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         L = _lib.lib()
-        ib = ctypes.c_void_p(in_bias.data_ptr()) if in_bias is not None else None
-        _lib.check(L.azg_winograd_in_nhwc(ctypes.c_void_p(x.data_ptr()), ib, ctypes.c_void_p(V.data_ptr()),
-                                          B, H, pad, C, m, s))
+        bias = ctypes.c_void_p(getattr(self, f"b{i}").data_ptr())
+        if not carried:
+            ib = ctypes.c_void_p(in_bias.data_ptr()) if in_bias is not None else None
+            _lib.check(L.azg_winograd_in_nhwc(ctypes.c_void_p(x.data_ptr()), ib, ctypes.c_void_p(V.data_ptr()),
+                                              B, H, pad, C, m, s))
         torch.bmm(V, U, out=M)
-        y = torch.empty((B, K, Ho, Ho), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
-        _lib.check(L.azg_winograd_out_nhwc(ctypes.c_void_p(M.data_ptr()), ctypes.c_void_p(getattr(self, f"b{i}").data_ptr()),
-                                           ctypes.c_void_p(y.data_ptr()), B, Ho, K, m, 1, s))
+        if fuse_next:
+            _lib.check(L.azg_winograd_mid_nhwc(ctypes.c_void_p(M.data_ptr()), bias,
+                                               ctypes.c_void_p(self._ws[0].data_ptr()), B, Ho, K, m, m2, s))
+            return None
+        y = torch.empty((B, K, Ho, Ho), device=dev, dtype=torch.float32, memory_format=torch.channels_last)
+        _lib.check(L.azg_winograd_out_nhwc(ctypes.c_void_p(M.data_ptr()), bias, ctypes.c_void_p(y.data_ptr()),
+                                           B, Ho, K, m, 1, s))
         return y
 
     def _pick(self, x, i, pad):
@@ -250,8 +271,13 @@ class InferenceNet(nn.Module):
                 impl = "miopen"  # a few leaves: the 16 small GEMMs lose to one direct conv
             impls.append(impl)
         pending = None  # bias of the previous conv, to be applied (with ReLU) by this one's input transform
+        carried = False  # this layer's V was written by the previous layer's fused transform
+        B, H = x.shape[0], self.n
         for i, pad in enumerate(self.pads, start=1):
             impl = impls[i - 1]
+            h_out = H + 2 * pad - 2
+            fuse_next = (fused and self.fuse_transforms and impl == "winograd" and i < 4
+                         and impls[i] == "winograd" and self.pads[i] == 0)
             if fused and impl == "auto":
                 impl = self._pick(x, i, pad)
             if hook:
@@ -261,8 +287,9 @@ class InferenceNet(nn.Module):
             elif impl == "azg":
                 x = self._conv_azg(x, i, pad)
             elif impl == "winograd":
-                x = self._conv_winograd(x, i, pad, in_bias=pending)
+                x = self._conv_winograd(x, i, pad, in_bias=pending, carried=carried, B=B, H=H, fuse_next=fuse_next)
                 pending = None
+                carried = fuse_next
             elif i == 1 and impls[1] == "winograd":
                 # conv1's bias + ReLU ride in conv2's Winograd input transform (no separate pass)
                 x = F.conv2d(x, self.w1, None, padding=pad)
@@ -271,6 +298,7 @@ class InferenceNet(nn.Module):
                 x = self._conv_miopen(x, i, pad)
             if hook:
                 hook(i, "stop")
+            H = h_out
         x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten, no copy
         x = torch.relu_(torch.addmm(self.fb1, x, self.fw1.t()))
         x = torch.relu_(torch.addmm(self.fb2, x, self.fw2.t()))

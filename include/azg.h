@@ -153,6 +153,12 @@ int  azg_winograd_in_nhwc(const float* x, const float* in_bias, float* V, int32_
                           int32_t c, int32_t m, void* stream);
 int  azg_winograd_out_nhwc(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,
                            int32_t m, int32_t relu, void* stream);
+/* Between two Winograd layers with no padding on the second (conv2->conv3->conv4):
+ * M of layer i (tile m_in, h x h outputs, c channels) -> relu(A^T M A + bias) ->
+ * V of layer i+1 (tile m_out, input h x h) in one pass; the activation stays
+ * on chip.  3 <= h <= 9, c % 64 == 0. */
+int  azg_winograd_mid_nhwc(const float* M, const float* bias, float* V, int32_t batch, int32_t h, int32_t c,
+                           int32_t m_in, int32_t m_out, void* stream);
 
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active

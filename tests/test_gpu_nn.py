@@ -115,3 +115,19 @@ def test_winograd_conv3x3_matches_torch(B, H, pad, m):
     want = torch.relu(torch.nn.functional.conv2d(x, w.cuda(), b, padding=pad))
     got = fast._conv_winograd(x, layer, pad)
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
+
+
+def test_winograd_fused_transforms_match_unfused():
+    """conv2->conv3->conv4 with the fused output/next-input transform (default) vs
+    separate output and input transforms: the same arithmetic, so equal results."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    torch.manual_seed(4)
+    net = InflexionNNet().cuda().eval()
+    a, b = InferenceNet(net).cuda(), InferenceNet(net).cuda()
+    b.fuse_transforms = False
+    x = (torch.rand(300, 4, 7, 7, device="cuda") < 0.3).float()
+    with torch.no_grad():
+        pa, va = a(x)
+        pb, vb = b(x)
+    assert torch.equal(pa, pb) and torch.equal(va, vb)
