@@ -281,6 +281,100 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
         }
 }
 
+// The network's first two layers' front end in one pass: conv1 (depth -> C
+// channels, 3x3, pad 1) + bias + ReLU computed directly from the NCHW leaf
+// planes, then conv2's Winograd input transform (pad 1) -- conv1's activation
+// never leaves the chip.  One wave per (image, 64 output channels of conv1),
+// one channel per lane: the image's planes are shared through LDS, the lane's
+// depth*9 weights sit in registers, its n x n output plane in its own LDS
+// column (no barrier needed for it).
+template <int MO>
+__global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restrict__ planes,
+                                                            const float* __restrict__ w1,
+                                                            const float* __restrict__ b1, float* __restrict__ Vout,
+                                                            int depth, int n, int C, long long To) {
+    using WO = WinoT<MO>;
+    constexpr int NO = WO::N;
+    constexpr int DMAX = 4;
+    extern __shared__ float lds[];
+    float* xs = lds;                                               // [depth][n][n]
+    float(*ys)[64] = reinterpret_cast<float(*)[64]>(lds + DMAX * 81);  // [n * n][64]
+    const int lane = threadIdx.x;
+    const int cblocks = C / 64;
+    const long long b = blockIdx.x / cblocks;
+    const int k = (blockIdx.x % cblocks) * 64 + lane;
+    for (int i = lane; i < depth * n * n; i += 64) xs[i] = planes[b * depth * n * n + i];
+    float w[DMAX * 9];
+#pragma unroll
+    for (int j = 0; j < DMAX * 9; ++j) w[j] = j < depth * 9 ? w1[(size_t)k * depth * 9 + j] : 0.f;
+    const float bk = b1[k];
+    __syncthreads();
+    for (int y = 0; y < n; ++y)
+        for (int x = 0; x < n; ++x) {
+            float acc = 0.f;
+#pragma unroll
+            for (int c = 0; c < DMAX; ++c) {
+                if (c >= depth) break;
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy) {
+                    const int iy = y + dy - 1;
+                    if (iy < 0 || iy >= n) continue;
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx) {
+                        const int ix = x + dx - 1;
+                        if (ix < 0 || ix >= n) continue;
+                        acc = fmaf(w[c * 9 + dy * 3 + dx], xs[(c * n + iy) * n + ix], acc);
+                    }
+                }
+            }
+            ys[y * n + x][lane] = fmaxf(acc + bk, 0.f);
+        }
+    const int to = (n + MO - 1) / MO;  // conv2: pad 1, n x n outputs
+    for (int ty = 0; ty < to; ++ty)
+        for (int tx = 0; tx < to; ++tx) {
+            const long long t = (b * to + ty) * to + tx;
+            float d[NO][NO];
+#pragma unroll
+            for (int u = 0; u < NO; ++u)
+#pragma unroll
+                for (int v = 0; v < NO; ++v) {
+                    const int iy = MO * ty - 1 + u, ix = MO * tx - 1 + v;
+                    d[u][v] = (iy >= 0 && iy < n && ix >= 0 && ix < n) ? ys[iy * n + ix][lane] : 0.f;
+                }
+            float sr[NO][NO];
+#pragma unroll
+            for (int v = 0; v < NO; ++v)
+#pragma unroll
+                for (int a = 0; a < NO; ++a) {
+                    float acc = 0.f;
+                    bool first = true;
+#pragma unroll
+                    for (int u = 0; u < NO; ++u) {
+                        if (WO::BT[a][u] == 0.f) continue;
+                        const float term = WO::BT[a][u] == 1.f ? d[u][v] : WO::BT[a][u] * d[u][v];
+                        acc = first ? term : acc + term;
+                        first = false;
+                    }
+                    sr[a][v] = acc;
+                }
+#pragma unroll
+            for (int a = 0; a < NO; ++a)
+#pragma unroll
+                for (int bb = 0; bb < NO; ++bb) {
+                    float acc = 0.f;
+                    bool first = true;
+#pragma unroll
+                    for (int v = 0; v < NO; ++v) {
+                        if (WO::BT[bb][v] == 0.f) continue;
+                        const float term = WO::BT[bb][v] == 1.f ? sr[a][v] : WO::BT[bb][v] * sr[a][v];
+                        acc = first ? term : acc + term;
+                        first = false;
+                    }
+                    Vout[((long long)(a * NO + bb) * To + t) * C + k] = acc;
+                }
+        }
+}
+
 // one thread per work item, rounded up to whole groups of 8 blocks (xcd_item)
 unsigned grid_for(long long n) {
     const long long blocks = (n + 255) / 256;
@@ -341,5 +435,22 @@ extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, float* V
         hipLaunchKernelGGL((winograd_mid_kernel<3, 2>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
     else
         hipLaunchKernelGGL((winograd_mid_kernel<3, 3>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+extern "C" int azg_winograd_first_nchw(const float* planes, const float* w1, const float* b1, float* V, int32_t batch,
+                                       int32_t depth, int32_t n, int32_t c, int32_t m, void* stream) {
+    if (!planes || !w1 || !b1 || !V || batch <= 0 || depth < 1 || depth > 4 || n < 3 || n > 9 || c <= 0 ||
+        c % 64 || (m != 2 && m != 3))
+        return AZG_ERR_ARG;
+    const int to = (n + m - 1) / m;
+    const long long To = (long long)batch * to * to;
+    const dim3 grid((unsigned)(batch * (c / 64)));
+    const size_t lds = (4 * 81 + (size_t)n * n * 64) * sizeof(float);
+    hipStream_t st = (hipStream_t)stream;
+    if (m == 2)
+        hipLaunchKernelGGL(winograd_first_kernel<2>, grid, dim3(64), lds, st, planes, w1, b1, V, depth, n, c, To);
+    else
+        hipLaunchKernelGGL(winograd_first_kernel<3>, grid, dim3(64), lds, st, planes, w1, b1, V, depth, n, c, To);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }

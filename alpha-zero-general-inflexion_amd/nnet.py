@@ -152,6 +152,8 @@ class InferenceNet(nn.Module):
             self.register_buffer(f"b{i}", b)
             # [9*Cin, Cout] k-major copy for the libazg implicit GEMM (k = (dy*3+dx)*Cin + c)
             self.register_buffer(f"wt{i}", w.permute(2, 3, 1, 0).reshape(-1, w.shape[0]).contiguous())
+            if i == 1:
+                self.register_buffer("w1c", w.contiguous())  # [K][depth][3][3] for the fused front end
             if i > 1 and conv in ("winograd", "auto"):
                 self.tiles[i] = winograd_tile(h_out)
                 self.register_buffer(f"u{i}", _winograd_u(w, self.tiles[i]))
@@ -183,6 +185,35 @@ class InferenceNet(nn.Module):
         # bias + ReLU inside the libazg conv's epilogue
         return _azg_conv3x3(x, getattr(self, f"wt{i}"), getattr(self, f"b{i}"), pad)
 
+    def _wino_need(self, i, B, H, pad, C, fuse_next):
+        """Workspace elements layer i needs: V [n^2][T][C], M [n^2][T][K] and, fused, the next layer's V."""
+        m, K = self.tiles[i], getattr(self, f"u{i}").shape[2]
+        Ho = H + 2 * pad - 2
+        t = (Ho + m - 1) // m
+        need = (m + 2) ** 2 * B * t * t * max(C, K)
+        if fuse_next:
+            m2 = self.tiles[i + 1]
+            t2 = (Ho - 2 + m2 - 1) // m2
+            need = max(need, (m2 + 2) ** 2 * B * t2 * t2 * K)
+        return need
+
+    def _ensure_ws(self, need, dev):
+        if self._ws is None or self._ws[0].numel() < need:
+            self._ws = (torch.empty(need, device=dev), torch.empty(need, device=dev))
+
+    def _first_winograd(self, s):
+        """conv1 + bias + ReLU + conv2's Winograd input transform straight from the NCHW
+        planes (azg_winograd_first_nchw); conv2's V is left in the workspace."""
+        import ctypes
+        from . import _lib
+        B = s.shape[0]
+        C = self.w1c.shape[0]
+        self._ensure_ws(self._wino_need(2, B, self.n, self.pads[1], C, True), s.device)
+        st = ctypes.c_void_p(torch.cuda.current_stream(s.device).cuda_stream)
+        _lib.check(_lib.lib().azg_winograd_first_nchw(
+            ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(self.w1c.data_ptr()), ctypes.c_void_p(self.b1.data_ptr()),
+            ctypes.c_void_p(self._ws[0].data_ptr()), B, self.depth, self.n, C, self.tiles[2], st))
+
     def _conv_winograd(self, x, i, pad, in_bias=None, carried=False, B=None, H=None, fuse_next=False):
         """Winograd F(m x m,3x3) layer i: libazg input transform (or, with carried=True,
         the V the previous layer's fused transform left in the workspace), the n^2 f32
@@ -206,15 +237,12 @@ class InferenceNet(nn.Module):
         Ho = H + 2 * pad - 2
         t = (Ho + m - 1) // m
         T = B * t * t
-        need = nn2 * T * max(C, K)
         if fuse_next:
             m2 = self.tiles[i + 1]
-            t2 = (Ho - 2 + m2 - 1) // m2
-            need = max(need, (m2 + 2) ** 2 * B * t2 * t2 * K)
-        if self._ws is None or self._ws[0].numel() < need:
-            if carried:
-                raise RuntimeError("Winograd workspace too small for a carried layer")
-            self._ws = (torch.empty(need, device=dev), torch.empty(need, device=dev))
+        if not carried:
+            self._ensure_ws(self._wino_need(i, B, H, pad, C, fuse_next), dev)
+        elif self._ws is None or self._ws[0].numel() < self._wino_need(i, B, H, pad, C, fuse_next):
+            raise RuntimeError("Winograd workspace too small for a carried layer")
         V = self._ws[0][:nn2 * T * C].view(nn2, T, C)
         M = self._ws[1][:nn2 * T * K].view(nn2, T, K)
         s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
@@ -261,7 +289,8 @@ class InferenceNet(nn.Module):
         return best[0]
 
     def forward(self, s):
-        x = s.view(-1, self.depth, self.n, self.n).contiguous(memory_format=torch.channels_last)
+        planes = s.view(-1, self.depth, self.n, self.n)
+        x = planes.contiguous(memory_format=torch.channels_last)
         hook = self.conv_hook
         fused = x.is_cuda
         impls = []
@@ -273,6 +302,8 @@ class InferenceNet(nn.Module):
         pending = None  # bias of the previous conv, to be applied (with ReLU) by this one's input transform
         carried = False  # this layer's V was written by the previous layer's fused transform
         B, H = x.shape[0], self.n
+        first_fused = (fused and self.fuse_transforms and impls[1] == "winograd" and self.pads == [1, 1, 0, 0]
+                       and self.depth <= 4 and 3 <= self.n <= 9 and self.w1c.shape[0] % 64 == 0)
         for i, pad in enumerate(self.pads, start=1):
             impl = impls[i - 1]
             h_out = H + 2 * pad - 2
@@ -282,7 +313,10 @@ class InferenceNet(nn.Module):
                 impl = self._pick(x, i, pad)
             if hook:
                 hook(i, "start")
-            if not fused:
+            if i == 1 and first_fused:
+                self._first_winograd(planes.contiguous())
+                carried = True
+            elif not fused:
                 x = torch.relu_(F.conv2d(x, getattr(self, f"w{i}"), getattr(self, f"b{i}"), padding=pad))
             elif impl == "azg":
                 x = self._conv_azg(x, i, pad)

@@ -159,6 +159,12 @@ int  azg_winograd_out_nhwc(const float* M, const float* bias, float* y, int32_t 
  * on chip.  3 <= h <= 9, c % 64 == 0. */
 int  azg_winograd_mid_nhwc(const float* M, const float* bias, float* V, int32_t batch, int32_t h, int32_t c,
                            int32_t m_in, int32_t m_out, void* stream);
+/* The first two layers' front end: conv1 (planes NCHW [batch, depth, n, n] ->
+ * c channels, 3x3, pad 1, weights w1 [c][depth][3][3], bias b1) + ReLU, then
+ * conv2's Winograd input transform (pad 1, tile m) -> V [(m+2)^2][T][c] in one
+ * pass.  depth <= 4, 3 <= n <= 9, c % 64 == 0. */
+int  azg_winograd_first_nchw(const float* planes, const float* w1, const float* b1, float* V, int32_t batch,
+                             int32_t depth, int32_t n, int32_t c, int32_t m, void* stream);
 
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active

@@ -118,8 +118,9 @@ def test_winograd_conv3x3_matches_torch(B, H, pad, m):
 
 
 def test_winograd_fused_transforms_match_unfused():
-    """conv2->conv3->conv4 with the fused output/next-input transform (default) vs
-    separate output and input transforms: the same arithmetic, so equal results."""
+    """The fused front end (conv1 + conv2's input transform) and the fused
+    output/next-input transforms (default) vs MIOpen conv1 and separate
+    transforms: same math, conv1 summed in another order (1e-5)."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
     torch.manual_seed(4)
@@ -130,4 +131,5 @@ def test_winograd_fused_transforms_match_unfused():
     with torch.no_grad():
         pa, va = a(x)
         pb, vb = b(x)
-    assert torch.equal(pa, pb) and torch.equal(va, vb)
+    torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(va, vb, rtol=1e-5, atol=1e-6)
