@@ -174,69 +174,108 @@ __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restr
     }
 }
 
-// Layer i's output transform fused with layer i+1's input transform (pad 0
-// between them, as conv2->conv3->conv4): one wave per (image, 64 channels),
-// each lane owning one channel.  The lane's h x h output plane of layer i
-// (bias + ReLU applied) is staged in LDS -- only that lane reads it back, so
-// no barrier -- and the next layer's tiles are transformed from it: layer i's
-// NHWC activation never goes to HBM.
-template <int MI, int MO>
-__global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restrict__ Min, const float* __restrict__ bias,
-                                                          float* __restrict__ Vout, int h, int C, long long Ti,
-                                                          long long To) {
-    using WI = WinoT<MI>;
-    using WO = WinoT<MO>;
-    constexpr int NI = WI::N, NO = WO::N;
-    extern __shared__ float ys_raw[];  // [h * h][64]
-    float(*ys)[64] = reinterpret_cast<float(*)[64]>(ys_raw);
-    const int lane = threadIdx.x;
-    const int cblocks = C / 64;
-    const long long b = blockIdx.x / cblocks;
-    const int c = (blockIdx.x % cblocks) * 64 + lane;
-    const int ti = (h + MI - 1) / MI, to = (h - 2 + MO - 1) / MO;  // tiles per side: layer i, layer i+1
-    const float bc = bias[c];
-    for (int ty = 0; ty < ti; ++ty)
-        for (int tx = 0; tx < ti; ++tx) {
-            const long long t = (b * ti + ty) * ti + tx;
-            float mm[NI][NI];
+// scalar (one channel) tile transforms: y = A^T m A (m x m) and V = B^T d B (n x n)
+template <int MI>
+__device__ __forceinline__ void out_tile(const float (&mm)[WinoT<MI>::N][WinoT<MI>::N], float (&y)[MI][MI]) {
+    using W = WinoT<MI>;
+    constexpr int N = W::N;
+    float sr[MI][N];
 #pragma unroll
-            for (int e = 0; e < NI * NI; ++e) mm[e / NI][e % NI] = Min[((long long)e * Ti + t) * C + c];
-            float sr[MI][NI];
+    for (int v = 0; v < N; ++v)
 #pragma unroll
-            for (int v = 0; v < NI; ++v)
+        for (int a = 0; a < MI; ++a) {
+            float acc = 0.f;
+            bool first = true;
 #pragma unroll
-                for (int a = 0; a < MI; ++a) {
-                    float acc = 0.f;
-                    bool first = true;
-#pragma unroll
-                    for (int u = 0; u < NI; ++u) {
-                        if (WI::AT[a][u] == 0.f) continue;
-                        const float term = WI::AT[a][u] == 1.f ? mm[u][v] : WI::AT[a][u] * mm[u][v];
-                        acc = first ? term : acc + term;
-                        first = false;
-                    }
-                    sr[a][v] = acc;
-                }
-#pragma unroll
-            for (int a = 0; a < MI; ++a)
-#pragma unroll
-                for (int q = 0; q < MI; ++q) {
-                    const int oy = MI * ty + a, ox = MI * tx + q;
-                    if (oy < h && ox < h) {
-                        float acc = 0.f;
-                        bool first = true;
-#pragma unroll
-                        for (int v = 0; v < NI; ++v) {
-                            if (WI::AT[q][v] == 0.f) continue;
-                            const float term = WI::AT[q][v] == 1.f ? sr[a][v] : WI::AT[q][v] * sr[a][v];
-                            acc = first ? term : acc + term;
-                            first = false;
-                        }
-                        ys[oy * h + ox][lane] = fmaxf(acc + bc, 0.f);
-                    }
-                }
+            for (int u = 0; u < N; ++u) {
+                if (W::AT[a][u] == 0.f) continue;
+                const float term = W::AT[a][u] == 1.f ? mm[u][v] : W::AT[a][u] * mm[u][v];
+                acc = first ? term : acc + term;
+                first = false;
+            }
+            sr[a][v] = acc;
         }
+#pragma unroll
+    for (int a = 0; a < MI; ++a)
+#pragma unroll
+        for (int q = 0; q < MI; ++q) {
+            float acc = 0.f;
+            bool first = true;
+#pragma unroll
+            for (int v = 0; v < N; ++v) {
+                if (W::AT[q][v] == 0.f) continue;
+                const float term = W::AT[q][v] == 1.f ? sr[a][v] : W::AT[q][v] * sr[a][v];
+                acc = first ? term : acc + term;
+                first = false;
+            }
+            y[a][q] = acc;
+        }
+}
+
+template <int MO>
+__device__ __forceinline__ void in_tile(const float (&d)[WinoT<MO>::N][WinoT<MO>::N],
+                                        float (&V)[WinoT<MO>::N][WinoT<MO>::N]) {
+    using W = WinoT<MO>;
+    constexpr int N = W::N;
+    float sr[N][N];
+#pragma unroll
+    for (int v = 0; v < N; ++v)
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            float acc = 0.f;
+            bool first = true;
+#pragma unroll
+            for (int u = 0; u < N; ++u) {
+                if (W::BT[a][u] == 0.f) continue;
+                const float term = W::BT[a][u] == 1.f ? d[u][v] : W::BT[a][u] * d[u][v];
+                acc = first ? term : acc + term;
+                first = false;
+            }
+            sr[a][v] = acc;
+        }
+#pragma unroll
+    for (int a = 0; a < N; ++a)
+#pragma unroll
+        for (int bb = 0; bb < N; ++bb) {
+            float acc = 0.f;
+            bool first = true;
+#pragma unroll
+            for (int v = 0; v < N; ++v) {
+                if (W::BT[bb][v] == 0.f) continue;
+                const float term = W::BT[bb][v] == 1.f ? sr[a][v] : W::BT[bb][v] * sr[a][v];
+                acc = first ? term : acc + term;
+                first = false;
+            }
+            V[a][bb] = acc;
+        }
+}
+
+// A lane's private h x h plane: in registers when the side is a compile-time
+// HC (loops fully unrolled, every index constant), else in its own LDS column.
+template <int HC>
+struct Plane {
+    float r[HC > 0 ? HC * HC : 1];
+    float* lds;
+    int lane;
+    __device__ __forceinline__ void put(int i, float v) {
+        if constexpr (HC > 0) r[i] = v;
+        else lds[i * 64 + lane] = v;
+    }
+    __device__ __forceinline__ float get(int i) const {
+        if constexpr (HC > 0) return r[i];
+        else return lds[i * 64 + lane];
+    }
+};
+
+// Next layer's input transform (pad `pad`) of the lane's h x h plane: V tiles out.
+template <int MO, int HC, class P>
+__device__ __forceinline__ void plane_to_V(const P& ys, int h, int pad, long long b, int c, int C, long long To,
+                                           float* __restrict__ Vout) {
+    constexpr int NO = WinoT<MO>::N;
+    const int to = (h + 2 * pad - 2 + MO - 1) / MO;
+#pragma unroll
     for (int ty = 0; ty < to; ++ty)
+#pragma unroll
         for (int tx = 0; tx < to; ++tx) {
             const long long t = (b * to + ty) * to + tx;
             float d[NO][NO];
@@ -244,41 +283,59 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
             for (int u = 0; u < NO; ++u)
 #pragma unroll
                 for (int v = 0; v < NO; ++v) {
-                    const int iy = MO * ty + u, ix = MO * tx + v;
-                    d[u][v] = (iy < h && ix < h) ? ys[iy * h + ix][lane] : 0.f;
+                    const int iy = MO * ty - pad + u, ix = MO * tx - pad + v;
+                    d[u][v] = (iy >= 0 && iy < h && ix >= 0 && ix < h) ? ys.get(iy * h + ix) : 0.f;
                 }
-            float sr[NO][NO];
-#pragma unroll
-            for (int v = 0; v < NO; ++v)
-#pragma unroll
-                for (int a = 0; a < NO; ++a) {
-                    float acc = 0.f;
-                    bool first = true;
-#pragma unroll
-                    for (int u = 0; u < NO; ++u) {
-                        if (WO::BT[a][u] == 0.f) continue;
-                        const float term = WO::BT[a][u] == 1.f ? d[u][v] : WO::BT[a][u] * d[u][v];
-                        acc = first ? term : acc + term;
-                        first = false;
-                    }
-                    sr[a][v] = acc;
-                }
+            float V[NO][NO];
+            in_tile<MO>(d, V);
 #pragma unroll
             for (int a = 0; a < NO; ++a)
 #pragma unroll
-                for (int bb = 0; bb < NO; ++bb) {
-                    float acc = 0.f;
-                    bool first = true;
+                for (int bb = 0; bb < NO; ++bb) Vout[((long long)(a * NO + bb) * To + t) * C + c] = V[a][bb];
+        }
+}
+
+// Layer i's output transform fused with layer i+1's input transform (pad 0
+// between them, as conv2->conv3->conv4): one wave per (image, 64 channels),
+// each lane owning one channel.  The lane's h x h output plane of layer i
+// (bias + ReLU applied) is kept in registers (compile-time side HC) or its own
+// LDS column -- only that lane reads it back, so no barrier -- and the next
+// layer's tiles are transformed from it: layer i's activation never goes to HBM.
+template <int MI, int MO, int HC>
+__global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restrict__ Min, const float* __restrict__ bias,
+                                                          float* __restrict__ Vout, int h_rt, int C, long long Ti,
+                                                          long long To) {
+    constexpr int NI = WinoT<MI>::N;
+    extern __shared__ float ys_raw[];  // [h * h][64] when HC == 0
+    const int h = HC > 0 ? HC : h_rt;
+    const int lane = threadIdx.x;
+    const int cblocks = C / 64;
+    const long long b = blockIdx.x / cblocks;
+    const int c = (blockIdx.x % cblocks) * 64 + lane;
+    const int ti = (h + MI - 1) / MI;
+    const float bc = bias[c];
+    Plane<HC> ys;
+    ys.lds = ys_raw;
+    ys.lane = lane;
 #pragma unroll
-                    for (int v = 0; v < NO; ++v) {
-                        if (WO::BT[bb][v] == 0.f) continue;
-                        const float term = WO::BT[bb][v] == 1.f ? sr[a][v] : WO::BT[bb][v] * sr[a][v];
-                        acc = first ? term : acc + term;
-                        first = false;
-                    }
-                    Vout[((long long)(a * NO + bb) * To + t) * C + c] = acc;
+    for (int ty = 0; ty < ti; ++ty)
+#pragma unroll
+        for (int tx = 0; tx < ti; ++tx) {
+            const long long t = (b * ti + ty) * ti + tx;
+            float mm[NI][NI];
+#pragma unroll
+            for (int e = 0; e < NI * NI; ++e) mm[e / NI][e % NI] = Min[((long long)e * Ti + t) * C + c];
+            float y[MI][MI];
+            out_tile<MI>(mm, y);
+#pragma unroll
+            for (int a = 0; a < MI; ++a)
+#pragma unroll
+                for (int q = 0; q < MI; ++q) {
+                    const int oy = MI * ty + a, ox = MI * tx + q;
+                    if (oy < h && ox < h) ys.put(oy * h + ox, fmaxf(y[a][q] + bc, 0.f));
                 }
         }
+    plane_to_V<MO, HC>(ys, h, 0, b, c, C, To, Vout);
 }
 
 // The network's first two layers' front end in one pass: conv1 (depth -> C
@@ -286,19 +343,17 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
 // planes, then conv2's Winograd input transform (pad 1) -- conv1's activation
 // never leaves the chip.  One wave per (image, 64 output channels of conv1),
 // one channel per lane: the image's planes are shared through LDS, the lane's
-// depth*9 weights sit in registers, its n x n output plane in its own LDS
-// column (no barrier needed for it).
-template <int MO>
+// depth*9 weights and its n x n output plane sit in registers (compile-time
+// side NC) or its own LDS column.
+template <int MO, int NC>
 __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restrict__ planes,
                                                             const float* __restrict__ w1,
                                                             const float* __restrict__ b1, float* __restrict__ Vout,
-                                                            int depth, int n, int C, long long To) {
-    using WO = WinoT<MO>;
-    constexpr int NO = WO::N;
+                                                            int depth, int n_rt, int C, long long To) {
     constexpr int DMAX = 4;
     extern __shared__ float lds[];
-    float* xs = lds;                                               // [depth][n][n]
-    float(*ys)[64] = reinterpret_cast<float(*)[64]>(lds + DMAX * 81);  // [n * n][64]
+    float* xs = lds;  // [depth][n][n], then (NC == 0) the lanes' planes [n * n][64]
+    const int n = NC > 0 ? NC : n_rt;
     const int lane = threadIdx.x;
     const int cblocks = C / 64;
     const long long b = blockIdx.x / cblocks;
@@ -309,7 +364,12 @@ __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restr
     for (int j = 0; j < DMAX * 9; ++j) w[j] = j < depth * 9 ? w1[(size_t)k * depth * 9 + j] : 0.f;
     const float bk = b1[k];
     __syncthreads();
+    Plane<NC> ys;
+    ys.lds = lds + DMAX * 81;
+    ys.lane = lane;
+#pragma unroll
     for (int y = 0; y < n; ++y)
+#pragma unroll
         for (int x = 0; x < n; ++x) {
             float acc = 0.f;
 #pragma unroll
@@ -327,52 +387,9 @@ __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restr
                     }
                 }
             }
-            ys[y * n + x][lane] = fmaxf(acc + bk, 0.f);
+            ys.put(y * n + x, fmaxf(acc + bk, 0.f));
         }
-    const int to = (n + MO - 1) / MO;  // conv2: pad 1, n x n outputs
-    for (int ty = 0; ty < to; ++ty)
-        for (int tx = 0; tx < to; ++tx) {
-            const long long t = (b * to + ty) * to + tx;
-            float d[NO][NO];
-#pragma unroll
-            for (int u = 0; u < NO; ++u)
-#pragma unroll
-                for (int v = 0; v < NO; ++v) {
-                    const int iy = MO * ty - 1 + u, ix = MO * tx - 1 + v;
-                    d[u][v] = (iy >= 0 && iy < n && ix >= 0 && ix < n) ? ys[iy * n + ix][lane] : 0.f;
-                }
-            float sr[NO][NO];
-#pragma unroll
-            for (int v = 0; v < NO; ++v)
-#pragma unroll
-                for (int a = 0; a < NO; ++a) {
-                    float acc = 0.f;
-                    bool first = true;
-#pragma unroll
-                    for (int u = 0; u < NO; ++u) {
-                        if (WO::BT[a][u] == 0.f) continue;
-                        const float term = WO::BT[a][u] == 1.f ? d[u][v] : WO::BT[a][u] * d[u][v];
-                        acc = first ? term : acc + term;
-                        first = false;
-                    }
-                    sr[a][v] = acc;
-                }
-#pragma unroll
-            for (int a = 0; a < NO; ++a)
-#pragma unroll
-                for (int bb = 0; bb < NO; ++bb) {
-                    float acc = 0.f;
-                    bool first = true;
-#pragma unroll
-                    for (int v = 0; v < NO; ++v) {
-                        if (WO::BT[bb][v] == 0.f) continue;
-                        const float term = WO::BT[bb][v] == 1.f ? sr[a][v] : WO::BT[bb][v] * sr[a][v];
-                        acc = first ? term : acc + term;
-                        first = false;
-                    }
-                    Vout[((long long)(a * NO + bb) * To + t) * C + k] = acc;
-                }
-        }
+    plane_to_V<MO, NC>(ys, n, 1, b, k, C, To, Vout);
 }
 
 // one thread per work item, rounded up to whole groups of 8 blocks (xcd_item)
@@ -427,14 +444,26 @@ extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, float* V
     const dim3 grid((unsigned)(batch * (c / 64)));
     const size_t lds = (size_t)h * h * 64 * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
+    // the board sides of the supported games get register-resident planes
+#define AZG_MID_REG(MI, MO, H)                                                                              \
+    if (m_in == MI && m_out == MO && h == H) {                                                              \
+        hipLaunchKernelGGL((winograd_mid_kernel<MI, MO, H>), grid, dim3(64), 0, st, M, bias, V, h, c, Ti, To); \
+        return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                           \
+    }
+    AZG_MID_REG(3, 3, 7)
+    AZG_MID_REG(3, 3, 5)
+    AZG_MID_REG(3, 3, 8)
+    AZG_MID_REG(3, 2, 6)
+    AZG_MID_REG(2, 2, 4)
+#undef AZG_MID_REG
     if (m_in == 2 && m_out == 2)
-        hipLaunchKernelGGL((winograd_mid_kernel<2, 2>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
+        hipLaunchKernelGGL((winograd_mid_kernel<2, 2, 0>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
     else if (m_in == 2)
-        hipLaunchKernelGGL((winograd_mid_kernel<2, 3>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
+        hipLaunchKernelGGL((winograd_mid_kernel<2, 3, 0>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
     else if (m_out == 2)
-        hipLaunchKernelGGL((winograd_mid_kernel<3, 2>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
+        hipLaunchKernelGGL((winograd_mid_kernel<3, 2, 0>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
     else
-        hipLaunchKernelGGL((winograd_mid_kernel<3, 3>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
+        hipLaunchKernelGGL((winograd_mid_kernel<3, 3, 0>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
@@ -446,11 +475,21 @@ extern "C" int azg_winograd_first_nchw(const float* planes, const float* w1, con
     const int to = (n + m - 1) / m;
     const long long To = (long long)batch * to * to;
     const dim3 grid((unsigned)(batch * (c / 64)));
-    const size_t lds = (4 * 81 + (size_t)n * n * 64) * sizeof(float);
+    const size_t lds_reg = 4 * 81 * sizeof(float), lds = (4 * 81 + (size_t)n * n * 64) * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
+#define AZG_FIRST_REG(MO, N)                                                                                     \
+    if (m == MO && n == N) {                                                                                     \
+        hipLaunchKernelGGL((winograd_first_kernel<MO, N>), grid, dim3(64), lds_reg, st, planes, w1, b1, V, depth, n, \
+                           c, To);                                                                              \
+        return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                               \
+    }
+    AZG_FIRST_REG(3, 7)
+    AZG_FIRST_REG(3, 8)
+    AZG_FIRST_REG(3, 6)
+#undef AZG_FIRST_REG
     if (m == 2)
-        hipLaunchKernelGGL(winograd_first_kernel<2>, grid, dim3(64), lds, st, planes, w1, b1, V, depth, n, c, To);
+        hipLaunchKernelGGL((winograd_first_kernel<2, 0>), grid, dim3(64), lds, st, planes, w1, b1, V, depth, n, c, To);
     else
-        hipLaunchKernelGGL(winograd_first_kernel<3>, grid, dim3(64), lds, st, planes, w1, b1, V, depth, n, c, To);
+        hipLaunchKernelGGL((winograd_first_kernel<3, 0>), grid, dim3(64), lds, st, planes, w1, b1, V, depth, n, c, To);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }

@@ -133,3 +133,20 @@ def test_winograd_fused_transforms_match_unfused():
         pb, vb = b(x)
     torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(va, vb, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,depth,A", [(7, 4, 343), (6, 2, 37), (8, 2, 65), (5, 4, 175), (9, 2, 82)])
+def test_inference_net_board_sizes(n, depth, A):
+    """The inference form (fused front end, fused Winograd transforms; register
+    planes for the supported boards, LDS planes otherwise) vs the reference module."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    torch.manual_seed(n)
+    net = InflexionNNet(n=n, depth=depth, action_size=A).cuda().eval()
+    fast = InferenceNet(net).cuda()
+    x = (torch.rand(160, depth, n, n, device="cuda") < 0.3).float()
+    with torch.no_grad():
+        p, v = fast(x)
+        logp, v_ref = net(x)
+    torch.testing.assert_close(p, torch.exp(logp), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(v.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
