@@ -60,6 +60,49 @@ __device__ __forceinline__ float4 combine(const float (&coef)[L], const float4* 
     return acc;
 }
 
+// One V element: f32, or its fp16 (hi, lo, hi) triple at columns c, C + c, 2C + c
+// of a 3C-wide row.
+template <bool SPLIT>
+__device__ __forceinline__ void store_v(void* V, long long row, int C, int c, float v, int* overflow) {
+    if constexpr (!SPLIT) {
+        ((float*)V)[row * C + c] = v;
+    } else {
+        const _Float16 hi = (_Float16)v;  // round to nearest even
+        const _Float16 lo = (_Float16)(v - (float)hi);
+        _Float16* r = (_Float16*)V + row * 3 * C;
+        r[c] = hi;
+        r[C + c] = lo;
+        r[2 * C + c] = hi;
+        if (!(fabsf(v) <= 65504.f)) atomicOr(overflow, 1);
+    }
+}
+
+// Four consecutive channels (c4 = c / 4) of one V row.
+template <bool SPLIT>
+__device__ __forceinline__ void store_v4(void* V, long long row, int C4, int c4, float4 v, int* overflow) {
+    if constexpr (!SPLIT) {
+        ((float4*)V)[row * C4 + c4] = v;
+    } else {
+        const float x[4] = {v.x, v.y, v.z, v.w};
+        union {
+            _Float16 h[4];
+            uint2 u;
+        } hi, lo;
+        bool bad = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            hi.h[j] = (_Float16)x[j];
+            lo.h[j] = (_Float16)(x[j] - (float)hi.h[j]);
+            bad |= !(fabsf(x[j]) <= 65504.f);
+        }
+        uint2* r = (uint2*)V + row * 3 * C4;
+        r[c4] = hi.u;
+        r[C4 + c4] = lo.u;
+        r[2 * C4 + c4] = hi.u;
+        if (bad) atomicOr(overflow, 1);
+    }
+}
+
 // Work item of a thread: block ids are dealt round-robin to the 8 XCDs, so the
 // block -> work mapping gives each XCD one contiguous eighth of the work:
 // neighbouring tiles, which share input halo pixels, then hit the same L2.
@@ -72,10 +115,11 @@ __device__ __forceinline__ long long xcd_item() {
 // tile index t = (b * tiles + ty) * tiles + tx
 // in_bias != null: x is the previous layer's raw output and relu(x + in_bias)
 // is applied on load (that layer's bias + ReLU fused here; padding stays 0)
-template <int M>
+template <int M, bool SPLIT>
 __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restrict__ x,
-                                                          const float4* __restrict__ in_bias, float4* __restrict__ V,
-                                                          int H, int pad, int C4, int tiles, long long T) {
+                                                          const float4* __restrict__ in_bias, void* __restrict__ V,
+                                                          int H, int pad, int C4, int tiles, long long T,
+                                                          int* overflow) {
     using W = WinoT<M>;
     constexpr int N = W::N;
     const long long i = xcd_item();
@@ -122,14 +166,15 @@ __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restri
     for (int a = 0; a < N; ++a) {
 #pragma unroll
         for (int bb = 0; bb < N; ++bb)
-            V[((long long)(a * N + bb) * T + t) * C4 + c4] = combine<N>(W::BT[bb], s[a]);
+            store_v4<SPLIT>(V, (long long)(a * N + bb) * T + t, C4, c4, combine<N>(W::BT[bb], s[a]), overflow);
     }
 }
 
 template <int M>
 __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restrict__ Min,
                                                            const float4* __restrict__ bias, float4* __restrict__ y,
-                                                           int Ho, int K4, int tiles, long long T, int relu) {
+                                                           int Ho, int K4, int tiles, long long T, int relu,
+                                                           float mscale) {
     using W = WinoT<M>;
     constexpr int N = W::N;
     const long long i = xcd_item();
@@ -142,7 +187,7 @@ __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restr
     const long long b = r / tiles;
     float4 m[N][N];
 #pragma unroll
-    for (int e = 0; e < N * N; ++e) m[e / N][e % N] = Min[((long long)e * T + t) * K4 + k4];
+    for (int e = 0; e < N * N; ++e) m[e / N][e % N] = f4scale(mscale, Min[((long long)e * T + t) * K4 + k4]);
     // s = A^T m (rows), then Y = s A (columns)
     float4 s[M][N];
 #pragma unroll
@@ -268,9 +313,9 @@ struct Plane {
 };
 
 // Next layer's input transform (pad `pad`) of the lane's h x h plane: V tiles out.
-template <int MO, int HC, class P>
+template <int MO, int HC, bool SPLIT, class P>
 __device__ __forceinline__ void plane_to_V(const P& ys, int h, int pad, long long b, int c, int C, long long To,
-                                           float* __restrict__ Vout) {
+                                           void* __restrict__ Vout, int* overflow) {
     constexpr int NO = WinoT<MO>::N;
     const int to = (h + 2 * pad - 2 + MO - 1) / MO;
 #pragma unroll
@@ -291,7 +336,8 @@ __device__ __forceinline__ void plane_to_V(const P& ys, int h, int pad, long lon
 #pragma unroll
             for (int a = 0; a < NO; ++a)
 #pragma unroll
-                for (int bb = 0; bb < NO; ++bb) Vout[((long long)(a * NO + bb) * To + t) * C + c] = V[a][bb];
+                for (int bb = 0; bb < NO; ++bb)
+                    store_v<SPLIT>(Vout, (long long)(a * NO + bb) * To + t, C, c, V[a][bb], overflow);
         }
 }
 
@@ -301,10 +347,10 @@ __device__ __forceinline__ void plane_to_V(const P& ys, int h, int pad, long lon
 // (bias + ReLU applied) is kept in registers (compile-time side HC) or its own
 // LDS column -- only that lane reads it back, so no barrier -- and the next
 // layer's tiles are transformed from it: layer i's activation never goes to HBM.
-template <int MI, int MO, int HC>
+template <int MI, int MO, int HC, bool SPLIT>
 __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restrict__ Min, const float* __restrict__ bias,
-                                                          float* __restrict__ Vout, int h_rt, int C, long long Ti,
-                                                          long long To) {
+                                                          void* __restrict__ Vout, int h_rt, int C, long long Ti,
+                                                          long long To, float mscale, int* overflow) {
     constexpr int NI = WinoT<MI>::N;
     extern __shared__ float ys_raw[];  // [h * h][64] when HC == 0
     const int h = HC > 0 ? HC : h_rt;
@@ -324,7 +370,7 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
             const long long t = (b * ti + ty) * ti + tx;
             float mm[NI][NI];
 #pragma unroll
-            for (int e = 0; e < NI * NI; ++e) mm[e / NI][e % NI] = Min[((long long)e * Ti + t) * C + c];
+            for (int e = 0; e < NI * NI; ++e) mm[e / NI][e % NI] = mscale * Min[((long long)e * Ti + t) * C + c];
             float y[MI][MI];
             out_tile<MI>(mm, y);
 #pragma unroll
@@ -335,7 +381,7 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
                     if (oy < h && ox < h) ys.put(oy * h + ox, fmaxf(y[a][q] + bc, 0.f));
                 }
         }
-    plane_to_V<MO, HC>(ys, h, 0, b, c, C, To, Vout);
+    plane_to_V<MO, HC, SPLIT>(ys, h, 0, b, c, C, To, Vout, overflow);
 }
 
 // The network's first two layers' front end in one pass: conv1 (depth -> C
@@ -345,11 +391,11 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
 // one channel per lane: the image's planes are shared through LDS, the lane's
 // depth*9 weights and its n x n output plane sit in registers (compile-time
 // side NC) or its own LDS column.
-template <int MO, int NC>
+template <int MO, int NC, bool SPLIT>
 __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restrict__ planes,
                                                             const float* __restrict__ w1,
-                                                            const float* __restrict__ b1, float* __restrict__ Vout,
-                                                            int depth, int n_rt, int C, long long To) {
+                                                            const float* __restrict__ b1, void* __restrict__ Vout,
+                                                            int depth, int n_rt, int C, long long To, int* overflow) {
     constexpr int DMAX = 4;
     extern __shared__ float lds[];
     float* xs = lds;  // [depth][n][n], then (NC == 0) the lanes' planes [n * n][64]
@@ -389,7 +435,7 @@ __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restr
             }
             ys.put(y * n + x, fmaxf(acc + bk, 0.f));
         }
-    plane_to_V<MO, NC>(ys, n, 1, b, k, C, To, Vout);
+    plane_to_V<MO, NC, SPLIT>(ys, n, 1, b, k, C, To, Vout, overflow);
 }
 
 // one thread per work item, rounded up to whole groups of 8 blocks (xcd_item)
@@ -397,28 +443,38 @@ unsigned grid_for(long long n) {
     const long long blocks = (n + 255) / 256;
     return (unsigned)(((blocks + 7) / 8) * 8);
 }
+
+bool bad_fmt(int vfmt, const int* overflow) {
+    return !(vfmt == AZG_WINO_F32 || (vfmt == AZG_WINO_SPLIT && overflow));
+}
 }  // namespace
 
-extern "C" int azg_winograd_in_nhwc(const float* x, const float* in_bias, float* V, int32_t batch, int32_t h_in,
-                                    int32_t pad, int32_t c, int32_t m, void* stream) {
+extern "C" int azg_winograd_in_nhwc(const float* x, const float* in_bias, void* V, int32_t batch, int32_t h_in,
+                                    int32_t pad, int32_t c, int32_t m, int32_t vfmt, int32_t* overflow,
+                                    void* stream) {
     const int h_out = h_in + 2 * pad - 2;
     if (!x || !V || batch <= 0 || h_out <= 0 || c <= 0 || c % 4 || (m != 2 && m != 3) || ((uintptr_t)x & 15) ||
-        ((uintptr_t)V & 15) || ((uintptr_t)in_bias & 15) ||
+        ((uintptr_t)V & 15) || ((uintptr_t)in_bias & 15) || bad_fmt(vfmt, overflow) ||
         (long long)batch * ((h_out + m - 1) / m) * ((h_out + m - 1) / m) * (c / 4) > (1ll << 38))
         return AZG_ERR_ARG;
     const int tiles = (h_out + m - 1) / m;
     const long long T = (long long)batch * tiles * tiles;
-    if (m == 2)
-        hipLaunchKernelGGL(winograd_in_kernel<2>, dim3(grid_for(T * (c / 4))), dim3(256), 0, (hipStream_t)stream,
-                           (const float4*)x, (const float4*)in_bias, (float4*)V, h_in, pad, c / 4, tiles, T);
-    else
-        hipLaunchKernelGGL(winograd_in_kernel<3>, dim3(grid_for(T * (c / 4))), dim3(256), 0, (hipStream_t)stream,
-                           (const float4*)x, (const float4*)in_bias, (float4*)V, h_in, pad, c / 4, tiles, T);
+    const dim3 grid(grid_for(T * (c / 4)));
+    hipStream_t st = (hipStream_t)stream;
+#define AZG_IN(MM, SP)                                                                                             \
+    if (m == MM && (vfmt == AZG_WINO_SPLIT) == SP)                                                                 \
+        hipLaunchKernelGGL((winograd_in_kernel<MM, SP>), grid, dim3(256), 0, st, (const float4*)x,                 \
+                           (const float4*)in_bias, V, h_in, pad, c / 4, tiles, T, overflow);
+    AZG_IN(2, false)
+    AZG_IN(3, false)
+    AZG_IN(2, true)
+    AZG_IN(3, true)
+#undef AZG_IN
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
 extern "C" int azg_winograd_out_nhwc(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out,
-                                     int32_t k, int32_t m, int32_t relu, void* stream) {
+                                     int32_t k, int32_t m, int32_t relu, float mscale, void* stream) {
     if (!M || !bias || !y || batch <= 0 || h_out <= 0 || k <= 0 || k % 4 || (m != 2 && m != 3) ||
         ((uintptr_t)M & 15) || ((uintptr_t)bias & 15) || ((uintptr_t)y & 15) ||
         (long long)batch * ((h_out + m - 1) / m) * ((h_out + m - 1) / m) * (k / 4) > (1ll << 38))
@@ -427,69 +483,84 @@ extern "C" int azg_winograd_out_nhwc(const float* M, const float* bias, float* y
     const long long T = (long long)batch * tiles * tiles;
     if (m == 2)
         hipLaunchKernelGGL(winograd_out_kernel<2>, dim3(grid_for(T * (k / 4))), dim3(256), 0, (hipStream_t)stream,
-                           (const float4*)M, (const float4*)bias, (float4*)y, h_out, k / 4, tiles, T, relu);
+                           (const float4*)M, (const float4*)bias, (float4*)y, h_out, k / 4, tiles, T, relu, mscale);
     else
         hipLaunchKernelGGL(winograd_out_kernel<3>, dim3(grid_for(T * (k / 4))), dim3(256), 0, (hipStream_t)stream,
-                           (const float4*)M, (const float4*)bias, (float4*)y, h_out, k / 4, tiles, T, relu);
+                           (const float4*)M, (const float4*)bias, (float4*)y, h_out, k / 4, tiles, T, relu, mscale);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
-extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, float* V, int32_t batch, int32_t h, int32_t c,
-                                     int32_t m_in, int32_t m_out, void* stream) {
+extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, void* V, int32_t batch, int32_t h, int32_t c,
+                                     int32_t m_in, int32_t m_out, float mscale, int32_t vfmt, int32_t* overflow,
+                                     void* stream) {
     if (!M || !bias || !V || batch <= 0 || h < 3 || h > 9 || c <= 0 || c % 64 || (m_in != 2 && m_in != 3) ||
-        (m_out != 2 && m_out != 3))
+        (m_out != 2 && m_out != 3) || bad_fmt(vfmt, overflow))
         return AZG_ERR_ARG;
     const int ti = (h + m_in - 1) / m_in, to = (h - 2 + m_out - 1) / m_out;
     const long long Ti = (long long)batch * ti * ti, To = (long long)batch * to * to;
     const dim3 grid((unsigned)(batch * (c / 64)));
     const size_t lds = (size_t)h * h * 64 * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
+    const bool split = vfmt == AZG_WINO_SPLIT;
     // the board sides of the supported games get register-resident planes
-#define AZG_MID_REG(MI, MO, H)                                                                              \
-    if (m_in == MI && m_out == MO && h == H) {                                                              \
-        hipLaunchKernelGGL((winograd_mid_kernel<MI, MO, H>), grid, dim3(64), 0, st, M, bias, V, h, c, Ti, To); \
-        return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                           \
+#define AZG_MID(MI, MO, H, SP, L)                                                                          \
+    {                                                                                                      \
+        hipLaunchKernelGGL((winograd_mid_kernel<MI, MO, H, SP>), grid, dim3(64), L, st, M, bias, V, h, c, Ti, \
+                           To, mscale, overflow);                                                          \
+        return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                          \
+    }
+#define AZG_MID_REG(MI, MO, H)                                   \
+    if (m_in == MI && m_out == MO && h == H) {                   \
+        if (split) AZG_MID(MI, MO, H, true, 0) else AZG_MID(MI, MO, H, false, 0) \
     }
     AZG_MID_REG(3, 3, 7)
     AZG_MID_REG(3, 3, 5)
     AZG_MID_REG(3, 3, 8)
     AZG_MID_REG(3, 2, 6)
     AZG_MID_REG(2, 2, 4)
+#define AZG_MID_LDS(MI, MO)                                       \
+    if (m_in == MI && m_out == MO) {                              \
+        if (split) AZG_MID(MI, MO, 0, true, lds) else AZG_MID(MI, MO, 0, false, lds) \
+    }
+    AZG_MID_LDS(2, 2)
+    AZG_MID_LDS(2, 3)
+    AZG_MID_LDS(3, 2)
+    AZG_MID_LDS(3, 3)
+#undef AZG_MID_LDS
 #undef AZG_MID_REG
-    if (m_in == 2 && m_out == 2)
-        hipLaunchKernelGGL((winograd_mid_kernel<2, 2, 0>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
-    else if (m_in == 2)
-        hipLaunchKernelGGL((winograd_mid_kernel<2, 3, 0>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
-    else if (m_out == 2)
-        hipLaunchKernelGGL((winograd_mid_kernel<3, 2, 0>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
-    else
-        hipLaunchKernelGGL((winograd_mid_kernel<3, 3, 0>), grid, dim3(64), lds, st, M, bias, V, h, c, Ti, To);
-    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+#undef AZG_MID
+    return AZG_ERR_ARG;
 }
 
-extern "C" int azg_winograd_first_nchw(const float* planes, const float* w1, const float* b1, float* V, int32_t batch,
-                                       int32_t depth, int32_t n, int32_t c, int32_t m, void* stream) {
+extern "C" int azg_winograd_first_nchw(const float* planes, const float* w1, const float* b1, void* V, int32_t batch,
+                                       int32_t depth, int32_t n, int32_t c, int32_t m, int32_t vfmt,
+                                       int32_t* overflow, void* stream) {
     if (!planes || !w1 || !b1 || !V || batch <= 0 || depth < 1 || depth > 4 || n < 3 || n > 9 || c <= 0 ||
-        c % 64 || (m != 2 && m != 3))
+        c % 64 || (m != 2 && m != 3) || bad_fmt(vfmt, overflow))
         return AZG_ERR_ARG;
     const int to = (n + m - 1) / m;
     const long long To = (long long)batch * to * to;
     const dim3 grid((unsigned)(batch * (c / 64)));
     const size_t lds_reg = 4 * 81 * sizeof(float), lds = (4 * 81 + (size_t)n * n * 64) * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
-#define AZG_FIRST_REG(MO, N)                                                                                     \
-    if (m == MO && n == N) {                                                                                     \
-        hipLaunchKernelGGL((winograd_first_kernel<MO, N>), grid, dim3(64), lds_reg, st, planes, w1, b1, V, depth, n, \
-                           c, To);                                                                              \
-        return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                               \
+    const bool split = vfmt == AZG_WINO_SPLIT;
+#define AZG_FIRST(MO, N, SP, L)                                                                                  \
+    {                                                                                                            \
+        hipLaunchKernelGGL((winograd_first_kernel<MO, N, SP>), grid, dim3(64), L, st, planes, w1, b1, V, depth, n, \
+                           c, To, overflow);                                                                     \
+        return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                                \
+    }
+#define AZG_FIRST_REG(MO, N)                                                  \
+    if (m == MO && n == N) {                                                  \
+        if (split) AZG_FIRST(MO, N, true, lds_reg) else AZG_FIRST(MO, N, false, lds_reg) \
     }
     AZG_FIRST_REG(3, 7)
     AZG_FIRST_REG(3, 8)
     AZG_FIRST_REG(3, 6)
 #undef AZG_FIRST_REG
-    if (m == 2)
-        hipLaunchKernelGGL((winograd_first_kernel<2, 0>), grid, dim3(64), lds, st, planes, w1, b1, V, depth, n, c, To);
-    else
-        hipLaunchKernelGGL((winograd_first_kernel<3, 0>), grid, dim3(64), lds, st, planes, w1, b1, V, depth, n, c, To);
-    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+    if (m == 2) {
+        if (split) AZG_FIRST(2, 0, true, lds) else AZG_FIRST(2, 0, false, lds)
+    }
+    if (split) AZG_FIRST(3, 0, true, lds) else AZG_FIRST(3, 0, false, lds)
+#undef AZG_FIRST
 }

@@ -104,6 +104,19 @@ def _winograd_u(w, m=2):
     return u.reshape(n * n, w.shape[1], w.shape[0]).float().contiguous()
 
 
+def _split_u(u):
+    """Operand B of the error-compensated Winograd GEMM: U scaled by 2^k (max |U| 2^k
+    in (512, 1024], so U's low halves stay out of fp16 subnormals), split as
+    hi = fp16(U 2^k), lo = fp16(U 2^k - hi), stacked [hi; hi; lo] along C to meet
+    V's [hi | lo | hi] rows.  Returns ([n^2][3C][K] fp16, 2^-k)."""
+    amax = float(u.abs().max())
+    k = int(np.floor(np.log2(1024.0 / amax))) if amax > 0 else 0
+    us = u.double() * (2.0 ** k)
+    hi = us.half()
+    lo = (us - hi.double()).half()
+    return torch.cat([hi, hi, lo], dim=1).contiguous(), 2.0 ** -k
+
+
 def _fold_bn(weight, bias, bn):
     """Eval-mode BatchNorm folded into the preceding conv/linear (f64 math)."""
     scale = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
@@ -125,18 +138,27 @@ class InferenceNet(nn.Module):
 
     outputs_probs = True
 
-    def __init__(self, net: InflexionNNet, conv="winograd"):
+    def __init__(self, net: InflexionNNet, conv="winograd", gemm="split"):
         """conv (conv2-4): "winograd" (default; Winograd F(2x2,3x3): libazg input /
         output transforms around 16 f32 GEMMs, bias + ReLU in the output transform,
         1.6x fewer multiply-adds), "miopen" (MIOpen implicit GEMM + one fused
         bias/ReLU pass), "azg" (libazg's f32-MFMA implicit GEMM with the bias/ReLU
         in its epilogue) or "auto" (per layer and input shape, whichever measured
         faster on first use).  All within the 1e-5 tolerance of the reference
-        network (tests/test_gpu_nn.py); measured side by side in DESIGN.md 4.1."""
+        network (tests/test_gpu_nn.py); measured side by side in DESIGN.md 4.1.
+
+        gemm (the Winograd GEMMs): "split" (default; each f32 operand split into
+        fp16 hi + lo, hi*hi + lo*hi + hi*lo on the fp16 MFMA with f32 accumulation:
+        f32-accurate products -- measured error at or below the f32 GEMM's -- at 2x
+        its speed) or "f32" (f32 MFMA GEMMs)."""
         super().__init__()
         if conv not in ("miopen", "azg", "auto", "winograd"):
             raise ValueError(f"unknown conv implementation {conv!r}")
+        if gemm not in ("split", "f32"):
+            raise ValueError(f"unknown gemm form {gemm!r}")
         self.conv_impl = conv
+        self.gemm = gemm
+        self.mscale = {}  # Winograd layer -> 2^-k undoing the split operand's scale
         self._choices = {}
         self._ws = None  # Winograd V / M workspace, grown to the largest layer seen
         self.tiles = {}  # Winograd output tile per conv layer
@@ -156,7 +178,10 @@ class InferenceNet(nn.Module):
                 self.register_buffer("w1c", w.contiguous())  # [K][depth][3][3] for the fused front end
             if i > 1 and conv in ("winograd", "auto"):
                 self.tiles[i] = winograd_tile(h_out)
-                self.register_buffer(f"u{i}", _winograd_u(w, self.tiles[i]))
+                u = _winograd_u(w, self.tiles[i])
+                self.register_buffer(f"u{i}", u)
+                u3, self.mscale[i] = _split_u(u)
+                self.register_buffer(f"u3_{i}", u3)
             self.pads.append(conv_i.padding[0])
             h = h_out
         s = net.n - 4
@@ -171,6 +196,23 @@ class InferenceNet(nn.Module):
         self.register_buffer("fb3", net.fc3.bias.detach().clone())
         self.register_buffer("fw4", net.fc4.weight.detach().clone())
         self.register_buffer("fb4", net.fc4.bias.detach().clone())
+        # sticky device flag: a split-GEMM operand fp16 could not hold (checked by check_range)
+        self.register_buffer("overflow", torch.zeros(1, dtype=torch.int32))
+
+    def set_winograd_layer(self, i, w, m):
+        """Replace conv i's Winograd weights by w [K][C][3][3] (BN already folded) with tile m."""
+        self.tiles[i] = m
+        u = _winograd_u(w, m).to(self.w1.device)
+        setattr(self, f"u{i}", u)
+        u3, self.mscale[i] = _split_u(u)
+        setattr(self, f"u3_{i}", u3)
+
+    def check_range(self):
+        """Raise if any split-GEMM operand since the last call was out of fp16 range
+        (|v| > 65504 or NaN): the GEMM would have been wrong, not just inexact."""
+        if self.gemm == "split" and int(self.overflow.item()) != 0:
+            self.overflow.zero_()
+            raise FloatingPointError("Winograd split-GEMM operand out of fp16 range; use InferenceNet(gemm='f32')")
 
     # optional hook: callable(layer_index, "start"|"stop") used by bench.py to
     # bracket each convolution with HIP events on the current stream
@@ -185,21 +227,31 @@ class InferenceNet(nn.Module):
         # bias + ReLU inside the libazg conv's epilogue
         return _azg_conv3x3(x, getattr(self, f"wt{i}"), getattr(self, f"b{i}"), pad)
 
+    def _v_elems(self, n2, T, C):
+        """f32 words of one V: [n^2][T][C] f32, or [n^2][T][3C] fp16 (split)."""
+        return n2 * T * C if self.gemm == "f32" else (3 * n2 * T * C + 1) // 2
+
     def _wino_need(self, i, B, H, pad, C, fuse_next):
-        """Workspace elements layer i needs: V [n^2][T][C], M [n^2][T][K] and, fused, the next layer's V."""
+        """Workspace words layer i needs: (V, or the next layer's V when fused; M [n^2][T][K])."""
         m, K = self.tiles[i], getattr(self, f"u{i}").shape[2]
         Ho = H + 2 * pad - 2
         t = (Ho + m - 1) // m
-        need = (m + 2) ** 2 * B * t * t * max(C, K)
+        need_v = self._v_elems((m + 2) ** 2, B * t * t, C)
         if fuse_next:
             m2 = self.tiles[i + 1]
             t2 = (Ho - 2 + m2 - 1) // m2
-            need = max(need, (m2 + 2) ** 2 * B * t2 * t2 * K)
-        return need
+            need_v = max(need_v, self._v_elems((m2 + 2) ** 2, B * t2 * t2, K))
+        return need_v, (m + 2) ** 2 * B * t * t * K
 
     def _ensure_ws(self, need, dev):
-        if self._ws is None or self._ws[0].numel() < need:
-            self._ws = (torch.empty(need, device=dev), torch.empty(need, device=dev))
+        if self._ws is None or self._ws[0].numel() < need[0] or self._ws[1].numel() < need[1]:
+            self._ws = (torch.empty(need[0], device=dev), torch.empty(need[1], device=dev))
+
+    def _ws_fits(self, need):
+        return self._ws is not None and self._ws[0].numel() >= need[0] and self._ws[1].numel() >= need[1]
+
+    def _vfmt(self):
+        return (0, None) if self.gemm == "f32" else (1, self.overflow.data_ptr())
 
     def _first_winograd(self, s):
         """conv1 + bias + ReLU + conv2's Winograd input transform straight from the NCHW
@@ -210,9 +262,11 @@ class InferenceNet(nn.Module):
         C = self.w1c.shape[0]
         self._ensure_ws(self._wino_need(2, B, self.n, self.pads[1], C, True), s.device)
         st = ctypes.c_void_p(torch.cuda.current_stream(s.device).cuda_stream)
+        fmt, ovf = self._vfmt()
         _lib.check(_lib.lib().azg_winograd_first_nchw(
             ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(self.w1c.data_ptr()), ctypes.c_void_p(self.b1.data_ptr()),
-            ctypes.c_void_p(self._ws[0].data_ptr()), B, self.depth, self.n, C, self.tiles[2], st))
+            ctypes.c_void_p(self._ws[0].data_ptr()), B, self.depth, self.n, C, self.tiles[2], fmt,
+            ctypes.c_void_p(ovf), st))
 
     def _conv_winograd(self, x, i, pad, in_bias=None, carried=False, B=None, H=None, fuse_next=False):
         """Winograd F(m x m,3x3) layer i: libazg input transform (or, with carried=True,
@@ -239,27 +293,39 @@ class InferenceNet(nn.Module):
         T = B * t * t
         if fuse_next:
             m2 = self.tiles[i + 1]
+        need = self._wino_need(i, B, H, pad, C, fuse_next)
         if not carried:
-            self._ensure_ws(self._wino_need(i, B, H, pad, C, fuse_next), dev)
-        elif self._ws is None or self._ws[0].numel() < self._wino_need(i, B, H, pad, C, fuse_next):
+            self._ensure_ws(need, dev)
+        elif not self._ws_fits(need):
             raise RuntimeError("Winograd workspace too small for a carried layer")
-        V = self._ws[0][:nn2 * T * C].view(nn2, T, C)
+        split = self.gemm == "split"
+        if split:
+            V = self._ws[0].view(torch.float16)[:nn2 * T * 3 * C].view(nn2, T, 3 * C)
+            mscale = self.mscale[i]
+        else:
+            V = self._ws[0][:nn2 * T * C].view(nn2, T, C)
+            mscale = 1.0
         M = self._ws[1][:nn2 * T * K].view(nn2, T, K)
         s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         L = _lib.lib()
         bias = ctypes.c_void_p(getattr(self, f"b{i}").data_ptr())
+        fmt, ovf = self._vfmt()
         if not carried:
             ib = ctypes.c_void_p(in_bias.data_ptr()) if in_bias is not None else None
             _lib.check(L.azg_winograd_in_nhwc(ctypes.c_void_p(x.data_ptr()), ib, ctypes.c_void_p(V.data_ptr()),
-                                              B, H, pad, C, m, s))
-        torch.bmm(V, U, out=M)
+                                              B, H, pad, C, m, fmt, ctypes.c_void_p(ovf), s))
+        if split:
+            torch.bmm(V, getattr(self, f"u3_{i}"), out_dtype=torch.float32, out=M)
+        else:
+            torch.bmm(V, U, out=M)
         if fuse_next:
             _lib.check(L.azg_winograd_mid_nhwc(ctypes.c_void_p(M.data_ptr()), bias,
-                                               ctypes.c_void_p(self._ws[0].data_ptr()), B, Ho, K, m, m2, s))
+                                               ctypes.c_void_p(self._ws[0].data_ptr()), B, Ho, K, m, m2,
+                                               mscale, fmt, ctypes.c_void_p(ovf), s))
             return None
         y = torch.empty((B, K, Ho, Ho), device=dev, dtype=torch.float32, memory_format=torch.channels_last)
         _lib.check(L.azg_winograd_out_nhwc(ctypes.c_void_p(M.data_ptr()), bias, ctypes.c_void_p(y.data_ptr()),
-                                           B, Ho, K, m, 1, s))
+                                           B, Ho, K, m, 1, mscale, s))
         return y
 
     def _pick(self, x, i, pad):

@@ -33,10 +33,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 F32_MFMA_PEAK_TF = 157.3         # MI355X_MICROARCH.md: f32 matrix peak (dense)
+F16_MFMA_PEAK_TF = 2500.0        # MI355X_MICROARCH.md: BF16/FP16 MFMA peak (dense)
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E spec peak
 EXPANSIONS_PER_GAME_REF = 8555   # reference random-init Inflexion episodes
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_G4096.json")
-PMC_FILE_WINOGRAD = os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd.json")
+PMC_FILE_WINOGRAD = {"f32": os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd.json"),
+                     "split": os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd_split.json")}
 
 PRESETS = {
     "C1": dict(game="othello", n=6, games=1, sims=25),
@@ -76,12 +78,12 @@ def tree_bytes_per_exp(A, planes_bytes, valid=87.0, d=1.33):
     return d * (12.0 * valid + 8.0) + 80.0 * d + (24.0 + 12.0 * valid) + planes_bytes + (A + 1) * 4.0 + 24.0 * d
 
 
-def load_pmc(G, game, impl):
+def load_pmc(G, game, impl, gemm="split"):
     """HBM-side bytes per launch from the committed PMC passes (tools/pmc_summary.py:
     rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs, FETCH doubled
     per the gfx950 correction).  Only valid for the workload and convolution
     implementation it was measured on."""
-    path = {"miopen": PMC_FILE, "winograd": PMC_FILE_WINOGRAD}.get(impl)
+    path = {"miopen": PMC_FILE, "winograd": PMC_FILE_WINOGRAD[gemm]}.get(impl)
     if G != 4096 or game != "inflexion" or not path or not os.path.exists(path):
         return None
     d = json.load(open(path))
@@ -91,7 +93,7 @@ def load_pmc(G, game, impl):
         return d[k].get("hbm_bytes_per_forward") or d[k]["hbm_bytes_sum_over_shapes"]
     if impl == "winograd":
         conv = tot("winograd_in") + tot("winograd_out") + tot("gemm (hipBLASLt)")
-        what = "winograd_in + the 16-GEMM batches + winograd_out (and the FC GEMMs, ~1%)"
+        what = "Winograd transforms + the GEMM batches (and the FC GEMMs, ~2%)"
     else:
         conv = tot("conv2-4 igemm")
         what = "conv2+3+4 igemm"
@@ -116,6 +118,8 @@ def parse():
     p.add_argument("--conv", default="winograd", choices=["auto", "miopen", "azg", "winograd"],
                    help="conv2-4 implementation of the inference net (MIOpen igemm + bias/ReLU pass, libazg f32-MFMA "
                         "implicit GEMM with fused epilogue, or auto: per layer, the faster one measured at first use)")
+    p.add_argument("--gemm", default="split", choices=["split", "f32"],
+                   help="Winograd GEMMs: split-fp16 (f32-accurate, 3 fp16 MFMA products) or f32 MFMA")
     p.add_argument("--net", default="inference", choices=["inference", "reference"],
                    help="inference: BN-folded NHWC InferenceNet; reference: InflexionNNet as written")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -207,7 +211,8 @@ def main():
     flop_leaf, conv_flop_leaf = net_flops(args.n, depth, A)
     torch.manual_seed(0)
     net = InflexionNNet(n=args.n, depth=depth, action_size=A).cuda().eval()
-    ev = (InferenceNet(net, conv=args.conv) if args.net == "inference" else net) if args.evaluator == "net" else "stub"
+    ev = ((InferenceNet(net, conv=args.conv, gemm=args.gemm) if args.net == "inference" else net)
+          if args.evaluator == "net" else "stub")
     G = args.games
     eng = SelfPlayEngine(G, sims=args.sims, cpuct=1, temp_threshold=30, max_turns=args.max_turns,
                          seed_base=0, first_game=rank * G, evaluator=ev, game=args.game, n=args.n)
@@ -281,6 +286,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st1 = eng.stats()
+    if hasattr(ev, "check_range"):
+        ev.check_range()  # split GEMM operands stayed in fp16 range (raises otherwise)
     exp = st1["expansions"] - st0["expansions"]
     sims_run = st1["sims"] - st0["sims"]
     n_timed = args.steps
@@ -324,11 +331,21 @@ def main():
             for i in (2, 3, 4):
                 impls[i] = (next((v for (li, _), v in ev._choices.items() if li == i), "miopen")
                             if ev.conv_impl == "auto" else ev.conv_impl)
-        names = {"miopen": "MIOpen igemm_fwd_gtcx35_nhwc_fp32 + libazg bias/ReLU pass",
-                 "azg": "libazg f32-MFMA implicit GEMM (LDS-DMA ring) + fused bias/ReLU",
-                 "winograd": "Winograd F(2x2,3x3): libazg transforms + 16 f32 GEMMs (hipBLASLt), bias/ReLU fused"}
-        conv_kernel_desc = ("conv2-4 per forward: " + "; ".join(f"conv{i} {names[m]}" for i, m in impls.items())
+        split = impl == "winograd" and getattr(ev, "gemm", "f32") == "split"
+
+        def name(i, m):
+            if m == "miopen":
+                return "MIOpen igemm_fwd_gtcx35_nhwc_fp32 + libazg bias/ReLU pass"
+            if m == "azg":
+                return "libazg f32-MFMA implicit GEMM (LDS-DMA ring) + fused bias/ReLU"
+            t = ev.tiles[i]
+            g = ("split-fp16 GEMMs (3 fp16 MFMA products, f32 accumulate; hipBLASLt)" if split
+                 else "f32 GEMMs (hipBLASLt)")
+            return f"Winograd F({t}x{t},3x3): libazg fused transforms + {(t + 2) ** 2} {g}"
+        conv_kernel_desc = ("conv2-4 per forward: " + "; ".join(f"conv{i} {name(i, m)}" for i, m in impls.items())
                             if impls else "whole forward (no conv hook)")
+        # split GEMMs execute 3 fp16 products per f32 multiply-add: priced against the fp16 MFMA peak
+        mfma_mult, mfma_peak = (3, F16_MFMA_PEAK_TF) if split else (1, F32_MFMA_PEAK_TF)
         tree_s = (sel_ms + exp_ms) / 1e3
         b_exp = tree_bytes_per_exp(A, depth * args.n * args.n * 4, VALID_ACTIONS.get((args.game, args.n), 87.0))
         tree_gbs = (exp / world) * b_exp / tree_s / 1e9 if tree_s > 0 else 0.0
@@ -345,6 +362,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "dtype_note": ("f32 network; Winograd GEMMs as error-compensated split-fp16 MFMA (hi*hi + lo*hi + hi*lo, "
+                           "f32 accumulation; error at or below the f32 GEMM's, tests/test_gpu_nn.py)") if split else
+                          "f32 network, f32 MFMA GEMMs",
             "data": f"synthetic: fresh self-play games, random-init InflexionNNet-architecture net "
                     f"(torch.manual_seed(0))" if args.evaluator == "net" else "synthetic: hash stub evaluator",
             "config": {"workload": f"{gname} self-play, {G} concurrent games/GPU x {args.sims} sims/move"
@@ -361,8 +381,10 @@ def main():
             "simulations": sims_run,
             "roofline": {"bound": "mfma",
                          "kernel": conv_kernel_desc,
-                         "achieved": conv_tflops, "peak": F32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                         "frac": conv_tflops / F32_MFMA_PEAK_TF, "traffic": None,
+                         "achieved": mfma_mult * conv_tflops, "peak": mfma_peak, "unit": "TFLOP/s",
+                         "frac": mfma_mult * conv_tflops / mfma_peak, "traffic": None,
+                         "mfma_dtype": "fp16 (split, 3 products per f32 multiply-add)" if split else "f32",
+                         "f32_equivalent_tflops": conv_tflops,
                          "direct_conv_equivalent_tflops": direct_tflops,
                          "per_launch": f"{leaves} leaves x {algo_conv_leaf / 1e6:.1f} MFLOP / {conv_avg * 1e3:.3f} ms "
                                        f"(HIP events around conv2+conv3+conv4)",
@@ -379,7 +401,7 @@ def main():
                            "wall_ms": elapsed * 1e3, "graph": bool(args.graph)},
             "iteration_sync_bytes": sync_bytes,
         }
-        pmc = load_pmc(G, args.game, impl)
+        pmc = load_pmc(G, args.game, impl, getattr(ev, "gemm", "f32"))
         if pmc:
             out["roofline"]["traffic"] = pmc["conv"]
             out["roofline"]["traffic_note"] = pmc["note"]

@@ -19,17 +19,19 @@ def test_bias_relu_kernel():
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("conv", ["miopen", "azg", "auto", "winograd"])
-def test_inference_net_vs_reference_gpu(conv):
+@pytest.mark.parametrize("conv,gemm", [("miopen", "split"), ("azg", "split"), ("auto", "split"),
+                                       ("winograd", "split"), ("winograd", "f32")])
+def test_inference_net_vs_reference_gpu(conv, gemm):
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
     d = dict(np.load(ol.os.path.join(ol.GOLDEN, "nnet_golden.npz")))
     torch.manual_seed(0)
     net = InflexionNNet().eval()
     x = torch.from_numpy(d["planes"].astype(np.float32))
-    fast = InferenceNet(net.cuda(), conv=conv).cuda()
+    fast = InferenceNet(net.cuda(), conv=conv, gemm=gemm).cuda()
     with torch.no_grad():
         p, v = fast(x.cuda())
+    fast.check_range()
     np.testing.assert_allclose(p.cpu().numpy(), d["P"], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(v.cpu().numpy().ravel(), d["v"], rtol=1e-5, atol=1e-6)
 
@@ -94,30 +96,31 @@ def test_azg_conv3x3_variants(variant, B, H, pad):
     torch.testing.assert_close(y, want, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("gemm", ["split", "f32"])
 @pytest.mark.parametrize("m", [2, 3])
 @pytest.mark.parametrize("B,H,pad", [(1, 7, 1), (37, 7, 1), (300, 7, 0), (129, 5, 0), (64, 8, 1), (5, 6, 0)])
-def test_winograd_conv3x3_matches_torch(B, H, pad, m):
-    """Winograd F(m x m,3x3) layer (libazg transforms + f32 bmm) vs torch conv2d + bias + ReLU."""
+def test_winograd_conv3x3_matches_torch(B, H, pad, m, gemm):
+    """Winograd F(m x m,3x3) layer (libazg transforms + split-fp16 or f32 bmm) vs torch conv2d + bias + ReLU."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
     torch.manual_seed(3)
     net = InflexionNNet(n=max(H, 5)).eval()
-    fast = InferenceNet(net, conv="winograd").cuda()
+    fast = InferenceNet(net, conv="winograd", gemm=gemm).cuda()
     C = N = 512
     w = torch.randn(N, C, 3, 3) * 0.02
-    from azg_amd.nnet import _winograd_u
     layer = 2
-    fast.tiles[layer] = m
-    setattr(fast, f"u{layer}", _winograd_u(w, m).cuda())
+    fast.set_winograd_layer(layer, w.cuda(), m)
     b = (torch.randn(N) * 0.1).cuda()
     setattr(fast, f"b{layer}", b)
     x = torch.relu(torch.randn(B, C, H, H, device="cuda")).contiguous(memory_format=torch.channels_last)
     want = torch.relu(torch.nn.functional.conv2d(x, w.cuda(), b, padding=pad))
     got = fast._conv_winograd(x, layer, pad)
+    fast.check_range()
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
 
 
-def test_winograd_fused_transforms_match_unfused():
+@pytest.mark.parametrize("gemm", ["split", "f32"])
+def test_winograd_fused_transforms_match_unfused(gemm):
     """The fused front end (conv1 + conv2's input transform) and the fused
     output/next-input transforms (default) vs MIOpen conv1 and separate
     transforms: same math, conv1 summed in another order (1e-5)."""
@@ -125,7 +128,7 @@ def test_winograd_fused_transforms_match_unfused():
     from azg_amd.nnet import InferenceNet, InflexionNNet
     torch.manual_seed(4)
     net = InflexionNNet().cuda().eval()
-    a, b = InferenceNet(net).cuda(), InferenceNet(net).cuda()
+    a, b = InferenceNet(net, gemm=gemm).cuda(), InferenceNet(net, gemm=gemm).cuda()
     b.fuse_transforms = False
     x = (torch.rand(300, 4, 7, 7, device="cuda") < 0.3).float()
     with torch.no_grad():
@@ -135,18 +138,56 @@ def test_winograd_fused_transforms_match_unfused():
     torch.testing.assert_close(va, vb, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("gemm", ["split", "f32"])
 @pytest.mark.parametrize("n,depth,A", [(7, 4, 343), (6, 2, 37), (8, 2, 65), (5, 4, 175), (9, 2, 82)])
-def test_inference_net_board_sizes(n, depth, A):
+def test_inference_net_board_sizes(n, depth, A, gemm):
     """The inference form (fused front end, fused Winograd transforms; register
     planes for the supported boards, LDS planes otherwise) vs the reference module."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
     torch.manual_seed(n)
     net = InflexionNNet(n=n, depth=depth, action_size=A).cuda().eval()
-    fast = InferenceNet(net).cuda()
+    fast = InferenceNet(net, gemm=gemm).cuda()
     x = (torch.rand(160, depth, n, n, device="cuda") < 0.3).float()
     with torch.no_grad():
         p, v = fast(x)
         logp, v_ref = net(x)
+    fast.check_range()
     torch.testing.assert_close(p, torch.exp(logp), rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(v.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
+
+
+def test_split_gemm_flags_fp16_overflow():
+    """A split-GEMM operand fp16 cannot hold is reported, not silently wrong."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    torch.manual_seed(5)
+    net = InflexionNNet().cuda().eval()
+    fast = InferenceNet(net).cuda()
+    x = torch.full((64, 4, 7, 7), 1e6, device="cuda")
+    with torch.no_grad():
+        fast(x)
+    with pytest.raises(FloatingPointError):
+        fast.check_range()
+    fast.check_range()  # the flag was cleared
+
+
+def test_split_gemm_error_not_above_f32():
+    """The split-fp16 forward's error against an f64 forward of the same inference
+    form is no larger than the f32-GEMM forward's (4096 leaves of random planes)."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    torch.manual_seed(6)
+    net = InflexionNNet().cuda().eval()
+    ref = InflexionNNet().cuda().eval().double()
+    ref.load_state_dict(net.state_dict())
+    x = (torch.rand(1024, 4, 7, 7, device="cuda") < 0.3).float()
+    with torch.no_grad():
+        logp, v64 = ref(x.double())
+        p64 = torch.exp(logp)
+        errs = {}
+        for gemm in ("split", "f32"):
+            p, v = InferenceNet(net, gemm=gemm).cuda()(x)
+            errs[gemm] = ((p.double() - p64).abs() / p64).max().item()
+    assert errs["split"] < 1e-5, errs
+    assert errs["split"] <= 1.5 * errs["f32"], errs
