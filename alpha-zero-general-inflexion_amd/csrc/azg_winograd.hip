@@ -1,63 +1,165 @@
-// azg_winograd.hip -- the leaf network's 3x3 convolutions as Winograd F(m x m, 3x3).
+// azg_winograd.hip -- the leaf network's 3x3 convolutions as Winograd convolutions
+// over mixed F(3,3) / F(2,3) tiles.
 //
-// conv2-4 of InflexionNNet.forward (InflexionNNet.py:43-45, BN folded) are
-// y = relu(bias + conv3x3(x, w)).  With m x m output tiles (n = m + 2 input
-// points per side), each tile is
-//     Y = A^T [ U (.) V ] A,   U = G g G^T (per (c, k)),   V = B^T d B (per (tile, c)),
-// and the sum over input channels c of U (.) V is, for each of the n*n tile
-// positions e, one GEMM  M_e[T x K] = V_e[T x C] x U_e[C x K]  (T = tiles).
-// Multiply-adds per output: n^2 / m^2 instead of 9 -- F(2,3): 4, F(3,3): 2.78 --
-// less the tile padding of outputs that are not a multiple of m.  The GEMMs
-// are f32 (hipBLASLt through torch.bmm); these kernels are the two transforms,
-// HBM-bound and coalesced (4 channels per lane as float4, consecutive lanes on
-// consecutive channels):
-//   * winograd_in : NHWC input (zero padding; optionally the previous layer's
-//                   bias + ReLU applied on load) -> V [n*n][T][C]
-//   * winograd_out: M [n*n][T][K] -> NHWC output, bias + ReLU fused, tile
-//                   padding cropped.
-// B and A have small integer entries (F(2,3): 0, +-1; F(3,3): up to 4), so the
-// transforms are adds and exact scalings except F(3,3)'s x3; U is formed in f64
-// by the caller (G has entries 1/2, 1/3, 1/6).  F(3,3)'s larger constants make
-// its f32 error ~3x F(2,3)'s.
+// conv2-4 of InflexionNNet.forward (InflexionNNet.py:39-45, BN folded) are
+// y = relu(bias + conv3x3(x, w)).  Winograd F(m,3) along one axis turns m outputs
+// into n = m + 2 transformed points; the 2-D transform is separable, so a tile may
+// use F(ma,3) down its rows and F(mb,3) across its columns:
+//     Y = A_ma^T [ U (.) V ] A_mb,  U = G_ma g G_mb^T (per (c, k)),  V = B_ma^T d B_mb.
+// An h-long output axis is cut into p = ceil(h/3) tiles, as many of side 3 as fit
+// and the rest of side 2 (h = 7: 3+2+2; 5: 3+2; 3: 3; 8: 3+3+2; 6: 3+3; 4: 2+2), the
+// fewest transformed points that cover it exactly: 13^2 instead of uniform F(3,3)'s
+// 15^2 for a 7x7 output, 9^2 instead of 10^2 for 5x5.
+//
+// Summed over input channels c, each transformed point e of a tile type
+// g = (ma, mb) is one GEMM  M_e[T_g x K] = V_e[T_g x C] x U_e[C x K].  Layout of V
+// (and M, with K for C): the groups (3,3), (3,2), (2,3), (2,2) one after another
+// (absent types skipped), group g as [P_g][batch * n_g][row] with P_g = (ma+2)(mb+2)
+// points and n_g tiles of that type per image, tiles row-major within the image.
+// The GEMMs (hipBLASLt through torch.bmm) are the caller's; these kernels are the
+// transforms, HBM-bound, consecutive lanes on consecutive channels:
+//   * winograd_in   : NHWC input (zero padding; optionally the previous layer's
+//                     bias + ReLU applied on load) -> V
+//   * winograd_out  : M -> NHWC output, bias + ReLU fused, tiles cropped
+//   * winograd_mid  : layer i's output transform + layer i+1's input transform in
+//                     one pass (the activation stays on chip)
+//   * winograd_first: conv1 + bias + ReLU from the NCHW planes + conv2's input
+//                     transform in one pass
+// B and A have small integer entries (F(2,3): 0, +-1; F(3,3): up to 4); U is formed
+// in f64 by the caller (G has entries 1/2, 1/3, 1/6).
+//
+// V is written in one of two formats (vfmt):
+//   AZG_WINO_F32  : f32 rows of C;
+//   AZG_WINO_SPLIT: fp16 rows of 3C = [hi | lo | hi], hi = fp16(v), lo = fp16(v - hi),
+//                   for the error-compensated GEMM M = [hi|lo|hi] x [Uh; Uh; Ul] =
+//                   hi Uh + lo Uh + hi Ul on the fp16 MFMA with f32 accumulation.
+//                   hi + lo holds v to 2^-22 relative (2^-25 absolute below
+//                   |v| = 2^-3), the dropped lo Ul term is ~2^-22, so the products
+//                   are f32-accurate; U is pre-scaled by a power of
+//                   two that mscale undoes exactly in the output transforms.
+//                   |v| > 65504 or NaN sets *overflow.
 #include <hip/hip_runtime.h>
 
 #include "../../include/azg.h"
 
 namespace {
 
-__device__ __forceinline__ float4 f4add(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
-__device__ __forceinline__ float4 f4scale(float c, float4 a) { return make_float4(c * a.x, c * a.y, c * a.z, c * a.w); }
+template <int V>
+struct IC {
+    static constexpr int value = V;
+};
+
+// tile sequence of an h-long output axis: p tiles, the first n3 of side 3, the rest 2
+struct WSeq {
+    int h, p, n3;
+    __host__ __device__ constexpr explicit WSeq(int h_)
+        : h(h_), p((h_ + 2) / 3), n3(h_ - 2 * ((h_ + 2) / 3) > 0 ? h_ - 2 * ((h_ + 2) / 3) : 0) {}
+    __host__ __device__ constexpr int m(int i) const { return i < n3 ? 3 : 2; }
+    __host__ __device__ constexpr int off(int i) const { return i < n3 ? 3 * i : 3 * n3 + 2 * (i - n3); }
+    __host__ __device__ constexpr int cnt(int mm) const { return mm == 3 ? n3 : p - n3; }
+    __host__ __device__ constexpr int idx(int i) const { return i < n3 ? i : i - n3; }  // index among its type
+    // rows of V (or M) before group (ma, mb); group order (3,3) (3,2) (2,3) (2,2)
+    __host__ __device__ constexpr long long base(int ma, int mb, long long B) const {
+        const int g = (ma == 3 ? 0 : 2) + (mb == 3 ? 0 : 1);
+        long long r = 0;
+        for (int q = 0; q < g; ++q) {
+            const int qa = q < 2 ? 3 : 2, qb = (q & 1) ? 2 : 3;
+            r += (long long)(qa + 2) * (qb + 2) * B * cnt(qa) * cnt(qb);
+        }
+        return r;
+    }
+    // row of point 0 of tile (i, j) of image b, and the row stride between points
+    __host__ __device__ constexpr long long row0(int i, int j, long long b, long long B) const {
+        const int ma = m(i), mb = m(j), ng = cnt(ma) * cnt(mb);
+        return base(ma, mb, B) + b * ng + (long long)idx(i) * cnt(mb) + idx(j);
+    }
+    __host__ __device__ constexpr long long pstride(int i, int j, long long B) const {
+        return B * cnt(m(i)) * cnt(m(j));
+    }
+};
+
+// run f(IC<ma>, IC<mb>): the tile bodies are compiled per type; with constant
+// ma, mb (unrolled compile-time sequences) the branches fold away
+template <class F>
+__device__ __forceinline__ void with_types(int ma, int mb, F&& f) {
+    if (ma == 3) {
+        if (mb == 3) f(IC<3>{}, IC<3>{});
+        else f(IC<3>{}, IC<2>{});
+    } else {
+        if (mb == 3) f(IC<2>{}, IC<3>{});
+        else f(IC<2>{}, IC<2>{});
+    }
+}
 
 // transform tables: B^T [n][n] (input), A^T [m][n] (output)
 template <int M>
 struct WinoT;
 template <>
 struct WinoT<2> {
-    static constexpr int N = 4;
     static constexpr float BT[4][4] = {{1, 0, -1, 0}, {0, 1, 1, 0}, {0, -1, 1, 0}, {0, 1, 0, -1}};
     static constexpr float AT[2][4] = {{1, 1, 1, 0}, {0, 1, -1, -1}};
 };
 template <>
 struct WinoT<3> {
-    static constexpr int N = 5;  // interpolation points 0, 1, -1, 2, inf
+    // F(3,3): interpolation points 0, 1, -1, 2, inf
     static constexpr float BT[5][5] = {
         {2, -1, -2, 1, 0}, {0, -2, -1, 1, 0}, {0, 2, -3, 1, 0}, {0, -1, 0, 1, 0}, {0, 2, -1, -2, 1}};
     static constexpr float AT[3][5] = {{1, 1, 1, 1, 0}, {0, 1, -1, 2, 0}, {0, 1, 1, 4, 1}};
 };
 
-// sum_j coef[j] * x[j], skipping zero coefficients at compile time (x1 folds)
-template <int L>
-__device__ __forceinline__ float4 combine(const float (&coef)[L], const float4* x) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+__device__ __forceinline__ float vadd(float a, float b) { return a + b; }
+__device__ __forceinline__ float vmul(float c, float a) { return c * a; }
+__device__ __forceinline__ float4 vadd(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 vmul(float c, float4 a) { return make_float4(c * a.x, c * a.y, c * a.z, c * a.w); }
+__device__ __forceinline__ float4 vrelu(float4 a) {
+    return make_float4(fmaxf(a.x, 0.f), fmaxf(a.y, 0.f), fmaxf(a.z, 0.f), fmaxf(a.w, 0.f));
+}
+
+// sum_j coef[j] * x(j), skipping zero coefficients at compile time (x1 folds)
+template <int L, class T, class X>
+__device__ __forceinline__ T combine(const float (&coef)[L], X&& x) {
+    T acc{};
     bool first = true;
 #pragma unroll
     for (int j = 0; j < L; ++j) {
         if (coef[j] == 0.f) continue;
-        const float4 term = coef[j] == 1.f ? x[j] : f4scale(coef[j], x[j]);
-        acc = first ? term : f4add(acc, term);
+        const T term = coef[j] == 1.f ? x(j) : vmul(coef[j], x(j));
+        acc = first ? term : vadd(acc, term);
         first = false;
     }
     return acc;
+}
+
+// V = B_ma^T d B_mb  (d, V: (ma+2) x (mb+2))
+template <int MA, int MB, class T>
+__device__ __forceinline__ void in_tile(const T (&d)[MA + 2][MB + 2], T (&V)[MA + 2][MB + 2]) {
+    constexpr int NA = MA + 2, NB = MB + 2;
+    T s[NA][NB];
+#pragma unroll
+    for (int v = 0; v < NB; ++v)
+#pragma unroll
+        for (int a = 0; a < NA; ++a) s[a][v] = combine<NA, T>(WinoT<MA>::BT[a], [&](int u) { return d[u][v]; });
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) V[a][bb] = combine<NB, T>(WinoT<MB>::BT[bb], [&](int v) { return s[a][v]; });
+}
+
+// Y = A_ma^T M A_mb  (M: (ma+2) x (mb+2), Y: ma x mb)
+template <int MA, int MB, class T>
+__device__ __forceinline__ void out_tile(const T (&mm)[MA + 2][MB + 2], T (&y)[MA][MB]) {
+    constexpr int NA = MA + 2, NB = MB + 2;
+    T s[MA][NB];
+#pragma unroll
+    for (int v = 0; v < NB; ++v)
+#pragma unroll
+        for (int a = 0; a < MA; ++a) s[a][v] = combine<NA, T>(WinoT<MA>::AT[a], [&](int u) { return mm[u][v]; });
+#pragma unroll
+    for (int a = 0; a < MA; ++a)
+#pragma unroll
+        for (int q = 0; q < MB; ++q) y[a][q] = combine<NB, T>(WinoT<MB>::AT[q], [&](int v) { return s[a][v]; });
 }
 
 // One V element: f32, or its fp16 (hi, lo, hi) triple at columns c, C + c, 2C + c
@@ -79,7 +181,7 @@ __device__ __forceinline__ void store_v(void* V, long long row, int C, int c, fl
 
 // Four consecutive channels (c4 = c / 4) of one V row.
 template <bool SPLIT>
-__device__ __forceinline__ void store_v4(void* V, long long row, int C4, int c4, float4 v, int* overflow) {
+__device__ __forceinline__ void store_v(void* V, long long row, int C4, int c4, float4 v, int* overflow) {
     if constexpr (!SPLIT) {
         ((float4*)V)[row * C4 + c4] = v;
     } else {
@@ -112,187 +214,81 @@ __device__ __forceinline__ long long xcd_item() {
     return (long long)vb * blockDim.x + threadIdx.x;
 }
 
-// tile index t = (b * tiles + ty) * tiles + tx
-// in_bias != null: x is the previous layer's raw output and relu(x + in_bias)
-// is applied on load (that layer's bias + ReLU fused here; padding stays 0)
-template <int M, bool SPLIT>
+// One thread per (tile, 4 channels); tiles image-major, row-major in the image.
+// in_bias != null: x is the previous layer's raw output and relu(x + in_bias) is
+// applied on load (that layer's bias + ReLU fused here; padding stays 0).
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restrict__ x,
                                                           const float4* __restrict__ in_bias, void* __restrict__ V,
-                                                          int H, int pad, int C4, int tiles, long long T,
-                                                          int* overflow) {
-    using W = WinoT<M>;
-    constexpr int N = W::N;
-    const long long i = xcd_item();
-    if (i >= T * C4) return;
-    const int c4 = (int)(i % C4);
-    const long long t = i / C4;
-    const int tx = (int)(t % tiles);
-    const long long r = t / tiles;
-    const int ty = (int)(r % tiles);
-    const long long b = r / tiles;
+                                                          int H, int pad, int C4, long long B, int* overflow) {
+    const WSeq S(H + 2 * pad - 2);
+    const long long item = xcd_item();
+    if (item >= B * S.p * S.p * C4) return;
+    const int c4 = (int)(item % C4);
+    const long long t = item / C4;
+    const int j = (int)(t % S.p);
+    const long long r = t / S.p;
+    const int i = (int)(r % S.p);
+    const long long b = r / S.p;
     const float4 ib = in_bias ? in_bias[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 d[N][N];
+    const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
+    const int y0 = S.off(i) - pad, x0 = S.off(j) - pad;
+    with_types(S.m(i), S.m(j), [&](auto A_, auto B_) {
+        constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+        float4 d[MA + 2][MB + 2];
 #pragma unroll
-    for (int u = 0; u < N; ++u) {
-        const int iy = M * ty - pad + u;
+        for (int u = 0; u < MA + 2; ++u)
 #pragma unroll
-        for (int v = 0; v < N; ++v) {
-            const int ix = M * tx - pad + v;
-            float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (iy >= 0 && iy < H && ix >= 0 && ix < H) {
-                z = x[((b * H + iy) * H + ix) * C4 + c4];
-                if (in_bias) {
-                    z = f4add(z, ib);
-                    z.x = fmaxf(z.x, 0.f);
-                    z.y = fmaxf(z.y, 0.f);
-                    z.z = fmaxf(z.z, 0.f);
-                    z.w = fmaxf(z.w, 0.f);
+            for (int v = 0; v < MB + 2; ++v) {
+                const int iy = y0 + u, ix = x0 + v;
+                float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (iy >= 0 && iy < H && ix >= 0 && ix < H) {
+                    z = x[((b * H + iy) * H + ix) * C4 + c4];
+                    if (in_bias) z = vrelu(vadd(z, ib));
                 }
+                d[u][v] = z;
             }
-            d[u][v] = z;
-        }
-    }
-    // s = B^T d (rows), then V = s B (columns)
-    float4 s[N][N];
+        float4 Vt[MA + 2][MB + 2];
+        in_tile<MA, MB>(d, Vt);
 #pragma unroll
-    for (int v = 0; v < N; ++v) {
-        float4 col[N];
-#pragma unroll
-        for (int u = 0; u < N; ++u) col[u] = d[u][v];
-#pragma unroll
-        for (int a = 0; a < N; ++a) s[a][v] = combine<N>(W::BT[a], col);
-    }
-#pragma unroll
-    for (int a = 0; a < N; ++a) {
-#pragma unroll
-        for (int bb = 0; bb < N; ++bb)
-            store_v4<SPLIT>(V, (long long)(a * N + bb) * T + t, C4, c4, combine<N>(W::BT[bb], s[a]), overflow);
-    }
+        for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
+            store_v<SPLIT>(V, row + e * ps, C4, c4, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
+    });
 }
 
-template <int M>
 __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restrict__ Min,
                                                            const float4* __restrict__ bias, float4* __restrict__ y,
-                                                           int Ho, int K4, int tiles, long long T, int relu,
-                                                           float mscale) {
-    using W = WinoT<M>;
-    constexpr int N = W::N;
-    const long long i = xcd_item();
-    if (i >= T * K4) return;
-    const int k4 = (int)(i % K4);
-    const long long t = i / K4;
-    const int tx = (int)(t % tiles);
-    const long long r = t / tiles;
-    const int ty = (int)(r % tiles);
-    const long long b = r / tiles;
-    float4 m[N][N];
-#pragma unroll
-    for (int e = 0; e < N * N; ++e) m[e / N][e % N] = f4scale(mscale, Min[((long long)e * T + t) * K4 + k4]);
-    // s = A^T m (rows), then Y = s A (columns)
-    float4 s[M][N];
-#pragma unroll
-    for (int v = 0; v < N; ++v) {
-        float4 col[N];
-#pragma unroll
-        for (int u = 0; u < N; ++u) col[u] = m[u][v];
-#pragma unroll
-        for (int a = 0; a < M; ++a) s[a][v] = combine<N>(W::AT[a], col);
-    }
+                                                           int Ho, int K4, long long B, int relu, float mscale) {
+    const WSeq S(Ho);
+    const long long item = xcd_item();
+    if (item >= B * S.p * S.p * K4) return;
+    const int k4 = (int)(item % K4);
+    const long long t = item / K4;
+    const int j = (int)(t % S.p);
+    const long long r = t / S.p;
+    const int i = (int)(r % S.p);
+    const long long b = r / S.p;
+    const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
     const float4 bb = bias[k4];
+    with_types(S.m(i), S.m(j), [&](auto A_, auto B_) {
+        constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+        float4 m[MA + 2][MB + 2];
 #pragma unroll
-    for (int a = 0; a < M; ++a) {
-        const int oy = M * ty + a;
+        for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
+            m[e / (MB + 2)][e % (MB + 2)] = vmul(mscale, Min[(row + e * ps) * K4 + k4]);
+        float4 yt[MA][MB];
+        out_tile<MA, MB>(m, yt);
 #pragma unroll
-        for (int c = 0; c < M; ++c) {
-            const int ox = M * tx + c;
-            if (oy < Ho && ox < Ho) {
-                float4 z = f4add(combine<N>(W::AT[c], s[a]), bb);
-                if (relu) {
-                    z.x = fmaxf(z.x, 0.f);
-                    z.y = fmaxf(z.y, 0.f);
-                    z.z = fmaxf(z.z, 0.f);
-                    z.w = fmaxf(z.w, 0.f);
-                }
+        for (int a = 0; a < MA; ++a)
+#pragma unroll
+            for (int q = 0; q < MB; ++q) {
+                const int oy = S.off(i) + a, ox = S.off(j) + q;
+                if (oy >= Ho || ox >= Ho) continue;  // h = 1: one 2-tile, cropped
+                float4 z = vadd(yt[a][q], bb);
+                if (relu) z = vrelu(z);
                 y[((b * Ho + oy) * Ho + ox) * K4 + k4] = z;
             }
-        }
-    }
-}
-
-// scalar (one channel) tile transforms: y = A^T m A (m x m) and V = B^T d B (n x n)
-template <int MI>
-__device__ __forceinline__ void out_tile(const float (&mm)[WinoT<MI>::N][WinoT<MI>::N], float (&y)[MI][MI]) {
-    using W = WinoT<MI>;
-    constexpr int N = W::N;
-    float sr[MI][N];
-#pragma unroll
-    for (int v = 0; v < N; ++v)
-#pragma unroll
-        for (int a = 0; a < MI; ++a) {
-            float acc = 0.f;
-            bool first = true;
-#pragma unroll
-            for (int u = 0; u < N; ++u) {
-                if (W::AT[a][u] == 0.f) continue;
-                const float term = W::AT[a][u] == 1.f ? mm[u][v] : W::AT[a][u] * mm[u][v];
-                acc = first ? term : acc + term;
-                first = false;
-            }
-            sr[a][v] = acc;
-        }
-#pragma unroll
-    for (int a = 0; a < MI; ++a)
-#pragma unroll
-        for (int q = 0; q < MI; ++q) {
-            float acc = 0.f;
-            bool first = true;
-#pragma unroll
-            for (int v = 0; v < N; ++v) {
-                if (W::AT[q][v] == 0.f) continue;
-                const float term = W::AT[q][v] == 1.f ? sr[a][v] : W::AT[q][v] * sr[a][v];
-                acc = first ? term : acc + term;
-                first = false;
-            }
-            y[a][q] = acc;
-        }
-}
-
-template <int MO>
-__device__ __forceinline__ void in_tile(const float (&d)[WinoT<MO>::N][WinoT<MO>::N],
-                                        float (&V)[WinoT<MO>::N][WinoT<MO>::N]) {
-    using W = WinoT<MO>;
-    constexpr int N = W::N;
-    float sr[N][N];
-#pragma unroll
-    for (int v = 0; v < N; ++v)
-#pragma unroll
-        for (int a = 0; a < N; ++a) {
-            float acc = 0.f;
-            bool first = true;
-#pragma unroll
-            for (int u = 0; u < N; ++u) {
-                if (W::BT[a][u] == 0.f) continue;
-                const float term = W::BT[a][u] == 1.f ? d[u][v] : W::BT[a][u] * d[u][v];
-                acc = first ? term : acc + term;
-                first = false;
-            }
-            sr[a][v] = acc;
-        }
-#pragma unroll
-    for (int a = 0; a < N; ++a)
-#pragma unroll
-        for (int bb = 0; bb < N; ++bb) {
-            float acc = 0.f;
-            bool first = true;
-#pragma unroll
-            for (int v = 0; v < N; ++v) {
-                if (W::BT[bb][v] == 0.f) continue;
-                const float term = W::BT[bb][v] == 1.f ? sr[a][v] : W::BT[bb][v] * sr[a][v];
-                acc = first ? term : acc + term;
-                first = false;
-            }
-            V[a][bb] = acc;
-        }
+    });
 }
 
 // A lane's private h x h plane: in registers when the side is a compile-time
@@ -312,33 +308,40 @@ struct Plane {
     }
 };
 
-// Next layer's input transform (pad `pad`) of the lane's h x h plane: V tiles out.
-template <int MO, int HC, bool SPLIT, class P>
-__device__ __forceinline__ void plane_to_V(const P& ys, int h, int pad, long long b, int c, int C, long long To,
+// The next layer's input transform (pad `pad`) of the lane's h x h plane: V out.
+// Loop bounds are compile-time for HC > 0 (p <= (HC + 4) / 3), 3 otherwise (h <= 9).
+template <int HC, bool SPLIT, class P>
+__device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, int pad, long long b, int c, int C, long long B,
                                            void* __restrict__ Vout, int* overflow) {
-    constexpr int NO = WinoT<MO>::N;
-    const int to = (h + 2 * pad - 2 + MO - 1) / MO;
+    constexpr int PMAX = HC > 0 ? (HC + 4) / 3 : 3;
+    const int h = HC > 0 ? HC : h_rt;
+    const WSeq S(h + 2 * pad - 2);
 #pragma unroll
-    for (int ty = 0; ty < to; ++ty)
+    for (int i = 0; i < PMAX; ++i) {
+        if (i >= S.p) break;
 #pragma unroll
-        for (int tx = 0; tx < to; ++tx) {
-            const long long t = (b * to + ty) * to + tx;
-            float d[NO][NO];
+        for (int j = 0; j < PMAX; ++j) {
+            if (j >= S.p) break;
+            const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
+            const int y0 = S.off(i) - pad, x0 = S.off(j) - pad;
+            with_types(S.m(i), S.m(j), [&](auto A_, auto B_) {
+                constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+                float d[MA + 2][MB + 2];
 #pragma unroll
-            for (int u = 0; u < NO; ++u)
+                for (int u = 0; u < MA + 2; ++u)
 #pragma unroll
-                for (int v = 0; v < NO; ++v) {
-                    const int iy = MO * ty - pad + u, ix = MO * tx - pad + v;
-                    d[u][v] = (iy >= 0 && iy < h && ix >= 0 && ix < h) ? ys.get(iy * h + ix) : 0.f;
-                }
-            float V[NO][NO];
-            in_tile<MO>(d, V);
+                    for (int v = 0; v < MB + 2; ++v) {
+                        const int iy = y0 + u, ix = x0 + v;
+                        d[u][v] = (iy >= 0 && iy < h && ix >= 0 && ix < h) ? ys.get(iy * h + ix) : 0.f;
+                    }
+                float Vt[MA + 2][MB + 2];
+                in_tile<MA, MB>(d, Vt);
 #pragma unroll
-            for (int a = 0; a < NO; ++a)
-#pragma unroll
-                for (int bb = 0; bb < NO; ++bb)
-                    store_v<SPLIT>(Vout, (long long)(a * NO + bb) * To + t, C, c, V[a][bb], overflow);
+                for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
+                    store_v<SPLIT>(Vout, row + e * ps, C, c, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
+            });
         }
+    }
 }
 
 // Layer i's output transform fused with layer i+1's input transform (pad 0
@@ -347,41 +350,47 @@ __device__ __forceinline__ void plane_to_V(const P& ys, int h, int pad, long lon
 // (bias + ReLU applied) is kept in registers (compile-time side HC) or its own
 // LDS column -- only that lane reads it back, so no barrier -- and the next
 // layer's tiles are transformed from it: layer i's activation never goes to HBM.
-template <int MI, int MO, int HC, bool SPLIT>
+template <int HC, bool SPLIT>
 __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restrict__ Min, const float* __restrict__ bias,
-                                                          void* __restrict__ Vout, int h_rt, int C, long long Ti,
-                                                          long long To, float mscale, int* overflow) {
-    constexpr int NI = WinoT<MI>::N;
+                                                          void* __restrict__ Vout, int h_rt, int C, long long B,
+                                                          float mscale, int* overflow) {
+    constexpr int PMAX = HC > 0 ? (HC + 2) / 3 : 3;
     extern __shared__ float ys_raw[];  // [h * h][64] when HC == 0
     const int h = HC > 0 ? HC : h_rt;
     const int lane = threadIdx.x;
     const int cblocks = C / 64;
     const long long b = blockIdx.x / cblocks;
     const int c = (blockIdx.x % cblocks) * 64 + lane;
-    const int ti = (h + MI - 1) / MI;
     const float bc = bias[c];
+    const WSeq S(h);
     Plane<HC> ys;
     ys.lds = ys_raw;
     ys.lane = lane;
 #pragma unroll
-    for (int ty = 0; ty < ti; ++ty)
+    for (int i = 0; i < PMAX; ++i) {
+        if (i >= S.p) break;
 #pragma unroll
-        for (int tx = 0; tx < ti; ++tx) {
-            const long long t = (b * ti + ty) * ti + tx;
-            float mm[NI][NI];
+        for (int j = 0; j < PMAX; ++j) {
+            if (j >= S.p) break;
+            const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
+            const int y0 = S.off(i), x0 = S.off(j);
+            with_types(S.m(i), S.m(j), [&](auto A_, auto B_) {
+                constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+                float mm[MA + 2][MB + 2];
 #pragma unroll
-            for (int e = 0; e < NI * NI; ++e) mm[e / NI][e % NI] = mscale * Min[((long long)e * Ti + t) * C + c];
-            float y[MI][MI];
-            out_tile<MI>(mm, y);
+                for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
+                    mm[e / (MB + 2)][e % (MB + 2)] = mscale * Min[(row + e * ps) * C + c];
+                float y[MA][MB];
+                out_tile<MA, MB>(mm, y);
 #pragma unroll
-            for (int a = 0; a < MI; ++a)
+                for (int a = 0; a < MA; ++a)
 #pragma unroll
-                for (int q = 0; q < MI; ++q) {
-                    const int oy = MI * ty + a, ox = MI * tx + q;
-                    if (oy < h && ox < h) ys.put(oy * h + ox, fmaxf(y[a][q] + bc, 0.f));
-                }
+                    for (int q = 0; q < MB; ++q)
+                        if (y0 + a < h && x0 + q < h) ys.put((y0 + a) * h + x0 + q, fmaxf(y[a][q] + bc, 0.f));
+            });
         }
-    plane_to_V<MO, HC, SPLIT>(ys, h, 0, b, c, C, To, Vout, overflow);
+    }
+    plane_to_V<HC, SPLIT>(ys, h, 0, b, c, C, B, Vout, overflow);
 }
 
 // The network's first two layers' front end in one pass: conv1 (depth -> C
@@ -391,11 +400,11 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
 // one channel per lane: the image's planes are shared through LDS, the lane's
 // depth*9 weights and its n x n output plane sit in registers (compile-time
 // side NC) or its own LDS column.
-template <int MO, int NC, bool SPLIT>
+template <int NC, bool SPLIT>
 __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restrict__ planes,
                                                             const float* __restrict__ w1,
                                                             const float* __restrict__ b1, void* __restrict__ Vout,
-                                                            int depth, int n_rt, int C, long long To, int* overflow) {
+                                                            int depth, int n_rt, int C, long long B, int* overflow) {
     constexpr int DMAX = 4;
     extern __shared__ float lds[];
     float* xs = lds;  // [depth][n][n], then (NC == 0) the lanes' planes [n * n][64]
@@ -435,7 +444,7 @@ __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restr
             }
             ys.put(y * n + x, fmaxf(acc + bk, 0.f));
         }
-    plane_to_V<MO, NC, SPLIT>(ys, n, 1, b, k, C, To, Vout, overflow);
+    plane_to_V<NC, SPLIT>(ys, n, 1, b, k, C, B, Vout, overflow);
 }
 
 // one thread per work item, rounded up to whole groups of 8 blocks (xcd_item)
@@ -444,123 +453,105 @@ unsigned grid_for(long long n) {
     return (unsigned)(((blocks + 7) / 8) * 8);
 }
 
-bool bad_fmt(int vfmt, const int* overflow) {
-    return !(vfmt == AZG_WINO_F32 || (vfmt == AZG_WINO_SPLIT && overflow));
-}
+bool bad_fmt(int vfmt, const int* overflow) { return !(vfmt == AZG_WINO_F32 || (vfmt == AZG_WINO_SPLIT && overflow)); }
 }  // namespace
 
+extern "C" int azg_winograd_layout(int32_t h_out, int32_t* seq, int32_t* groups) {
+    if (h_out < 1 || h_out > 64) return AZG_ERR_ARG;
+    const WSeq S(h_out);
+    if (seq)
+        for (int i = 0; i < S.p; ++i) seq[i] = S.m(i);
+    if (groups)  // tiles per image of each group (3,3) (3,2) (2,3) (2,2)
+        for (int g = 0; g < 4; ++g) groups[g] = S.cnt(g < 2 ? 3 : 2) * S.cnt((g & 1) ? 2 : 3);
+    return S.p;
+}
+
 extern "C" int azg_winograd_in_nhwc(const float* x, const float* in_bias, void* V, int32_t batch, int32_t h_in,
-                                    int32_t pad, int32_t c, int32_t m, int32_t vfmt, int32_t* overflow,
-                                    void* stream) {
+                                    int32_t pad, int32_t c, int32_t vfmt, int32_t* overflow, void* stream) {
     const int h_out = h_in + 2 * pad - 2;
-    if (!x || !V || batch <= 0 || h_out <= 0 || c <= 0 || c % 4 || (m != 2 && m != 3) || ((uintptr_t)x & 15) ||
+    if (!x || !V || batch <= 0 || h_out <= 0 || h_out > 64 || c <= 0 || c % 4 || ((uintptr_t)x & 15) ||
         ((uintptr_t)V & 15) || ((uintptr_t)in_bias & 15) || bad_fmt(vfmt, overflow) ||
-        (long long)batch * ((h_out + m - 1) / m) * ((h_out + m - 1) / m) * (c / 4) > (1ll << 38))
+        (long long)batch * h_out * h_out * (c / 4) > (1ll << 38))
         return AZG_ERR_ARG;
-    const int tiles = (h_out + m - 1) / m;
-    const long long T = (long long)batch * tiles * tiles;
-    const dim3 grid(grid_for(T * (c / 4)));
+    const WSeq S(h_out);
+    const dim3 grid(grid_for((long long)batch * S.p * S.p * (c / 4)));
     hipStream_t st = (hipStream_t)stream;
-#define AZG_IN(MM, SP)                                                                                             \
-    if (m == MM && (vfmt == AZG_WINO_SPLIT) == SP)                                                                 \
-        hipLaunchKernelGGL((winograd_in_kernel<MM, SP>), grid, dim3(256), 0, st, (const float4*)x,                 \
-                           (const float4*)in_bias, V, h_in, pad, c / 4, tiles, T, overflow);
-    AZG_IN(2, false)
-    AZG_IN(3, false)
-    AZG_IN(2, true)
-    AZG_IN(3, true)
-#undef AZG_IN
+    if (vfmt == AZG_WINO_SPLIT)
+        hipLaunchKernelGGL(winograd_in_kernel<true>, grid, dim3(256), 0, st, (const float4*)x, (const float4*)in_bias,
+                           V, h_in, pad, c / 4, (long long)batch, overflow);
+    else
+        hipLaunchKernelGGL(winograd_in_kernel<false>, grid, dim3(256), 0, st, (const float4*)x,
+                           (const float4*)in_bias, V, h_in, pad, c / 4, (long long)batch, overflow);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
 extern "C" int azg_winograd_out_nhwc(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out,
-                                     int32_t k, int32_t m, int32_t relu, float mscale, void* stream) {
-    if (!M || !bias || !y || batch <= 0 || h_out <= 0 || k <= 0 || k % 4 || (m != 2 && m != 3) ||
-        ((uintptr_t)M & 15) || ((uintptr_t)bias & 15) || ((uintptr_t)y & 15) ||
-        (long long)batch * ((h_out + m - 1) / m) * ((h_out + m - 1) / m) * (k / 4) > (1ll << 38))
+                                     int32_t k, int32_t relu, float mscale, void* stream) {
+    if (!M || !bias || !y || batch <= 0 || h_out <= 0 || h_out > 64 || k <= 0 || k % 4 || ((uintptr_t)M & 15) ||
+        ((uintptr_t)bias & 15) || ((uintptr_t)y & 15) || (long long)batch * h_out * h_out * (k / 4) > (1ll << 38))
         return AZG_ERR_ARG;
-    const int tiles = (h_out + m - 1) / m;
-    const long long T = (long long)batch * tiles * tiles;
-    if (m == 2)
-        hipLaunchKernelGGL(winograd_out_kernel<2>, dim3(grid_for(T * (k / 4))), dim3(256), 0, (hipStream_t)stream,
-                           (const float4*)M, (const float4*)bias, (float4*)y, h_out, k / 4, tiles, T, relu, mscale);
-    else
-        hipLaunchKernelGGL(winograd_out_kernel<3>, dim3(grid_for(T * (k / 4))), dim3(256), 0, (hipStream_t)stream,
-                           (const float4*)M, (const float4*)bias, (float4*)y, h_out, k / 4, tiles, T, relu, mscale);
+    const WSeq S(h_out);
+    hipLaunchKernelGGL(winograd_out_kernel, dim3(grid_for((long long)batch * S.p * S.p * (k / 4))), dim3(256), 0,
+                       (hipStream_t)stream, (const float4*)M, (const float4*)bias, (float4*)y, h_out, k / 4,
+                       (long long)batch, relu, mscale);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
 extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, void* V, int32_t batch, int32_t h, int32_t c,
-                                     int32_t m_in, int32_t m_out, float mscale, int32_t vfmt, int32_t* overflow,
-                                     void* stream) {
-    if (!M || !bias || !V || batch <= 0 || h < 3 || h > 9 || c <= 0 || c % 64 || (m_in != 2 && m_in != 3) ||
-        (m_out != 2 && m_out != 3) || bad_fmt(vfmt, overflow))
+                                     float mscale, int32_t vfmt, int32_t* overflow, void* stream) {
+    if (!M || !bias || !V || batch <= 0 || h < 3 || h > 9 || c <= 0 || c % 64 || bad_fmt(vfmt, overflow))
         return AZG_ERR_ARG;
-    const int ti = (h + m_in - 1) / m_in, to = (h - 2 + m_out - 1) / m_out;
-    const long long Ti = (long long)batch * ti * ti, To = (long long)batch * to * to;
     const dim3 grid((unsigned)(batch * (c / 64)));
     const size_t lds = (size_t)h * h * 64 * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
     const bool split = vfmt == AZG_WINO_SPLIT;
+    const long long B = batch;
+#define AZG_MID(H, SP, L)                                                                                          \
+    {                                                                                                              \
+        hipLaunchKernelGGL((winograd_mid_kernel<H, SP>), grid, dim3(64), L, st, M, bias, V, h, c, B, mscale,        \
+                           overflow);                                                                              \
+        return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                                  \
+    }
     // the board sides of the supported games get register-resident planes
-#define AZG_MID(MI, MO, H, SP, L)                                                                          \
-    {                                                                                                      \
-        hipLaunchKernelGGL((winograd_mid_kernel<MI, MO, H, SP>), grid, dim3(64), L, st, M, bias, V, h, c, Ti, \
-                           To, mscale, overflow);                                                          \
-        return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                          \
+#define AZG_MID_REG(H)                                           \
+    if (h == H) {                                                \
+        if (split) AZG_MID(H, true, 0) else AZG_MID(H, false, 0) \
     }
-#define AZG_MID_REG(MI, MO, H)                                   \
-    if (m_in == MI && m_out == MO && h == H) {                   \
-        if (split) AZG_MID(MI, MO, H, true, 0) else AZG_MID(MI, MO, H, false, 0) \
-    }
-    AZG_MID_REG(3, 3, 7)
-    AZG_MID_REG(3, 3, 5)
-    AZG_MID_REG(3, 3, 8)
-    AZG_MID_REG(3, 2, 6)
-    AZG_MID_REG(2, 2, 4)
-#define AZG_MID_LDS(MI, MO)                                       \
-    if (m_in == MI && m_out == MO) {                              \
-        if (split) AZG_MID(MI, MO, 0, true, lds) else AZG_MID(MI, MO, 0, false, lds) \
-    }
-    AZG_MID_LDS(2, 2)
-    AZG_MID_LDS(2, 3)
-    AZG_MID_LDS(3, 2)
-    AZG_MID_LDS(3, 3)
-#undef AZG_MID_LDS
+    AZG_MID_REG(7)
+    AZG_MID_REG(5)
+    AZG_MID_REG(8)
+    AZG_MID_REG(6)
+    AZG_MID_REG(4)
 #undef AZG_MID_REG
+    if (split) AZG_MID(0, true, lds) else AZG_MID(0, false, lds)
 #undef AZG_MID
-    return AZG_ERR_ARG;
 }
 
 extern "C" int azg_winograd_first_nchw(const float* planes, const float* w1, const float* b1, void* V, int32_t batch,
-                                       int32_t depth, int32_t n, int32_t c, int32_t m, int32_t vfmt,
-                                       int32_t* overflow, void* stream) {
+                                       int32_t depth, int32_t n, int32_t c, int32_t vfmt, int32_t* overflow,
+                                       void* stream) {
     if (!planes || !w1 || !b1 || !V || batch <= 0 || depth < 1 || depth > 4 || n < 3 || n > 9 || c <= 0 ||
-        c % 64 || (m != 2 && m != 3) || bad_fmt(vfmt, overflow))
+        c % 64 || bad_fmt(vfmt, overflow))
         return AZG_ERR_ARG;
-    const int to = (n + m - 1) / m;
-    const long long To = (long long)batch * to * to;
     const dim3 grid((unsigned)(batch * (c / 64)));
     const size_t lds_reg = 4 * 81 * sizeof(float), lds = (4 * 81 + (size_t)n * n * 64) * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
     const bool split = vfmt == AZG_WINO_SPLIT;
-#define AZG_FIRST(MO, N, SP, L)                                                                                  \
-    {                                                                                                            \
-        hipLaunchKernelGGL((winograd_first_kernel<MO, N, SP>), grid, dim3(64), L, st, planes, w1, b1, V, depth, n, \
-                           c, To, overflow);                                                                     \
-        return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                                \
+    const long long B = batch;
+#define AZG_FIRST(N, SP, L)                                                                                       \
+    {                                                                                                             \
+        hipLaunchKernelGGL((winograd_first_kernel<N, SP>), grid, dim3(64), L, st, planes, w1, b1, V, depth, n, c, \
+                           B, overflow);                                                                          \
+        return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                                 \
     }
-#define AZG_FIRST_REG(MO, N)                                                  \
-    if (m == MO && n == N) {                                                  \
-        if (split) AZG_FIRST(MO, N, true, lds_reg) else AZG_FIRST(MO, N, false, lds_reg) \
+#define AZG_FIRST_REG(N)                                                         \
+    if (n == N) {                                                                \
+        if (split) AZG_FIRST(N, true, lds_reg) else AZG_FIRST(N, false, lds_reg) \
     }
-    AZG_FIRST_REG(3, 7)
-    AZG_FIRST_REG(3, 8)
-    AZG_FIRST_REG(3, 6)
+    AZG_FIRST_REG(7)
+    AZG_FIRST_REG(8)
+    AZG_FIRST_REG(6)
 #undef AZG_FIRST_REG
-    if (m == 2) {
-        if (split) AZG_FIRST(2, 0, true, lds) else AZG_FIRST(2, 0, false, lds)
-    }
-    if (split) AZG_FIRST(3, 0, true, lds) else AZG_FIRST(3, 0, false, lds)
+    if (split) AZG_FIRST(0, true, lds) else AZG_FIRST(0, false, lds)
 #undef AZG_FIRST
 }

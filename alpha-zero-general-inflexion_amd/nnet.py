@@ -83,25 +83,50 @@ def _azg_conv3x3(x, wt, b, pad):
     return y
 
 
-# Winograd F(m x m, 3x3) weight transforms G [n][3], n = m + 2 (azg_winograd.hip holds B^T, A^T)
+# Winograd F(m, 3) weight transforms G [m+2][3] (azg_winograd.hip holds B^T, A^T)
 WINOGRAD_G = {2: [[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]],
               3: [[0.5, 0.0, 0.0], [-0.5, -0.5, -0.5], [-1 / 6, 1 / 6, -1 / 6], [1 / 6, 1 / 3, 2 / 3],
                   [0.0, 0.0, 1.0]]}
 
 
-def winograd_tile(h_out):
-    """Output tile m (2 or 3) with the fewest GEMM multiply-adds (m+2)^2 ceil(h/m)^2
-    for an h_out x h_out output: 3 for 7x7 (225 vs 256), 5x5, 3x3; 2 for 4x4, 2x2."""
-    return min((2, 3), key=lambda m: ((m + 2) * ((h_out + m - 1) // m)) ** 2)
+def winograd_seq(h_out):
+    """Tile sides along an h_out-long output axis (azg_winograd.hip WSeq, mirrored by
+    azg_winograd_layout): p = ceil(h/3) tiles, as many of side 3 as fit, the rest 2 --
+    7: [3, 2, 2], 5: [3, 2], 3: [3], 8: [3, 3, 2], 4: [2, 2]."""
+    p = (h_out + 2) // 3
+    n3 = max(h_out - 2 * p, 0)
+    return [3] * n3 + [2] * (p - n3)
 
 
-def _winograd_u(w, m=2):
-    """Winograd F(m x m,3x3) weights U[e = n a + b][c][k] = (G g_kc G^T)[a][b], formed in
-    f64 and rounded once (G has entries 1/2, 1/3, 1/6)."""
-    G = torch.tensor(WINOGRAD_G[m], dtype=torch.float64, device=w.device)
-    n = m + 2
-    u = torch.einsum("ar,kcrs,bs->abck", G, w.double(), G)
-    return u.reshape(n * n, w.shape[1], w.shape[0]).float().contiguous()
+def winograd_groups(h_out):
+    """Tile types of an h_out x h_out output in the kernels' order (3,3) (3,2) (2,3) (2,2),
+    present ones only: [(ma, mb, points (ma+2)(mb+2), tiles per image)]."""
+    seq = winograd_seq(h_out)
+    cnt = {3: seq.count(3), 2: seq.count(2)}
+    out = []
+    for ma, mb in ((3, 3), (3, 2), (2, 3), (2, 2)):
+        n = cnt[ma] * cnt[mb]
+        if n:
+            out.append((ma, mb, (ma + 2) * (mb + 2), n))
+    return out
+
+
+def winograd_points(h_out):
+    """Transformed points per image (GEMM rows per image): (sum of (m + 2))^2."""
+    return sum(m + 2 for m in winograd_seq(h_out)) ** 2
+
+
+def _winograd_u(w, h_out):
+    """Winograd weights of a layer with an h_out x h_out output, the groups of
+    winograd_groups one after another: U[e = (ma+2) a + b][c][k] = (G_ma g_kc G_mb^T)[a][b],
+    formed in f64 and rounded once (G has entries 1/2, 1/3, 1/6).  [points][C][K]."""
+    us = []
+    for ma, mb, P, _ in winograd_groups(h_out):
+        Ga = torch.tensor(WINOGRAD_G[ma], dtype=torch.float64, device=w.device)
+        Gb = torch.tensor(WINOGRAD_G[mb], dtype=torch.float64, device=w.device)
+        u = torch.einsum("ar,kcrs,bs->abck", Ga, w.detach().double(), Gb)
+        us.append(u.reshape(P, w.shape[1], w.shape[0]))
+    return torch.cat(us).float().contiguous()
 
 
 def _split_u(u):
@@ -109,7 +134,7 @@ def _split_u(u):
     in (512, 1024], so U's low halves stay out of fp16 subnormals), split as
     hi = fp16(U 2^k), lo = fp16(U 2^k - hi), stacked [hi; hi; lo] along C to meet
     V's [hi | lo | hi] rows.  Returns ([n^2][3C][K] fp16, 2^-k)."""
-    amax = float(u.abs().max())
+    amax = float(u.detach().abs().max())
     k = int(np.floor(np.log2(1024.0 / amax))) if amax > 0 else 0
     us = u.double() * (2.0 ** k)
     hi = us.half()
@@ -161,7 +186,7 @@ class InferenceNet(nn.Module):
         self.mscale = {}  # Winograd layer -> 2^-k undoing the split operand's scale
         self._choices = {}
         self._ws = None  # Winograd V / M workspace, grown to the largest layer seen
-        self.tiles = {}  # Winograd output tile per conv layer
+        self.h_out = {}  # output side per conv layer
         self.fuse_transforms = True  # conv2->3->4: output + next input transform in one pass
         self.n, self.depth, c = net.n, net.depth, net.num_channels
         self.pads = []
@@ -176,9 +201,9 @@ class InferenceNet(nn.Module):
             self.register_buffer(f"wt{i}", w.permute(2, 3, 1, 0).reshape(-1, w.shape[0]).contiguous())
             if i == 1:
                 self.register_buffer("w1c", w.contiguous())  # [K][depth][3][3] for the fused front end
+            self.h_out[i] = h_out
             if i > 1 and conv in ("winograd", "auto"):
-                self.tiles[i] = winograd_tile(h_out)
-                u = _winograd_u(w, self.tiles[i])
+                u = _winograd_u(w, h_out)
                 self.register_buffer(f"u{i}", u)
                 u3, self.mscale[i] = _split_u(u)
                 self.register_buffer(f"u3_{i}", u3)
@@ -199,10 +224,11 @@ class InferenceNet(nn.Module):
         # sticky device flag: a split-GEMM operand fp16 could not hold (checked by check_range)
         self.register_buffer("overflow", torch.zeros(1, dtype=torch.int32))
 
-    def set_winograd_layer(self, i, w, m):
-        """Replace conv i's Winograd weights by w [K][C][3][3] (BN already folded) with tile m."""
-        self.tiles[i] = m
-        u = _winograd_u(w, m).to(self.w1.device)
+    def set_winograd_layer(self, i, w, h_out):
+        """Replace conv i's Winograd weights by w [K][C][3][3] (BN already folded) for an
+        h_out x h_out output."""
+        self.h_out[i] = h_out
+        u = _winograd_u(w, h_out).to(self.w1.device)
         setattr(self, f"u{i}", u)
         u3, self.mscale[i] = _split_u(u)
         setattr(self, f"u3_{i}", u3)
@@ -227,21 +253,18 @@ class InferenceNet(nn.Module):
         # bias + ReLU inside the libazg conv's epilogue
         return _azg_conv3x3(x, getattr(self, f"wt{i}"), getattr(self, f"b{i}"), pad)
 
-    def _v_elems(self, n2, T, C):
-        """f32 words of one V: [n^2][T][C] f32, or [n^2][T][3C] fp16 (split)."""
-        return n2 * T * C if self.gemm == "f32" else (3 * n2 * T * C + 1) // 2
+    def _v_words(self, rows, C):
+        """f32 words of a V with `rows` rows: f32 rows of C, or fp16 rows of 3C (split)."""
+        return rows * C if self.gemm == "f32" else (3 * rows * C + 1) // 2
 
-    def _wino_need(self, i, B, H, pad, C, fuse_next):
-        """Workspace words layer i needs: (V, or the next layer's V when fused; M [n^2][T][K])."""
-        m, K = self.tiles[i], getattr(self, f"u{i}").shape[2]
-        Ho = H + 2 * pad - 2
-        t = (Ho + m - 1) // m
-        need_v = self._v_elems((m + 2) ** 2, B * t * t, C)
+    def _wino_need(self, i, B, C, fuse_next):
+        """Workspace words layer i needs: (its V, or the next layer's V when larger and fused; its M)."""
+        K = getattr(self, f"u{i}").shape[2]
+        rows = B * winograd_points(self.h_out[i])
+        need_v = self._v_words(rows, C)
         if fuse_next:
-            m2 = self.tiles[i + 1]
-            t2 = (Ho - 2 + m2 - 1) // m2
-            need_v = max(need_v, self._v_elems((m2 + 2) ** 2, B * t2 * t2, K))
-        return need_v, (m + 2) ** 2 * B * t * t * K
+            need_v = max(need_v, self._v_words(B * winograd_points(self.h_out[i + 1]), K))
+        return need_v, rows * K
 
     def _ensure_ws(self, need, dev):
         if self._ws is None or self._ws[0].numel() < need[0] or self._ws[1].numel() < need[1]:
@@ -260,20 +283,44 @@ class InferenceNet(nn.Module):
         from . import _lib
         B = s.shape[0]
         C = self.w1c.shape[0]
-        self._ensure_ws(self._wino_need(2, B, self.n, self.pads[1], C, True), s.device)
+        self._ensure_ws(self._wino_need(2, B, C, True), s.device)
         st = ctypes.c_void_p(torch.cuda.current_stream(s.device).cuda_stream)
         fmt, ovf = self._vfmt()
         _lib.check(_lib.lib().azg_winograd_first_nchw(
             ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(self.w1c.data_ptr()), ctypes.c_void_p(self.b1.data_ptr()),
-            ctypes.c_void_p(self._ws[0].data_ptr()), B, self.depth, self.n, C, self.tiles[2], fmt,
-            ctypes.c_void_p(ovf), st))
+            ctypes.c_void_p(self._ws[0].data_ptr()), B, self.depth, self.n, C, fmt, ctypes.c_void_p(ovf), st))
+
+    def _winograd_gemms(self, i, B, C, K):
+        """M = V x U for every transformed point of layer i: one torch.bmm (hipBLASLt) per
+        run of tile groups with equal tiles per image (7x7: 3 calls, 5x5: 1, 3x3: 1)."""
+        split = self.gemm == "split"
+        W = 3 * C if split else C
+        Vflat = self._ws[0].view(torch.float16) if split else self._ws[0]
+        U = getattr(self, f"u3_{i}") if split else getattr(self, f"u{i}")
+        runs = []
+        for _, _, P, n in winograd_groups(self.h_out[i]):
+            if runs and runs[-1][1] == n:
+                runs[-1][0] += P
+            else:
+                runs.append([P, n])
+        row = pt = 0
+        for P, n in runs:
+            T = B * n
+            V = Vflat[row * W:(row + P * T) * W].view(P, T, W)
+            M = self._ws[1][row * K:(row + P * T) * K].view(P, T, K)
+            if split:
+                torch.bmm(V, U[pt:pt + P], out_dtype=torch.float32, out=M)
+            else:
+                torch.bmm(V, U[pt:pt + P], out=M)
+            row += P * T
+            pt += P
 
     def _conv_winograd(self, x, i, pad, in_bias=None, carried=False, B=None, H=None, fuse_next=False):
-        """Winograd F(m x m,3x3) layer i: libazg input transform (or, with carried=True,
-        the V the previous layer's fused transform left in the workspace), the n^2 f32
-        GEMMs (torch.bmm -> hipBLASLt), then either the output transform with bias + ReLU
-        (returns the NHWC activation) or, with fuse_next, the fused output / next-input
-        transform writing layer i+1's V (returns None) (azg_winograd.hip)."""
+        """Winograd layer i (mixed F(3,3)/F(2,3) tiles, azg_winograd.hip): libazg input
+        transform (or, with carried=True, the V the previous layer's fused transform left
+        in the workspace), the GEMMs (_winograd_gemms), then either the output transform
+        with bias + ReLU (returns the NHWC activation) or, with fuse_next, the fused
+        output / next-input transform writing layer i+1's V (returns None)."""
         import ctypes
         from . import _lib
         if not carried:
@@ -284,48 +331,31 @@ class InferenceNet(nn.Module):
         else:
             C = getattr(self, f"u{i}").shape[1]
             dev = self._ws[0].device
-        U = getattr(self, f"u{i}")
-        m = self.tiles[i]
-        nn2 = (m + 2) ** 2
-        K = U.shape[2]
+        K = getattr(self, f"u{i}").shape[2]
         Ho = H + 2 * pad - 2
-        t = (Ho + m - 1) // m
-        T = B * t * t
-        if fuse_next:
-            m2 = self.tiles[i + 1]
-        need = self._wino_need(i, B, H, pad, C, fuse_next)
+        if Ho != self.h_out[i]:
+            raise ValueError(f"conv{i}: input side {H} gives {Ho}x{Ho} outputs, the weights are for {self.h_out[i]}")
+        need = self._wino_need(i, B, C, fuse_next)
         if not carried:
             self._ensure_ws(need, dev)
         elif not self._ws_fits(need):
             raise RuntimeError("Winograd workspace too small for a carried layer")
-        split = self.gemm == "split"
-        if split:
-            V = self._ws[0].view(torch.float16)[:nn2 * T * 3 * C].view(nn2, T, 3 * C)
-            mscale = self.mscale[i]
-        else:
-            V = self._ws[0][:nn2 * T * C].view(nn2, T, C)
-            mscale = 1.0
-        M = self._ws[1][:nn2 * T * K].view(nn2, T, K)
+        mscale = self.mscale[i] if self.gemm == "split" else 1.0
         s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         L = _lib.lib()
         bias = ctypes.c_void_p(getattr(self, f"b{i}").data_ptr())
         fmt, ovf = self._vfmt()
+        V, M = ctypes.c_void_p(self._ws[0].data_ptr()), ctypes.c_void_p(self._ws[1].data_ptr())
         if not carried:
             ib = ctypes.c_void_p(in_bias.data_ptr()) if in_bias is not None else None
-            _lib.check(L.azg_winograd_in_nhwc(ctypes.c_void_p(x.data_ptr()), ib, ctypes.c_void_p(V.data_ptr()),
-                                              B, H, pad, C, m, fmt, ctypes.c_void_p(ovf), s))
-        if split:
-            torch.bmm(V, getattr(self, f"u3_{i}"), out_dtype=torch.float32, out=M)
-        else:
-            torch.bmm(V, U, out=M)
+            _lib.check(L.azg_winograd_in_nhwc(ctypes.c_void_p(x.data_ptr()), ib, V, B, H, pad, C, fmt,
+                                              ctypes.c_void_p(ovf), s))
+        self._winograd_gemms(i, B, C, K)
         if fuse_next:
-            _lib.check(L.azg_winograd_mid_nhwc(ctypes.c_void_p(M.data_ptr()), bias,
-                                               ctypes.c_void_p(self._ws[0].data_ptr()), B, Ho, K, m, m2,
-                                               mscale, fmt, ctypes.c_void_p(ovf), s))
+            _lib.check(L.azg_winograd_mid_nhwc(M, bias, V, B, Ho, K, mscale, fmt, ctypes.c_void_p(ovf), s))
             return None
         y = torch.empty((B, K, Ho, Ho), device=dev, dtype=torch.float32, memory_format=torch.channels_last)
-        _lib.check(L.azg_winograd_out_nhwc(ctypes.c_void_p(M.data_ptr()), bias, ctypes.c_void_p(y.data_ptr()),
-                                           B, Ho, K, m, 1, mscale, s))
+        _lib.check(L.azg_winograd_out_nhwc(M, bias, ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, mscale, s))
         return y
 
     def _pick(self, x, i, pad):

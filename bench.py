@@ -58,10 +58,12 @@ def net_flops(n, depth, A, c=512):
     return conv1 + conv234 + fc, conv234
 
 
-def winograd_flops(n, c=512, tiles=(3, 3, 3)):
-    """GEMM FLOPs per leaf of conv2-4 as Winograd F(m x m,3x3) (m per layer, nnet.winograd_tile):
-    (m+2)^2 x 2 C K per m x m output tile, ceil(h_out/m)^2 tiles (7x7 board: 183.5 M vs 391.6 M direct)."""
-    return sum((m + 2) ** 2 * 2 * c * c * ((h + m - 1) // m) ** 2 for h, m in zip((n, n - 2, n - 4), tiles))
+def winograd_flops(n, c=512):
+    """GEMM FLOPs per leaf of conv2-4 as mixed F(3,3)/F(2,3) Winograd (nnet.winograd_points:
+    (sum of tile sides + 2)^2 transformed points per image x 2 C K): 7x7 board
+    (13^2 + 9^2 + 5^2) x 2 x 512^2 = 144.2 M vs 391.6 M direct."""
+    from azg_amd.nnet import winograd_points
+    return sum(winograd_points(h) * 2 * c * c for h in (n, n - 2, n - 4))
 
 
 # mean valid actions per visited node (SURVEY 8(d): 87 for 7x7 Inflexion; legal
@@ -319,8 +321,7 @@ def main():
         conv_avg = conv_ms / n_forwards / 1e3 if conv_ms > 0 else nn_avg
         impl = getattr(ev, "conv_impl", None) if not isinstance(ev, str) else None
         # algorithmic FLOPs of conv2-4 as computed: the Winograd path does fewer
-        algo_conv_leaf = (winograd_flops(args.n, tiles=tuple(ev.tiles[i] for i in (2, 3, 4)))
-                          if impl == "winograd" else conv_flop_leaf)
+        algo_conv_leaf = winograd_flops(args.n) if impl == "winograd" else conv_flop_leaf
         conv_flops = leaves * (algo_conv_leaf if conv_ms > 0 else flop_leaf)
         conv_tflops = conv_flops / conv_avg / 1e12 if conv_avg > 0 else 0.0
         direct_tflops = leaves * conv_flop_leaf / conv_avg / 1e12 if conv_ms > 0 and conv_avg > 0 else None
@@ -338,10 +339,12 @@ def main():
                 return "MIOpen igemm_fwd_gtcx35_nhwc_fp32 + libazg bias/ReLU pass"
             if m == "azg":
                 return "libazg f32-MFMA implicit GEMM (LDS-DMA ring) + fused bias/ReLU"
-            t = ev.tiles[i]
+            from azg_amd.nnet import winograd_points, winograd_seq
             g = ("split-fp16 GEMMs (3 fp16 MFMA products, f32 accumulate; hipBLASLt)" if split
                  else "f32 GEMMs (hipBLASLt)")
-            return f"Winograd F({t}x{t},3x3): libazg fused transforms + {(t + 2) ** 2} {g}"
+            seq = "+".join(map(str, winograd_seq(ev.h_out[i])))
+            return (f"Winograd {seq} tiles per axis (F(3,3)/F(2,3)): libazg fused transforms + "
+                    f"{winograd_points(ev.h_out[i])}-point {g}")
         conv_kernel_desc = ("conv2-4 per forward: " + "; ".join(f"conv{i} {name(i, m)}" for i, m in impls.items())
                             if impls else "whole forward (no conv hook)")
         # split GEMMs execute 3 fp16 products per f32 multiply-add: priced against the fp16 MFMA peak

@@ -138,41 +138,45 @@ int  azg_conv3x3_bias_relu_nhwc(const float* x, const float* wt, const float* bi
 int  azg_conv3x3_variant(int variant, const float* x, const float* wt, const float* bias, float* y, int32_t batch,
                          int32_t h_in, int32_t pad, int32_t c_in, int32_t c_out, void* stream);
 
-/* Leaf-network 3x3 convolution as Winograd F(m x m, 3x3), m = 2 or 3
- * (azg_winograd.hip): the same layer as azg_conv3x3_bias_relu_nhwc in three steps,
- * with n = m + 2, T = batch * t * t tiles, t = ceil(h_out / m):
+/* Leaf-network 3x3 convolutions as Winograd convolutions over mixed F(3,3) /
+ * F(2,3) tiles (azg_winograd.hip).  They replace the convolutions of
+ * InflexionNNet.forward (InflexionNNet.py:39-45, BN folded).  An h-long output axis
+ * is cut into p = ceil(h/3) tiles, as many of side 3 as fit, the rest of side 2
+ * (7 = 3+2+2, 5 = 3+2); azg_winograd_layout returns p, writes the sides to seq[p]
+ * and the tiles per image of the groups (3,3) (3,2) (2,3) (2,2) to groups[4].
+ * V and M hold the groups one after another, group g = (ma, mb) as
+ * [P_g = (ma+2)(mb+2) points][batch * tiles_g][row], tiles row-major per image.
  *   azg_winograd_in_nhwc : x NHWC [batch, h_in, h_in, c] (zero padding `pad`) ->
  *                          V (B^T d B per tile and channel, format vfmt below);
  *                          with in_bias != NULL, relu(x + in_bias[c]) is
  *                          transformed (the previous layer's bias + ReLU fused);
- *   (caller)             : M[e] = V[e] x U[e] for e < n*n, U [n*n][c][k] = G g G^T
+ *   (caller)             : M_e = V_e x U_e per point e, U = G_ma g G_mb^T
  *                          (times mscale^-1, a power of two, for split V);
- *   azg_winograd_out_nhwc: M [n*n][T][k] f32 -> y NHWC [batch, h_out, h_out, k] =
+ *   azg_winograd_out_nhwc: M f32 (rows of k) -> y NHWC [batch, h_out, h_out, k] =
  *                          A^T (mscale M) A + bias, ReLU if relu != 0.
- * V formats: AZG_WINO_F32 f32 [n*n][T][c]; AZG_WINO_SPLIT fp16 [n*n][T][3c] with
- * rows [hi | lo | hi], hi = fp16(v), lo = fp16(v - hi) -- the A operand of the
+ * V formats: AZG_WINO_F32 f32 rows of c; AZG_WINO_SPLIT fp16 rows of 3c =
+ * [hi | lo | hi], hi = fp16(v), lo = fp16(v - hi) -- the A operand of the
  * error-compensated GEMM [hi|lo|hi] x [Uh; Uh; Ul] (f32 accumulation); a value
  * fp16 cannot hold (|v| > 65504, NaN) sets *overflow (device int, required).
- * c % 4 == 0, k % 4 == 0, 16-B aligned pointers.
- * These replace the convolutions of InflexionNNet.forward (InflexionNNet.py:39-45). */
+ * c % 4 == 0, k % 4 == 0, 16-B aligned pointers, h_out <= 64. */
 enum { AZG_WINO_F32 = 0, AZG_WINO_SPLIT = 1 };
+int  azg_winograd_layout(int32_t h_out, int32_t* seq, int32_t* groups);
 int  azg_winograd_in_nhwc(const float* x, const float* in_bias, void* V, int32_t batch, int32_t h_in, int32_t pad,
-                          int32_t c, int32_t m, int32_t vfmt, int32_t* overflow, void* stream);
+                          int32_t c, int32_t vfmt, int32_t* overflow, void* stream);
 int  azg_winograd_out_nhwc(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,
-                           int32_t m, int32_t relu, float mscale, void* stream);
+                           int32_t relu, float mscale, void* stream);
 /* Between two Winograd layers with no padding on the second (conv2->conv3->conv4):
- * M of layer i (tile m_in, h x h outputs, c channels) -> relu(A^T (mscale M) A +
- * bias) -> V of layer i+1 (tile m_out, input h x h, format vfmt) in one pass; the
- * activation stays on chip.  3 <= h <= 9, c % 64 == 0. */
+ * M of layer i (h x h outputs, c channels) -> relu(A^T (mscale M) A + bias) -> V of
+ * layer i+1 (input h x h, format vfmt) in one pass; the activation stays on chip.
+ * 3 <= h <= 9, c % 64 == 0. */
 int  azg_winograd_mid_nhwc(const float* M, const float* bias, void* V, int32_t batch, int32_t h, int32_t c,
-                           int32_t m_in, int32_t m_out, float mscale, int32_t vfmt, int32_t* overflow, void* stream);
+                           float mscale, int32_t vfmt, int32_t* overflow, void* stream);
 /* The first two layers' front end: conv1 (planes NCHW [batch, depth, n, n] ->
  * c channels, 3x3, pad 1, weights w1 [c][depth][3][3], bias b1) + ReLU, then
- * conv2's Winograd input transform (pad 1, tile m) -> V (format vfmt) in one
- * pass.  depth <= 4, 3 <= n <= 9, c % 64 == 0. */
+ * conv2's Winograd input transform (pad 1) -> V (format vfmt) in one pass.
+ * depth <= 4, 3 <= n <= 9, c % 64 == 0. */
 int  azg_winograd_first_nchw(const float* planes, const float* w1, const float* b1, void* V, int32_t batch,
-                             int32_t depth, int32_t n, int32_t c, int32_t m, int32_t vfmt, int32_t* overflow,
-                             void* stream);
+                             int32_t depth, int32_t n, int32_t c, int32_t vfmt, int32_t* overflow, void* stream);
 
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active

@@ -97,10 +97,11 @@ def test_azg_conv3x3_variants(variant, B, H, pad):
 
 
 @pytest.mark.parametrize("gemm", ["split", "f32"])
-@pytest.mark.parametrize("m", [2, 3])
-@pytest.mark.parametrize("B,H,pad", [(1, 7, 1), (37, 7, 1), (300, 7, 0), (129, 5, 0), (64, 8, 1), (5, 6, 0)])
-def test_winograd_conv3x3_matches_torch(B, H, pad, m, gemm):
-    """Winograd F(m x m,3x3) layer (libazg transforms + split-fp16 or f32 bmm) vs torch conv2d + bias + ReLU."""
+@pytest.mark.parametrize("B,H,pad", [(1, 7, 1), (37, 7, 1), (300, 7, 0), (129, 5, 0), (64, 8, 1), (5, 6, 0),
+                                     (3, 4, 1), (7, 9, 1), (2, 11, 0), (3, 3, 1)])
+def test_winograd_conv3x3_matches_torch(B, H, pad, gemm):
+    """Winograd layer (mixed F(3,3)/F(2,3) tiles: every tile-type group; libazg
+    transforms + split-fp16 or f32 bmm) vs torch conv2d + bias + ReLU."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
     torch.manual_seed(3)
@@ -109,7 +110,7 @@ def test_winograd_conv3x3_matches_torch(B, H, pad, m, gemm):
     C = N = 512
     w = torch.randn(N, C, 3, 3) * 0.02
     layer = 2
-    fast.set_winograd_layer(layer, w.cuda(), m)
+    fast.set_winograd_layer(layer, w.cuda(), H + 2 * pad - 2)
     b = (torch.randn(N) * 0.1).cuda()
     setattr(fast, f"b{layer}", b)
     x = torch.relu(torch.randn(B, C, H, H, device="cuda")).contiguous(memory_format=torch.channels_last)

@@ -63,3 +63,23 @@ def test_inference_net_matches_reference_net():
         p2, v2 = InferenceNet(net)(x)
     np.testing.assert_allclose(p2.numpy(), torch.exp(lp).numpy(), rtol=1e-5, atol=1e-8)
     np.testing.assert_allclose(v2.numpy(), v.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_winograd_layout_matches_libazg():
+    """The Python mirror of the mixed-tile layout (GEMM grouping, U order) agrees with
+    the kernels' own (azg_winograd_layout), and covers each axis exactly."""
+    import ctypes
+    from azg_amd import _lib
+    from azg_amd.nnet import winograd_groups, winograd_points, winograd_seq
+    L = _lib.lib()
+    assert winograd_seq(7) == [3, 2, 2] and winograd_seq(5) == [3, 2] and winograd_seq(3) == [3]
+    assert winograd_points(7) == 169 and winograd_points(5) == 81 and winograd_points(3) == 25
+    for h in range(1, 30):
+        seq = (ctypes.c_int32 * 16)()
+        groups = (ctypes.c_int32 * 4)()
+        p = L.azg_winograd_layout(h, seq, groups)
+        assert list(seq[:p]) == winograd_seq(h), h
+        assert sum(winograd_seq(h)) == max(h, 2), h  # exact cover (h = 1 pads to one 2-tile)
+        want = {(ma, mb): n for ma, mb, _, n in winograd_groups(h)}
+        for g, (ma, mb) in enumerate(((3, 3), (3, 2), (2, 3), (2, 2))):
+            assert groups[g] == want.get((ma, mb), 0), (h, g)
