@@ -28,8 +28,10 @@
 // B and A have small integer entries (F(2,3): 0, +-1; F(3,3): up to 4); U is formed
 // in f64 by the caller (G has entries 1/2, 1/3, 1/6).
 //
-// V is written in one of two formats (vfmt):
+// V is written in one of three formats (vfmt):
 //   AZG_WINO_F32  : f32 rows of C;
+//   AZG_WINO_SPLIT2: fp16 rows of 2C = [hi | lo], the A operand of libazg's split
+//                   GEMM (azg_split_gemm.hip), which forms the three products itself;
 //   AZG_WINO_SPLIT: fp16 rows of 3C = [hi | lo | hi], hi = fp16(v), lo = fp16(v - hi),
 //                   for the error-compensated GEMM M = [hi|lo|hi] x [Uh; Uh; Ul] =
 //                   hi Uh + lo Uh + hi Ul on the fp16 MFMA with f32 accumulation.
@@ -162,27 +164,28 @@ __device__ __forceinline__ void out_tile(const T (&mm)[MA + 2][MB + 2], T (&y)[M
         for (int q = 0; q < MB; ++q) y[a][q] = combine<NB, T>(WinoT<MB>::AT[q], [&](int v) { return s[a][v]; });
 }
 
-// One V element: f32, or its fp16 (hi, lo, hi) triple at columns c, C + c, 2C + c
-// of a 3C-wide row.
-template <bool SPLIT>
+// One V element: f32 (FMT 0); its fp16 (hi, lo, hi) at columns c, C + c, 2C + c of
+// a 3C-wide row (FMT 1, AZG_WINO_SPLIT); or (hi, lo) at c, C + c of a 2C-wide row
+// (FMT 2, AZG_WINO_SPLIT2).
+template <int FMT>
 __device__ __forceinline__ void store_v(void* V, long long row, int C, int c, float v, int* overflow) {
-    if constexpr (!SPLIT) {
+    if constexpr (FMT == AZG_WINO_F32) {
         ((float*)V)[row * C + c] = v;
     } else {
         const _Float16 hi = (_Float16)v;  // round to nearest even
         const _Float16 lo = (_Float16)(v - (float)hi);
-        _Float16* r = (_Float16*)V + row * 3 * C;
+        _Float16* r = (_Float16*)V + row * (FMT == AZG_WINO_SPLIT ? 3 : 2) * C;
         r[c] = hi;
         r[C + c] = lo;
-        r[2 * C + c] = hi;
+        if constexpr (FMT == AZG_WINO_SPLIT) r[2 * C + c] = hi;
         if (!(fabsf(v) <= 65504.f)) atomicOr(overflow, 1);
     }
 }
 
 // Four consecutive channels (c4 = c / 4) of one V row.
-template <bool SPLIT>
+template <int FMT>
 __device__ __forceinline__ void store_v(void* V, long long row, int C4, int c4, float4 v, int* overflow) {
-    if constexpr (!SPLIT) {
+    if constexpr (FMT == AZG_WINO_F32) {
         ((float4*)V)[row * C4 + c4] = v;
     } else {
         const float x[4] = {v.x, v.y, v.z, v.w};
@@ -197,10 +200,10 @@ __device__ __forceinline__ void store_v(void* V, long long row, int C4, int c4, 
             lo.h[j] = (_Float16)(x[j] - (float)hi.h[j]);
             bad |= !(fabsf(x[j]) <= 65504.f);
         }
-        uint2* r = (uint2*)V + row * 3 * C4;
+        uint2* r = (uint2*)V + row * (FMT == AZG_WINO_SPLIT ? 3 : 2) * C4;
         r[c4] = hi.u;
         r[C4 + c4] = lo.u;
-        r[2 * C4 + c4] = hi.u;
+        if constexpr (FMT == AZG_WINO_SPLIT) r[2 * C4 + c4] = hi.u;
         if (bad) atomicOr(overflow, 1);
     }
 }
@@ -217,7 +220,7 @@ __device__ __forceinline__ long long xcd_item() {
 // One thread per (tile, 4 channels); tiles image-major, row-major in the image.
 // in_bias != null: x is the previous layer's raw output and relu(x + in_bias) is
 // applied on load (that layer's bias + ReLU fused here; padding stays 0).
-template <bool SPLIT>
+template <int FMT>
 __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restrict__ x,
                                                           const float4* __restrict__ in_bias, void* __restrict__ V,
                                                           int H, int pad, int C4, long long B, int* overflow) {
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restri
         in_tile<MA, MB>(d, Vt);
 #pragma unroll
         for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
-            store_v<SPLIT>(V, row + e * ps, C4, c4, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
+            store_v<FMT>(V, row + e * ps, C4, c4, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
     });
 }
 
@@ -310,7 +313,7 @@ struct Plane {
 
 // The next layer's input transform (pad `pad`) of the lane's h x h plane: V out.
 // Loop bounds are compile-time for HC > 0 (p <= (HC + 4) / 3), 3 otherwise (h <= 9).
-template <int HC, bool SPLIT, class P>
+template <int HC, int FMT, class P>
 __device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, int pad, long long b, int c, int C, long long B,
                                            void* __restrict__ Vout, int* overflow) {
     constexpr int PMAX = HC > 0 ? (HC + 4) / 3 : 3;
@@ -338,7 +341,7 @@ __device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, int pad, long 
                 in_tile<MA, MB>(d, Vt);
 #pragma unroll
                 for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
-                    store_v<SPLIT>(Vout, row + e * ps, C, c, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
+                    store_v<FMT>(Vout, row + e * ps, C, c, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
             });
         }
     }
@@ -350,7 +353,7 @@ __device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, int pad, long 
 // (bias + ReLU applied) is kept in registers (compile-time side HC) or its own
 // LDS column -- only that lane reads it back, so no barrier -- and the next
 // layer's tiles are transformed from it: layer i's activation never goes to HBM.
-template <int HC, bool SPLIT>
+template <int HC, int FMT>
 __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restrict__ Min, const float* __restrict__ bias,
                                                           void* __restrict__ Vout, int h_rt, int C, long long B,
                                                           float mscale, int* overflow) {
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
             });
         }
     }
-    plane_to_V<HC, SPLIT>(ys, h, 0, b, c, C, B, Vout, overflow);
+    plane_to_V<HC, FMT>(ys, h, 0, b, c, C, B, Vout, overflow);
 }
 
 // The network's first two layers' front end in one pass: conv1 (depth -> C
@@ -400,7 +403,7 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
 // one channel per lane: the image's planes are shared through LDS, the lane's
 // depth*9 weights and its n x n output plane sit in registers (compile-time
 // side NC) or its own LDS column.
-template <int NC, bool SPLIT>
+template <int NC, int FMT>
 __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restrict__ planes,
                                                             const float* __restrict__ w1,
                                                             const float* __restrict__ b1, void* __restrict__ Vout,
@@ -444,7 +447,7 @@ __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restr
             }
             ys.put(y * n + x, fmaxf(acc + bk, 0.f));
         }
-    plane_to_V<NC, SPLIT>(ys, n, 1, b, k, C, B, Vout, overflow);
+    plane_to_V<NC, FMT>(ys, n, 1, b, k, C, B, Vout, overflow);
 }
 
 // one thread per work item, rounded up to whole groups of 8 blocks (xcd_item)
@@ -453,7 +456,9 @@ unsigned grid_for(long long n) {
     return (unsigned)(((blocks + 7) / 8) * 8);
 }
 
-bool bad_fmt(int vfmt, const int* overflow) { return !(vfmt == AZG_WINO_F32 || (vfmt == AZG_WINO_SPLIT && overflow)); }
+bool bad_fmt(int vfmt, const int* overflow) {
+    return !(vfmt == AZG_WINO_F32 || ((vfmt == AZG_WINO_SPLIT || vfmt == AZG_WINO_SPLIT2) && overflow));
+}
 }  // namespace
 
 extern "C" int azg_winograd_layout(int32_t h_out, int32_t* seq, int32_t* groups) {
@@ -476,12 +481,14 @@ extern "C" int azg_winograd_in_nhwc(const float* x, const float* in_bias, void* 
     const WSeq S(h_out);
     const dim3 grid(grid_for((long long)batch * S.p * S.p * (c / 4)));
     hipStream_t st = (hipStream_t)stream;
-    if (vfmt == AZG_WINO_SPLIT)
-        hipLaunchKernelGGL(winograd_in_kernel<true>, grid, dim3(256), 0, st, (const float4*)x, (const float4*)in_bias,
+#define AZG_IN(F)                                                                                            \
+    if (vfmt == F)                                                                                           \
+        hipLaunchKernelGGL(winograd_in_kernel<F>, grid, dim3(256), 0, st, (const float4*)x, (const float4*)in_bias, \
                            V, h_in, pad, c / 4, (long long)batch, overflow);
-    else
-        hipLaunchKernelGGL(winograd_in_kernel<false>, grid, dim3(256), 0, st, (const float4*)x,
-                           (const float4*)in_bias, V, h_in, pad, c / 4, (long long)batch, overflow);
+    AZG_IN(AZG_WINO_F32)
+    AZG_IN(AZG_WINO_SPLIT)
+    AZG_IN(AZG_WINO_SPLIT2)
+#undef AZG_IN
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
@@ -504,7 +511,6 @@ extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, void* V,
     const dim3 grid((unsigned)(batch * (c / 64)));
     const size_t lds = (size_t)h * h * 64 * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
-    const bool split = vfmt == AZG_WINO_SPLIT;
     const long long B = batch;
 #define AZG_MID(H, SP, L)                                                                                          \
     {                                                                                                              \
@@ -513,17 +519,22 @@ extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, void* V,
         return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                                  \
     }
     // the board sides of the supported games get register-resident planes
-#define AZG_MID_REG(H)                                           \
-    if (h == H) {                                                \
-        if (split) AZG_MID(H, true, 0) else AZG_MID(H, false, 0) \
+#define AZG_MID_FMT(H, L)                       \
+    {                                           \
+        if (vfmt == AZG_WINO_SPLIT2) AZG_MID(H, AZG_WINO_SPLIT2, L) \
+        if (vfmt == AZG_WINO_SPLIT) AZG_MID(H, AZG_WINO_SPLIT, L)   \
+        AZG_MID(H, AZG_WINO_F32, L)                                 \
     }
+#define AZG_MID_REG(H) \
+    if (h == H) AZG_MID_FMT(H, 0)
     AZG_MID_REG(7)
     AZG_MID_REG(5)
     AZG_MID_REG(8)
     AZG_MID_REG(6)
     AZG_MID_REG(4)
 #undef AZG_MID_REG
-    if (split) AZG_MID(0, true, lds) else AZG_MID(0, false, lds)
+    AZG_MID_FMT(0, lds)
+#undef AZG_MID_FMT
 #undef AZG_MID
 }
 
@@ -536,7 +547,6 @@ extern "C" int azg_winograd_first_nchw(const float* planes, const float* w1, con
     const dim3 grid((unsigned)(batch * (c / 64)));
     const size_t lds_reg = 4 * 81 * sizeof(float), lds = (4 * 81 + (size_t)n * n * 64) * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
-    const bool split = vfmt == AZG_WINO_SPLIT;
     const long long B = batch;
 #define AZG_FIRST(N, SP, L)                                                                                       \
     {                                                                                                             \
@@ -544,14 +554,19 @@ extern "C" int azg_winograd_first_nchw(const float* planes, const float* w1, con
                            B, overflow);                                                                          \
         return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                                 \
     }
-#define AZG_FIRST_REG(N)                                                         \
-    if (n == N) {                                                                \
-        if (split) AZG_FIRST(N, true, lds_reg) else AZG_FIRST(N, false, lds_reg) \
+#define AZG_FIRST_FMT(N, L)                                          \
+    {                                                                \
+        if (vfmt == AZG_WINO_SPLIT2) AZG_FIRST(N, AZG_WINO_SPLIT2, L) \
+        if (vfmt == AZG_WINO_SPLIT) AZG_FIRST(N, AZG_WINO_SPLIT, L)   \
+        AZG_FIRST(N, AZG_WINO_F32, L)                                 \
     }
+#define AZG_FIRST_REG(N) \
+    if (n == N) AZG_FIRST_FMT(N, lds_reg)
     AZG_FIRST_REG(7)
     AZG_FIRST_REG(8)
     AZG_FIRST_REG(6)
 #undef AZG_FIRST_REG
-    if (split) AZG_FIRST(0, true, lds) else AZG_FIRST(0, false, lds)
+    AZG_FIRST_FMT(0, lds)
+#undef AZG_FIRST_FMT
 #undef AZG_FIRST
 }

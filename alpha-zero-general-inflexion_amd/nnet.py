@@ -130,16 +130,25 @@ def _winograd_u(w, h_out):
 
 
 def _split_u(u):
-    """Operand B of the error-compensated Winograd GEMM: U scaled by 2^k (max |U| 2^k
-    in (512, 1024], so U's low halves stay out of fp16 subnormals), split as
-    hi = fp16(U 2^k), lo = fp16(U 2^k - hi), stacked [hi; hi; lo] along C to meet
-    V's [hi | lo | hi] rows.  Returns ([n^2][3C][K] fp16, 2^-k)."""
+    """Split-GEMM weights: U scaled by 2^k (max |U| 2^k in (512, 1024], so U's low
+    halves stay out of fp16 subnormals), split exactly as hi = fp16(U 2^k),
+    lo = fp16(U 2^k - hi).  Returns (hi, lo) [points][C][K] fp16 and 2^-k."""
     amax = float(u.detach().abs().max())
     k = int(np.floor(np.log2(1024.0 / amax))) if amax > 0 else 0
-    us = u.double() * (2.0 ** k)
+    us = u.detach().double() * (2.0 ** k)
     hi = us.half()
     lo = (us - hi.double()).half()
-    return torch.cat([hi, hi, lo], dim=1).contiguous(), 2.0 ** -k
+    return hi, lo, 2.0 ** -k
+
+
+def _split_operands(u, gemm):
+    """Operand B of the split GEMM form: "split" (libazg azg_split_gemm): U^T rows
+    [hi | lo], [points][K][2C]; "split_blas" (hipBLASLt): [hi; hi; lo] stacked along C,
+    [points][3C][K], to meet V's [hi | lo | hi] rows.  Returns (B, 2^-k)."""
+    hi, lo, scale = _split_u(u)
+    if gemm == "split":
+        return torch.cat([hi.transpose(1, 2), lo.transpose(1, 2)], dim=2).contiguous(), scale
+    return torch.cat([hi, hi, lo], dim=1).contiguous(), scale
 
 
 def _fold_bn(weight, bias, bn):
@@ -173,15 +182,18 @@ class InferenceNet(nn.Module):
         network (tests/test_gpu_nn.py); measured side by side in DESIGN.md 4.1.
 
         gemm (the Winograd GEMMs): "split" (default; each f32 operand split into
-        fp16 hi + lo, hi*hi + lo*hi + hi*lo on the fp16 MFMA with f32 accumulation:
-        f32-accurate products -- measured error at or below the f32 GEMM's -- at 2x
-        its speed) or "f32" (f32 MFMA GEMMs)."""
+        fp16 hi + lo, hi*hi + lo*hi + hi*lo on the fp16 MFMA with f32 accumulation in
+        libazg's hand-written GEMM: f32-accurate products -- measured error at or below
+        the f32 GEMM's), "split_blas" (the same products as one hipBLASLt fp16 GEMM
+        over [hi | lo | hi] rows) or "f32" (f32 MFMA GEMMs, hipBLASLt)."""
         super().__init__()
         if conv not in ("miopen", "azg", "auto", "winograd"):
             raise ValueError(f"unknown conv implementation {conv!r}")
-        if gemm not in ("split", "f32"):
+        if gemm not in ("split", "split_blas", "f32"):
             raise ValueError(f"unknown gemm form {gemm!r}")
         self.conv_impl = conv
+        if gemm == "split" and (net.num_channels % 256 or net.num_channels % 32):
+            gemm = "split_blas"  # libazg's split GEMM tiles K by 256
         self.gemm = gemm
         self.mscale = {}  # Winograd layer -> 2^-k undoing the split operand's scale
         self._choices = {}
@@ -205,8 +217,9 @@ class InferenceNet(nn.Module):
             if i > 1 and conv in ("winograd", "auto"):
                 u = _winograd_u(w, h_out)
                 self.register_buffer(f"u{i}", u)
-                u3, self.mscale[i] = _split_u(u)
-                self.register_buffer(f"u3_{i}", u3)
+                if gemm != "f32":
+                    ub, self.mscale[i] = _split_operands(u, gemm)
+                    self.register_buffer(f"us_{i}", ub)
             self.pads.append(conv_i.padding[0])
             h = h_out
         s = net.n - 4
@@ -230,13 +243,14 @@ class InferenceNet(nn.Module):
         self.h_out[i] = h_out
         u = _winograd_u(w, h_out).to(self.w1.device)
         setattr(self, f"u{i}", u)
-        u3, self.mscale[i] = _split_u(u)
-        setattr(self, f"u3_{i}", u3)
+        if self.gemm != "f32":
+            ub, self.mscale[i] = _split_operands(u, self.gemm)
+            setattr(self, f"us_{i}", ub)
 
     def check_range(self):
         """Raise if any split-GEMM operand since the last call was out of fp16 range
         (|v| > 65504 or NaN): the GEMM would have been wrong, not just inexact."""
-        if self.gemm == "split" and int(self.overflow.item()) != 0:
+        if self.gemm != "f32" and int(self.overflow.item()) != 0:
             self.overflow.zero_()
             raise FloatingPointError("Winograd split-GEMM operand out of fp16 range; use InferenceNet(gemm='f32')")
 
@@ -254,8 +268,8 @@ class InferenceNet(nn.Module):
         return _azg_conv3x3(x, getattr(self, f"wt{i}"), getattr(self, f"b{i}"), pad)
 
     def _v_words(self, rows, C):
-        """f32 words of a V with `rows` rows: f32 rows of C, or fp16 rows of 3C (split)."""
-        return rows * C if self.gemm == "f32" else (3 * rows * C + 1) // 2
+        """f32 words of a V with `rows` rows: f32 rows of C, fp16 rows of 2C (split) or 3C (split_blas)."""
+        return rows * C if self.gemm in ("f32", "split") else (3 * rows * C + 1) // 2
 
     def _wino_need(self, i, B, C, fuse_next):
         """Workspace words layer i needs: (its V, or the next layer's V when larger and fused; its M)."""
@@ -274,7 +288,10 @@ class InferenceNet(nn.Module):
         return self._ws is not None and self._ws[0].numel() >= need[0] and self._ws[1].numel() >= need[1]
 
     def _vfmt(self):
-        return (0, None) if self.gemm == "f32" else (1, self.overflow.data_ptr())
+        """(azg.h AZG_WINO_* format of V, overflow flag pointer)."""
+        if self.gemm == "f32":
+            return 0, None
+        return (2 if self.gemm == "split" else 1), self.overflow.data_ptr()
 
     def _first_winograd(self, s):
         """conv1 + bias + ReLU + conv2's Winograd input transform straight from the NCHW
@@ -291,18 +308,29 @@ class InferenceNet(nn.Module):
             ctypes.c_void_p(self._ws[0].data_ptr()), B, self.depth, self.n, C, fmt, ctypes.c_void_p(ovf), st))
 
     def _winograd_gemms(self, i, B, C, K):
-        """M = V x U for every transformed point of layer i: one torch.bmm (hipBLASLt) per
-        run of tile groups with equal tiles per image (7x7: 3 calls, 5x5: 1, 3x3: 1)."""
-        split = self.gemm == "split"
-        W = 3 * C if split else C
-        Vflat = self._ws[0].view(torch.float16) if split else self._ws[0]
-        U = getattr(self, f"u3_{i}") if split else getattr(self, f"u{i}")
+        """M = V x U for every transformed point of layer i, by runs of tile groups with
+        equal tiles per image (7x7: 3 runs, 5x5: 1, 3x3: 1): one libazg azg_split_gemm
+        launch for all runs ("split"), or one torch.bmm (hipBLASLt) per run."""
         runs = []
         for _, _, P, n in winograd_groups(self.h_out[i]):
             if runs and runs[-1][1] == n:
                 runs[-1][0] += P
             else:
                 runs.append([P, n])
+        if self.gemm == "split":
+            import ctypes
+            from . import _lib
+            pts = (ctypes.c_int32 * len(runs))(*[P for P, _ in runs])
+            rows = (ctypes.c_int32 * len(runs))(*[B * n for _, n in runs])
+            _lib.check(_lib.lib().azg_split_gemm(
+                ctypes.c_void_p(self._ws[0].data_ptr()), ctypes.c_void_p(getattr(self, f"us_{i}").data_ptr()),
+                ctypes.c_void_p(self._ws[1].data_ptr()), len(runs), pts, rows, C, K,
+                ctypes.c_void_p(torch.cuda.current_stream(self._ws[0].device).cuda_stream)))
+            return
+        split = self.gemm == "split_blas"
+        W = 3 * C if split else C
+        Vflat = self._ws[0].view(torch.float16) if split else self._ws[0]
+        U = getattr(self, f"us_{i}") if split else getattr(self, f"u{i}")
         row = pt = 0
         for P, n in runs:
             T = B * n
@@ -340,7 +368,7 @@ class InferenceNet(nn.Module):
             self._ensure_ws(need, dev)
         elif not self._ws_fits(need):
             raise RuntimeError("Winograd workspace too small for a carried layer")
-        mscale = self.mscale[i] if self.gemm == "split" else 1.0
+        mscale = self.mscale[i] if self.gemm != "f32" else 1.0
         s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         L = _lib.lib()
         bias = ctypes.c_void_p(getattr(self, f"b{i}").data_ptr())

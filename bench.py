@@ -38,6 +38,7 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E spec peak
 EXPANSIONS_PER_GAME_REF = 8555   # reference random-init Inflexion episodes
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_G4096.json")
 PMC_FILE_WINOGRAD = {"f32": os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd.json"),
+                     "split_blas": os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd_split_blas.json"),
                      "split": os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd_split.json")}
 
 PRESETS = {
@@ -94,7 +95,8 @@ def load_pmc(G, game, impl, gemm="split"):
             return 0.0
         return d[k].get("hbm_bytes_per_forward") or d[k]["hbm_bytes_sum_over_shapes"]
     if impl == "winograd":
-        conv = tot("winograd_in") + tot("winograd_out") + tot("gemm (hipBLASLt)")
+        conv = sum(tot(k) for k in ("winograd_first", "winograd_mid", "winograd_in", "winograd_out",
+                                      "gemm (hipBLASLt)"))
         what = "Winograd transforms + the GEMM batches (and the FC GEMMs, ~2%)"
     else:
         conv = tot("conv2-4 igemm")
@@ -120,8 +122,9 @@ def parse():
     p.add_argument("--conv", default="winograd", choices=["auto", "miopen", "azg", "winograd"],
                    help="conv2-4 implementation of the inference net (MIOpen igemm + bias/ReLU pass, libazg f32-MFMA "
                         "implicit GEMM with fused epilogue, or auto: per layer, the faster one measured at first use)")
-    p.add_argument("--gemm", default="split", choices=["split", "f32"],
-                   help="Winograd GEMMs: split-fp16 (f32-accurate, 3 fp16 MFMA products) or f32 MFMA")
+    p.add_argument("--gemm", default="split", choices=["split", "split_blas", "f32"],
+                   help="Winograd GEMMs: split-fp16 (f32-accurate, 3 fp16 MFMA products) in libazg's kernel "
+                        "or hipBLASLt, or f32 MFMA")
     p.add_argument("--net", default="inference", choices=["inference", "reference"],
                    help="inference: BN-folded NHWC InferenceNet; reference: InflexionNNet as written")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -332,7 +335,7 @@ def main():
             for i in (2, 3, 4):
                 impls[i] = (next((v for (li, _), v in ev._choices.items() if li == i), "miopen")
                             if ev.conv_impl == "auto" else ev.conv_impl)
-        split = impl == "winograd" and getattr(ev, "gemm", "f32") == "split"
+        split = impl == "winograd" and getattr(ev, "gemm", "f32") in ("split", "split_blas")
 
         def name(i, m):
             if m == "miopen":
@@ -340,8 +343,9 @@ def main():
             if m == "azg":
                 return "libazg f32-MFMA implicit GEMM (LDS-DMA ring) + fused bias/ReLU"
             from azg_amd.nnet import winograd_points, winograd_seq
-            g = ("split-fp16 GEMMs (3 fp16 MFMA products, f32 accumulate; hipBLASLt)" if split
-                 else "f32 GEMMs (hipBLASLt)")
+            g = {"split": "split-fp16 GEMMs (3 fp16 MFMA products, f32 accumulate; libazg azg_split_gemm)",
+                 "split_blas": "split-fp16 GEMMs (3 fp16 MFMA products, f32 accumulate; hipBLASLt)",
+                 "f32": "f32 GEMMs (hipBLASLt)"}[ev.gemm]
             seq = "+".join(map(str, winograd_seq(ev.h_out[i])))
             return (f"Winograd {seq} tiles per axis (F(3,3)/F(2,3)): libazg fused transforms + "
                     f"{winograd_points(ev.h_out[i])}-point {g}")

@@ -154,12 +154,13 @@ int  azg_conv3x3_variant(int variant, const float* x, const float* wt, const flo
  *                          (times mscale^-1, a power of two, for split V);
  *   azg_winograd_out_nhwc: M f32 (rows of k) -> y NHWC [batch, h_out, h_out, k] =
  *                          A^T (mscale M) A + bias, ReLU if relu != 0.
- * V formats: AZG_WINO_F32 f32 rows of c; AZG_WINO_SPLIT fp16 rows of 3c =
+ * V formats: AZG_WINO_F32 f32 rows of c; AZG_WINO_SPLIT2 fp16 rows of 2c = [hi | lo]
+ * (the A operand of azg_split_gemm); AZG_WINO_SPLIT fp16 rows of 3c =
  * [hi | lo | hi], hi = fp16(v), lo = fp16(v - hi) -- the A operand of the
  * error-compensated GEMM [hi|lo|hi] x [Uh; Uh; Ul] (f32 accumulation); a value
  * fp16 cannot hold (|v| > 65504, NaN) sets *overflow (device int, required).
  * c % 4 == 0, k % 4 == 0, 16-B aligned pointers, h_out <= 64. */
-enum { AZG_WINO_F32 = 0, AZG_WINO_SPLIT = 1 };
+enum { AZG_WINO_F32 = 0, AZG_WINO_SPLIT = 1, AZG_WINO_SPLIT2 = 2 };
 int  azg_winograd_layout(int32_t h_out, int32_t* seq, int32_t* groups);
 int  azg_winograd_in_nhwc(const float* x, const float* in_bias, void* V, int32_t batch, int32_t h_in, int32_t pad,
                           int32_t c, int32_t vfmt, int32_t* overflow, void* stream);
@@ -177,6 +178,15 @@ int  azg_winograd_mid_nhwc(const float* M, const float* bias, void* V, int32_t b
  * depth <= 4, 3 <= n <= 9, c % 64 == 0. */
 int  azg_winograd_first_nchw(const float* planes, const float* w1, const float* b1, void* V, int32_t batch,
                              int32_t depth, int32_t n, int32_t c, int32_t vfmt, int32_t* overflow, void* stream);
+/* The Winograd GEMMs of one layer as an error-compensated fp16 MFMA GEMM
+ * (azg_split_gemm.hip): for every point e of nruns runs (run r: points[r]
+ * points with rows[r] rows each, stored one after another),
+ *   M_e [rows x k] f32 = A_e x B_e^T,  A_e [rows][2c] fp16 rows [hi | lo] (V in
+ *   AZG_WINO_SPLIT2), B_e [k][2c] fp16 rows [hi | lo] (U^T, points of all runs in
+ *   order), computed as hi.hi + lo.hi + hi.lo with f32 accumulation.
+ * c % 32 == 0, k % 256 == 0, nruns <= 4, 16-B aligned pointers. */
+int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, const int32_t* points,
+                    const int32_t* rows, int32_t c, int32_t k, void* stream);
 
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active

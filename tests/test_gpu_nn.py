@@ -20,7 +20,7 @@ def test_bias_relu_kernel():
 
 
 @pytest.mark.parametrize("conv,gemm", [("miopen", "split"), ("azg", "split"), ("auto", "split"),
-                                       ("winograd", "split"), ("winograd", "f32")])
+                                       ("winograd", "split"), ("winograd", "split_blas"), ("winograd", "f32")])
 def test_inference_net_vs_reference_gpu(conv, gemm):
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
@@ -96,7 +96,7 @@ def test_azg_conv3x3_variants(variant, B, H, pad):
     torch.testing.assert_close(y, want, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("gemm", ["split", "f32"])
+@pytest.mark.parametrize("gemm", ["split", "split_blas", "f32"])
 @pytest.mark.parametrize("B,H,pad", [(1, 7, 1), (37, 7, 1), (300, 7, 0), (129, 5, 0), (64, 8, 1), (5, 6, 0),
                                      (3, 4, 1), (7, 9, 1), (2, 11, 0), (3, 3, 1)])
 def test_winograd_conv3x3_matches_torch(B, H, pad, gemm):
@@ -120,7 +120,7 @@ def test_winograd_conv3x3_matches_torch(B, H, pad, gemm):
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("gemm", ["split", "f32"])
+@pytest.mark.parametrize("gemm", ["split", "split_blas", "f32"])
 def test_winograd_fused_transforms_match_unfused(gemm):
     """The fused front end (conv1 + conv2's input transform) and the fused
     output/next-input transforms (default) vs MIOpen conv1 and separate
@@ -139,7 +139,7 @@ def test_winograd_fused_transforms_match_unfused(gemm):
     torch.testing.assert_close(va, vb, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("gemm", ["split", "f32"])
+@pytest.mark.parametrize("gemm", ["split", "split_blas", "f32"])
 @pytest.mark.parametrize("n,depth,A", [(7, 4, 343), (6, 2, 37), (8, 2, 65), (5, 4, 175), (9, 2, 82)])
 def test_inference_net_board_sizes(n, depth, A, gemm):
     """The inference form (fused front end, fused Winograd transforms; register
@@ -187,8 +187,42 @@ def test_split_gemm_error_not_above_f32():
         logp, v64 = ref(x.double())
         p64 = torch.exp(logp)
         errs = {}
-        for gemm in ("split", "f32"):
+        for gemm in ("split", "split_blas", "f32"):
             p, v = InferenceNet(net, gemm=gemm).cuda()(x)
             errs[gemm] = ((p.double() - p64).abs() / p64).max().item()
-    assert errs["split"] < 1e-5, errs
+    assert errs["split"] < 1e-5 and errs["split_blas"] < 1e-5, errs
     assert errs["split"] <= 1.5 * errs["f32"], errs
+    assert errs["split_blas"] <= 1.5 * errs["f32"], errs
+
+
+@pytest.mark.parametrize("runs", [[(25, 4096)], [(3, 300), (5, 37), (2, 513)], [(1, 1)]])
+def test_split_gemm_kernel_matches_reference(runs):
+    """libazg azg_split_gemm (hand-written fp16 MFMA, LDS-DMA): M = Ah.Bh + Al.Bh + Ah.Bl
+    for every point of every run, against the same products in f64 (ragged row counts)."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    torch.manual_seed(7)
+    C, K = 512, 512
+    P = sum(p for p, _ in runs)
+    A = torch.cat([torch.randn(p * t, 2 * C, device="cuda").half() for p, t in runs]).contiguous()
+    Bt = torch.randn(P, K, 2 * C, device="cuda").half()
+    M = torch.full((sum(p * t for p, t in runs) * K,), float("nan"), device="cuda")
+    pts = (ctypes.c_int32 * len(runs))(*[p for p, _ in runs])
+    rows = (ctypes.c_int32 * len(runs))(*[t for _, t in runs])
+    _lib.check(_lib.lib().azg_split_gemm(ctypes.c_void_p(A.data_ptr()), ctypes.c_void_p(Bt.data_ptr()),
+                                         ctypes.c_void_p(M.data_ptr()), len(runs), pts, rows, C, K,
+                                         ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    a_row = m_row = pt = 0
+    for p, t in runs:
+        a = A[a_row:a_row + p * t].view(p, t, 2 * C).double()
+        b = Bt[pt:pt + p].double()
+        ah, al, bh, bl = a[..., :C], a[..., C:], b[..., :C], b[..., C:]
+        want = ah @ bh.transpose(1, 2) + al @ bh.transpose(1, 2) + ah @ bl.transpose(1, 2)
+        got = M[m_row * K:(m_row + p * t) * K].view(p, t, K).double()
+        scale = want.abs().max().item()
+        assert (got - want).abs().max().item() <= 2e-6 * scale, (p, t)
+        a_row += p * t
+        m_row += p * t
+        pt += p

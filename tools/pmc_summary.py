@@ -41,6 +41,10 @@ def group(name):
         return "move_end_kernel"
     if "bias_relu" in name:
         return "bias_relu_nhwc"
+    if "winograd_first" in name:
+        return "winograd_first"
+    if "winograd_mid" in name:
+        return "winograd_mid"
     if "winograd_in" in name:
         return "winograd_in"
     if "winograd_out" in name:
