@@ -14,20 +14,28 @@
 //
 // Tiling: 256 x 256 output tile per 512-thread workgroup (8 waves as 2 (rows) x 4
 // (cols), 128 x 64 per wave = 8 x 4 accumulators of 16 x 16), 32 channels per
-// K stage.  Both operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4,
+// K stage.  Both operands go global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds,
 // 1 KB per wave-instruction) into two stage buffers of 64 KB; an LDS row is one
 // tile row's 32 channels: hi (4 x 16 B) then lo (4 x 16 B), 16-B chunk c stored at
 // c ^ ((row >> 1) & 7), so each 16-lane group of a ds_read_b128 (16 rows, one
-// chunk) covers all 16 slots of the 256-B bank row (conflict-free).  Per stage a
-// wave reads its operands (16 A + 8 B ds_read_b128), issues the next stage's DMA
-// (8 per wave), then runs 96 MFMAs; a vmcnt(0) + barrier closes the stage, so the
-// DMA lands under the MFMAs and the reads never wait on a DMA in flight.
+// chunk) covers all 16 slots of the 256-B bank row (conflict-free).  A stage is
+// 16 A + 8 B ds_read_b128 and 96 MFMAs per wave plus 8 DMA issues; variant 0
+// (default) runs them in that order with a vmcnt(0) + barrier per stage, variant 1
+// overlaps each phase's reads with the previous phase's MFMAs, variant 2 runs one
+// wave per SIMD on 128 x 128 per wave (below).  Measured on conv2's shape
+// (tools/split_gemm_bench.py, profiles/r01_split_gemm_*.json): variant 0 975-1006
+// TF/s of fp16 MFMA work, variant 1 912-945, variant 2 922; hipBLASLt on the
+// [hi|lo|hi] form 825-845.  PMC (tools/split_gemm_pmc.py): no LDS bank conflicts,
+// A read from HBM once (L2 hit rate 78%), MFMA busy ~49% (variant 0): the rest is
+// the per-stage barrier / DMA wait and the LDS-DMA issue cost.
 //
 // The tiles of all GEMMs of a layer (runs of points with equal T) are one grid;
 // block ids are dealt to the 8 XCDs round-robin, so the mapping gives each XCD a
 // contiguous range of tiles: a row tile's two column tiles run side by side on
 // one XCD and share its A tile through that L2.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "../../include/azg.h"
 
@@ -52,6 +60,20 @@ struct SGArgs {
     long long a_off[SG_MAXRUNS], m_off[SG_MAXRUNS];
 };
 
+// B tile row R of the LDS image (column block j = (R % 64) / 16, lane lr = R % 16 of
+// a wave's 64 columns) holds output column 64 (R / 64) + 4 lr + j: lane lr's four
+// column blocks are then four adjacent columns, stored as one 16-B write per row in
+// the epilogue.  LDS rows R and R + 16 (j, j + 1) are adjacent columns, so the B
+// DMA's second descriptor starts one row on.
+__device__ __forceinline__ int b_col(int R) { return (R & ~63) | ((R & 15) << 2) | ((R >> 4) & 3); }
+
+// byte address of a __shared__ location in the workgroup's LDS (operand of ds_* asm)
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// Variant 0: per stage, all operand reads, then the next stage's DMA, then 96 MFMAs,
+// then vmcnt(0) + barrier (reads and MFMAs of a wave do not overlap).
 __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * SG_STAGEB];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -77,30 +99,39 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
     // DMA sources: wave w fills tile rows 32w + 8i + lane/8 (i < 4) of A and of B;
     // lane%8 is the physical 16-B chunk, holding logical chunk lc = phys ^ ((row>>1)&7):
     // hi channels 8lc.. (lc < 4) or lo channels 8(lc-4).. of the stage
-    const _Float16* asrc[4];
-    const _Float16* bsrc[4];
+    // DMA by buffer_load ... lds: two descriptors per operand (SGPRs), the second
+    // based 16 rows further on with 16 rows fewer in range, serve row groups i < 2
+    // and i >= 2 with the same two lane offsets (the chunk swizzle differs between
+    // even and odd i); the wave-uniform soffset is the stage's column (inside the
+    // row), so the range check decides on the row alone: A rows past T load as
+    // zeros (never stored), nothing past the operand is read
+    const auto ar0 = __builtin_amdgcn_make_buffer_rsrc((void*)Ae, 0, T * C2 * 2, 0x00020000);
+    const auto ar1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Ae + 16 * C2), 0, (T > 16 ? T - 16 : 0) * C2 * 2,
+                                                       0x00020000);
+    const auto br0 = __builtin_amdgcn_make_buffer_rsrc((void*)Be, 0, K * C2 * 2, 0x00020000);
+    const auto br1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Be + C2), 0, (K - 1) * C2 * 2, 0x00020000);
+    int aoff[2], boff[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 2; ++i) {
         const int R = 32 * wid + 8 * i + (lane >> 3);
         const int lc = (lane & 7) ^ ((R >> 1) & 7);
         const int col = lc < 4 ? 8 * lc : C + 8 * (lc - 4);
-        const int arow = m0 + R < T ? m0 + R : T - 1;  // rows past T: loaded, never stored
-        asrc[i] = Ae + (long long)arow * C2 + col;
-        bsrc[i] = Be + (long long)(n0 + R) * C2 + col;
+        aoff[i] = ((m0 + R) * C2 + col) * 2;
+        boff[i] = ((n0 + b_col(R)) * C2 + col) * 2;
     }
     auto issue = [&](int ks, int buf) {
         char* base = smem + buf * SG_STAGEB + (32 * wid) * SG_ROWB;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + ks * SG_BK),
-                                             (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB), 16, 0,
-                                             0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
+                                                     (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
+                                                     16, aoff[i & 1], ks * SG_BK * 2, 0, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + ks * SG_BK),
-                                             (__attribute__((address_space(3))) void*)(base + SG_TILEB +
-                                                                                      8 * i * SG_ROWB),
-                                             16, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
+                                                     (__attribute__((address_space(3))) void*)(base + SG_TILEB +
+                                                                                              8 * i * SG_ROWB),
+                                                     16, boff[i & 1], ks * SG_BK * 2, 0, 0);
     };
 
     // operand reads: wave (wm, wn) = rows 128 wm.., cols 64 wn..; lane holds row lane%16
@@ -151,26 +182,509 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
         __syncthreads();
     }
 
-    // epilogue: C/D map of 16x16x32: col = lane % 16, row = 4 (lane / 16) + reg
+    // epilogue: C/D map of 16x16x32: col = lane % 16, row = 4 (lane / 16) + reg; the
+    // lane's four column blocks are adjacent columns (b_col): one 16-B store per row
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int row = m0 + wm * 128 + 16 * i + 4 * ch + q;
             if (row >= T) continue;
-            float* out = Me + (long long)row * K + n0 + wn * 64 + lr;
+            *(f32x4*)(Me + (long long)row * K + n0 + wn * 64 + 4 * lr) =
+                f32x4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Variant 1: the stage's 96 MFMAs in 4 phases of 2 row blocks (24 MFMAs);
+// each phase's ds_reads (the next phase's A fragments; in phase 3 the next stage's
+// B fragments and phase-0 A) are issued before its MFMAs and land under them, so a
+// wave's MFMAs never wait for a whole stage of reads.  The reads are inline asm:
+// hipcc counts no LDS-DMA alias scopes and would otherwise drain vmcnt (the next
+// stage's DMA, in flight) before every ds_read.  Each read is waited for by an
+// explicit lgkmcnt(0) naming its destinations ("+v") at the start of the phase
+// that consumes it.  One barrier per stage, after phase 2: this wave's reads of
+// the stage buffer are complete (lgkmcnt) and the next stage's DMA has landed
+// (vmcnt(0): nothing else is outstanding), so in phase 3 every wave may read the
+// next buffer and refill this one (stage s+2).  B fragments alternate between two
+// register sets by stage parity (loop unrolled by 2), A fragments between two sets
+// by phase parity: no register copies.
+template <unsigned V>
+struct UC {
+    static constexpr unsigned value = V;
+};
+struct Frag2 {
+    f16x8 h[2], l[2];
+};
+struct Frag4 {
+    f16x8 h[4], l[4];
+};
+
+// A fragments of phase P (row blocks 2P, 2P+1): hi and lo, 4 ds_read_b128; OFF is
+// the stage buffer's byte offset, folded into the instruction's 16-bit offset
+template <int P, unsigned OFF>
+__device__ __forceinline__ void read_a(Frag2& a, unsigned hi, unsigned lo) {
+    asm volatile(
+        "ds_read_b128 %0, %4 offset:%c6\n\t"
+        "ds_read_b128 %1, %4 offset:%c7\n\t"
+        "ds_read_b128 %2, %5 offset:%c6\n\t"
+        "ds_read_b128 %3, %5 offset:%c7"
+        : "=v"(a.h[0]), "=v"(a.h[1]), "=v"(a.l[0]), "=v"(a.l[1])
+        : "v"(hi), "v"(lo), "i"(OFF + P * 2 * 16 * SG_ROWB), "i"(OFF + (P * 2 + 1) * 16 * SG_ROWB));
+}
+// B fragments of column block J: hi and lo, 2 ds_read_b128
+template <int J, unsigned OFF>
+__device__ __forceinline__ void read_b(Frag4& b, unsigned hi, unsigned lo) {
+    asm volatile(
+        "ds_read_b128 %0, %2 offset:%c4\n\t"
+        "ds_read_b128 %1, %3 offset:%c4"
+        : "=v"(b.h[J]), "=v"(b.l[J])
+        : "v"(hi), "v"(lo), "i"(OFF + J * 16 * SG_ROWB));
+}
+__device__ __forceinline__ void wait_a(Frag2& a) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a.h[0]), "+v"(a.h[1]), "+v"(a.l[0]), "+v"(a.l[1]));
+}
+__device__ __forceinline__ void wait_ab(Frag2& a, Frag4& b) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(a.h[0]), "+v"(a.h[1]), "+v"(a.l[0]), "+v"(a.l[1]), "+v"(b.h[0]), "+v"(b.h[1]),
+                   "+v"(b.h[2]), "+v"(b.h[3]), "+v"(b.l[0]), "+v"(b.l[1]), "+v"(b.l[2]), "+v"(b.l[3]));
+}
+// 24 MFMAs of row blocks I0, I0+1: hi.hi, lo.hi, hi.lo per accumulator, the three
+// products of one accumulator 8 MFMAs apart
+template <int I0>
+__device__ __forceinline__ void mma_phase(f32x4 (&acc)[8][4], const Frag2& a, const Frag4& b) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) out[16 * j] = acc[i][j][q];
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[I0 + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[ii], b.h[j], acc[I0 + ii][j], 0, 0, 0);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[I0 + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.l[ii], b.h[j], acc[I0 + ii][j], 0, 0, 0);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[I0 + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[ii], b.l[j], acc[I0 + ii][j], 0, 0, 0);
+}
+// The 6 MFMAs of row blocks I0, I0+1 with column block J (phase 3 retires the B
+// fragments one column block at a time so the next stage's reuse their registers)
+template <int I0, int J>
+__device__ __forceinline__ void mma_col(f32x4 (&acc)[8][4], const Frag2& a, const Frag4& b) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) acc[I0 + ii][J] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[ii], b.h[J], acc[I0 + ii][J], 0, 0, 0);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) acc[I0 + ii][J] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.l[ii], b.h[J], acc[I0 + ii][J], 0, 0, 0);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) acc[I0 + ii][J] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[ii], b.l[J], acc[I0 + ii][J], 0, 0, 0);
+}
+
+__global__ __launch_bounds__(512, 1) void split_gemm_pipe_kernel(SGArgs g) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * SG_STAGEB];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    int L;
+    {
+        const int bid = blockIdx.x, xcd = bid % 8, q = g.total / 8, rr = g.total % 8;
+        L = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+    }
+    int r = 0;
+    while (r + 1 < g.nruns && L >= g.tile0[r + 1]) ++r;
+    const int u = L - g.tile0[r];
+    const int nt = u % g.ntn;
+    const int mt = (u / g.ntn) % g.mtiles[r];
+    const int e = u / (g.ntn * g.mtiles[r]);
+    const int T = g.rows[r], C = g.C, K = g.K, C2 = 2 * C;
+    const int m0 = mt * SG_BM, n0 = nt * SG_BN;
+    const _Float16* Ae = g.A + g.a_off[r] + (long long)e * T * C2;
+    const _Float16* Be = g.Bt + (long long)(g.b_pt0[r] + e) * K * C2;
+    float* Me = g.M + g.m_off[r] + (long long)e * T * K;
+
+    // DMA by buffer_load ... lds: two descriptors per operand (SGPRs), the second
+    // based 16 rows further on with 16 rows fewer in range, serve row groups i < 2
+    // and i >= 2 with the same two lane offsets (the chunk swizzle differs between
+    // even and odd i); the wave-uniform soffset is the stage's column (inside the
+    // row), so the range check decides on the row alone: A rows past T load as
+    // zeros (never stored), nothing past the operand is read
+    const auto ar0 = __builtin_amdgcn_make_buffer_rsrc((void*)Ae, 0, T * C2 * 2, 0x00020000);
+    const auto ar1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Ae + 16 * C2), 0, (T > 16 ? T - 16 : 0) * C2 * 2,
+                                                       0x00020000);
+    const auto br0 = __builtin_amdgcn_make_buffer_rsrc((void*)Be, 0, K * C2 * 2, 0x00020000);
+    const auto br1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Be + C2), 0, (K - 1) * C2 * 2, 0x00020000);
+    int aoff[2], boff[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int R = 32 * wid + 8 * i + (lane >> 3);
+        const int lc = (lane & 7) ^ ((R >> 1) & 7);
+        const int col = lc < 4 ? 8 * lc : C + 8 * (lc - 4);
+        aoff[i] = ((m0 + R) * C2 + col) * 2;
+        boff[i] = ((n0 + b_col(R)) * C2 + col) * 2;
+    }
+    // LDS: [A stage 0 | A stage 1 | B stage 0 | B stage 1], 32 KB each, so every
+    // operand read is one of four base registers plus an immediate offset
+    auto issue = [&](int ks, int buf) {
+        char* base = smem + buf * SG_TILEB + (32 * wid) * SG_ROWB;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
+                                                     (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
+                                                     16, aoff[i & 1], ks * SG_BK * 2, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
+                                                     (__attribute__((address_space(3))) void*)(base + 2 * SG_TILEB +
+                                                                                              8 * i * SG_ROWB),
+                                                     16, boff[i & 1], ks * SG_BK * 2, 0, 0);
+    };
+
+    const int wm = wid >> 2, wn = wid & 3;
+    const int lr = lane & 15, sw = lr >> 1, ch = lane >> 4;
+    const unsigned s0 = lds_addr(smem);
+    const unsigned a_hi = s0 + (wm * 128 + lr) * SG_ROWB + 16 * (ch ^ sw);
+    const unsigned a_lo = s0 + (wm * 128 + lr) * SG_ROWB + 16 * ((4 + ch) ^ sw);
+    const unsigned b_hi = s0 + 2 * SG_TILEB + (wn * 64 + lr) * SG_ROWB + 16 * (ch ^ sw);
+    const unsigned b_lo = s0 + 2 * SG_TILEB + (wn * 64 + lr) * SG_ROWB + 16 * ((4 + ch) ^ sw);
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nks = C / SG_BK;  // even (C % 64 == 0)
+    Frag2 ax, ay;
+    Frag4 b;
+    issue(0, 0);
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage 0 landed (this wave)
+    __builtin_amdgcn_s_barrier();
+    read_b<0, 0>(b, b_hi, b_lo);
+    read_b<1, 0>(b, b_hi, b_lo);
+    read_b<2, 0>(b, b_hi, b_lo);
+    read_b<3, 0>(b, b_hi, b_lo);
+    read_a<0, 0>(ax, a_hi, a_lo);
+
+    // one stage, its buffer at byte offset CO (of the A and of the B region), the
+    // next stage's at NO
+    auto stage = [&](int ks, auto co_t) {
+        constexpr unsigned CO = decltype(co_t)::value, NO = SG_TILEB - CO;
+        wait_ab(ax, b);
+        read_a<1, CO>(ay, a_hi, a_lo);
+        mma_phase<0>(acc, ax, b);
+        __builtin_amdgcn_sched_barrier(0);
+        wait_a(ay);
+        read_a<2, CO>(ax, a_hi, a_lo);
+        mma_phase<2>(acc, ay, b);
+        __builtin_amdgcn_sched_barrier(0);
+        wait_a(ax);
+        read_a<3, CO>(ay, a_hi, a_lo);
+        mma_phase<4>(acc, ax, b);
+        __builtin_amdgcn_sched_barrier(0);
+        wait_a(ay);  // this wave's reads of the stage buffer are done
+        if (ks + 1 < nks) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage ks+1 landed (this wave)
+            __builtin_amdgcn_s_barrier();                     // ... for every wave; buffer CO free
+            if (ks + 2 < nks) issue(ks + 2, ks & 1);
+            read_a<0, NO>(ax, a_hi, a_lo);
+            mma_col<6, 0>(acc, ay, b);
+            __builtin_amdgcn_sched_barrier(0);
+            read_b<0, NO>(b, b_hi, b_lo);
+            mma_col<6, 1>(acc, ay, b);
+            __builtin_amdgcn_sched_barrier(0);
+            read_b<1, NO>(b, b_hi, b_lo);
+            mma_col<6, 2>(acc, ay, b);
+            __builtin_amdgcn_sched_barrier(0);
+            read_b<2, NO>(b, b_hi, b_lo);
+            mma_col<6, 3>(acc, ay, b);
+            __builtin_amdgcn_sched_barrier(0);
+            read_b<3, NO>(b, b_hi, b_lo);
+        } else {
+            mma_phase<6>(acc, ay, b);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    for (int ks = 0; ks < nks; ks += 2) {
+        stage(ks, UC<0>{});
+        stage(ks + 1, UC<SG_TILEB>{});
+    }
+
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = m0 + wm * 128 + 16 * i + 4 * ch + q;
+            if (row >= T) continue;
+            *(f32x4*)(Me + (long long)row * K + n0 + wn * 64 + 4 * lr) =
+                f32x4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Variant 2: one wave per SIMD (4 waves, 2 x 2, 128 x 128 per wave = 8 x 8
+// accumulators of 16 x 16, 256 accumulator registers held in AGPRs).  Against the
+// 8-wave variants each A element is read from LDS by 2 waves instead of 4: 128 KB
+// of ds_read per stage instead of 192 KB for the same 256 x 256 x 32 work.  A wave
+// keeps the stage's 8 B fragments (hi, lo) in registers and streams its 8 A
+// fragments through a 4-slot ring, two row blocks ahead.  One barrier per stage,
+// at row block 6: the wave's reads of the stage buffer have all landed (A[7] was
+// issued at row block 5) and the next stage's DMA has landed (vmcnt(0)); after it
+// the stage buffer is refilled (stage + 2) and row blocks 6 and 7 run column block
+// by column block, each column block's B fragments replaced by the next stage's
+// as soon as its 6 MFMAs are issued.  Operand reads are inline-asm ds_read_b128 with explicit lgkmcnt waits
+// (as variant 1); LDS is [A stage 0 | A stage 1 | B stage 0 | B stage 1].
+constexpr int W4_ROWB = SG_ROWB;
+constexpr int W4_TILEB = SG_TILEB;
+
+// wave column tile of 128: LDS row R (block j = (R % 128) / 16, lane lr = R % 16)
+// holds output column 128 (R / 128) + 8 lr + j, so a lane's 8 column blocks are 8
+// adjacent columns (two 16-B stores per row in the epilogue)
+__device__ __forceinline__ int b_col128(int R) { return (R & ~127) | ((R & 15) << 3) | ((R >> 4) & 7); }
+
+struct FragA {
+    f16x8 h, l;
+};
+struct FragB8 {
+    f16x8 h[8], l[8];
+};
+
+template <unsigned OFF>
+__device__ __forceinline__ void w4_read_a(FragA& a, unsigned hi, unsigned lo) {
+    asm volatile(
+        "ds_read_b128 %0, %2 offset:%c4\n\t"
+        "ds_read_b128 %1, %3 offset:%c4"
+        : "=v"(a.h), "=v"(a.l)
+        : "v"(hi), "v"(lo), "i"(OFF));
+}
+// B fragments of column block J (hi, lo)
+template <int J, unsigned OFF>
+__device__ __forceinline__ void w4_read_b(FragB8& b, unsigned hi, unsigned lo) {
+    asm volatile(
+        "ds_read_b128 %0, %2 offset:%c4\n\t"
+        "ds_read_b128 %1, %3 offset:%c4"
+        : "=v"(b.h[J]), "=v"(b.l[J])
+        : "v"(hi), "v"(lo), "i"(OFF + J * 16 * W4_ROWB));
+}
+// s_waitcnt lgkmcnt(N) that the compiler sees as defining the awaited registers
+template <int N>
+__device__ __forceinline__ void w4_wait(FragA& a) {
+    asm volatile("s_waitcnt lgkmcnt(%c2)" : "+v"(a.h), "+v"(a.l) : "i"(N));
+}
+template <int N>
+__device__ __forceinline__ void w4_wait(FragA& a, FragB8& b) {
+    asm volatile("s_waitcnt lgkmcnt(%c18)"
+                 : "+v"(a.h), "+v"(a.l), "+v"(b.h[0]), "+v"(b.l[0]), "+v"(b.h[1]), "+v"(b.l[1]), "+v"(b.h[2]),
+                   "+v"(b.l[2]), "+v"(b.h[3]), "+v"(b.l[3]), "+v"(b.h[4]), "+v"(b.l[4]), "+v"(b.h[5]), "+v"(b.l[5]),
+                   "+v"(b.h[6]), "+v"(b.l[6]), "+v"(b.h[7]), "+v"(b.l[7])
+                 : "i"(N));
+}
+// One MFMA accumulating in place in AGPRs ("+a"): left to itself, hipcc keeps
+// part of the 256 accumulators in VGPRs and shuffles them between the register
+// files every stage.  MFMA-to-MFMA accumulator chains are interlocked in hardware;
+// the epilogue waits out the last results (s_nop) before reading them.
+__device__ __forceinline__ void w4_mfma(f32x4& c, const f16x8& a, const f16x8& b) {
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+// the 24 MFMAs of row block I: hi.hi, lo.hi, hi.lo for the 8 column blocks
+template <int I>
+__device__ __forceinline__ void w4_mma(f32x4 (&acc)[8][8], const FragA& a, const FragB8& b) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w4_mfma(acc[I][j], a.h, b.h[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w4_mfma(acc[I][j], a.l, b.h[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w4_mfma(acc[I][j], a.h, b.l[j]);
+}
+// the 6 MFMAs of row blocks 6, 7 with column block J (the stage's last two row
+// blocks retire the B fragments one column block at a time, so the next stage's
+// are read into the same registers)
+template <int J>
+__device__ __forceinline__ void w4_mma_col(f32x4 (&acc)[8][8], const FragA& a6, const FragA& a7, const FragB8& b) {
+    w4_mfma(acc[6][J], a6.h, b.h[J]);
+    w4_mfma(acc[7][J], a7.h, b.h[J]);
+    w4_mfma(acc[6][J], a6.l, b.h[J]);
+    w4_mfma(acc[7][J], a7.l, b.h[J]);
+    w4_mfma(acc[6][J], a6.h, b.l[J]);
+    w4_mfma(acc[7][J], a7.h, b.l[J]);
+}
+
+__global__ __launch_bounds__(256, 1) void split_gemm_w4_kernel(SGArgs g) {
+    __shared__ __attribute__((aligned(16))) char smem[4 * W4_TILEB];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    int L;
+    {
+        const int bid = blockIdx.x, xcd = bid % 8, q = g.total / 8, rr = g.total % 8;
+        L = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+    }
+    int r = 0;
+    while (r + 1 < g.nruns && L >= g.tile0[r + 1]) ++r;
+    const int u = L - g.tile0[r];
+    const int nt = u % g.ntn;
+    const int mt = (u / g.ntn) % g.mtiles[r];
+    const int e = u / (g.ntn * g.mtiles[r]);
+    const int T = g.rows[r], C = g.C, K = g.K, C2 = 2 * C;
+    const int m0 = mt * SG_BM, n0 = nt * SG_BN;
+    const _Float16* Ae = g.A + g.a_off[r] + (long long)e * T * C2;
+    const _Float16* Be = g.Bt + (long long)(g.b_pt0[r] + e) * K * C2;
+    float* Me = g.M + g.m_off[r] + (long long)e * T * K;
+
+    // DMA: wave w fills LDS rows 64 w + 8 i + lane / 8 (i < 8) of A and of B.  Row
+    // groups 2d and 2d + 1 share descriptor d (based 16 rows on for A, one column
+    // row on for B: b_col128), with one lane offset for even and one for odd i;
+    // the soffset is the stage's column, so the range check decides on the row
+    const auto mk = [&](const _Float16* base, int nrows) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (nrows > 0 ? nrows : 0) * C2 * 2, 0x00020000);
+    };
+    const auto ar0 = mk(Ae, T), ar1 = mk(Ae + 16 * C2, T - 16), ar2 = mk(Ae + 32 * C2, T - 32),
+               ar3 = mk(Ae + 48 * C2, T - 48);
+    const auto br0 = mk(Be, K), br1 = mk(Be + C2, K - 1), br2 = mk(Be + 2 * C2, K - 2), br3 = mk(Be + 3 * C2, K - 3);
+    int aoff[2], boff[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int R = 64 * wid + 8 * i + (lane >> 3);
+        const int lc = (lane & 7) ^ ((R >> 1) & 7);
+        const int col = lc < 4 ? 8 * lc : C + 8 * (lc - 4);
+        aoff[i] = ((m0 + R) * C2 + col) * 2;
+        boff[i] = ((n0 + b_col128(R)) * C2 + col) * 2;
+    }
+    auto issue = [&](int ks, int buf) {
+        char* abase = smem + buf * W4_TILEB + (64 * wid) * W4_ROWB;
+        char* bbase = abase + 2 * W4_TILEB;
+        const int so = ks * SG_BK * 2;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const auto rs = i < 2 ? ar0 : i < 4 ? ar1 : i < 6 ? ar2 : ar3;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(abase + 8 * i * W4_ROWB),
+                                                     16, aoff[i & 1], so, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const auto rs = i < 2 ? br0 : i < 4 ? br1 : i < 6 ? br2 : br3;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(bbase + 8 * i * W4_ROWB),
+                                                     16, boff[i & 1], so, 0, 0);
+        }
+    };
+
+    // operand reads: wave (wm, wn) = rows 128 wm.., cols 128 wn..; lane holds row (col)
+    // lane % 16 of a 16-block, channels 8 (lane / 16).. of hi and of lo
+    const int wm = wid >> 1, wn = wid & 1;
+    const int lr = lane & 15, sw = lr >> 1, ch = lane >> 4;
+    const unsigned s0 = lds_addr(smem);
+    const unsigned a_hi = s0 + (wm * 128 + lr) * W4_ROWB + 16 * (ch ^ sw);
+    const unsigned a_lo = s0 + (wm * 128 + lr) * W4_ROWB + 16 * ((4 + ch) ^ sw);
+    const unsigned b_hi = s0 + 2 * W4_TILEB + (wn * 128 + lr) * W4_ROWB + 16 * (ch ^ sw);
+    const unsigned b_lo = s0 + 2 * W4_TILEB + (wn * 128 + lr) * W4_ROWB + 16 * ((4 + ch) ^ sw);
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nks = C / SG_BK;  // even (C % 64 == 0)
+    FragA a[4];
+    FragB8 b;
+    constexpr unsigned RB = 16 * W4_ROWB;  // bytes per 16-row block
+    issue(0, 0);
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // stage 0 landed (this wave)
+    __builtin_amdgcn_s_barrier();
+    // read order of a stage's first fragments: A[0], B[0..7], A[1]
+    w4_read_a<0>(a[0], a_hi, a_lo);
+    w4_read_b<0, 0>(b, b_hi, b_lo);
+    w4_read_b<1, 0>(b, b_hi, b_lo);
+    w4_read_b<2, 0>(b, b_hi, b_lo);
+    w4_read_b<3, 0>(b, b_hi, b_lo);
+    w4_read_b<4, 0>(b, b_hi, b_lo);
+    w4_read_b<5, 0>(b, b_hi, b_lo);
+    w4_read_b<6, 0>(b, b_hi, b_lo);
+    w4_read_b<7, 0>(b, b_hi, b_lo);
+    w4_read_a<RB>(a[1], a_hi, a_lo);
+
+    // one stage, its buffer at byte offset CO of the A and of the B region; the last
+    // stage (LAST) reads nothing further.  Straight-line per stage (no register
+    // phis), the loop unrolled by 2 for the buffer parity, the last 2 stages peeled
+    auto stage = [&](int ks, auto co_t, auto last_t) {
+        constexpr unsigned CO = decltype(co_t)::value, NO = W4_TILEB - CO;
+        constexpr bool LAST = decltype(last_t)::value;
+        w4_wait<2>(a[0], b);  // B and A[0] landed (A[1] may be in flight)
+        w4_read_a<CO + 2 * RB>(a[2], a_hi, a_lo);
+        w4_mma<0>(acc, a[0], b);
+        w4_wait<2>(a[1]);
+        w4_read_a<CO + 3 * RB>(a[3], a_hi, a_lo);
+        w4_mma<1>(acc, a[1], b);
+        w4_wait<2>(a[2]);
+        w4_read_a<CO + 4 * RB>(a[0], a_hi, a_lo);
+        w4_mma<2>(acc, a[2], b);
+        w4_wait<2>(a[3]);
+        w4_read_a<CO + 5 * RB>(a[1], a_hi, a_lo);
+        w4_mma<3>(acc, a[3], b);
+        w4_wait<2>(a[0]);
+        w4_read_a<CO + 6 * RB>(a[2], a_hi, a_lo);
+        w4_mma<4>(acc, a[0], b);
+        w4_wait<2>(a[1]);
+        w4_read_a<CO + 7 * RB>(a[3], a_hi, a_lo);
+        w4_mma<5>(acc, a[1], b);
+        w4_wait<0>(a[2]);  // A[6], A[7]: this wave's reads of the stage buffer are done
+        w4_wait<0>(a[3]);
+        if constexpr (!LAST) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage ks+1 landed (this wave)
+            __builtin_amdgcn_s_barrier();                     // ... for every wave; buffer CO free
+            if (ks + 2 < nks) issue(ks + 2, ks & 1);
+            w4_read_a<NO>(a[0], a_hi, a_lo);
+            w4_mma_col<0>(acc, a[2], a[3], b);
+            w4_read_b<0, NO>(b, b_hi, b_lo);
+            w4_mma_col<1>(acc, a[2], a[3], b);
+            w4_read_b<1, NO>(b, b_hi, b_lo);
+            w4_mma_col<2>(acc, a[2], a[3], b);
+            w4_read_b<2, NO>(b, b_hi, b_lo);
+            w4_mma_col<3>(acc, a[2], a[3], b);
+            w4_read_b<3, NO>(b, b_hi, b_lo);
+            w4_mma_col<4>(acc, a[2], a[3], b);
+            w4_read_b<4, NO>(b, b_hi, b_lo);
+            w4_mma_col<5>(acc, a[2], a[3], b);
+            w4_read_b<5, NO>(b, b_hi, b_lo);
+            w4_mma_col<6>(acc, a[2], a[3], b);
+            w4_read_b<6, NO>(b, b_hi, b_lo);
+            w4_mma_col<7>(acc, a[2], a[3], b);
+            w4_read_b<7, NO>(b, b_hi, b_lo);
+            w4_read_a<NO + RB>(a[1], a_hi, a_lo);
+        } else {
+            w4_mma<6>(acc, a[2], b);
+            w4_mma<7>(acc, a[3], b);
+        }
+    };
+    for (int ks = 0; ks < nks - 2; ks += 2) {
+        stage(ks, UC<0>{}, std::false_type{});
+        stage(ks + 1, UC<W4_TILEB>{}, std::false_type{});
+    }
+    stage(nks - 2, UC<0>{}, std::false_type{});
+    stage(nks - 1, UC<W4_TILEB>{}, std::true_type{});
+
+    // epilogue: lane (lr, ch) holds rows 4 ch + q of each row block, columns
+    // 8 lr .. 8 lr + 7 of the wave's 128 (b_col128): two 16-B stores per row.
+    // The last MFMAs' results are waited out first (asm MFMAs carry no hazard
+    // tracking): 4 x s_nop 15 > the 16x16x32 result latency
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = m0 + wm * 128 + 16 * i + 4 * ch + q;
+            if (row >= T) continue;
+            float* out = Me + (long long)row * K + n0 + wn * 128 + 8 * lr;
+            *(f32x4*)out = f32x4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
+            *(f32x4*)(out + 4) = f32x4{acc[i][4][q], acc[i][5][q], acc[i][6][q], acc[i][7][q]};
         }
     }
 }
 
 }  // namespace
 
-extern "C" int azg_split_gemm(const void* A, const void* Bt, float* M, int32_t nruns, const int32_t* points,
-                              const int32_t* rows, int32_t c, int32_t k, void* stream) {
-    if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % SG_BK ||
-        k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15))
+static int split_gemm_launch(int variant, const void* A, const void* Bt, float* M, int32_t nruns,
+                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream) {
+    if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % (2 * SG_BK) ||
+        k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
+        variant > 2)
         return AZG_ERR_ARG;
     SGArgs g{};
     g.A = (const _Float16*)A;
@@ -200,6 +714,21 @@ extern "C" int azg_split_gemm(const void* A, const void* Bt, float* M, int32_t n
     }
     g.tile0[nruns] = tiles;
     g.total = tiles;
-    hipLaunchKernelGGL(split_gemm_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
+    if (variant == 0)
+        hipLaunchKernelGGL(split_gemm_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 1)
+        hipLaunchKernelGGL(split_gemm_pipe_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
+    else
+        hipLaunchKernelGGL(split_gemm_w4_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, g);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+extern "C" int azg_split_gemm(const void* A, const void* Bt, float* M, int32_t nruns, const int32_t* points,
+                              const int32_t* rows, int32_t c, int32_t k, void* stream) {
+    return split_gemm_launch(0, A, Bt, M, nruns, points, rows, c, k, stream);
+}
+
+extern "C" int azg_split_gemm_variant(int32_t variant, const void* A, const void* Bt, float* M, int32_t nruns,
+                                      const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream) {
+    return split_gemm_launch(variant, A, Bt, M, nruns, points, rows, c, k, stream);
 }

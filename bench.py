@@ -96,7 +96,7 @@ def load_pmc(G, game, impl, gemm="split"):
         return d[k].get("hbm_bytes_per_forward") or d[k]["hbm_bytes_sum_over_shapes"]
     if impl == "winograd":
         conv = sum(tot(k) for k in ("winograd_first", "winograd_mid", "winograd_in", "winograd_out",
-                                      "gemm (hipBLASLt)"))
+                                      "split_gemm", "gemm (hipBLASLt)"))
         what = "Winograd transforms + the GEMM batches (and the FC GEMMs, ~2%)"
     else:
         conv = tot("conv2-4 igemm")

@@ -184,9 +184,14 @@ int  azg_winograd_first_nchw(const float* planes, const float* w1, const float* 
  *   M_e [rows x k] f32 = A_e x B_e^T,  A_e [rows][2c] fp16 rows [hi | lo] (V in
  *   AZG_WINO_SPLIT2), B_e [k][2c] fp16 rows [hi | lo] (U^T, points of all runs in
  *   order), computed as hi.hi + lo.hi + hi.lo with f32 accumulation.
- * c % 32 == 0, k % 256 == 0, nruns <= 4, 16-B aligned pointers. */
+ * c % 64 == 0, k % 256 == 0, nruns <= 4, 16-B aligned pointers. */
 int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, const int32_t* points,
                     const int32_t* rows, int32_t c, int32_t k, void* stream);
+/* The same with an explicit kernel schedule (0: reads, then MFMAs per stage, the
+ * azg_split_gemm default; 1: reads overlapped with MFMAs; 2: one wave per SIMD,
+ * 128 x 128 per wave); for tests and probes. */
+int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, float* m, int32_t nruns,
+                            const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
 
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active

@@ -195,24 +195,28 @@ def test_split_gemm_error_not_above_f32():
     assert errs["split_blas"] <= 1.5 * errs["f32"], errs
 
 
-@pytest.mark.parametrize("runs", [[(25, 4096)], [(3, 300), (5, 37), (2, 513)], [(1, 1)]])
-def test_split_gemm_kernel_matches_reference(runs):
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("runs,C,K", [([(25, 4096)], 512, 512), ([(3, 300), (5, 37), (2, 513)], 512, 512),
+                                      ([(1, 1)], 512, 512), ([(2, 77), (1, 256)], 64, 256),
+                                      ([(4, 129)], 128, 768)])
+def test_split_gemm_kernel_matches_reference(variant, runs, C, K):
     """libazg azg_split_gemm (hand-written fp16 MFMA, LDS-DMA): M = Ah.Bh + Al.Bh + Ah.Bl
-    for every point of every run, against the same products in f64 (ragged row counts)."""
+    for every point of every run, against the same products in f64 (ragged row counts,
+    the smallest channel counts, both kernel schedules)."""
     import ctypes
     import azg_amd  # noqa: F401
     from azg_amd import _lib
     torch.manual_seed(7)
-    C, K = 512, 512
     P = sum(p for p, _ in runs)
     A = torch.cat([torch.randn(p * t, 2 * C, device="cuda").half() for p, t in runs]).contiguous()
     Bt = torch.randn(P, K, 2 * C, device="cuda").half()
     M = torch.full((sum(p * t for p, t in runs) * K,), float("nan"), device="cuda")
     pts = (ctypes.c_int32 * len(runs))(*[p for p, _ in runs])
     rows = (ctypes.c_int32 * len(runs))(*[t for _, t in runs])
-    _lib.check(_lib.lib().azg_split_gemm(ctypes.c_void_p(A.data_ptr()), ctypes.c_void_p(Bt.data_ptr()),
-                                         ctypes.c_void_p(M.data_ptr()), len(runs), pts, rows, C, K,
-                                         ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    _lib.check(_lib.lib().azg_split_gemm_variant(variant, ctypes.c_void_p(A.data_ptr()),
+                                                 ctypes.c_void_p(Bt.data_ptr()), ctypes.c_void_p(M.data_ptr()),
+                                                 len(runs), pts, rows, C, K,
+                                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     torch.cuda.synchronize()
     a_row = m_row = pt = 0
     for p, t in runs:

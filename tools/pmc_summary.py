@@ -49,6 +49,8 @@ def group(name):
         return "winograd_in"
     if "winograd_out" in name:
         return "winograd_out"
+    if "split_gemm" in name:
+        return "split_gemm"
     if name.startswith("Cijk_"):
         return "gemm (hipBLASLt)"
     return None

@@ -1,0 +1,91 @@
+"""Time libazg's split GEMM (azg_split_gemm) on the leaf network's Winograd GEMM shapes
+at 4096 leaves against the same products as one hipBLASLt fp16 GEMM ([hi|lo|hi] rows)
+and the f32 GEMM.  TF/s are of the executed fp16 MFMA work (3 products per f32
+multiply-add).
+
+    python tools/split_gemm_bench.py > gpurun_out/split_gemm_bench.json
+"""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import azg_amd  # noqa: E402,F401
+from azg_amd import _lib  # noqa: E402
+
+LAYERS = {"conv2": [(25, 4096), (40, 8192), (16, 16384)], "conv3": [(81, 4096)], "conv4": [(25, 4096)]}
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    C = K = 512
+    L = _lib.lib()
+    out = []
+    for name, runs in LAYERS.items():
+        P = sum(p for p, _ in runs)
+        rows = sum(p * t for p, t in runs)
+        A = torch.randn(rows, 2 * C, device="cuda").half()
+        Bt = torch.randn(P, K, 2 * C, device="cuda").half()
+        M = torch.empty(rows * K, device="cuda")
+        pts = (ctypes.c_int32 * len(runs))(*[p for p, _ in runs])
+        rws = (ctypes.c_int32 * len(runs))(*[t for _, t in runs])
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+        def azg_variant(v):
+            def fn():
+                _lib.check(L.azg_split_gemm_variant(v, ctypes.c_void_p(A.data_ptr()), ctypes.c_void_p(Bt.data_ptr()),
+                                                    ctypes.c_void_p(M.data_ptr()), len(runs), pts, rws, C, K, st))
+            return fn
+
+        A3 = torch.randn(rows, 3 * C, device="cuda").half()
+        B3 = torch.randn(P, 3 * C, K, device="cuda").half()
+        Vf = torch.randn(rows, C, device="cuda")
+        Uf = torch.randn(P, C, K, device="cuda")
+
+        def blas():
+            r = pt = 0
+            for p, t in runs:
+                torch.bmm(A3[r:r + p * t].view(p, t, 3 * C), B3[pt:pt + p], out_dtype=torch.float32,
+                          out=M[r * K:(r + p * t) * K].view(p, t, K))
+                r += p * t
+                pt += p
+
+        def f32():
+            r = pt = 0
+            for p, t in runs:
+                torch.bmm(Vf[r:r + p * t].view(p, t, C), Uf[pt:pt + p], out=M[r * K:(r + p * t) * K].view(p, t, K))
+                r += p * t
+                pt += p
+
+        flops16 = 3 * 2.0 * rows * C * K
+        row = {"layer": name, "runs": runs}
+        for k, fn in (("azg", azg_variant(0)), ("azg_v1", azg_variant(1)), ("azg_v2", azg_variant(2)),
+                      ("hipblaslt_split", blas),
+                      ("hipblaslt_f32", f32)):
+            ms = timeit(fn)
+            row[k + "_ms"] = ms
+            row[k + "_tflops"] = (flops16 if k != "hipblaslt_f32" else flops16 / 3) / ms / 1e9
+        print(json.dumps(row), flush=True)
+        out.append(row)
+        del A, Bt, M, A3, B3, Vf, Uf
+        torch.cuda.empty_cache()
+    return out
+
+
+if __name__ == "__main__":
+    main()
