@@ -19,15 +19,18 @@
 // tile row's 32 channels: hi (4 x 16 B) then lo (4 x 16 B), 16-B chunk c stored at
 // c ^ ((row >> 1) & 7), so each 16-lane group of a ds_read_b128 (16 rows, one
 // chunk) covers all 16 slots of the 256-B bank row (conflict-free).  A stage is
-// 16 A + 8 B ds_read_b128 and 96 MFMAs per wave plus 8 DMA issues; variant 0
-// (default) runs them in that order with a vmcnt(0) + barrier per stage, variant 1
+// 16 A + 8 B ds_read_b128 and 96 MFMAs per wave plus 8 DMA issues; variant 0 runs
+// them in that order with a vmcnt(0) + barrier per stage, one tile per workgroup;
+// variant 4 (default) is variant 0 as a persistent kernel (one workgroup per CU,
+// the next tile's first stage loaded under the current tile's last); variant 1
 // overlaps each phase's reads with the previous phase's MFMAs, variant 2 runs one
-// wave per SIMD on 128 x 128 per wave (below).  Measured on conv2's shape
-// (tools/split_gemm_bench.py, profiles/r01_split_gemm_*.json): variant 0 975-1006
-// TF/s of fp16 MFMA work, variant 1 912-945, variant 2 922; hipBLASLt on the
-// [hi|lo|hi] form 825-845.  PMC (tools/split_gemm_pmc.py): no LDS bank conflicts,
-// A read from HBM once (L2 hit rate 78%), MFMA busy ~49% (variant 0): the rest is
-// the per-stage barrier / DMA wait and the LDS-DMA issue cost.
+// wave per SIMD on 128 x 128 per wave, variant 3 spreads the DMA issue between the
+// MFMAs.  Measured on conv2's shape (tools/split_gemm_bench.py, round-robin medians,
+// profiles/r01_split_gemm_bench.json), TF/s of fp16 MFMA work: variant 4 1016,
+// 0 977, 1 967, 3 951, 2 903; hipBLASLt on the [hi|lo|hi] form 900.  PMC
+// (tools/split_gemm_pmc.py): no LDS bank conflicts, A read from HBM once (L2 hit
+// rate 78%), MFMA busy 56% (variant 4; 49% variant 0): the rest is the per-stage
+// barrier, operand-read and LDS-DMA issue bubble.
 //
 // The tiles of all GEMMs of a layer (runs of points with equal T) are one grid;
 // block ids are dealt to the 8 XCDs round-robin, so the mapping gives each XCD a
@@ -74,6 +77,9 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 
 // Variant 0: per stage, all operand reads, then the next stage's DMA, then 96 MFMAs,
 // then vmcnt(0) + barrier (reads and MFMAs of a wave do not overlap).
+// Variant 3 (ILV = true): the same, with the next stage's 8 DMA pieces issued one per
+// row block between the MFMAs instead of in one burst before them.
+template <bool ILV>
 __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * SG_STAGEB];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -133,6 +139,20 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
                                                                                               8 * i * SG_ROWB),
                                                      16, boff[i & 1], ks * SG_BK * 2, 0, 0);
     };
+    // DMA piece p of a stage (p < 4: A row group p, else B row group p - 4)
+    auto issue_piece = [&](int ks, int buf, int p) {
+        char* base = smem + buf * SG_STAGEB + (32 * wid) * SG_ROWB;
+        const int q = p & 3;
+        if (p < 4)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 2 ? ar0 : ar1,
+                                                     (__attribute__((address_space(3))) void*)(base + 8 * q * SG_ROWB),
+                                                     16, aoff[q & 1], ks * SG_BK * 2, 0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 2 ? br0 : br1,
+                                                     (__attribute__((address_space(3))) void*)(base + SG_TILEB +
+                                                                                              8 * q * SG_ROWB),
+                                                     16, boff[q & 1], ks * SG_BK * 2, 0, 0);
+    };
 
     // operand reads: wave (wm, wn) = rows 128 wm.., cols 64 wn..; lane holds row lane%16
     // of a 16-row block, channels 8 (lane/16).. of the 32 (hi) and the same of lo
@@ -167,16 +187,22 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
             ah[i] = *(const f16x8*)(st + a_hi + 16 * i * SG_ROWB);
             al[i] = *(const f16x8*)(st + a_lo + 16 * i * SG_ROWB);
         }
-        if (ks + 1 < nks) issue(ks + 1, (ks + 1) & 1);
+        if (!ILV && ks + 1 < nks) issue(ks + 1, (ks + 1) & 1);
         __builtin_amdgcn_sched_barrier(0);  // the DMA issue stays ahead of the MFMAs
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 8; ++i) {
+            if (ILV && ks + 1 < nks) {
+                issue_piece(ks + 1, (ks + 1) & 1, i);
+                __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
             }
+            if (ILV) __builtin_amdgcn_sched_barrier(0);
+        }
         __builtin_amdgcn_sched_barrier(0);  // ... and the stage's closing wait behind them
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -193,6 +219,150 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
             *(f32x4*)(Me + (long long)row * K + n0 + wn * 64 + 4 * lr) =
                 f32x4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
         }
+    }
+}
+
+// Variant 4: variant 0 as a persistent kernel.  One workgroup per CU walks a
+// strided sequence of tiles inside its XCD's contiguous range; the last stage of a
+// tile issues the next tile's stage-0 DMA (its first-stage load latency hides
+// under the last stage's MFMAs), and a tile's epilogue stores drain under the next
+// tile's first stage (the stage's closing vmcnt(0) is the first wait on them).
+struct SGTile {
+    const _Float16* Ae;
+    const _Float16* Be;
+    float* Me;
+    int T, m0, n0;
+};
+
+__device__ __forceinline__ SGTile sg_tile(const SGArgs& g, int L) {
+    int r = 0;
+    while (r + 1 < g.nruns && L >= g.tile0[r + 1]) ++r;
+    const int u = L - g.tile0[r];
+    const int nt = u % g.ntn;
+    const int mt = (u / g.ntn) % g.mtiles[r];
+    const int e = u / (g.ntn * g.mtiles[r]);
+    const int T = g.rows[r], C2 = 2 * g.C, K = g.K;
+    SGTile t;
+    t.Ae = g.A + g.a_off[r] + (long long)e * T * C2;
+    t.Be = g.Bt + (long long)(g.b_pt0[r] + e) * K * C2;
+    t.Me = g.M + g.m_off[r] + (long long)e * T * K;
+    t.T = T;
+    t.m0 = mt * SG_BM;
+    t.n0 = nt * SG_BN;
+    return t;
+}
+
+__global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * SG_STAGEB];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int C = g.C, K = g.K, C2 = 2 * C;
+
+    // this block's tiles: its XCD's contiguous range (as the one-tile variants deal
+    // it), strided by the number of blocks on the XCD
+    const int xcd = blockIdx.x % 8, kb = blockIdx.x / 8;
+    const int nblk = ((int)gridDim.x - xcd + 7) / 8;
+    const int q8 = g.total / 8, rr = g.total % 8;
+    const int start = xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8;
+    const int cnt = q8 + (xcd < rr ? 1 : 0);
+    if (kb >= cnt) return;
+
+    // per-lane DMA geometry (tile independent part) and operand read addresses
+    int arow[2], brow[2], dcol[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int R = 32 * wid + 8 * i + (lane >> 3);
+        const int lc = (lane & 7) ^ ((R >> 1) & 7);
+        dcol[i] = lc < 4 ? 8 * lc : C + 8 * (lc - 4);
+        arow[i] = R;
+        brow[i] = b_col(R);
+    }
+    const int wm = wid >> 2, wn = wid & 3;
+    const int lr = lane & 15, sw = lr >> 1;
+    const int ch = lane >> 4;
+    const int a_hi = (wm * 128 + lr) * SG_ROWB + 16 * (ch ^ sw);
+    const int a_lo = (wm * 128 + lr) * SG_ROWB + 16 * ((4 + ch) ^ sw);
+    const int b_hi = SG_TILEB + (wn * 64 + lr) * SG_ROWB + 16 * (ch ^ sw);
+    const int b_lo = SG_TILEB + (wn * 64 + lr) * SG_ROWB + 16 * ((4 + ch) ^ sw);
+
+    // DMA of stage ks of tile t into buffer buf (descriptors as variant 0)
+    auto issue = [&](const SGTile& t, int ks, int buf) {
+        const auto ar0 = __builtin_amdgcn_make_buffer_rsrc((void*)t.Ae, 0, t.T * C2 * 2, 0x00020000);
+        const auto ar1 = __builtin_amdgcn_make_buffer_rsrc((void*)(t.Ae + 16 * C2), 0,
+                                                           (t.T > 16 ? t.T - 16 : 0) * C2 * 2, 0x00020000);
+        const auto br0 = __builtin_amdgcn_make_buffer_rsrc((void*)t.Be, 0, K * C2 * 2, 0x00020000);
+        const auto br1 = __builtin_amdgcn_make_buffer_rsrc((void*)(t.Be + C2), 0, (K - 1) * C2 * 2, 0x00020000);
+        char* base = smem + buf * SG_STAGEB + (32 * wid) * SG_ROWB;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
+                                                     (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
+                                                     16, ((t.m0 + arow[i & 1]) * C2 + dcol[i & 1]) * 2,
+                                                     ks * SG_BK * 2, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
+                                                     (__attribute__((address_space(3))) void*)(base + SG_TILEB +
+                                                                                              8 * i * SG_ROWB),
+                                                     16, ((t.n0 + brow[i & 1]) * C2 + dcol[i & 1]) * 2,
+                                                     ks * SG_BK * 2, 0, 0);
+    };
+
+    const int nks = C / SG_BK;  // even: every tile starts in buffer 0
+    SGTile cur = sg_tile(g, start + kb);
+    issue(cur, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int it = kb;;) {
+        const int nx = it + nblk;
+        const bool more = nx < cnt;
+        const SGTile nxt = sg_tile(g, start + (more ? nx : it));
+
+        f32x4 acc[8][4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < nks; ++ks) {
+            const char* st = smem + (ks & 1) * SG_STAGEB;
+            f16x8 ah[8], al[8], bh[4], bl[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bh[j] = *(const f16x8*)(st + b_hi + 16 * j * SG_ROWB);
+                bl[j] = *(const f16x8*)(st + b_lo + 16 * j * SG_ROWB);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                ah[i] = *(const f16x8*)(st + a_hi + 16 * i * SG_ROWB);
+                al[i] = *(const f16x8*)(st + a_lo + 16 * i * SG_ROWB);
+            }
+            if (ks + 1 < nks) issue(cur, ks + 1, (ks + 1) & 1);
+            else if (more) issue(nxt, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = cur.m0 + wm * 128 + 16 * i + 4 * ch + q;
+                if (row >= cur.T) continue;
+                *(f32x4*)(cur.Me + (long long)row * K + cur.n0 + wn * 64 + 4 * lr) =
+                    f32x4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
+            }
+        }
+        if (!more) break;
+        it = nx;
+        cur = nxt;
     }
 }
 
@@ -680,11 +850,23 @@ __global__ __launch_bounds__(256, 1) void split_gemm_w4_kernel(SGArgs g) {
 
 }  // namespace
 
+// one workgroup per CU (a block fills a CU: 128 KB of LDS), at most one per tile
+static unsigned persistent_blocks(int tiles) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return (unsigned)(tiles < cus ? tiles : cus);
+}
+
 static int split_gemm_launch(int variant, const void* A, const void* Bt, float* M, int32_t nruns,
                              const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream) {
     if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % (2 * SG_BK) ||
         k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
-        variant > 2)
+        variant > 4)
         return AZG_ERR_ARG;
     SGArgs g{};
     g.A = (const _Float16*)A;
@@ -715,9 +897,14 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
     g.tile0[nruns] = tiles;
     g.total = tiles;
     if (variant == 0)
-        hipLaunchKernelGGL(split_gemm_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
+        hipLaunchKernelGGL(split_gemm_kernel<false>, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 3)
+        hipLaunchKernelGGL(split_gemm_kernel<true>, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 1)
         hipLaunchKernelGGL(split_gemm_pipe_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 4)
+        hipLaunchKernelGGL(split_gemm_persist_kernel, dim3(persistent_blocks(tiles)), dim3(512), 0,
+                           (hipStream_t)stream, g);
     else
         hipLaunchKernelGGL(split_gemm_w4_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, g);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
@@ -725,7 +912,7 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
 
 extern "C" int azg_split_gemm(const void* A, const void* Bt, float* M, int32_t nruns, const int32_t* points,
                               const int32_t* rows, int32_t c, int32_t k, void* stream) {
-    return split_gemm_launch(0, A, Bt, M, nruns, points, rows, c, k, stream);
+    return split_gemm_launch(4, A, Bt, M, nruns, points, rows, c, k, stream);
 }
 
 extern "C" int azg_split_gemm_variant(int32_t variant, const void* A, const void* Bt, float* M, int32_t nruns,

@@ -187,9 +187,10 @@ int  azg_winograd_first_nchw(const float* planes, const float* w1, const float* 
  * c % 64 == 0, k % 256 == 0, nruns <= 4, 16-B aligned pointers. */
 int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, const int32_t* points,
                     const int32_t* rows, int32_t c, int32_t k, void* stream);
-/* The same with an explicit kernel schedule (0: reads, then MFMAs per stage, the
- * azg_split_gemm default; 1: reads overlapped with MFMAs; 2: one wave per SIMD,
- * 128 x 128 per wave); for tests and probes. */
+/* The same with an explicit kernel schedule (0: reads, then MFMAs per stage, one
+ * tile per workgroup; 1: reads overlapped with MFMAs; 2: one wave per SIMD,
+ * 128 x 128 per wave; 3: variant 0 with the DMA issue spread between the MFMAs;
+ * 4: variant 0 persistent, the azg_split_gemm default); for tests and probes. */
 int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, float* m, int32_t nruns,
                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
 

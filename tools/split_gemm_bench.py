@@ -1,7 +1,7 @@
 """Time libazg's split GEMM (azg_split_gemm) on the leaf network's Winograd GEMM shapes
-at 4096 leaves against the same products as one hipBLASLt fp16 GEMM ([hi|lo|hi] rows)
-and the f32 GEMM.  TF/s are of the executed fp16 MFMA work (3 products per f32
-multiply-add).
+at 4096 leaves, every kernel variant, against the same products as one hipBLASLt fp16
+GEMM ([hi|lo|hi] rows) and the f32 GEMM; median (and best) of 7 round-robin rounds.
+TF/s are of the executed fp16 MFMA work (3 products per f32 multiply-add).
 
     python tools/split_gemm_bench.py > gpurun_out/split_gemm_bench.json
 """
@@ -19,9 +19,7 @@ from azg_amd import _lib  # noqa: E402
 LAYERS = {"conv2": [(25, 4096), (40, 8192), (16, 16384)], "conv3": [(81, 4096)], "conv4": [(25, 4096)]}
 
 
-def timeit(fn, reps=20):
-    for _ in range(3):
-        fn()
+def timeit(fn, reps=10):
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     a.record()
@@ -30,6 +28,21 @@ def timeit(fn, reps=20):
     b.record()
     b.synchronize()
     return a.elapsed_time(b) / reps
+
+
+def time_all(fns, rounds=7):
+    """Round-robin over the candidates (the order rotates per round) after a warm-up
+    of every one, so clock ramps and box state do not favour whichever runs first;
+    returns {name: (median ms, min ms)} over the rounds."""
+    for _, fn in fns:
+        for _ in range(5):
+            fn()
+    ms = {k: [] for k, _ in fns}
+    for r in range(rounds):
+        order = fns[r % len(fns):] + fns[:r % len(fns)]
+        for k, fn in order:
+            ms[k].append(timeit(fn))
+    return {k: (sorted(v)[len(v) // 2], min(v)) for k, v in ms.items()}
 
 
 def main():
@@ -74,12 +87,13 @@ def main():
 
         flops16 = 3 * 2.0 * rows * C * K
         row = {"layer": name, "runs": runs}
-        for k, fn in (("azg", azg_variant(0)), ("azg_v1", azg_variant(1)), ("azg_v2", azg_variant(2)),
-                      ("hipblaslt_split", blas),
-                      ("hipblaslt_f32", f32)):
-            ms = timeit(fn)
-            row[k + "_ms"] = ms
-            row[k + "_tflops"] = (flops16 if k != "hipblaslt_f32" else flops16 / 3) / ms / 1e9
+        fns = [("azg_v%d" % v, azg_variant(v)) for v in (0, 1, 2, 3, 4)] + [("hipblaslt_split", blas),
+                                                                         ("hipblaslt_f32", f32)]
+        for k, (med, mn) in time_all(fns).items():
+            fl = flops16 if k != "hipblaslt_f32" else flops16 / 3
+            row[k + "_ms"] = med
+            row[k + "_tflops"] = fl / med / 1e9
+            row[k + "_best_tflops"] = fl / mn / 1e9
         print(json.dumps(row), flush=True)
         out.append(row)
         del A, Bt, M, A3, B3, Vf, Uf
