@@ -69,6 +69,7 @@ SIGNATURES = [
     ("azg_winograd_layout", ctypes.c_int, [_I32, _VP, _VP]),
     ("azg_winograd_in_nhwc", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
     ("azg_winograd_out_nhwc", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, ctypes.c_float, _VP]),
+    ("azg_winograd_out_split", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, ctypes.c_float, _I32, _VP, _VP]),
     ("azg_winograd_mid_nhwc", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, ctypes.c_float, _I32, _VP, _VP]),
     ("azg_winograd_first_nchw", ctypes.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
     ("azg_split_gemm", ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP]),

@@ -20,7 +20,9 @@
 // transforms, HBM-bound, consecutive lanes on consecutive channels:
 //   * winograd_in   : NHWC input (zero padding; optionally the previous layer's
 //                     bias + ReLU applied on load) -> V
-//   * winograd_out  : M -> NHWC output, bias + ReLU fused, tiles cropped
+//   * winograd_out  : M -> NHWC output, bias + ReLU fused, tiles cropped; or (split
+//                     formats) the flattened activation as one split row per image,
+//                     fc1's A operand
 //   * winograd_mid  : layer i's output transform + layer i+1's input transform in
 //                     one pass (the activation stays on chip)
 //   * winograd_first: conv1 + bias + ReLU from the NCHW planes + conv2's input
@@ -259,9 +261,14 @@ __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restri
     });
 }
 
+// FMT = AZG_WINO_F32: y is the NHWC f32 activation.  Otherwise y is one fp16 row
+// per image in V format FMT over the image's flattened NHWC activation (width
+// Ho * Ho * K): the A operand of a split GEMM over it (the network's fc1).
+template <int FMT>
 __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restrict__ Min,
-                                                           const float4* __restrict__ bias, float4* __restrict__ y,
-                                                           int Ho, int K4, long long B, int relu, float mscale) {
+                                                           const float4* __restrict__ bias, void* __restrict__ y,
+                                                           int Ho, int K4, long long B, int relu, float mscale,
+                                                           int* overflow) {
     const WSeq S(Ho);
     const long long item = xcd_item();
     if (item >= B * S.p * S.p * K4) return;
@@ -289,7 +296,10 @@ __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restr
                 if (oy >= Ho || ox >= Ho) continue;  // h = 1: one 2-tile, cropped
                 float4 z = vadd(yt[a][q], bb);
                 if (relu) z = vrelu(z);
-                y[((b * Ho + oy) * Ho + ox) * K4 + k4] = z;
+                if constexpr (FMT == AZG_WINO_F32)
+                    ((float4*)y)[((b * Ho + oy) * Ho + ox) * K4 + k4] = z;
+                else
+                    store_v<FMT>(y, b, Ho * Ho * K4, (oy * Ho + ox) * K4 + k4, z, overflow);
             }
     });
 }
@@ -498,9 +508,28 @@ extern "C" int azg_winograd_out_nhwc(const float* M, const float* bias, float* y
         ((uintptr_t)bias & 15) || ((uintptr_t)y & 15) || (long long)batch * h_out * h_out * (k / 4) > (1ll << 38))
         return AZG_ERR_ARG;
     const WSeq S(h_out);
-    hipLaunchKernelGGL(winograd_out_kernel, dim3(grid_for((long long)batch * S.p * S.p * (k / 4))), dim3(256), 0,
-                       (hipStream_t)stream, (const float4*)M, (const float4*)bias, (float4*)y, h_out, k / 4,
-                       (long long)batch, relu, mscale);
+    hipLaunchKernelGGL(winograd_out_kernel<AZG_WINO_F32>, dim3(grid_for((long long)batch * S.p * S.p * (k / 4))),
+                       dim3(256), 0, (hipStream_t)stream, (const float4*)M, (const float4*)bias, (void*)y, h_out,
+                       k / 4, (long long)batch, relu, mscale, (int*)nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+extern "C" int azg_winograd_out_split(const float* M, const float* bias, void* y, int32_t batch, int32_t h_out,
+                                      int32_t k, int32_t relu, float mscale, int32_t vfmt, int32_t* overflow,
+                                      void* stream) {
+    if (!M || !bias || !y || batch <= 0 || h_out <= 0 || h_out > 64 || k <= 0 || k % 4 || ((uintptr_t)M & 15) ||
+        ((uintptr_t)bias & 15) || ((uintptr_t)y & 15) || vfmt == AZG_WINO_F32 || bad_fmt(vfmt, overflow) ||
+        (long long)h_out * h_out * k > (1ll << 28) || (long long)batch * h_out * h_out * (k / 4) > (1ll << 38))
+        return AZG_ERR_ARG;
+    const WSeq S(h_out);
+    const dim3 grid(grid_for((long long)batch * S.p * S.p * (k / 4)));
+    hipStream_t st = (hipStream_t)stream;
+    if (vfmt == AZG_WINO_SPLIT)
+        hipLaunchKernelGGL(winograd_out_kernel<AZG_WINO_SPLIT>, grid, dim3(256), 0, st, (const float4*)M,
+                           (const float4*)bias, y, h_out, k / 4, (long long)batch, relu, mscale, overflow);
+    else
+        hipLaunchKernelGGL(winograd_out_kernel<AZG_WINO_SPLIT2>, grid, dim3(256), 0, st, (const float4*)M,
+                           (const float4*)bias, y, h_out, k / 4, (long long)batch, relu, mscale, overflow);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 

@@ -166,6 +166,13 @@ int  azg_winograd_in_nhwc(const float* x, const float* in_bias, void* V, int32_t
                           int32_t c, int32_t vfmt, int32_t* overflow, void* stream);
 int  azg_winograd_out_nhwc(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,
                            int32_t relu, float mscale, void* stream);
+/* The output transform writing, instead of the NHWC activation, one row per image of
+ * the flattened NHWC activation (width h_out*h_out*k) in split format vfmt
+ * (AZG_WINO_SPLIT [hi|lo|hi] or AZG_WINO_SPLIT2 [hi|lo]): the A operand of a split
+ * GEMM over it (the network's fc1, InflexionNNet.py:47).  Same checks as above;
+ * out-of-range values set *overflow. */
+int  azg_winograd_out_split(const float* M, const float* bias, void* y, int32_t batch, int32_t h_out, int32_t k,
+                            int32_t relu, float mscale, int32_t vfmt, int32_t* overflow, void* stream);
 /* Between two Winograd layers with no padding on the second (conv2->conv3->conv4):
  * M of layer i (h x h outputs, c channels) -> relu(A^T (mscale M) A + bias) -> V of
  * layer i+1 (input h x h, format vfmt) in one pass; the activation stays on chip.
