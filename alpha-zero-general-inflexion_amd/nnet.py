@@ -226,6 +226,13 @@ class InferenceNet(nn.Module):
         w1, b1 = _fold_bn(net.fc1.weight.detach(), net.fc1.bias.detach(), net.fc_bn1)
         w1 = w1.reshape(-1, c, s, s).permute(0, 2, 3, 1).reshape(w1.shape[0], -1)  # (c,h,w) -> (h,w,c)
         self.register_buffer("fw1", w1.contiguous())
+        # fc1 as a split-fp16 GEMM (with a split GEMM form): conv4's output transform
+        # writes the flattened activation as [hi | lo | hi] rows, fc1's weights are
+        # stacked [hi; hi; lo] (scaled by a power of two, undone with the bias)
+        self.fc1_split = gemm != "f32"
+        if self.fc1_split:
+            whi, wlo, self.fc1_scale = _split_u(w1.t().unsqueeze(0))
+            self.register_buffer("fw1_s", torch.cat([whi, whi, wlo], dim=1).contiguous())
         self.register_buffer("fb1", b1)
         w2, b2 = _fold_bn(net.fc2.weight.detach(), net.fc2.bias.detach(), net.fc_bn2)
         self.register_buffer("fw2", w2.contiguous())
@@ -343,7 +350,8 @@ class InferenceNet(nn.Module):
             row += P * T
             pt += P
 
-    def _conv_winograd(self, x, i, pad, in_bias=None, carried=False, B=None, H=None, fuse_next=False):
+    def _conv_winograd(self, x, i, pad, in_bias=None, carried=False, B=None, H=None, fuse_next=False,
+                       split_out=False):
         """Winograd layer i (mixed F(3,3)/F(2,3) tiles, azg_winograd.hip): libazg input
         transform (or, with carried=True, the V the previous layer's fused transform left
         in the workspace), the GEMMs (_winograd_gemms), then either the output transform
@@ -382,6 +390,12 @@ class InferenceNet(nn.Module):
         if fuse_next:
             _lib.check(L.azg_winograd_mid_nhwc(M, bias, V, B, Ho, K, mscale, fmt, ctypes.c_void_p(ovf), s))
             return None
+        if split_out:
+            # the flattened NHWC activation as one [hi | lo | hi] fp16 row per image (fc1's A operand)
+            y = torch.empty((B, 3 * Ho * Ho * K), device=dev, dtype=torch.float16)
+            _lib.check(L.azg_winograd_out_split(M, bias, ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, mscale, 1,
+                                                ctypes.c_void_p(self.overflow.data_ptr()), s))
+            return y
         y = torch.empty((B, K, Ho, Ho), device=dev, dtype=torch.float32, memory_format=torch.channels_last)
         _lib.check(L.azg_winograd_out_nhwc(M, bias, ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, mscale, s))
         return y
@@ -445,7 +459,11 @@ class InferenceNet(nn.Module):
             elif impl == "azg":
                 x = self._conv_azg(x, i, pad)
             elif impl == "winograd":
-                x = self._conv_winograd(x, i, pad, in_bias=pending, carried=carried, B=B, H=H, fuse_next=fuse_next)
+                split_out = i == 4 and self.fc1_split and self.gemm != "f32"
+                x = self._conv_winograd(x, i, pad, in_bias=pending, carried=carried, B=B, H=H, fuse_next=fuse_next,
+                                        split_out=split_out)
+                if split_out:
+                    x = ("split", x)
                 pending = None
                 carried = fuse_next
             elif i == 1 and impls[1] == "winograd":
@@ -457,8 +475,15 @@ class InferenceNet(nn.Module):
             if hook:
                 hook(i, "stop")
             H = h_out
-        x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten, no copy
-        x = torch.relu_(torch.addmm(self.fb1, x, self.fw1.t()))
+        if isinstance(x, tuple):
+            # fc1 + folded fc_bn1 + ReLU: hi.Wh + lo.Wh + hi.Wl on the fp16 MFMA (hipBLASLt), f32 accumulation
+            a3 = x[1]
+            m1 = torch.empty((1, a3.shape[0], self.fw1_s.shape[2]), device=a3.device, dtype=torch.float32)
+            torch.bmm(a3.unsqueeze(0), self.fw1_s, out_dtype=torch.float32, out=m1)
+            x = torch.relu_(torch.add(self.fb1, m1[0], alpha=self.fc1_scale))
+        else:
+            x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten, no copy
+            x = torch.relu_(torch.addmm(self.fb1, x, self.fw1.t()))
         x = torch.relu_(torch.addmm(self.fb2, x, self.fw2.t()))
         p = torch.softmax(torch.addmm(self.fb3, x, self.fw3.t()), dim=1)
         v = torch.tanh(torch.addmm(self.fb4, x, self.fw4.t()))

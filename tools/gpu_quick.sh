@@ -1,0 +1,8 @@
+set -e
+O=gpurun_out/r1s3j
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_nn.py tests/test_gpu_dropin.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err
+R=$PWD
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof -o run -- python3 $R/bench.py --no-cpu-baseline > $R/$O/bench_prof.json 2> $R/$O/prof.err
