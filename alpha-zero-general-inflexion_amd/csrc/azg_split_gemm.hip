@@ -252,9 +252,14 @@ __device__ __forceinline__ SGTile sg_tile(const SGArgs& g, int L) {
     return t;
 }
 
+// DW = waves that issue the DMA: 8 (variant 4: 4 pieces per operand each) or 4
+// (variant 5: waves 0-3, one per SIMD, 8 pieces per operand each, so on every SIMD
+// one wave's DMA issue runs beside the other wave's MFMAs)
+template <int DW>
 __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * SG_STAGEB];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // wid through readfirstlane: the compiler then knows it is wave-uniform (DW < 8 branches on it)
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int C = g.C, K = g.K, C2 = 2 * C;
 
     // this block's tiles: its XCD's contiguous range (as the one-tile variants deal
@@ -266,7 +271,9 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
     const int cnt = q8 + (xcd < rr ? 1 : 0);
     if (kb >= cnt) return;
 
-    // per-lane DMA geometry (tile independent part) and operand read addresses
+    // per-lane DMA geometry (tile independent part): wave w fills LDS rows
+    // 32 w + 8 i + lane / 8 (i < 4) of A and of B; with DW = 4, waves 0-3 also fill
+    // the rows of waves 4-7 (128 rows on: b_col(R + 128) = b_col(R) + 128)
     int arow[2], brow[2], dcol[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -284,27 +291,36 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
     const int b_hi = SG_TILEB + (wn * 64 + lr) * SG_ROWB + 16 * (ch ^ sw);
     const int b_lo = SG_TILEB + (wn * 64 + lr) * SG_ROWB + 16 * ((4 + ch) ^ sw);
 
-    // DMA of stage ks of tile t into buffer buf (descriptors as variant 0)
+    // DMA of stage ks of tile t into buffer buf (descriptors as variant 0; the
+    // second half's 128 rows on)
     auto issue = [&](const SGTile& t, int ks, int buf) {
-        const auto ar0 = __builtin_amdgcn_make_buffer_rsrc((void*)t.Ae, 0, t.T * C2 * 2, 0x00020000);
-        const auto ar1 = __builtin_amdgcn_make_buffer_rsrc((void*)(t.Ae + 16 * C2), 0,
-                                                           (t.T > 16 ? t.T - 16 : 0) * C2 * 2, 0x00020000);
-        const auto br0 = __builtin_amdgcn_make_buffer_rsrc((void*)t.Be, 0, K * C2 * 2, 0x00020000);
-        const auto br1 = __builtin_amdgcn_make_buffer_rsrc((void*)(t.Be + C2), 0, (K - 1) * C2 * 2, 0x00020000);
-        char* base = smem + buf * SG_STAGEB + (32 * wid) * SG_ROWB;
+        if (DW < 8 && wid >= DW) return;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
-                                                     (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
-                                                     16, ((t.m0 + arow[i & 1]) * C2 + dcol[i & 1]) * 2,
-                                                     ks * SG_BK * 2, 0, 0);
+        for (int h = 0; h < 8 / DW; ++h) {
+            const int T = t.T - 128 * h;
+            const _Float16* Ae = t.Ae + 128 * h * C2;
+            const _Float16* Be = t.Be + 128 * h * C2;
+            const auto ar0 = __builtin_amdgcn_make_buffer_rsrc((void*)Ae, 0, (T > 0 ? T : 0) * C2 * 2, 0x00020000);
+            const auto ar1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Ae + 16 * C2), 0, (T > 16 ? T - 16 : 0) * C2 * 2,
+                                                               0x00020000);
+            const auto br0 = __builtin_amdgcn_make_buffer_rsrc((void*)Be, 0, (K - 128 * h) * C2 * 2, 0x00020000);
+            const auto br1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Be + C2), 0, (K - 128 * h - 1) * C2 * 2,
+                                                               0x00020000);
+            char* base = smem + buf * SG_STAGEB + (32 * wid + 128 * h) * SG_ROWB;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
-                                                     (__attribute__((address_space(3))) void*)(base + SG_TILEB +
-                                                                                              8 * i * SG_ROWB),
-                                                     16, ((t.n0 + brow[i & 1]) * C2 + dcol[i & 1]) * 2,
-                                                     ks * SG_BK * 2, 0, 0);
+            for (int i = 0; i < 4; ++i)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
+                                                         (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
+                                                         16, ((t.m0 + arow[i & 1]) * C2 + dcol[i & 1]) * 2,
+                                                         ks * SG_BK * 2, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
+                                                         (__attribute__((address_space(3))) void*)(base + SG_TILEB +
+                                                                                                  8 * i * SG_ROWB),
+                                                         16, ((t.n0 + brow[i & 1]) * C2 + dcol[i & 1]) * 2,
+                                                         ks * SG_BK * 2, 0, 0);
+        }
     };
 
     const int nks = C / SG_BK;  // even: every tile starts in buffer 0
@@ -866,7 +882,7 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
                              const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream) {
     if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % (2 * SG_BK) ||
         k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
-        variant > 4)
+        variant > 5)
         return AZG_ERR_ARG;
     SGArgs g{};
     g.A = (const _Float16*)A;
@@ -903,7 +919,10 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
     else if (variant == 1)
         hipLaunchKernelGGL(split_gemm_pipe_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 4)
-        hipLaunchKernelGGL(split_gemm_persist_kernel, dim3(persistent_blocks(tiles)), dim3(512), 0,
+        hipLaunchKernelGGL(split_gemm_persist_kernel<8>, dim3(persistent_blocks(tiles)), dim3(512), 0,
+                           (hipStream_t)stream, g);
+    else if (variant == 5)
+        hipLaunchKernelGGL(split_gemm_persist_kernel<4>, dim3(persistent_blocks(tiles)), dim3(512), 0,
                            (hipStream_t)stream, g);
     else
         hipLaunchKernelGGL(split_gemm_w4_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, g);

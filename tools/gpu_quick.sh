@@ -1,5 +1,5 @@
 set -e
-O=gpurun_out/r1s3j
+O=gpurun_out/${1:-quick}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_nn.py tests/test_gpu_dropin.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
