@@ -53,6 +53,7 @@ SIGNATURES = [
     ("azg_sim_end", ctypes.c_int, [_VP, _VP, _I32, _VP, _VP]),
     ("azg_stub_eval", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     ("azg_move_end", ctypes.c_int, [_VP, _VP]),
+    ("azg_refill", ctypes.c_int, [_VP, _VP, _I64, _U32, _VP, _I64, _VP, _VP, _VP, _VP, _VP, _VP]),
     ("azg_active_games", ctypes.c_int, [_VP, ctypes.POINTER(_I32), _VP]),
     ("azg_get_state", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     ("azg_set_root", ctypes.c_int, [_VP, _I32, _VP, _I32, _I32, _VP]),

@@ -125,10 +125,24 @@ class Coach:
     # ---------------------------------------------------------------- learn loop
     def selfplay_examples(self, num_games, evaluator=None, seed_base=0, first_game=0, maxlen=None):
         """One iteration's self-play (Coach.py:106-112) as num_games concurrent
-        games; the examples (last maxlen, default args.maxlenOfQueue) are built on
-        the GPU and returned as a device ExampleSet."""
-        from .examples import engine_examples
+        games (or, with args.selfplaySlots = S < num_games, through S engine slots
+        that refill as games end); the examples (last maxlen, default
+        args.maxlenOfQueue) are built on the GPU and returned as a device ExampleSet."""
+        from .engine import game_spec
+        from .examples import engine_examples, examples_from_records
         maxlen = int(self.args.maxlenOfQueue if maxlen is None else maxlen)
+        slots = int(self.args.get("selfplaySlots", 0) or 0)
+        if 0 < slots < num_games:
+            # continuous batching: num_games games through `slots` engine slots
+            # (azg_refill); same examples, game for game, as one slot per game
+            eng = self._engine(slots, evaluator, seed_base, first_game)
+            try:
+                r = eng.play_games(num_games, first_game=first_game)
+            finally:
+                eng.close()
+            name, n, max_turns = game_spec(self.game)
+            return examples_from_records(name, n, max_turns, int(self.args.tempThreshold), r["moves"],
+                                         r["actions"], r["counts"], self.label_mode, maxlen)
         eng = self._engine(num_games, evaluator, seed_base, first_game)
         try:
             eng.play()

@@ -140,6 +140,8 @@ int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
     ALLOC(d.leaf_cs, G);
     ALLOC(d.leaf_slot, G);
     ALLOC(d.moves, G);
+    ALLOC(d.game_id, G);
+    ALLOC(d.harvested, G);
     ALLOC(d.rec_action, G * (size_t)d.max_moves);
     ALLOC(d.rec_temp, G * (size_t)d.max_moves);
     if (cfg->flags & AZG_FLAG_RECORD) ALLOC(d.rec_counts, G * (size_t)d.max_moves * A);
@@ -174,6 +176,27 @@ int azg_reset(azg_engine* e, uint32_t seed_base, int64_t first_game, void* strea
     e->cfg.seed_base = seed_base;
     e->cfg.first_game = first_game;
     HIP_TRY(e->ops.reset(e->d, seed_base, (long long)first_game, (hipStream_t)stream));
+    return 0;
+}
+
+int azg_refill(azg_engine* e, int64_t* next_game, int64_t end_game, uint32_t seed_base, int64_t* count,
+               int64_t cap, int64_t* ids, int32_t* moves, int32_t* actions, int8_t* temps, int32_t* counts,
+               void* stream) {
+    if (!e || !next_game || !count || cap < 0 || (cap > 0 && (!ids || !moves || !actions || !temps)))
+        return fail(AZG_ERR_ARG, "null argument or negative cap");
+    if (counts && !e->d.rec_counts) return fail(AZG_ERR_ARG, "counts requested but the engine records none");
+    azg::RefillArgs X;
+    X.next_game = (unsigned long long*)next_game;
+    X.end_game = (long long)end_game;
+    X.seed_base = seed_base;
+    X.count = (unsigned long long*)count;
+    X.cap = (long long)cap;
+    X.ids = ids;
+    X.moves = moves;
+    X.actions = actions;
+    X.temps = temps;
+    X.counts = counts;
+    HIP_TRY(e->ops.refill(e->d, X, (hipStream_t)stream));
     return 0;
 }
 

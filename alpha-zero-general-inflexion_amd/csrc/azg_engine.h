@@ -64,6 +64,8 @@ struct Dev {
 
     // per-move record
     int32_t* moves;      // [G]
+    int64_t* game_id;    // [G]  global game index of the slot's game (seed = seed_base + game_id)
+    int32_t* harvested;  // [G]  continuous batching: the finished game was handed off, slot idle
     int32_t* rec_action; // [G*max_moves]
     int8_t* rec_temp;    // [G*max_moves]
     int32_t* rec_counts; // [G*max_moves*A] or null

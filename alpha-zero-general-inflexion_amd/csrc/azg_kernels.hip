@@ -1072,11 +1072,12 @@ __global__ __launch_bounds__(WAVE) void root_counts_kernel(Dev E, int g, int32_t
         out[a] = id >= 0 ? (int)(E.node_N[node_row<R>(E, g, id) + a] & 0x7fffffffu) : 0;
 }
 
-// Fresh games in every slot (Coach.py:110-111): initial board, RED to move,
-// numpy RandomState(seed) per slot, empty tree.
+// A fresh game in slot g (Coach.py:110-111): initial board, RED to move, numpy
+// RandomState(seed), empty tree; global game index gid.  Per-slot counters are
+// cleared only by a full reset (refilled slots keep accumulating them).
 template <class R>
-__global__ __launch_bounds__(WAVE) void reset_kernel(Dev E, uint32_t seed_base, long long first_game) {
-    const int g = blockIdx.x, lane = lane_id();
+__device__ void reset_slot(const Dev& E, int g, uint32_t seed, long long gid, bool clear_stats) {
+    const int lane = lane_id();
     E.board[(size_t)g * 64 + lane] = lane < R::CELLS ? (int8_t)R::initial_cell(lane) : (int8_t)0;
     if (lane == 0) {
         E.turn[g] = 0;
@@ -1087,14 +1088,18 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Dev E, uint32_t seed_base, 
         E.active[g] = 1;
         E.moves[g] = 0;
         E.err[g] = 0;
+        E.game_id[g] = gid;
+        E.harvested[g] = 0;
         E.free_top[g] = E.M;
         E.live[g] = 0;
-        E.st_exp[g] = E.st_term[g] = E.st_fallback[g] = E.st_sims[g] = 0;
-        E.st_depth[g] = E.st_live_max[g] = 0;
+        if (clear_stats) {
+            E.st_exp[g] = E.st_term[g] = E.st_fallback[g] = E.st_sims[g] = 0;
+            E.st_depth[g] = E.st_live_max[g] = 0;
+        }
         E.leaf_kind[g] = LEAF_NONE;
         // init_genrand (RandomState.seed): sequential recurrence, one lane
         uint32_t* mt = E.mt + (size_t)g * MT_N;
-        uint32_t x = seed_base + (uint32_t)(first_game + g);
+        uint32_t x = seed;
         mt[0] = x;
         for (int i = 1; i < MT_N; ++i) {
             x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
@@ -1109,6 +1114,57 @@ __global__ __launch_bounds__(WAVE) void reset_kernel(Dev E, uint32_t seed_base, 
     }
     uint64_t* T64 = E.table + (size_t)g * E.H;
     for (int s = lane; s < E.H; s += WAVE) T64[s] = 0ull;
+}
+
+// Every slot: the game with global index first_game + g, seeded seed_base + index.
+template <class R>
+__global__ __launch_bounds__(WAVE) void reset_kernel(Dev E, uint32_t seed_base, long long first_game) {
+    const int g = blockIdx.x;
+    reset_slot<R>(E, g, seed_base + (uint32_t)(first_game + g), first_game + g, true);
+}
+
+// Continuous batching: a slot whose game has ended hands its
+// record (game index, moves, actions, temps, root counts) to row j of the
+// completed-game buffers (j from a device counter, so rows are in completion
+// order) and starts the next global game index at once; past end_game it goes
+// idle.  Each game is still seeded by its global index, so its record equals the
+// one-game-per-slot run's, whatever slot or moment it ran in.
+template <class R>
+__global__ __launch_bounds__(WAVE) void refill_kernel(Dev E, RefillArgs X) {
+    const int g = blockIdx.x, lane = lane_id();
+    if (E.active[g] || E.harvested[g] || E.err[g]) return;
+    const long long gid = E.game_id[g];
+    unsigned j = 0xffffffffu, klo = 0, khi = 0;
+    if (lane == 0) {
+        if (gid < X.end_game) j = (unsigned)atomicAdd(X.count, 1ull);
+        const unsigned long long k = atomicAdd(X.next_game, 1ull);
+        klo = (unsigned)k;
+        khi = (unsigned)(k >> 32);
+    }
+    j = __shfl(j, 0);
+    const long long k = (long long)(((unsigned long long)__shfl(khi, 0) << 32) | __shfl(klo, 0));
+    if (j != 0xffffffffu && (long long)j < X.cap) {
+        const int m = E.moves[g], mm = m < E.max_moves ? m : E.max_moves;
+        const size_t src = (size_t)g * E.max_moves, dst = (size_t)j * E.max_moves;
+        if (lane == 0) {
+            X.ids[j] = gid;
+            X.moves[j] = m;
+        }
+        for (int i = lane; i < mm; i += WAVE) {
+            X.actions[dst + i] = E.rec_action[src + i];
+            X.temps[dst + i] = E.rec_temp[src + i];
+        }
+        if (X.counts && E.rec_counts) {  // rows of A (odd for Inflexion): dword copies
+            const int32_t* sc = E.rec_counts + src * R::A;
+            int32_t* dc = X.counts + dst * R::A;
+            const size_t n = (size_t)mm * R::A;
+            for (size_t i = lane; i < n; i += WAVE) dc[i] = sc[i];
+        }
+    }
+    if (k < X.end_game)
+        reset_slot<R>(E, g, X.seed_base + (uint32_t)k, k, false);
+    else if (lane == 0)
+        E.harvested[g] = 1;
 }
 
 // [0] active slots, [1] first error code
@@ -1334,6 +1390,10 @@ struct Impl {
         hipLaunchKernelGGL(reset_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, seed_base, first_game);
         return hipGetLastError();
     }
+    static hipError_t refill(const Dev& E, const RefillArgs& X, hipStream_t st) {
+        hipLaunchKernelGGL(refill_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, X);
+        return hipGetLastError();
+    }
 };
 
 template <class R>
@@ -1350,6 +1410,7 @@ static GameOps make_ops() {
     o.move_end = &Impl<R>::move_end;
     o.root_counts = &Impl<R>::root_counts;
     o.reset = &Impl<R>::reset;
+    o.refill = &Impl<R>::refill;
     o.opponent = &Impl<R>::opponent;
     o.replay = &Impl<R>::replay;
     o.emit = &Impl<R>::emit;

@@ -35,6 +35,20 @@ struct ExampleArgs {
     float* vs;                // [maxlen]
 };
 
+// arguments of the refill kernel (azg_refill, continuous batching)
+struct RefillArgs {
+    unsigned long long* next_game;  // device counter: next global game index to start
+    long long end_game;             // games below end_game are started / handed off
+    uint32_t seed_base;
+    unsigned long long* count;      // device counter: games handed off so far
+    long long cap;                  // rows of the completed-game buffers
+    int64_t* ids;                   // [cap]
+    int32_t* moves;                 // [cap]
+    int32_t* actions;               // [cap * max_moves]
+    int8_t* temps;                  // [cap * max_moves]
+    int32_t* counts;                // [cap * max_moves * A] or null
+};
+
 struct GameOps {
     int cells;    // board cells (lanes in use)
     int actions;  // A = max_actions
@@ -47,6 +61,7 @@ struct GameOps {
     hipError_t (*move_end)(const Dev&, hipStream_t);
     hipError_t (*root_counts)(const Dev&, int g, int32_t* out, hipStream_t);
     hipError_t (*reset)(const Dev&, uint32_t seed_base, long long first_game, hipStream_t);
+    hipError_t (*refill)(const Dev&, const RefillArgs&, hipStream_t);
     hipError_t (*opponent)(const Dev&, int kind, hipStream_t);
     hipError_t (*replay)(const ExampleArgs&, hipStream_t);
     hipError_t (*emit)(const ExampleArgs&, hipStream_t);

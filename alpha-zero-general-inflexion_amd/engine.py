@@ -168,6 +168,45 @@ class SelfPlayEngine:
             m += 1
         return m
 
+    def play_games(self, num_games, first_game=None, check_every=1):
+        """Continuous batching (azg_refill): play the num_games games
+        with global indices first_game .. first_game + num_games - 1 through the G
+        slots.  A slot whose game ends hands its record off and starts the next index
+        at once, so no slot waits for the longest game of a batch.  Each game is
+        seeded by its own index, so its record is the one a slot of its own would
+        produce (tests/test_gpu_parity.py).  Returns the records ordered by game
+        index, as device tensors: {"ids" [N], "moves" [N], "actions" [N, max_moves],
+        "temps" [N, max_moves], "counts" [N, max_moves, A] or None}."""
+        fg = self.cfg.first_game if first_game is None else int(first_game)
+        n = int(num_games)
+        if n < 1:
+            raise ValueError("num_games must be >= 1")
+        self.reset(first_game=fg)
+        dev, MM = self.device, self.max_moves
+        with torch.cuda.device(dev):
+            nxt = torch.tensor([fg + self.G], dtype=torch.int64, device=dev)
+            cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+            ids = torch.full((n,), -1, dtype=torch.int64, device=dev)
+            moves = torch.zeros(n, dtype=torch.int32, device=dev)
+            actions = torch.zeros((n, MM), dtype=torch.int32, device=dev)
+            temps = torch.zeros((n, MM), dtype=torch.int8, device=dev)
+            counts = torch.zeros((n, MM, self.A), dtype=torch.int32, device=dev) if self.record else None
+        args = (_ptr(nxt), fg + n, self.cfg.seed_base, _ptr(cnt), n, _ptr(ids), _ptr(moves), _ptr(actions),
+                _ptr(temps), _ptr(counts) if counts is not None else None)
+        k = 0
+        while True:
+            self.move()
+            check(self.L.azg_refill(self.h, *args, self._stream()))
+            k += 1
+            if k % check_every == 0 and self.active() == 0:
+                break
+        done = int(cnt.item())
+        if done != n:
+            raise _lib.AzgError(f"play_games: {done} of {n} games completed")
+        order = torch.argsort(ids)
+        return {"ids": ids[order], "moves": moves[order], "actions": actions[order], "temps": temps[order],
+                "counts": counts[order] if counts is not None else None}
+
     def reset(self, seed_base=None, first_game=None):
         sb = self.cfg.seed_base if seed_base is None else int(seed_base) & 0xFFFFFFFF
         fg = self.cfg.first_game if first_game is None else int(first_game)

@@ -96,6 +96,19 @@ int  azg_stub_eval(azg_engine* e, const float* leaf_planes, float* P, float* v, 
 /* Root policy, sampling, move application, recording, node GC. */
 int  azg_move_end(azg_engine* e, void* stream);
 
+/* Continuous batching: call after azg_move_end.  Every slot
+ * whose game has ended hands its record to row j of the caller's completed-game
+ * buffers (j = atomicAdd(*count, 1), completion order; only games with index <
+ * end_game, and only while j < cap): ids[j] = global game index, moves[j],
+ * actions / temps [j][max_moves], counts [j][max_moves][A] (NULL to skip); the
+ * slot then starts global game k = atomicAdd(*next_game, 1) (seed seed_base + k,
+ * fresh tree) if k < end_game, else goes idle.  next_game and count are device
+ * int64 counters the caller initialises (next_game = first_game + G after
+ * azg_reset).  A game's record is the same whichever slot it ran in. */
+int  azg_refill(azg_engine* e, int64_t* next_game, int64_t end_game, uint32_t seed_base, int64_t* count,
+                int64_t cap, int64_t* ids, int32_t* moves, int32_t* actions, int8_t* temps, int32_t* counts,
+                void* stream);
+
 /* Number of slots whose game is still ongoing (synchronises the stream). */
 int  azg_active_games(azg_engine* e, int32_t* out, void* stream);
 

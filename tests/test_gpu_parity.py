@@ -145,3 +145,33 @@ def test_engine_records_zero_copy_view(azg):
     assert np.array_equal(moves.cpu().numpy(), rec["moves"])
     assert np.array_equal(actions.cpu().numpy(), rec["actions"])
     assert np.array_equal(counts.cpu().numpy(), rec["counts"])
+
+
+@pytest.mark.parametrize("game,n,max_turns,kind", [("inflexion", 7, 40, ol.INFLEXION), ("othello", 6, 0, ol.OTHELLO)])
+def test_refill_games_match_oracle(azg, game, n, max_turns, kind):
+    """Continuous batching (azg_refill): 27 games through 8 slots, each slot starting
+    the next global game index as soon as its game ends; every game's record
+    equals the oracle episode seeded by that index (bit-exact), whatever slot and
+    moment it ran in.  Othello games differ in length, so slots refill out of step."""
+    cfg = dict(sims=25, cpuct=1, temp_threshold=30)
+    first, N = 700, 27
+    e = azg.SelfPlayEngine(8, max_turns=max_turns if game == "inflexion" else 343, first_game=first,
+                           evaluator="stub", game=game, n=n, **cfg)
+    r = e.play_games(N)
+    assert e.stats()["error"] == 0
+    ids = r["ids"].cpu().numpy()
+    assert ids.tolist() == list(range(first, first + N))
+    moves, actions = r["moves"].cpu().numpy(), r["actions"].cpu().numpy()
+    temps, counts = r["temps"].cpu().numpy(), r["counts"].cpu().numpy()
+    lengths = set()
+    for i, k in enumerate(ids):
+        o = ol.episode(n, max_turns, cfg["sims"], cfg["cpuct"], cfg["temp_threshold"], int(k), kind=kind)
+        m = o["moves"]
+        lengths.add(m)
+        assert moves[i] == m, k
+        assert np.array_equal(actions[i, :m], o["actions"]), k
+        assert np.array_equal(temps[i, :m], o["temps"]), k
+        assert np.array_equal(counts[i, :m], o["counts"]), k
+    assert e.active() == 0
+    if game == "othello":
+        assert len(lengths) > 1  # the slots did refill out of step

@@ -160,3 +160,21 @@ def test_learn_loop_small(tmp_path):
     assert any(not torch.equal(w0[k], v) for k, v in nnet.nnet.state_dict().items())
     assert set(c.last_pit) == {"random", "greedy"} and all(sum(r) == 4 for r in c.last_pit.values())
     assert torch.isfinite(c.last_losses).all()
+
+
+@pytest.mark.parametrize("game_name,n", [("inflexion", 7), ("othello", 6)])
+def test_selfplay_slots_refill_same_examples(game_name, n):
+    """Coach.selfplay_examples with args.selfplaySlots = 5 < numEps (continuous
+    batching through azg_refill) gives exactly the examples of one slot per game."""
+    import azg_amd  # noqa: F401
+    from azg_amd.coach import Coach
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.othello import OthelloGame
+    game = InflexionGame(7, max_turns=30, max_power=6) if game_name == "inflexion" else OthelloGame(n)
+    base = dict(numEps=13, tempThreshold=10, maxlenOfQueue=10**9, numMCTSSims=8, cpuct=1)
+    full = Coach(game, "stub", Args(base)).selfplay_examples(13, first_game=40)
+    slim = Coach(game, "stub", Args(base, selfplaySlots=5)).selfplay_examples(13, first_game=40)
+    assert len(full) == len(slim) > 0
+    assert torch.equal(full.planes, slim.planes)
+    assert torch.equal(full.pis, slim.pis)
+    assert torch.equal(full.vs, slim.vs)
