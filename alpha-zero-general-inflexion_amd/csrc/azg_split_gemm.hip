@@ -255,7 +255,11 @@ __device__ __forceinline__ SGTile sg_tile(const SGArgs& g, int L) {
 // DW = waves that issue the DMA: 8 (variant 4: 4 pieces per operand each) or 4
 // (variant 5: waves 0-3, one per SIMD, 8 pieces per operand each, so on every SIMD
 // one wave's DMA issue runs beside the other wave's MFMAs)
-template <int DW>
+// PROBE = true (variant 6, timing probe only, wrong results): every descriptor has
+// zero records, so the DMA moves no global data (LDS gets zeros) while the
+// instruction stream, waits and barriers stay: prices the operand traffic
+// (MI355X_MICROARCH.md / cdna_hip_programming.md, zero-record descriptor).
+template <int DW, bool PROBE = false>
 __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * SG_STAGEB];
     // wid through readfirstlane: the compiler then knows it is wave-uniform (DW < 8 branches on it)
@@ -300,12 +304,14 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
             const int T = t.T - 128 * h;
             const _Float16* Ae = t.Ae + 128 * h * C2;
             const _Float16* Be = t.Be + 128 * h * C2;
-            const auto ar0 = __builtin_amdgcn_make_buffer_rsrc((void*)Ae, 0, (T > 0 ? T : 0) * C2 * 2, 0x00020000);
-            const auto ar1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Ae + 16 * C2), 0, (T > 16 ? T - 16 : 0) * C2 * 2,
+            const auto ar0 = __builtin_amdgcn_make_buffer_rsrc((void*)Ae, 0, PROBE ? 0 : (T > 0 ? T : 0) * C2 * 2,
                                                                0x00020000);
-            const auto br0 = __builtin_amdgcn_make_buffer_rsrc((void*)Be, 0, (K - 128 * h) * C2 * 2, 0x00020000);
-            const auto br1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Be + C2), 0, (K - 128 * h - 1) * C2 * 2,
+            const auto ar1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Ae + 16 * C2), 0,
+                                                               PROBE ? 0 : (T > 16 ? T - 16 : 0) * C2 * 2, 0x00020000);
+            const auto br0 = __builtin_amdgcn_make_buffer_rsrc((void*)Be, 0, PROBE ? 0 : (K - 128 * h) * C2 * 2,
                                                                0x00020000);
+            const auto br1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Be + C2), 0,
+                                                               PROBE ? 0 : (K - 128 * h - 1) * C2 * 2, 0x00020000);
             char* base = smem + buf * SG_STAGEB + (32 * wid + 128 * h) * SG_ROWB;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -882,7 +888,7 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
                              const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream) {
     if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % (2 * SG_BK) ||
         k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
-        variant > 5)
+        variant > 6)
         return AZG_ERR_ARG;
     SGArgs g{};
     g.A = (const _Float16*)A;
@@ -923,6 +929,9 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
                            (hipStream_t)stream, g);
     else if (variant == 5)
         hipLaunchKernelGGL(split_gemm_persist_kernel<4>, dim3(persistent_blocks(tiles)), dim3(512), 0,
+                           (hipStream_t)stream, g);
+    else if (variant == 6)
+        hipLaunchKernelGGL((split_gemm_persist_kernel<8, true>), dim3(persistent_blocks(tiles)), dim3(512), 0,
                            (hipStream_t)stream, g);
     else
         hipLaunchKernelGGL(split_gemm_w4_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, g);

@@ -37,6 +37,7 @@ F16_MFMA_PEAK_TF = 2500.0        # MI355X_MICROARCH.md: BF16/FP16 MFMA peak (den
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E spec peak
 EXPANSIONS_PER_GAME_REF = 8555   # reference random-init Inflexion episodes
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_G4096.json")
+GEMM_PMC_FILE = os.path.join(ROOT, "profiles", "r01_split_gemm_pmc_v4.json")  # the azg_split_gemm default
 PMC_FILE_WINOGRAD = {"f32": os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd.json"),
                      "split_blas": os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd_split_blas.json"),
                      "split": os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd_split.json")}
@@ -413,6 +414,13 @@ def main():
             out["roofline"]["traffic"] = pmc["conv"]
             out["roofline"]["traffic_note"] = pmc["note"]
             out["roofline_tree"]["traffic"] = pmc["tree"]
+        if split and getattr(ev, "gemm", "") == "split" and os.path.exists(GEMM_PMC_FILE):
+            d = json.load(open(GEMM_PMC_FILE))
+            out["roofline"]["mfma_busy_frac"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * d["GRBM_GUI_ACTIVE"] / 8)
+            out["roofline"]["mfma_busy_note"] = (
+                f"{os.path.relpath(GEMM_PMC_FILE, ROOT)}: SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 "
+                "XCDs) of the default split GEMM alone on conv2's shape (tools/split_gemm_pmc.py); the MFMA pipes' "
+                "busy share at the clock the chip holds under this load")
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, depth, A)
         print(json.dumps(out), flush=True)

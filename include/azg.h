@@ -210,7 +210,9 @@ int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, cons
 /* The same with an explicit kernel schedule (0: reads, then MFMAs per stage, one
  * tile per workgroup; 1: reads overlapped with MFMAs; 2: one wave per SIMD,
  * 128 x 128 per wave; 3: variant 0 with the DMA issue spread between the MFMAs;
- * 4: variant 0 persistent, the azg_split_gemm default); for tests and probes. */
+ * 4: variant 0 persistent, the azg_split_gemm default; 5: variant 4 with the DMA
+ * issued by waves 0-3; 6: timing probe of variant 4 with zero-record descriptors,
+ * results WRONG); for tests and probes. */
 int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, float* m, int32_t nruns,
                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
 
