@@ -259,7 +259,17 @@ __device__ __forceinline__ SGTile sg_tile(const SGArgs& g, int L) {
 // zero records, so the DMA moves no global data (LDS gets zeros) while the
 // instruction stream, waits and barriers stay: prices the operand traffic
 // (MI355X_MICROARCH.md / cdna_hip_programming.md, zero-record descriptor).
-template <int DW, bool PROBE = false>
+//
+// PP = true (variant 7, with DW = 4): ping-pong.  Waves 0-3 (X: one per SIMD, rows
+// 0-127 of the tile) and waves 4-7 (Y, rows 128-255) run half a stage apart, a
+// barrier per half-stage: while one wave of a SIMD reads its operands from LDS the
+// other runs its 96 MFMAs, so the MFMA pipe does not stand idle behind every
+// stage's operand reads.  X issues the DMA (its own and Y's rows) right after its
+// reads of stage j, into the buffer Y finished reading a half-stage earlier, and
+// waits for it at the end of its MFMA half-step.
+// SPR = true (variant 8): the non-ping-pong loop issues a row block's hi.hi,
+// lo.hi, hi.lo MFMAs 4 apart instead of back to back on one accumulator.
+template <int DW, bool PROBE = false, bool PP = false, bool SPR = false>
 __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * SG_STAGEB];
     // wid through readfirstlane: the compiler then knows it is wave-uniform (DW < 8 branches on it)
@@ -344,6 +354,62 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
         for (int i = 0; i < 8; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (PP) {
+            const bool X = wid < 4;
+            f16x8 ah[8], al[8], bh[4], bl[4];
+            auto read = [&](int ks) {
+                const char* st = smem + (ks & 1) * SG_STAGEB;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    bh[j] = *(const f16x8*)(st + b_hi + 16 * j * SG_ROWB);
+                    bl[j] = *(const f16x8*)(st + b_lo + 16 * j * SG_ROWB);
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    ah[i] = *(const f16x8*)(st + a_hi + 16 * i * SG_ROWB);
+                    al[i] = *(const f16x8*)(st + a_lo + 16 * i * SG_ROWB);
+                }
+            };
+            auto mma = [&]() {  // per row block: hi.hi, lo.hi, hi.lo of its 4 accumulators, 4 MFMAs apart
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                }
+            };
+            // half-step hs: X reads stage hs/2 (even hs; + the next stage's DMA) and
+            // computes stage (hs-1)/2 (odd hs); Y reads at odd hs and computes at even
+            // hs > 0, one stage behind.  One instance of each body (register phis).
+            for (int hs = 0; hs <= 2 * nks; ++hs) {
+                const bool odd = hs & 1;
+                const bool do_read = X ? (!odd && hs < 2 * nks) : odd;
+                const bool do_mma = X ? odd : (!odd && hs > 0);
+                const int ks = X ? (hs >> 1) : ((hs - 1) >> 1);
+                if (do_read) {
+                    read(ks);
+                    if (X) {
+                        if (ks + 1 < nks) issue(cur, ks + 1, (ks + 1) & 1);
+                        else if (more) issue(nxt, 0, 0);
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (do_mma) {
+                    mma();
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (X) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+            }
+        } else
         for (int ks = 0; ks < nks; ++ks) {
             const char* st = smem + (ks & 1) * SG_STAGEB;
             f16x8 ah[8], al[8], bh[4], bl[4];
@@ -360,14 +426,29 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
             if (ks + 1 < nks) issue(cur, ks + 1, (ks + 1) & 1);
             else if (more) issue(nxt, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (SPR) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+                for (int i = 0; i < 8; ++i) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
                 }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    }
+            }
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -888,7 +969,7 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
                              const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream) {
     if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % (2 * SG_BK) ||
         k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
-        variant > 6)
+        variant > 8)
         return AZG_ERR_ARG;
     SGArgs g{};
     g.A = (const _Float16*)A;
@@ -933,6 +1014,12 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
     else if (variant == 6)
         hipLaunchKernelGGL((split_gemm_persist_kernel<8, true>), dim3(persistent_blocks(tiles)), dim3(512), 0,
                            (hipStream_t)stream, g);
+    else if (variant == 7)
+        hipLaunchKernelGGL((split_gemm_persist_kernel<4, false, true>), dim3(persistent_blocks(tiles)), dim3(512), 0,
+                           (hipStream_t)stream, g);
+    else if (variant == 8)
+        hipLaunchKernelGGL((split_gemm_persist_kernel<8, false, false, true>), dim3(persistent_blocks(tiles)),
+                           dim3(512), 0, (hipStream_t)stream, g);
     else
         hipLaunchKernelGGL(split_gemm_w4_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, g);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;

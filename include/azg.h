@@ -212,7 +212,8 @@ int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, cons
  * 128 x 128 per wave; 3: variant 0 with the DMA issue spread between the MFMAs;
  * 4: variant 0 persistent, the azg_split_gemm default; 5: variant 4 with the DMA
  * issued by waves 0-3; 6: timing probe of variant 4 with zero-record descriptors,
- * results WRONG); for tests and probes. */
+ * results WRONG; 7: ping-pong, the two waves of a SIMD half a stage apart; 8:
+ * variant 4 with each accumulator's products 4 MFMAs apart); for tests and probes. */
 int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, float* m, int32_t nruns,
                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
 

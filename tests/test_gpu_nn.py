@@ -72,7 +72,7 @@ def test_azg_conv3x3_matches_torch(B, H, pad):
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 8])
 @pytest.mark.parametrize("B,H,pad", [(37, 7, 1), (129, 5, 0), (3, 6, 1)])
 def test_azg_conv3x3_variants(variant, B, H, pad):
     """Every libazg conv tile variant (incl. the LDS-DMA ring) on ragged pixel counts."""
@@ -195,7 +195,7 @@ def test_split_gemm_error_not_above_f32():
     assert errs["split_blas"] <= 1.5 * errs["f32"], errs
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 8])
 @pytest.mark.parametrize("runs,C,K", [([(25, 4096)], 512, 512), ([(3, 300), (5, 37), (2, 513)], 512, 512),
                                       ([(1, 1)], 512, 512), ([(2, 77), (1, 256)], 64, 256),
                                       ([(4, 129)], 128, 768)])
