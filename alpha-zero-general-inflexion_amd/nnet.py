@@ -22,6 +22,7 @@ import torch.nn.functional as F
 
 DEFAULT_ARGS = dict(lr=0.001, dropout=0.3, epochs=10, batch_size=512, num_channels=512)
 WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C1: 1 game)
+FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
 
 
 class InflexionNNet(nn.Module):
@@ -459,7 +460,7 @@ class InferenceNet(nn.Module):
             elif impl == "azg":
                 x = self._conv_azg(x, i, pad)
             elif impl == "winograd":
-                split_out = i == 4 and self.fc1_split and self.gemm != "f32"
+                split_out = i == 4 and self.fc1_split and self.gemm != "f32" and B >= FC1_SPLIT_MIN_BATCH
                 x = self._conv_winograd(x, i, pad, in_bias=pending, carried=carried, B=B, H=H, fuse_next=fuse_next,
                                         split_out=split_out)
                 if split_out:
