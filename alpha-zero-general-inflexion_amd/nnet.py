@@ -242,6 +242,9 @@ class InferenceNet(nn.Module):
         self.register_buffer("fb3", net.fc3.bias.detach().clone())
         self.register_buffer("fw4", net.fc4.weight.detach().clone())
         self.register_buffer("fb4", net.fc4.bias.detach().clone())
+        # fc3 and fc4 read the same activation: one GEMM over their stacked rows
+        self.register_buffer("fw34", torch.cat([self.fw3, self.fw4], dim=0).contiguous())
+        self.register_buffer("fb34", torch.cat([self.fb3, self.fb4]).contiguous())
         # sticky device flag: a split-GEMM operand fp16 could not hold (checked by check_range)
         self.register_buffer("overflow", torch.zeros(1, dtype=torch.int32))
 
@@ -486,8 +489,10 @@ class InferenceNet(nn.Module):
             x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten, no copy
             x = torch.relu_(torch.addmm(self.fb1, x, self.fw1.t()))
         x = torch.relu_(torch.addmm(self.fb2, x, self.fw2.t()))
-        p = torch.softmax(torch.addmm(self.fb3, x, self.fw3.t()), dim=1)
-        v = torch.tanh(torch.addmm(self.fb4, x, self.fw4.t()))
+        pv = torch.addmm(self.fb34, x, self.fw34.t())  # [B, A + 1]: fc3 logits | fc4
+        A = self.fw3.shape[0]
+        p = torch.softmax(pv[:, :A], dim=1)
+        v = torch.tanh(pv[:, A:])
         return p, v
 
 
