@@ -61,6 +61,7 @@ struct SGArgs {
     int total;             // tiles of all runs
     int points[SG_MAXRUNS], rows[SG_MAXRUNS], mtiles[SG_MAXRUNS], tile0[SG_MAXRUNS + 1], b_pt0[SG_MAXRUNS];
     long long a_off[SG_MAXRUNS], m_off[SG_MAXRUNS];
+    unsigned long long* stamps;  // diagnostic build only: per-wave segment cycle sums
 };
 
 // B tile row R of the LDS image (column block j = (R % 64) / 16, lane lr = R % 16 of
@@ -269,7 +270,24 @@ __device__ __forceinline__ SGTile sg_tile(const SGArgs& g, int L) {
 // waits for it at the end of its MFMA half-step.
 // SPR = true (variant 8): the non-ping-pong loop issues a row block's hi.hi,
 // lo.hi, hi.lo MFMAs 4 apart instead of back to back on one accumulator.
-template <int DW, bool PROBE = false, bool PP = false, bool SPR = false>
+// STAMP = true (azg_split_gemm_stamps, a diagnostic build, never the product path):
+// s_memtime stamps split each stage into [operand reads + DMA issue, reads landed],
+// [MFMA issue], [vmcnt(0)], [barrier] and the epilogue; per-wave sums go to g.stamps
+// (MI355X guide, in-kernel stamps: read the shares, not the length).
+__device__ __forceinline__ unsigned long long sg_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
+// DEF = true (variant 11): deferred epilogue.  A tile's accumulators are stored
+// during the next tile's first stage, each row block's four rows just before that
+// row block's first MFMAs overwrite them, so the chip-wide burst of M stores at the
+// end of every tile (all CUs finish their tiles together) runs under MFMAs instead
+// of stalling every wave (the stamp build put the epilogue at 11% of wave time).
+template <int DW, bool PROBE = false, bool PP = false, bool SPR = false, bool STAMP = false, bool DEF = false>
 __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * SG_STAGEB];
     // wid through readfirstlane: the compiler then knows it is wave-uniform (DW < 8 branches on it)
@@ -344,16 +362,35 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
     issue(cur, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    unsigned long long stq[5] = {0, 0, 0, 0, 0};
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    SGTile prev = cur;  // DEF: the tile whose accumulators are still to be stored
+    bool have_prev = false;
+    // rows 4 ch + q of row block i of tile t, 4 adjacent columns per lane (b_col)
+    auto store_rows = [&](const SGTile& t, int i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = t.m0 + wm * 128 + 16 * i + 4 * ch + q;
+            if (row < t.T)
+                *(f32x4*)(t.Me + (long long)row * K + t.n0 + wn * 64 + 4 * lr) =
+                    f32x4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
+        }
+    };
     for (int it = kb;;) {
         const int nx = it + nblk;
         const bool more = nx < cnt;
         const SGTile nxt = sg_tile(g, start + (more ? nx : it));
 
-        f32x4 acc[8][4];
+        if constexpr (!DEF) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < 8; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
         if constexpr (PP) {
             const bool X = wid < 4;
             f16x8 ah[8], al[8], bh[4], bl[4];
@@ -411,6 +448,8 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
             }
         } else
         for (int ks = 0; ks < nks; ++ks) {
+            unsigned long long t0 = 0;
+            if constexpr (STAMP) t0 = sg_stamp();
             const char* st = smem + (ks & 1) * SG_STAGEB;
             f16x8 ah[8], al[8], bh[4], bl[4];
 #pragma unroll
@@ -426,6 +465,8 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
             if (ks + 1 < nks) issue(cur, ks + 1, (ks + 1) & 1);
             else if (more) issue(nxt, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
+            unsigned long long t1 = 0;
+            if constexpr (STAMP) t1 = sg_stamp();
             if constexpr (SPR) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
@@ -441,31 +482,55 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
                 }
             } else {
 #pragma unroll
-                for (int i = 0; i < 8; ++i)
+                for (int i = 0; i < 8; ++i) {
+                    if (DEF && ks == 0) {
+                        if (have_prev) store_rows(prev, i);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
                     }
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
+            unsigned long long t2 = 0, t3 = 0, t4 = 0;
+            if constexpr (STAMP) t2 = sg_stamp();
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr (STAMP) t3 = sg_stamp();
             __syncthreads();
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int row = cur.m0 + wm * 128 + 16 * i + 4 * ch + q;
-                if (row >= cur.T) continue;
-                *(f32x4*)(cur.Me + (long long)row * K + cur.n0 + wn * 64 + 4 * lr) =
-                    f32x4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
+            if constexpr (STAMP) {
+                t4 = sg_stamp();
+                stq[0] += t1 - t0;
+                stq[1] += t2 - t1;
+                stq[2] += t3 - t2;
+                stq[3] += t4 - t3;
             }
         }
+        unsigned long long te = 0;
+        if constexpr (STAMP) te = sg_stamp();
+        if constexpr (DEF) {
+            prev = cur;
+            have_prev = true;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) store_rows(cur, i);
+        }
+        if constexpr (STAMP) stq[4] += sg_stamp() - te;
         if (!more) break;
         it = nx;
         cur = nxt;
+    }
+    if constexpr (DEF) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) store_rows(prev, i);
+    }
+    if constexpr (STAMP) {
+        if (lane == 0)
+            for (int i = 0; i < 5; ++i) g.stamps[((size_t)blockIdx.x * 8 + wid) * 5 + i] = stq[i];
     }
 }
 
@@ -966,10 +1031,11 @@ static unsigned persistent_blocks(int tiles) {
 }
 
 static int split_gemm_launch(int variant, const void* A, const void* Bt, float* M, int32_t nruns,
-                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream) {
+                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream,
+                             unsigned long long* stamps = nullptr) {
     if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % (2 * SG_BK) ||
         k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
-        variant > 8)
+        variant > 11 || variant == 9 || (variant == 10) != (stamps != nullptr))
         return AZG_ERR_ARG;
     SGArgs g{};
     g.A = (const _Float16*)A;
@@ -999,6 +1065,7 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
     }
     g.tile0[nruns] = tiles;
     g.total = tiles;
+    g.stamps = stamps;
     if (variant == 0)
         hipLaunchKernelGGL(split_gemm_kernel<false>, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 3)
@@ -1020,6 +1087,12 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
     else if (variant == 8)
         hipLaunchKernelGGL((split_gemm_persist_kernel<8, false, false, true>), dim3(persistent_blocks(tiles)),
                            dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 11)
+        hipLaunchKernelGGL((split_gemm_persist_kernel<8, false, false, false, false, true>),
+                           dim3(persistent_blocks(tiles)), dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 10)
+        hipLaunchKernelGGL((split_gemm_persist_kernel<8, false, false, false, true>), dim3(persistent_blocks(tiles)),
+                           dim3(512), 0, (hipStream_t)stream, g);
     else
         hipLaunchKernelGGL(split_gemm_w4_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, g);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
@@ -1033,4 +1106,11 @@ extern "C" int azg_split_gemm(const void* A, const void* Bt, float* M, int32_t n
 extern "C" int azg_split_gemm_variant(int32_t variant, const void* A, const void* Bt, float* M, int32_t nruns,
                                       const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream) {
     return split_gemm_launch(variant, A, Bt, M, nruns, points, rows, c, k, stream);
+}
+
+extern "C" int azg_split_gemm_stamps(const void* A, const void* Bt, float* M, int32_t nruns, const int32_t* points,
+                                     const int32_t* rows, int32_t c, int32_t k, uint64_t* stamps, int64_t cap,
+                                     void* stream) {
+    if (!stamps || cap < (int64_t)persistent_blocks(1 << 30) * 8 * 5) return AZG_ERR_ARG;
+    return split_gemm_launch(10, A, Bt, M, nruns, points, rows, c, k, stream, (unsigned long long*)stamps);
 }

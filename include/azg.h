@@ -213,9 +213,17 @@ int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, cons
  * 4: variant 0 persistent, the azg_split_gemm default; 5: variant 4 with the DMA
  * issued by waves 0-3; 6: timing probe of variant 4 with zero-record descriptors,
  * results WRONG; 7: ping-pong, the two waves of a SIMD half a stage apart; 8:
- * variant 4 with each accumulator's products 4 MFMAs apart); for tests and probes. */
+ * variant 4 with each accumulator's products 4 MFMAs apart; 11: variant 4 with each
+ * tile's stores deferred into the next tile's first stage); for tests and probes. */
 int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, float* m, int32_t nruns,
                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
+/* Diagnostic build of the default split GEMM with in-kernel s_memtime stamps
+ * (results as azg_split_gemm): per wave (block b, wave w) the cycle sums of
+ * [operand reads + DMA issue], [MFMA issue], [vmcnt wait], [barrier], [epilogue]
+ * at stamps[(b * 8 + w) * 5 + i]; cap >= CUs * 40 entries.  Its run time is not
+ * the kernel's: read the shares. */
+int  azg_split_gemm_stamps(const void* a, const void* bt, float* m, int32_t nruns, const int32_t* points,
+                           const int32_t* rows, int32_t c, int32_t k, uint64_t* stamps, int64_t cap, void* stream);
 
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active
