@@ -1,0 +1,53 @@
+"""Trainer throughput probe: NNetWrapper.train_examples (512 channels, batch 512, Adam)
+in memory-format, cudnn.benchmark, Adam and train_dtype variants, on synthetic examples.
+
+    python tools/train_probe.py > gpurun_out/train_probe.json
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import azg_amd  # noqa: E402,F401
+from azg_amd.examples import ExampleSet  # noqa: E402
+from azg_amd.inflexion import InflexionGame  # noqa: E402
+from azg_amd.nnet import NNetWrapper  # noqa: E402
+
+
+def run(label, channels_last=False, benchmark=False, batches=30, dtype="f32", fused=False):
+    torch.backends.cudnn.benchmark = benchmark
+    torch.manual_seed(0)
+    w = NNetWrapper(InflexionGame(7), dict(epochs=1, batch_size=512, fused_adam=fused, train_dtype=dtype), device="cuda")
+    if channels_last:
+        w.nnet.to(memory_format=torch.channels_last)
+    E = 512 * batches
+    g = torch.Generator(device="cpu").manual_seed(1)
+    planes = (torch.rand((E, 4, 7, 7), generator=g) < 0.3).float().cuda()
+    if channels_last:
+        planes = planes.contiguous(memory_format=torch.channels_last)
+    exs = ExampleSet(planes, torch.softmax(torch.randn((E, 343), generator=g), 1).cuda(),
+                     (torch.randint(0, 2, (E,), generator=g).float() * 2 - 1).cuda())
+    np.random.seed(0)
+    w.train_examples(ExampleSet(exs.planes[:2048], exs.pis[:2048], exs.vs[:2048]))  # warm up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    losses = w.train_examples(exs)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    row = {"form": label, "examples_per_s": E / dt, "TFLOP_per_s": E * 3 * 404.3e6 / dt / 1e12,
+           "final_losses": losses[-1].tolist()}
+    print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    run("nchw")
+    run("nchw+benchmark", benchmark=True)
+    run("channels_last", channels_last=True)
+    run("channels_last+benchmark", channels_last=True, benchmark=True)
+    run("nchw+fused_adam", fused=True)
+    run("nchw+bf16_autocast", dtype="bf16")
+    run("nchw+bf16_autocast+fused_adam", dtype="bf16", fused=True)
