@@ -534,6 +534,158 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
     }
 }
 
+// Variant 12: ping-pong with the DMA split evenly and one stage stream across tiles.
+// Waves 0-3 (X, rows 0-127 of the tile, one per SIMD) and 4-7 (Y, rows 128-255) run
+// half a stage apart, one barrier per half-step: while one wave of a SIMD reads its
+// operands the other runs its 96 MFMAs.  Every wave issues the DMA of its own 32 LDS
+// rows (as variant 4), X for stage s + 1 right after its reads of stage s, Y for
+// stage s + 2 right after its reads of stage s (into the buffer it has just read;
+// X read it a half-step earlier), so both groups' reading half-steps carry 8 DMA
+// issues per wave (variant 7 put all 16 on X).  The stages of a block's tiles form
+// one stream (s = tile * nks + k-stage): a group stores its accumulators right after
+// its last MFMA half-step of a tile, and the other group keeps computing meanwhile,
+// so no half-step stands empty between tiles.  Landing: X waits vmcnt(0) at the end
+// of its MFMA half-step (its stage s + 1 part); Y at the end of its reading
+// half-step waits for all but the 8 DMA pieces it has just issued (its stage s + 1
+// part, issued a stage earlier), before the barrier that precedes X's read of s + 1.
+__global__ __launch_bounds__(512, 1) void split_gemm_pp2_kernel(SGArgs g) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * SG_STAGEB];
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int C = g.C, K = g.K, C2 = 2 * C;
+    const int xcd = blockIdx.x % 8, kb = blockIdx.x / 8;
+    const int nblk = ((int)gridDim.x - xcd + 7) / 8;
+    const int q8 = g.total / 8, rr = g.total % 8;
+    const int start = xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8;
+    const int cnt = q8 + (xcd < rr ? 1 : 0);
+    if (kb >= cnt) return;  // uniform over the workgroup
+    const int nks = C / SG_BK;
+    const int S = ((cnt - kb + nblk - 1) / nblk) * nks;  // this block's stages
+    const bool X = wid < 4;
+
+    int arow[2], brow[2], dcol[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int R = 32 * wid + 8 * i + (lane >> 3);
+        const int lc = (lane & 7) ^ ((R >> 1) & 7);
+        dcol[i] = lc < 4 ? 8 * lc : C + 8 * (lc - 4);
+        arow[i] = R;
+        brow[i] = b_col(R);
+    }
+    const int wm = wid >> 2, wn = wid & 3;
+    const int lr = lane & 15, sw = lr >> 1;
+    const int ch = lane >> 4;
+    const int a_hi = (wm * 128 + lr) * SG_ROWB + 16 * (ch ^ sw);
+    const int a_lo = (wm * 128 + lr) * SG_ROWB + 16 * ((4 + ch) ^ sw);
+    const int b_hi = SG_TILEB + (wn * 64 + lr) * SG_ROWB + 16 * (ch ^ sw);
+    const int b_lo = SG_TILEB + (wn * 64 + lr) * SG_ROWB + 16 * ((4 + ch) ^ sw);
+
+    auto tile_of = [&](int s) { return sg_tile(g, start + kb + (s / nks) * nblk); };
+    // this wave's 8 DMA pieces of stream stage s (its 32 rows of A and of B)
+    auto issue = [&](int s) {
+        const SGTile t = tile_of(s);
+        const int ks = s % nks;
+        const int T = t.T;
+        const auto ar0 = __builtin_amdgcn_make_buffer_rsrc((void*)t.Ae, 0, T * C2 * 2, 0x00020000);
+        const auto ar1 = __builtin_amdgcn_make_buffer_rsrc((void*)(t.Ae + 16 * C2), 0, (T > 16 ? T - 16 : 0) * C2 * 2,
+                                                           0x00020000);
+        const auto br0 = __builtin_amdgcn_make_buffer_rsrc((void*)t.Be, 0, K * C2 * 2, 0x00020000);
+        const auto br1 = __builtin_amdgcn_make_buffer_rsrc((void*)(t.Be + C2), 0, (K - 1) * C2 * 2, 0x00020000);
+        char* base = smem + (s & 1) * SG_STAGEB + (32 * wid) * SG_ROWB;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
+                                                     (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
+                                                     16, ((t.m0 + arow[i & 1]) * C2 + dcol[i & 1]) * 2,
+                                                     ks * SG_BK * 2, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
+                                                     (__attribute__((address_space(3))) void*)(base + SG_TILEB +
+                                                                                              8 * i * SG_ROWB),
+                                                     16, ((t.n0 + brow[i & 1]) * C2 + dcol[i & 1]) * 2,
+                                                     ks * SG_BK * 2, 0, 0);
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f16x8 ah[8], al[8], bh[4], bl[4];
+
+    issue(0);
+    if (!X && S > 1) issue(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    // half-step hs: X reads stage hs/2 (even hs) and computes stage (hs-1)/2 (odd hs);
+    // Y reads stage (hs-1)/2 (odd hs) and computes stage hs/2 - 1 (even hs > 0)
+    for (int hs = 0; hs <= 2 * S; ++hs) {
+        const bool odd = hs & 1;
+        const bool do_read = X ? (!odd && hs < 2 * S) : odd;
+        const bool do_mma = X ? odd : (!odd && hs > 0);
+        const int s = odd ? (hs - 1) >> 1 : (X ? hs >> 1 : (hs >> 1) - 1);
+        bool issued = false;
+        if (do_read) {
+            const char* st = smem + (s & 1) * SG_STAGEB;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bh[j] = *(const f16x8*)(st + b_hi + 16 * j * SG_ROWB);
+                bl[j] = *(const f16x8*)(st + b_lo + 16 * j * SG_ROWB);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                ah[i] = *(const f16x8*)(st + a_hi + 16 * i * SG_ROWB);
+                al[i] = *(const f16x8*)(st + a_lo + 16 * i * SG_ROWB);
+            }
+            if (X) {
+                if (s + 1 < S) issue(s + 1);  // the other buffer: both groups finished stage s - 1
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this buffer's reads landed ...
+                if (s + 2 < S) {                                      // ... before it is refilled
+                    issue(s + 2);
+                    issued = true;
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (do_mma) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                }
+            if ((s + 1) % nks == 0) {  // the tile's last stage: store and clear
+                const SGTile t = tile_of(s);
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int row = t.m0 + wm * 128 + 16 * i + 4 * ch + q;
+                        if (row < t.T)
+                            *(f32x4*)(t.Me + (long long)row * K + t.n0 + wn * 64 + 4 * lr) =
+                                f32x4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
+                    }
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (odd) {
+            if (X || !issued) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Variant 1: the stage's 96 MFMAs in 4 phases of 2 row blocks (24 MFMAs);
 // each phase's ds_reads (the next phase's A fragments; in phase 3 the next stage's
@@ -1035,7 +1187,7 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
                              unsigned long long* stamps = nullptr) {
     if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % (2 * SG_BK) ||
         k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
-        variant > 11 || variant == 9 || (variant == 10) != (stamps != nullptr))
+        variant > 12 || variant == 9 || (variant == 10) != (stamps != nullptr))
         return AZG_ERR_ARG;
     SGArgs g{};
     g.A = (const _Float16*)A;
@@ -1090,6 +1242,8 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
     else if (variant == 11)
         hipLaunchKernelGGL((split_gemm_persist_kernel<8, false, false, false, false, true>),
                            dim3(persistent_blocks(tiles)), dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 12)
+        hipLaunchKernelGGL(split_gemm_pp2_kernel, dim3(persistent_blocks(tiles)), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 10)
         hipLaunchKernelGGL((split_gemm_persist_kernel<8, false, false, false, true>), dim3(persistent_blocks(tiles)),
                            dim3(512), 0, (hipStream_t)stream, g);

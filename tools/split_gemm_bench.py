@@ -87,7 +87,7 @@ def main():
 
         flops16 = 3 * 2.0 * rows * C * K
         row = {"layer": name, "runs": runs}
-        fns = [("azg_v%d" % v, azg_variant(v)) for v in (0, 4, 8, 11)] + [("hipblaslt_split", blas),
+        fns = [("azg_v%d" % v, azg_variant(v)) for v in (0, 4, 7, 12)] + [("hipblaslt_split", blas),
                                                                          ("hipblaslt_f32", f32)]
         for k, (med, mn) in time_all(fns).items():
             fl = flops16 if k != "hipblaslt_f32" else flops16 / 3
