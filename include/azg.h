@@ -214,7 +214,8 @@ int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, cons
  * issued by waves 0-3; 6: timing probe of variant 4 with zero-record descriptors,
  * results WRONG; 7: ping-pong, the two waves of a SIMD half a stage apart; 8:
  * variant 4 with each accumulator's products 4 MFMAs apart; 11: variant 4 with each
- * tile's stores deferred into the next tile's first stage); for tests and probes. */
+ * tile's stores deferred into the next tile's first stage; 12: ping-pong with each
+ * wave's own DMA and one stage stream across tiles); for tests and probes. */
 int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, float* m, int32_t nruns,
                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
 /* Diagnostic build of the default split GEMM with in-kernel s_memtime stamps
