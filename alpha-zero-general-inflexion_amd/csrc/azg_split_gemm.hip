@@ -6,8 +6,9 @@
 //     M = Vh Uh + Vl Uh + Vh Ul      (the 2^-22 Vl Ul term dropped)
 // computed by v_mfma_f32_16x16x32_f16 with f32 accumulation: f32-accurate products
 //  at the fp16 MFMA rate.  Operands are stored once per half:
-//   A = V_e : [T][2C] fp16 rows [hi(C) | lo(C)]     (the transforms write them)
-//   B = U_e : [K][2C] fp16 rows [hi(C) | lo(C)]     (U^T, formed once per weight set)
+//   A = V_e : [T][2C] fp16 rows of 32-channel blocks [hi(32) | lo(32)] (the transforms
+//             write them, AZG_WINO_SPLIT2)
+//   B = U_e : [K][2C] fp16 rows, the same blocks (U^T, formed once per weight set)
 // i.e. 4 bytes per operand element, as f32, where a library GEMM needs the A
 // row [hi | lo | hi] (6 bytes).  U is pre-scaled by a power of two that the
 // output transform undoes.
@@ -52,6 +53,10 @@ constexpr int SG_ROWB = 128;                 // LDS bytes per tile row per stage
 constexpr int SG_TILEB = SG_BM * SG_ROWB;    // 32 KB per operand per stage
 constexpr int SG_STAGEB = 2 * SG_TILEB;      // A then B
 constexpr int SG_MAXRUNS = 4;
+// Operand rows are 32-channel blocks [hi(32) | lo(32)] (AZG_WINO_SPLIT2): stage ks of a
+// row is the one 128-B line at byte 128 ks, logical chunk lc (hi 8 lc.. for lc < 4, lo
+// 8 (lc - 4).. after) at 16 lc within it.
+constexpr int SG_STAGE_SOFF = 2 * SG_BK * 2;
 
 struct SGArgs {
     const _Float16* A;
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
     for (int i = 0; i < 2; ++i) {
         const int R = 32 * wid + 8 * i + (lane >> 3);
         const int lc = (lane & 7) ^ ((R >> 1) & 7);
-        const int col = lc < 4 ? 8 * lc : C + 8 * (lc - 4);
+        const int col = 8 * lc;
         aoff[i] = ((m0 + R) * C2 + col) * 2;
         boff[i] = ((n0 + b_col(R)) * C2 + col) * 2;
     }
@@ -132,13 +137,13 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
         for (int i = 0; i < 4; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
                                                      (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
-                                                     16, aoff[i & 1], ks * SG_BK * 2, 0, 0);
+                                                     16, aoff[i & 1], ks * SG_STAGE_SOFF, 0, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
                                                      (__attribute__((address_space(3))) void*)(base + SG_TILEB +
                                                                                               8 * i * SG_ROWB),
-                                                     16, boff[i & 1], ks * SG_BK * 2, 0, 0);
+                                                     16, boff[i & 1], ks * SG_STAGE_SOFF, 0, 0);
     };
     // DMA piece p of a stage (p < 4: A row group p, else B row group p - 4)
     auto issue_piece = [&](int ks, int buf, int p) {
@@ -147,12 +152,12 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
         if (p < 4)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 2 ? ar0 : ar1,
                                                      (__attribute__((address_space(3))) void*)(base + 8 * q * SG_ROWB),
-                                                     16, aoff[q & 1], ks * SG_BK * 2, 0, 0);
+                                                     16, aoff[q & 1], ks * SG_STAGE_SOFF, 0, 0);
         else
             __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 2 ? br0 : br1,
                                                      (__attribute__((address_space(3))) void*)(base + SG_TILEB +
                                                                                               8 * q * SG_ROWB),
-                                                     16, boff[q & 1], ks * SG_BK * 2, 0, 0);
+                                                     16, boff[q & 1], ks * SG_STAGE_SOFF, 0, 0);
     };
 
     // operand reads: wave (wm, wn) = rows 128 wm.., cols 64 wn..; lane holds row lane%16
@@ -287,7 +292,11 @@ __device__ __forceinline__ unsigned long long sg_stamp() {
 // row block's first MFMAs overwrite them, so the chip-wide burst of M stores at the
 // end of every tile (all CUs finish their tiles together) runs under MFMAs instead
 // of stalling every wave (the stamp build put the epilogue at 11% of wave time).
-template <int DW, bool PROBE = false, bool PP = false, bool SPR = false, bool STAMP = false, bool DEF = false>
+// PZ = 1 / 2 (variants 15 / 16, timing probes only, wrong results): as PROBE, but only
+// the B (15) or only the A (16) descriptors have zero records, pricing each operand's
+// share of the global -> LDS feed.
+template <int DW, bool PROBE = false, bool PP = false, bool SPR = false, bool STAMP = false, bool DEF = false,
+          int PZ = 0>
 __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * SG_STAGEB];
     // wid through readfirstlane: the compiler then knows it is wave-uniform (DW < 8 branches on it)
@@ -311,7 +320,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
     for (int i = 0; i < 2; ++i) {
         const int R = 32 * wid + 8 * i + (lane >> 3);
         const int lc = (lane & 7) ^ ((R >> 1) & 7);
-        dcol[i] = lc < 4 ? 8 * lc : C + 8 * (lc - 4);
+        dcol[i] = 8 * lc;
         arow[i] = R;
         brow[i] = b_col(R);
     }
@@ -332,28 +341,29 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
             const int T = t.T - 128 * h;
             const _Float16* Ae = t.Ae + 128 * h * C2;
             const _Float16* Be = t.Be + 128 * h * C2;
-            const auto ar0 = __builtin_amdgcn_make_buffer_rsrc((void*)Ae, 0, PROBE ? 0 : (T > 0 ? T : 0) * C2 * 2,
+            constexpr bool ZA = PROBE || PZ == 2, ZB = PROBE || PZ == 1;
+            const auto ar0 = __builtin_amdgcn_make_buffer_rsrc((void*)Ae, 0, ZA ? 0 : (T > 0 ? T : 0) * C2 * 2,
                                                                0x00020000);
             const auto ar1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Ae + 16 * C2), 0,
-                                                               PROBE ? 0 : (T > 16 ? T - 16 : 0) * C2 * 2, 0x00020000);
-            const auto br0 = __builtin_amdgcn_make_buffer_rsrc((void*)Be, 0, PROBE ? 0 : (K - 128 * h) * C2 * 2,
+                                                               ZA ? 0 : (T > 16 ? T - 16 : 0) * C2 * 2, 0x00020000);
+            const auto br0 = __builtin_amdgcn_make_buffer_rsrc((void*)Be, 0, ZB ? 0 : (K - 128 * h) * C2 * 2,
                                                                0x00020000);
             const auto br1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Be + C2), 0,
-                                                               PROBE ? 0 : (K - 128 * h - 1) * C2 * 2, 0x00020000);
+                                                               ZB ? 0 : (K - 128 * h - 1) * C2 * 2, 0x00020000);
             char* base = smem + buf * SG_STAGEB + (32 * wid + 128 * h) * SG_ROWB;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
                                                          (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
                                                          16, ((t.m0 + arow[i & 1]) * C2 + dcol[i & 1]) * 2,
-                                                         ks * SG_BK * 2, 0, 0);
+                                                         ks * SG_STAGE_SOFF, 0, 0);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
                                                          (__attribute__((address_space(3))) void*)(base + SG_TILEB +
                                                                                                   8 * i * SG_ROWB),
                                                          16, ((t.n0 + brow[i & 1]) * C2 + dcol[i & 1]) * 2,
-                                                         ks * SG_BK * 2, 0, 0);
+                                                         ks * SG_STAGE_SOFF, 0, 0);
         }
     };
 
@@ -567,7 +577,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_pp2_kernel(SGArgs g) {
     for (int i = 0; i < 2; ++i) {
         const int R = 32 * wid + 8 * i + (lane >> 3);
         const int lc = (lane & 7) ^ ((R >> 1) & 7);
-        dcol[i] = lc < 4 ? 8 * lc : C + 8 * (lc - 4);
+        dcol[i] = 8 * lc;
         arow[i] = R;
         brow[i] = b_col(R);
     }
@@ -596,14 +606,14 @@ __global__ __launch_bounds__(512, 1) void split_gemm_pp2_kernel(SGArgs g) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
                                                      (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
                                                      16, ((t.m0 + arow[i & 1]) * C2 + dcol[i & 1]) * 2,
-                                                     ks * SG_BK * 2, 0, 0);
+                                                     ks * SG_STAGE_SOFF, 0, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
                                                      (__attribute__((address_space(3))) void*)(base + SG_TILEB +
                                                                                               8 * i * SG_ROWB),
                                                      16, ((t.n0 + brow[i & 1]) * C2 + dcol[i & 1]) * 2,
-                                                     ks * SG_BK * 2, 0, 0);
+                                                     ks * SG_STAGE_SOFF, 0, 0);
     };
 
     f32x4 acc[8][4];
@@ -805,7 +815,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_pipe_kernel(SGArgs g) {
     for (int i = 0; i < 2; ++i) {
         const int R = 32 * wid + 8 * i + (lane >> 3);
         const int lc = (lane & 7) ^ ((R >> 1) & 7);
-        const int col = lc < 4 ? 8 * lc : C + 8 * (lc - 4);
+        const int col = 8 * lc;
         aoff[i] = ((m0 + R) * C2 + col) * 2;
         boff[i] = ((n0 + b_col(R)) * C2 + col) * 2;
     }
@@ -817,13 +827,13 @@ __global__ __launch_bounds__(512, 1) void split_gemm_pipe_kernel(SGArgs g) {
         for (int i = 0; i < 4; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
                                                      (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
-                                                     16, aoff[i & 1], ks * SG_BK * 2, 0, 0);
+                                                     16, aoff[i & 1], ks * SG_STAGE_SOFF, 0, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
                                                      (__attribute__((address_space(3))) void*)(base + 2 * SG_TILEB +
                                                                                               8 * i * SG_ROWB),
-                                                     16, boff[i & 1], ks * SG_BK * 2, 0, 0);
+                                                     16, boff[i & 1], ks * SG_STAGE_SOFF, 0, 0);
     };
 
     const int wm = wid >> 2, wn = wid & 3;
@@ -1032,14 +1042,14 @@ __global__ __launch_bounds__(256, 1) void split_gemm_w4_kernel(SGArgs g) {
     for (int i = 0; i < 2; ++i) {
         const int R = 64 * wid + 8 * i + (lane >> 3);
         const int lc = (lane & 7) ^ ((R >> 1) & 7);
-        const int col = lc < 4 ? 8 * lc : C + 8 * (lc - 4);
+        const int col = 8 * lc;
         aoff[i] = ((m0 + R) * C2 + col) * 2;
         boff[i] = ((n0 + b_col128(R)) * C2 + col) * 2;
     }
     auto issue = [&](int ks, int buf) {
         char* abase = smem + buf * W4_TILEB + (64 * wid) * W4_ROWB;
         char* bbase = abase + 2 * W4_TILEB;
-        const int so = ks * SG_BK * 2;
+        const int so = ks * SG_STAGE_SOFF;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const auto rs = i < 2 ? ar0 : i < 4 ? ar1 : i < 6 ? ar2 : ar3;
@@ -1187,7 +1197,7 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
                              unsigned long long* stamps = nullptr) {
     if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % (2 * SG_BK) ||
         k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
-        variant > 12 || variant == 9 || (variant == 10) != (stamps != nullptr))
+        variant > 16 || variant == 9 || variant == 13 || variant == 14 || (variant == 10) != (stamps != nullptr))
         return AZG_ERR_ARG;
     SGArgs g{};
     g.A = (const _Float16*)A;
@@ -1244,6 +1254,12 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
                            dim3(persistent_blocks(tiles)), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 12)
         hipLaunchKernelGGL(split_gemm_pp2_kernel, dim3(persistent_blocks(tiles)), dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 15)
+        hipLaunchKernelGGL((split_gemm_persist_kernel<8, false, false, false, false, false, 1>),
+                           dim3(persistent_blocks(tiles)), dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 16)
+        hipLaunchKernelGGL((split_gemm_persist_kernel<8, false, false, false, false, false, 2>),
+                           dim3(persistent_blocks(tiles)), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 10)
         hipLaunchKernelGGL((split_gemm_persist_kernel<8, false, false, false, true>), dim3(persistent_blocks(tiles)),
                            dim3(512), 0, (hipStream_t)stream, g);

@@ -167,8 +167,9 @@ __device__ __forceinline__ void out_tile(const T (&mm)[MA + 2][MB + 2], T (&y)[M
 }
 
 // One V element: f32 (FMT 0); its fp16 (hi, lo, hi) at columns c, C + c, 2C + c of
-// a 3C-wide row (FMT 1, AZG_WINO_SPLIT); or (hi, lo) at c, C + c of a 2C-wide row
-// (FMT 2, AZG_WINO_SPLIT2).
+// a 3C-wide row (FMT 1, AZG_WINO_SPLIT); or (hi, lo) in a 2C-wide row of 32-channel
+// blocks [hi(32) | lo(32)], at 64 (c / 32) + c % 32 and 32 further (FMT 2,
+// AZG_WINO_SPLIT2: a split-GEMM stage of 32 channels is one 128-B line per row).
 template <int FMT>
 __device__ __forceinline__ void store_v(void* V, long long row, int C, int c, float v, int* overflow) {
     if constexpr (FMT == AZG_WINO_F32) {
@@ -177,9 +178,15 @@ __device__ __forceinline__ void store_v(void* V, long long row, int C, int c, fl
         const _Float16 hi = (_Float16)v;  // round to nearest even
         const _Float16 lo = (_Float16)(v - (float)hi);
         _Float16* r = (_Float16*)V + row * (FMT == AZG_WINO_SPLIT ? 3 : 2) * C;
-        r[c] = hi;
-        r[C + c] = lo;
-        if constexpr (FMT == AZG_WINO_SPLIT) r[2 * C + c] = hi;
+        if constexpr (FMT == AZG_WINO_SPLIT) {
+            r[c] = hi;
+            r[C + c] = lo;
+            r[2 * C + c] = hi;
+        } else {
+            const int o = 64 * (c >> 5) + (c & 31);
+            r[o] = hi;
+            r[o + 32] = lo;
+        }
         if (!(fabsf(v) <= 65504.f)) atomicOr(overflow, 1);
     }
 }
@@ -203,9 +210,15 @@ __device__ __forceinline__ void store_v(void* V, long long row, int C4, int c4, 
             bad |= !(fabsf(x[j]) <= 65504.f);
         }
         uint2* r = (uint2*)V + row * (FMT == AZG_WINO_SPLIT ? 3 : 2) * C4;
-        r[c4] = hi.u;
-        r[C4 + c4] = lo.u;
-        if constexpr (FMT == AZG_WINO_SPLIT) r[2 * C4 + c4] = hi.u;
+        if constexpr (FMT == AZG_WINO_SPLIT) {
+            r[c4] = hi.u;
+            r[C4 + c4] = lo.u;
+            r[2 * C4 + c4] = hi.u;
+        } else {  // 32-channel blocks: 8 uint2 of hi, then 8 of lo
+            const int o = 16 * (c4 >> 3) + (c4 & 7);
+            r[o] = hi.u;
+            r[o + 8] = lo.u;
+        }
         if (bad) atomicOr(overflow, 1);
     }
 }
@@ -486,6 +499,7 @@ extern "C" int azg_winograd_in_nhwc(const float* x, const float* in_bias, void* 
     const int h_out = h_in + 2 * pad - 2;
     if (!x || !V || batch <= 0 || h_out <= 0 || h_out > 64 || c <= 0 || c % 4 || ((uintptr_t)x & 15) ||
         ((uintptr_t)V & 15) || ((uintptr_t)in_bias & 15) || bad_fmt(vfmt, overflow) ||
+        (vfmt == AZG_WINO_SPLIT2 && c % 32) ||
         (long long)batch * h_out * h_out * (c / 4) > (1ll << 38))
         return AZG_ERR_ARG;
     const WSeq S(h_out);
@@ -519,6 +533,7 @@ extern "C" int azg_winograd_out_split(const float* M, const float* bias, void* y
                                       void* stream) {
     if (!M || !bias || !y || batch <= 0 || h_out <= 0 || h_out > 64 || k <= 0 || k % 4 || ((uintptr_t)M & 15) ||
         ((uintptr_t)bias & 15) || ((uintptr_t)y & 15) || vfmt == AZG_WINO_F32 || bad_fmt(vfmt, overflow) ||
+        (vfmt == AZG_WINO_SPLIT2 && k % 32) ||
         (long long)h_out * h_out * k > (1ll << 28) || (long long)batch * h_out * h_out * (k / 4) > (1ll << 38))
         return AZG_ERR_ARG;
     const WSeq S(h_out);

@@ -148,13 +148,29 @@ def _split_u(u):
     return hi, lo, 2.0 ** -k
 
 
+def split2_rows(hi, lo):
+    """[..., C] hi and lo halves -> [..., 2C] rows of 32-channel blocks [hi(32) | lo(32)]
+    (azg.h AZG_WINO_SPLIT2, the split GEMM's operand layout)."""
+    sh = hi.shape
+    return torch.cat([hi.reshape(*sh[:-1], sh[-1] // 32, 32), lo.reshape(*sh[:-1], sh[-1] // 32, 32)],
+                     dim=-1).reshape(*sh[:-1], 2 * sh[-1]).contiguous()
+
+
+def split2_halves(rows):
+    """Inverse of split2_rows: [..., 2C] -> (hi, lo) [..., C]."""
+    sh = rows.shape
+    b = rows.reshape(*sh[:-1], sh[-1] // 64, 64)
+    return b[..., :32].reshape(*sh[:-1], sh[-1] // 2), b[..., 32:].reshape(*sh[:-1], sh[-1] // 2)
+
+
 def _split_operands(u, gemm):
-    """Operand B of the split GEMM form: "split" (libazg azg_split_gemm): U^T rows
-    [hi | lo], [points][K][2C]; "split_blas" (hipBLASLt): [hi; hi; lo] stacked along C,
-    [points][3C][K], to meet V's [hi | lo | hi] rows.  Returns (B, 2^-k)."""
+    """Operand B of the split GEMM form: "split" (libazg azg_split_gemm): U^T rows of
+    32-channel blocks [hi(32) | lo(32)], [points][K][2C] (as V in AZG_WINO_SPLIT2);
+    "split_blas" (hipBLASLt): [hi; hi; lo] stacked along C, [points][3C][K], to meet V's
+    [hi | lo | hi] rows.  Returns (B, 2^-k)."""
     hi, lo, scale = _split_u(u)
     if gemm == "split":
-        return torch.cat([hi.transpose(1, 2), lo.transpose(1, 2)], dim=2).contiguous(), scale
+        return split2_rows(hi.transpose(1, 2), lo.transpose(1, 2)), scale
     return torch.cat([hi, hi, lo], dim=1).contiguous(), scale
 
 

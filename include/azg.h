@@ -167,8 +167,9 @@ int  azg_conv3x3_variant(int variant, const float* x, const float* wt, const flo
  *                          (times mscale^-1, a power of two, for split V);
  *   azg_winograd_out_nhwc: M f32 (rows of k) -> y NHWC [batch, h_out, h_out, k] =
  *                          A^T (mscale M) A + bias, ReLU if relu != 0.
- * V formats: AZG_WINO_F32 f32 rows of c; AZG_WINO_SPLIT2 fp16 rows of 2c = [hi | lo]
- * (the A operand of azg_split_gemm); AZG_WINO_SPLIT fp16 rows of 3c =
+ * V formats: AZG_WINO_F32 f32 rows of c; AZG_WINO_SPLIT2 fp16 rows of 2c in 32-channel
+ * blocks [hi(32) | lo(32)] (channel j's hi at 64 (j / 32) + j % 32, its lo 32 further;
+ * c % 32 == 0; the A operand of azg_split_gemm); AZG_WINO_SPLIT fp16 rows of 3c =
  * [hi | lo | hi], hi = fp16(v), lo = fp16(v - hi) -- the A operand of the
  * error-compensated GEMM [hi|lo|hi] x [Uh; Uh; Ul] (f32 accumulation); a value
  * fp16 cannot hold (|v| > 65504, NaN) sets *overflow (device int, required).
@@ -201,9 +202,10 @@ int  azg_winograd_first_nchw(const float* planes, const float* w1, const float* 
 /* The Winograd GEMMs of one layer as an error-compensated fp16 MFMA GEMM
  * (azg_split_gemm.hip): for every point e of nruns runs (run r: points[r]
  * points with rows[r] rows each, stored one after another),
- *   M_e [rows x k] f32 = A_e x B_e^T,  A_e [rows][2c] fp16 rows [hi | lo] (V in
- *   AZG_WINO_SPLIT2), B_e [k][2c] fp16 rows [hi | lo] (U^T, points of all runs in
- *   order), computed as hi.hi + lo.hi + hi.lo with f32 accumulation.
+ *   M_e [rows x k] f32 = A_e x B_e^T,  A_e [rows][2c] fp16 rows of 32-channel
+ *   [hi | lo] blocks (V in AZG_WINO_SPLIT2), B_e [k][2c] fp16 rows in the same blocks
+ *   (U^T, points of all runs in order), computed as hi.hi + lo.hi + hi.lo with f32
+ *   accumulation.
  * c % 64 == 0, k % 256 == 0, nruns <= 4, 16-B aligned pointers. */
 int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, const int32_t* points,
                     const int32_t* rows, int32_t c, int32_t k, void* stream);

@@ -206,6 +206,7 @@ def test_split_gemm_kernel_matches_reference(variant, runs, C, K):
     import ctypes
     import azg_amd  # noqa: F401
     from azg_amd import _lib
+    from azg_amd.nnet import split2_halves
     torch.manual_seed(7)
     P = sum(p for p, _ in runs)
     A = torch.cat([torch.randn(p * t, 2 * C, device="cuda").half() for p, t in runs]).contiguous()
@@ -222,7 +223,7 @@ def test_split_gemm_kernel_matches_reference(variant, runs, C, K):
     for p, t in runs:
         a = A[a_row:a_row + p * t].view(p, t, 2 * C).double()
         b = Bt[pt:pt + p].double()
-        ah, al, bh, bl = a[..., :C], a[..., C:], b[..., :C], b[..., C:]
+        (ah, al), (bh, bl) = split2_halves(a), split2_halves(b)  # 32-channel [hi | lo] blocks
         want = ah @ bh.transpose(1, 2) + al @ bh.transpose(1, 2) + ah @ bl.transpose(1, 2)
         got = M[m_row * K:(m_row + p * t) * K].view(p, t, K).double()
         scale = want.abs().max().item()

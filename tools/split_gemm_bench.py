@@ -16,6 +16,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import azg_amd  # noqa: E402,F401
 from azg_amd import _lib  # noqa: E402
 
+# AZG_SG_VARIANTS="4,6,15,16" times the probes instead (6/15/16 give wrong results by design)
+VARIANTS = tuple(int(v) for v in os.environ.get("AZG_SG_VARIANTS", "0,4,7,12").split(","))
 LAYERS = {"conv2": [(25, 4096), (40, 8192), (16, 16384)], "conv3": [(81, 4096)], "conv4": [(25, 4096)]}
 
 
@@ -87,7 +89,7 @@ def main():
 
         flops16 = 3 * 2.0 * rows * C * K
         row = {"layer": name, "runs": runs}
-        fns = [("azg_v%d" % v, azg_variant(v)) for v in (0, 4, 7, 12)] + [("hipblaslt_split", blas),
+        fns = [("azg_v%d" % v, azg_variant(v)) for v in VARIANTS] + [("hipblaslt_split", blas),
                                                                          ("hipblaslt_f32", f32)]
         for k, (med, mn) in time_all(fns).items():
             fl = flops16 if k != "hipblaslt_f32" else flops16 / 3

@@ -4,6 +4,8 @@
 //   mode 0: as today, [hi(512) | lo(512)] rows: two 2-byte stores per point (128 B per
 //           wave-instruction each)
 //   mode 1: [hi0 lo0 hi1 lo1 ...] rows: one 4-byte store per point (256 B per instruction)
+//   mode 2: 32-channel blocks [hi(32) | lo(32)] (AZG_WINO_SPLIT2): two 2-byte stores per
+//           point, each two 64-B pieces
 // Same bytes, same grid; prints TB/s per mode.  Build and run:
 //   hipcc --offload-arch=gfx950 -O3 -o tools/store_probe tools/store_probe.hip && tools/store_probe
 #include <hip/hip_runtime.h>
@@ -24,6 +26,10 @@ __global__ __launch_bounds__(64) void store_kernel(_Float16* V, float seed) {
         if constexpr (MODE == 0) {
             row[c] = hi;
             row[C + c] = lo;
+        } else if constexpr (MODE == 2) {
+            const int o = 64 * (c >> 5) + (c & 31);
+            row[o] = hi;
+            row[o + 32] = lo;
         } else {
             union {
                 _Float16 h[2];
@@ -45,10 +51,11 @@ int main() {
     hipEventCreate(&b);
     const dim3 grid(IMAGES * (C / 64)), block(64);
     for (int round = 0; round < 3; ++round)
-        for (int mode = 0; mode < 2; ++mode) {
+        for (int mode = 0; mode < 3; ++mode) {
             auto launch = [&]() {
                 if (mode == 0) hipLaunchKernelGGL(store_kernel<0>, grid, block, 0, 0, V, 0.37f);
-                else hipLaunchKernelGGL(store_kernel<1>, grid, block, 0, 0, V, 0.37f);
+                else if (mode == 1) hipLaunchKernelGGL(store_kernel<1>, grid, block, 0, 0, V, 0.37f);
+                else hipLaunchKernelGGL(store_kernel<2>, grid, block, 0, 0, V, 0.37f);
             };
             for (int w = 0; w < 3; ++w) launch();
             hipEventRecord(a);
