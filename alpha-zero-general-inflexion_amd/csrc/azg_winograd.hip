@@ -191,6 +191,23 @@ __device__ __forceinline__ void store_v(void* V, long long row, int C, int c, fl
     }
 }
 
+// One V element per lane of a full wave whose lanes hold 64 consecutive channels
+// c0 + lane (c0 % 64 == 0), in AZG_WINO_SPLIT2: one v_permlane32_swap turns (hi, lo)
+// into the two 32-channel blocks [hi(32) | lo(32)] as they lie in the row, so each of
+// the two stores writes one whole 128-B line (per-lane stores would write each line
+// in two 64-B halves from two instructions).
+__device__ __forceinline__ void store_v2_wave(void* V, long long row, int C, int c0, int lane, float v,
+                                              int* overflow) {
+    const _Float16 hi = (_Float16)v;  // round to nearest even
+    const _Float16 lo = (_Float16)(v - (float)hi);
+    const auto sw = __builtin_amdgcn_permlane32_swap((unsigned)__builtin_bit_cast(unsigned short, hi),
+                                                     (unsigned)__builtin_bit_cast(unsigned short, lo), false, false);
+    unsigned short* r = (unsigned short*)V + row * 2 * C + 2 * c0 + lane;
+    r[0] = (unsigned short)sw[0];   // lanes 0-31: hi of c0 + lane; 32-63: lo of c0 + lane - 32
+    r[64] = (unsigned short)sw[1];  // the same for channels c0 + 32 ..
+    if (!(fabsf(v) <= 65504.f)) atomicOr(overflow, 1);
+}
+
 // Four consecutive channels (c4 = c / 4) of one V row.
 template <int FMT>
 __device__ __forceinline__ void store_v(void* V, long long row, int C4, int c4, float4 v, int* overflow) {
@@ -363,8 +380,13 @@ __device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, int pad, long 
                 float Vt[MA + 2][MB + 2];
                 in_tile<MA, MB>(d, Vt);
 #pragma unroll
-                for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
-                    store_v<FMT>(Vout, row + e * ps, C, c, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
+                for (int e = 0; e < (MA + 2) * (MB + 2); ++e) {
+                    if constexpr (FMT == AZG_WINO_SPLIT2)  // the wave's lanes are channels c & ~63 ..
+                        store_v2_wave(Vout, row + e * ps, C, c & ~63, c & 63, Vt[e / (MB + 2)][e % (MB + 2)],
+                                      overflow);
+                    else
+                        store_v<FMT>(Vout, row + e * ps, C, c, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
+                }
             });
         }
     }
