@@ -27,11 +27,12 @@
 // overlaps each phase's reads with the previous phase's MFMAs, variant 2 runs one
 // wave per SIMD on 128 x 128 per wave, variant 3 spreads the DMA issue between the
 // MFMAs.  Measured on conv2's shape (tools/split_gemm_bench.py, round-robin medians,
-// profiles/r01_split_gemm_bench.json), TF/s of fp16 MFMA work: variant 4 1016,
-// 0 977, 1 967, 3 951, 2 903; hipBLASLt on the [hi|lo|hi] form 900.  PMC
-// (tools/split_gemm_pmc.py): no LDS bank conflicts, A read from HBM once (L2 hit
-// rate 78%), MFMA busy 56% (variant 4; 49% variant 0): the rest is the per-stage
-// barrier, operand-read and LDS-DMA issue bubble.
+// profiles/r01_split_gemm_bench.json), TF/s of fp16 MFMA work: variant 4 1116,
+// 7 1091, 12 1073, 0 1072; hipBLASLt on the [hi|lo|hi] form 903.  PMC
+// (tools/split_gemm_pmc.py): no LDS bank conflicts, MFMA busy 61% (variant 4).  The
+// bound is the global -> LDS operand feed (~5.8 TB/s chip-wide; zeroing either
+// operand's DMA runs 33% faster, both 50%: variants 6, 15, 16), which is why the
+// operand rows are 32-channel [hi | lo] blocks (one 128-B line per row per stage).
 //
 // The tiles of all GEMMs of a layer (runs of points with equal T) are one grid;
 // block ids are dealt to the 8 XCDs round-robin, so the mapping gives each XCD a
