@@ -381,6 +381,15 @@ __device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, int pad, long 
                 in_tile<MA, MB>(d, Vt);
 #pragma unroll
                 for (int e = 0; e < (MA + 2) * (MB + 2); ++e) {
+#ifdef AZG_PROBE_OLD_V_LAYOUT  // timing probe only (tools/mid_probe.py): the earlier [hi(C) | lo(C)] rows
+                    if constexpr (FMT == AZG_WINO_SPLIT2) {
+                        const float x = Vt[e / (MB + 2)][e % (MB + 2)];
+                        const _Float16 hi = (_Float16)x, lo = (_Float16)(x - (float)hi);
+                        _Float16* r = (_Float16*)Vout + (row + e * ps) * 2 * C;
+                        r[c] = hi;
+                        r[C + c] = lo;
+                    } else
+#endif
                     if constexpr (FMT == AZG_WINO_SPLIT2)  // the wave's lanes are channels c & ~63 ..
                         store_v2_wave(Vout, row + e * ps, C, c & ~63, c & 63, Vt[e / (MB + 2)][e % (MB + 2)],
                                       overflow);
