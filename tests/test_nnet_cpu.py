@@ -83,3 +83,25 @@ def test_winograd_layout_matches_libazg():
         want = {(ma, mb): n for ma, mb, _, n in winograd_groups(h)}
         for g, (ma, mb) in enumerate(((3, 3), (3, 2), (2, 3), (2, 2))):
             assert groups[g] == want.get((ma, mb), 0), (h, g)
+
+
+def test_split2_operand_blocks():
+    """The split GEMM's operand rows (azg.h AZG_WINO_SPLIT2): 32-channel blocks
+    [hi(32) | lo(32)], channel j's hi at 64 (j // 32) + j % 32 and its lo 32 further;
+    split2_halves inverts split2_rows, and _split_operands("split") lays U^T out so."""
+    import torch
+    from azg_amd.nnet import _split_operands, _split_u, split2_halves, split2_rows
+    hi = torch.arange(3 * 128, dtype=torch.float32).reshape(3, 128).half()
+    lo = -hi
+    r = split2_rows(hi, lo)
+    assert r.shape == (3, 256)
+    for j in (0, 31, 32, 77, 127):
+        assert r[1, 64 * (j // 32) + j % 32] == hi[1, j] and r[1, 64 * (j // 32) + 32 + j % 32] == lo[1, j]
+    h2, l2 = split2_halves(r)
+    assert torch.equal(h2, hi) and torch.equal(l2, lo)
+    u = torch.randn(2, 64, 256, dtype=torch.float64)  # [points][C][K]
+    b, scale = _split_operands(u, "split")
+    uh, ul, s2 = _split_u(u)
+    bh, bl = split2_halves(b)
+    assert scale == s2 and b.shape == (2, 256, 128)
+    assert torch.equal(bh, uh.transpose(1, 2)) and torch.equal(bl, ul.transpose(1, 2))
