@@ -87,10 +87,12 @@ _lib = None
 
 def build(force=False):
     """Compile libazg.so for gfx950 in-tree (hipcc; no GPU needed)."""
-    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if os.path.isfile(os.path.join(CSRC, f))]
     newest = max(os.path.getmtime(s) for s in srcs)
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
-        subprocess.check_call(["make", "-s", "-C", CSRC])
+        if force:
+            subprocess.check_call(["make", "-s", "-C", CSRC, "clean"])
+        subprocess.check_call(["make", "-s", "-j8", "-C", CSRC])
     return LIB_PATH
 
 

@@ -23,10 +23,14 @@ Each slot has its own numpy stream seeded by its game index (the reference's
 Pool workers draw from unseeded per-process streams, so its arena results are
 not reproducible run to run).
 """
+import logging
+
 import numpy as np
 
 from .engine import SelfPlayEngine, game_spec
 from .flags import GameOutcome
+
+log = logging.getLogger(__name__)
 
 _OUT = {0: GameOutcome.ONGOING, 1: GameOutcome.DRAW, 2: GameOutcome.WON, 3: GameOutcome.LOST}
 
@@ -37,16 +41,32 @@ class BatchedArena:
             raise ValueError(f"unknown opponent {opponent!r}")
         self.game, self.nnet, self.args, self.opponent = game, nnet, args, opponent
         if evaluator is None:
-            from .nnet import InferenceNet, NNetWrapper
-            evaluator = InferenceNet(nnet.nnet) if isinstance(nnet, NNetWrapper) else nnet
+            evaluator = self._inference_form("split")
         self.evaluator = evaluator
         self.seed_base, self.first_game = seed_base, first_game
         self.last_engine_state = None
 
+    def _inference_form(self, gemm):
+        from .nnet import InferenceNet, NNetWrapper
+        return InferenceNet(self.nnet.nnet, gemm=gemm) if isinstance(self.nnet, NNetWrapper) else self.nnet
+
     def playGames(self, num, verbose=False):
-        """Arena.playGames (Arena.py:90-142): (MCTS player wins, baseline wins, draws)."""
+        """Arena.playGames (Arena.py:90-142): (MCTS player wins, baseline wins, draws).
+        If the split-fp16 network met an operand out of fp16 range, the games are
+        replayed (same seeds, same result as a first run) with the f32-GEMM form."""
         if not (isinstance(num, int) and num >= 2):
             raise AssertionError("num must be an int >= 2")
+        try:
+            return self._play(num)
+        except FloatingPointError:
+            f32 = self._inference_form("f32")
+            if f32 is self.evaluator:
+                raise
+            log.warning("arena: split-fp16 operand out of range; replaying with InferenceNet(gemm='f32')")
+            self.evaluator = f32
+            return self._play(num)
+
+    def _play(self, num):
         name, n, max_turns = game_spec(self.game)
         eng = SelfPlayEngine(num, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct, temp_threshold=0,
                              max_turns=max_turns, game=name, n=n, seed_base=self.seed_base,
@@ -58,6 +78,7 @@ class BatchedArena:
             while eng.active() > 0:
                 eng.move()  # searches in the slots where the MCTS player (RED) is to move
                 eng.opponent_move(self.opponent)
+            eng.check_evaluator()
             st = eng.state()
             self.last_moves = eng.read_moves(counts=False)
             err = eng.stats()["error"]

@@ -97,25 +97,42 @@ class Coach:
                               seed_base=seed_base, first_game=first_game,
                               evaluator=evaluator if evaluator is not None else self.evaluator())
 
-    def evaluator(self):
+    def evaluator(self, gemm="split"):
         """The leaf evaluator for the engine: an NNetWrapper's current weights as
         the inference form (BN folded, NHWC; nnet.InferenceNet), else self.nnet
         itself (a module, or "stub")."""
         from .nnet import InferenceNet, NNetWrapper
         if isinstance(self.nnet, NNetWrapper):
-            return InferenceNet(self.nnet.nnet)
+            return InferenceNet(self.nnet.nnet, gemm=gemm)
         return self.nnet
+
+    def _range_checked(self, run, evaluator):
+        """run(evaluator) -> result; if the split-fp16 network met an operand out of
+        fp16 range (FloatingPointError from SelfPlayEngine.check_evaluator), rerun
+        with the f32-GEMM form.  Games are seeded by their index, so the rerun's
+        records are the ones a first f32 run would have produced."""
+        ev = evaluator if evaluator is not None else self.evaluator()
+        try:
+            return run(ev)
+        except FloatingPointError:
+            if evaluator is not None or ev is self.nnet:
+                raise
+            log.warning("self-play: split-fp16 operand out of range; replaying with InferenceNet(gemm='f32')")
+            return run(self.evaluator(gemm="f32"))
 
     def selfplay_batch(self, num_games, evaluator=None, seed_base=0, first_game=0, return_records=False):
         """Play num_games complete games concurrently on the GPU engine and
         return their examples (same format as executeEpisode)."""
         g0 = self.game
-        eng = self._engine(num_games, evaluator, seed_base, first_game)
-        try:
-            eng.play()
-            rec = eng.read_moves()
-        finally:
-            eng.close()
+
+        def run(ev):
+            eng = self._engine(num_games, ev, seed_base, first_game)
+            try:
+                eng.play()
+                return eng.read_moves()
+            finally:
+                eng.close()
+        rec = self._range_checked(run, evaluator)
         examples = []
         for i in range(num_games):
             examples += examples_from_record(g0, rec["actions"][i], rec["temps"][i], rec["counts"][i],
@@ -135,20 +152,25 @@ class Coach:
         if 0 < slots < num_games:
             # continuous batching: num_games games through `slots` engine slots
             # (azg_refill); same examples, game for game, as one slot per game
-            eng = self._engine(slots, evaluator, seed_base, first_game)
-            try:
-                r = eng.play_games(num_games, first_game=first_game)
-            finally:
-                eng.close()
+            def run(ev):
+                eng = self._engine(slots, ev, seed_base, first_game)
+                try:
+                    return eng.play_games(num_games, first_game=first_game)
+                finally:
+                    eng.close()
+            r = self._range_checked(run, evaluator)
             name, n, max_turns = game_spec(self.game)
             return examples_from_records(name, n, max_turns, int(self.args.tempThreshold), r["moves"],
                                          r["actions"], r["counts"], self.label_mode, maxlen)
-        eng = self._engine(num_games, evaluator, seed_base, first_game)
-        try:
-            eng.play()
-            return engine_examples(eng, int(self.args.tempThreshold), self.label_mode, maxlen)
-        finally:
-            eng.close()
+
+        def run(ev):
+            eng = self._engine(num_games, ev, seed_base, first_game)
+            try:
+                eng.play()
+                return engine_examples(eng, int(self.args.tempThreshold), self.label_mode, maxlen)
+            finally:
+                eng.close()
+        return self._range_checked(run, evaluator)
 
     def _selfplay_iteration(self, i, group):
         """Self-play of iteration i over all ranks; examples land on the trainer (rank 0)."""
@@ -161,9 +183,20 @@ class Coach:
             return self.selfplay_examples(eps, first_game=(i - 1) * eps)
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         broadcast_weights(self.nnet.nnet, src=0, group=group)
-        eng = self._engine(eps, None, 0, ((i - 1) * world + rank) * eps)
+        first = ((i - 1) * world + rank) * eps
+
+        def run(ev):
+            eng = self._engine(eps, ev, 0, first)
+            try:
+                eng.play()
+            except BaseException:
+                eng.close()
+                raise
+            return eng
+        # a rank whose split-fp16 net overflows replays its games in f32 before the
+        # gather, which every rank then enters exactly once
+        eng = self._range_checked(run, None)
         try:
-            eng.play()
             rec, _ = gather_records(eng, dst=0, group=group)
         finally:
             eng.close()
@@ -186,6 +219,8 @@ class Coach:
         distributed = group is not None or (dist.is_available() and dist.is_initialized()
                                             and dist.get_world_size() > 1)
         trainer = not distributed or dist.get_rank(group) == 0
+        if distributed:
+            self.agree_skip_first(group)
         pit_interval = 5
         for i in range(1, int(self.args.numIters) + 1):
             log.info("Starting Iter #%d ...", i)
@@ -212,6 +247,19 @@ class Coach:
         if distributed:
             from .dist import broadcast_weights
             broadcast_weights(self.nnet.nnet, src=0, group=group)
+
+    def agree_skip_first(self, group=None):
+        """Make every rank follow the trainer's skipFirstSelfPlay (loadTrainExamples is
+        naturally called on the trainer only), so all ranks enter iteration 1's
+        collectives alike."""
+        import torch.distributed as dist
+        from .dist import group_src
+        dev = (torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl"
+               else torch.device("cpu"))
+        flag = torch.tensor([int(self.skipFirstSelfPlay)], dtype=torch.int64, device=dev)
+        dist.broadcast(flag, src=group_src(group, 0), group=group)
+        self.skipFirstSelfPlay = bool(flag.item())
+        return self.skipFirstSelfPlay
 
     def pit_baselines(self):
         """Coach.py:158-165: the new net's MCTSPlayer against RandomPlayer and

@@ -86,13 +86,15 @@ int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
         return fail(AZG_ERR_ARG, "unsupported game: built for InflexionGame(7), OthelloGame(6), OthelloGame(8)");
     if (cfg->num_games <= 0 || cfg->sims <= 0 || cfg->max_turns < 0)
         return fail(AZG_ERR_ARG, "num_games, sims must be > 0 and max_turns >= 0");
+    int device = 0;
+    HIP_TRY(hipGetDevice(&device));
     auto* e = new azg_engine();
     memset(&e->d, 0, sizeof(Dev));
     e->cfg = *cfg;
     e->ops = ops;
+    e->device = device;
     const size_t A = (size_t)ops.actions, ROW = (size_t)ops.row;
     e->bytes = 0;
-    HIP_TRY(hipGetDevice(&e->device));
     Dev& d = e->d;
     d.G = cfg->num_games;
     d.M = cfg->node_capacity > 0 ? cfg->node_capacity : 16 * cfg->sims + 128;

@@ -7,7 +7,7 @@ iteration's examples and trains -- two collectives run over RCCL (backend
 "nccl" on ROCm) on xGMI:
 
   * gather of every rank's compact move records to the trainer rank
-    (all_gather of per-rank sizes, then one all_gather of padded buffers);
+    (an all_reduce of the sizes, then gathers into the trainer only);
   * broadcast of the trainer's weights (one flat f32 buffer, ~50 MB).
 
 A compact move record is (moves made, actions, root visit counts as int16 --
@@ -54,8 +54,27 @@ def gather_records(engine, dst=0, group=None):
     return gather_record_tensors(moves, actions, counts, dst, group, actions_per_move=engine.A)
 
 
+def group_src(group, rank):
+    """Global rank of `rank` in `group` (torch's src/dst arguments are global ranks)."""
+    if group is None or group is dist.group.WORLD:
+        return int(rank)
+    return dist.get_global_rank(group, int(rank))
+
+
+def _gather(t, dst, group):
+    """dist.gather of equal-shaped tensors into one [ws, ...] tensor on dst only."""
+    ws = dist.get_world_size(group)
+    if dist.get_rank(group) == dst:
+        out = torch.empty((ws,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.gather(t, list(out.unbind(0)), dst=group_src(group, dst), group=group)
+        return out
+    dist.gather(t, None, dst=group_src(group, dst), group=group)
+    return None
+
+
 def gather_record_tensors(moves, actions, counts, dst=0, group=None, actions_per_move=343):
-    """gather_records on plain tensors (any device the group's backend serves)."""
+    """gather_records on plain tensors (any device the group's backend serves).
+    Only `dst` allocates and receives the other ranks' records."""
     A = counts.shape[2] if counts is not None else int(actions_per_move)
     m_local = torch.stack([torch.max(moves).to(torch.int64),
                            (counts.max() if counts is not None and counts.numel() else moves.new_zeros(())).to(
@@ -64,28 +83,26 @@ def gather_record_tensors(moves, actions, counts, dst=0, group=None, actions_per
     dist.all_reduce(m_all, op=dist.ReduceOp.MAX, group=group)
     m, cmax = (int(x) for x in m_all.tolist())
     ctype = torch.int16 if cmax <= 32767 else torch.int32
-    ws = dist.get_world_size(group)
     G = moves.shape[0]
     act = actions[:, :m].contiguous()
     cnt = counts[:, :m].to(ctype).contiguous() if counts is not None else torch.zeros(
         (G, m, A), dtype=ctype, device=moves.device)
-    mv = moves.clone()
-    out_mv = torch.empty((ws * G,), dtype=mv.dtype, device=mv.device)
-    out_act = torch.empty((ws * G, m), dtype=act.dtype, device=act.device)
-    out_cnt = torch.empty((ws * G, m, A), dtype=cnt.dtype, device=cnt.device)
-    dist.all_gather_into_tensor(out_mv, mv, group=group)
-    dist.all_gather_into_tensor(out_act, act, group=group)
+    mv = moves.contiguous()
+    out_mv = _gather(mv, dst, group)
+    out_act = _gather(act, dst, group)
     # moved as raw bytes (RCCL/gloo have no int16 type)
-    dist.all_gather_into_tensor(out_cnt.view(torch.uint8), cnt.view(torch.uint8), group=group)
+    out_cnt = _gather(cnt.view(torch.uint8), dst, group)
     sent = mv.numel() * 4 + act.numel() * 4 + cnt.numel() * cnt.element_size()
-    if dist.get_rank(group) == dst:
-        return (out_mv, out_act, out_cnt), sent
+    if out_mv is not None:
+        return (out_mv.reshape(-1), out_act.reshape(-1, m), out_cnt.view(ctype).reshape(-1, m, A)), sent
     return None, sent
 
 
 def broadcast_weights(module, src=0, group=None):
-    """Broadcast every parameter and buffer of `module` from `src`: the f32 ones as
-    one flat buffer, the rest (BatchNorm's num_batches_tracked) as one int64 buffer."""
+    """Broadcast every parameter and buffer of `module` from `src` (a rank of `group`):
+    the f32 ones as one flat buffer, the rest (BatchNorm's num_batches_tracked) as one
+    int64 buffer."""
+    src = group_src(group, src)
     tensors = list(module.parameters()) + list(module.buffers())
     f32 = [t for t in tensors if t.dtype == torch.float32]
     rest = [t for t in tensors if t.dtype != torch.float32]

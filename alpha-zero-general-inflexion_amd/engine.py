@@ -166,7 +166,17 @@ class SelfPlayEngine:
         while self.active() > 0 and (max_moves is None or m < max_moves):
             self.move()
             m += 1
+        self.check_evaluator()
         return m
+
+    def check_evaluator(self):
+        """Raise FloatingPointError if the evaluator's split-fp16 GEMMs met an operand
+        fp16 cannot hold since the last check (InferenceNet.check_range): its priors and
+        values would be wrong, not just inexact.  play(), play_games(), the arena and the
+        drop-in MCTS call this; callers rerun with InferenceNet(gemm="f32")."""
+        chk = getattr(self.evaluator, "check_range", None)
+        if chk is not None:
+            chk()
 
     def play_games(self, num_games, first_game=None, check_every=1):
         """Continuous batching (azg_refill): play the num_games games
@@ -200,6 +210,7 @@ class SelfPlayEngine:
             k += 1
             if k % check_every == 0 and self.active() == 0:
                 break
+        self.check_evaluator()
         done = int(cnt.item())
         if done != n:
             raise _lib.AzgError(f"play_games: {done} of {n} games completed")

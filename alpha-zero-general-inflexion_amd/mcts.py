@@ -4,7 +4,8 @@
     pi = mcts.getActionProb(game, temp)     # same result as the reference, bit for bit
 
 The tree lives in the engine (one game slot, no node GC, so the tree persists
-across calls exactly like the reference's dicts).  The reference draws its
+across calls exactly like the reference's dicts; the node pool holds a whole
+game's tree, and a search that still fills it raises AzgError).  The reference draws its
 random symmetries from numpy's *global* RandomState (InflexionGame.py:120-121);
 this class hands that stream to the engine before the simulations and takes it
 back afterwards, so interleaving with the caller's own np.random use
@@ -38,14 +39,25 @@ def _evaluator_of(nnet, device):
     raise TypeError("nnet must be a NNetWrapper-like object, a torch module or 'stub'")
 
 
-class MCTS:
-    DEFAULT_NODE_CAPACITY = 32768
+MAX_NODE_CAPACITY = (1 << 21) - 1  # azg_create's limit
 
+
+def whole_game_capacity(sims, game):
+    """Nodes a whole game's tree can reach: one expansion per simulation, sims per
+    move, at most max_turns + 1 moves (2n^2 for Othello: every move fills a cell or
+    passes, and two passes end it).  The reference keeps every node for the game
+    (MCTS.py:24-30), so the drop-in sizes its pool to hold them all."""
+    name, n, max_turns = game_spec(game)
+    moves = 2 * n * n if name == "othello" or max_turns <= 0 else max_turns + 1
+    return min(int(sims) * moves + 64, MAX_NODE_CAPACITY)
+
+
+class MCTS:
     def __init__(self, nnet, args, device=None, node_capacity=None):
         self.nnet = nnet
         self.args = args
         self.device = torch.device(device) if device is not None else torch.device("cuda")
-        self.node_capacity = node_capacity or self.DEFAULT_NODE_CAPACITY
+        self.node_capacity = node_capacity  # None: whole_game_capacity
         self._engine = None
         self._max_turns = None
 
@@ -55,11 +67,11 @@ class MCTS:
             if self._engine is not None:
                 self._engine.close()
             name, n, max_turns = spec
+            cap = self.node_capacity or whole_game_capacity(self.args.numMCTSSims, game)
             self._engine = SelfPlayEngine(1, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct,
                                           temp_threshold=1, max_turns=max_turns, game=name, n=n,
                                           evaluator=_evaluator_of(self.nnet, self.device), device=self.device,
-                                          node_capacity=self.node_capacity, max_depth=1024, gc=False,
-                                          record=False)
+                                          node_capacity=cap, max_depth=1024, gc=False, record=False)
             self._max_turns = spec
         return self._engine
 
@@ -72,6 +84,10 @@ class MCTS:
         eng.set_root(0, game._board, game._curr_turn, game.player.num)
         for _ in range(sims):
             eng.simulate()
+        # a full node pool (or any engine error) stops the slot's search: raise rather
+        # than return counts from a truncated search (azg_active_games reports it)
+        eng.active()
+        eng.check_evaluator()
         mt, pos = eng.get_rng(0)
         np.random.set_state((state[0], mt, pos, state[3], state[4]))
         return eng

@@ -29,7 +29,7 @@ def _worker(rank, world, port, q):
         actions = torch.arange(G * MM, dtype=torch.int32).reshape(G, MM) + 1000 * rank
         counts = (torch.arange(G * MM * 343, dtype=torch.int32).reshape(G, MM, 343) % 97) + rank
         out, sent = ad.gather_record_tensors(moves, actions, counts, dst=0)
-        res = {"sent": sent}
+        res = {"sent": sent, "none_off_dst": out is None}
         if rank == 0:
             mv, act, cnt = out
             res["moves"] = mv.tolist()
@@ -53,9 +53,63 @@ def _worker(rank, world, port, q):
         res["sent2"] = sent2
         if rank == 0:
             res["big_ok"] = out2[2].dtype == torch.int32 and int(out2[2][G, 0, 0]) == 40000
+        # the trainer's skipFirstSelfPlay decides for every rank (a rank-0-only
+        # loadTrainExamples must not leave the ranks in different collectives)
+        from azg_amd.coach import Coach
+        c = Coach(None, "stub", None)
+        c.skipFirstSelfPlay = rank == 0
+        res["skip"] = c.agree_skip_first()
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
+
+
+def _worker3(rank, world, port, q):
+    """world 3, subgroup of global ranks [1, 2]: group rank 0 is global rank 1."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import azg_amd  # noqa: F401
+        from azg_amd import dist as ad
+        from azg_amd.coach import Coach
+        from azg_amd.nnet import InflexionNNet
+        grp = dist.new_group([1, 2])
+        res = {}
+        if rank in (1, 2):
+            torch.manual_seed(rank)
+            net = InflexionNNet(num_channels=8)
+            ad.broadcast_weights(net, src=0, group=grp)  # group rank 0 = global rank 1
+            torch.manual_seed(1)
+            ref = InflexionNNet(num_channels=8)
+            res["bcast_ok"] = all(torch.equal(a, b) for a, b in zip(net.state_dict().values(),
+                                                                      ref.state_dict().values()))
+            moves = torch.tensor([rank, rank + 1], dtype=torch.int32)
+            actions = torch.full((2, 4), rank, dtype=torch.int32)
+            counts = torch.full((2, 4, 5), rank, dtype=torch.int32)
+            out, _ = ad.gather_record_tensors(moves, actions, counts, dst=0, group=grp)
+            res["gather"] = None if out is None else out[0].tolist()
+            c = Coach(None, "stub", None)
+            c.skipFirstSelfPlay = rank == 1
+            res["skip"] = c.agree_skip_first(grp)
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_subgroup_ranks_world3():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker3, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1]["bcast_ok"] and res[2]["bcast_ok"]
+    assert res[1]["gather"] == [1, 2, 2, 3] and res[2]["gather"] is None
+    assert res[1]["skip"] is True and res[2]["skip"] is True
 
 
 def test_gather_and_broadcast_world2():
@@ -76,3 +130,5 @@ def test_gather_and_broadcast_world2():
     assert res[0]["bcast_ok"] and res[1]["bcast_ok"]
     assert res[1]["bcast_bytes"] == res[0]["bcast_bytes"] > 0
     assert r0["big_ok"] and res[1]["sent2"] > res[1]["sent"]
+    assert res[1]["none_off_dst"] and not res[0]["none_off_dst"]
+    assert res[0]["skip"] is True and res[1]["skip"] is True

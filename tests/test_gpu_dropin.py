@@ -97,3 +97,68 @@ def test_real_net_dropin_runs_and_is_close_to_cpu_net():
         p2, v2 = w.predict(planes.astype(np.int64))
         np.testing.assert_allclose(p2, P, rtol=1e-5, atol=1e-7)
         np.testing.assert_allclose(v2[0], v, rtol=1e-5, atol=1e-6)
+
+
+def test_dropin_pool_sized_for_whole_game_and_full_pool_raises():
+    """the drop-in's node pool holds a whole game's tree (sims per move x
+    moves), and a search that still fills a (deliberately small) pool raises instead of
+    returning counts from a truncated search."""
+    import azg_amd  # noqa: F401
+    from azg_amd._lib import AzgError
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.mcts import MCTS, whole_game_capacity
+
+    args = Args(numMCTSSims=25, cpuct=1, tempThreshold=30)
+    game = InflexionGame(7, max_turns=343, max_power=6)
+    assert whole_game_capacity(25, game) == 25 * 344 + 64
+    assert whole_game_capacity(100, game) == 100 * 344 + 64
+    np.random.seed(3)
+    small = MCTS("stub", args, node_capacity=40)
+    g = game.restarted()
+    small.getActionProb(g, temp=1)  # 25 nodes: fits
+    g = g.to_next_state(int(np.argmax(small._engine.root_counts(0))))
+    with pytest.raises(AzgError):
+        small.getActionProb(g, temp=1)  # up to 50 nodes: the pool of 40 fills
+    np.random.seed(3)
+    full = MCTS("stub", args)
+    assert full._engine_for(game).cfg.node_capacity == whole_game_capacity(25, game)
+
+
+def test_engine_raises_on_split_gemm_range_flag():
+    """a split-fp16 evaluator whose range flag trips makes play() raise, and the
+    Coach replays the games with the f32-GEMM form (same records as an f32 run)."""
+    import azg_amd  # noqa: F401
+    from azg_amd.coach import Coach
+    from azg_amd.engine import SelfPlayEngine
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.nnet import InferenceNet, InflexionNNet, NNetWrapper
+
+    torch.manual_seed(0)
+    net = InflexionNNet().cuda().eval()
+    fast = InferenceNet(net)
+    eng = SelfPlayEngine(4, evaluator=fast, sims=2, max_turns=6)
+    fast.overflow.fill_(1)  # as the GEMM's range check would
+    with pytest.raises(FloatingPointError):
+        eng.play()
+    eng.close()
+    assert int(fast.overflow.item()) == 0  # the check clears the sticky flag
+
+    args = Args(numMCTSSims=2, cpuct=1, tempThreshold=3, maxlenOfQueue=200000)
+    game = InflexionGame(7, max_turns=6, max_power=6)
+    wrapper = NNetWrapper(game)
+    wrapper.nnet = net
+    coach = Coach(game, wrapper, args)
+    made = []
+
+    def evaluator(gemm="split"):
+        ev = InferenceNet(net, gemm=gemm)
+        if gemm == "split":
+            ev.overflow.fill_(1)
+        made.append(gemm)
+        return ev
+    coach.evaluator = evaluator
+    ex = coach.selfplay_examples(4)
+    assert made == ["split", "f32"]
+    coach.evaluator = lambda gemm="split": InferenceNet(net, gemm="f32")
+    ref = coach.selfplay_examples(4)
+    assert torch.equal(ex.pis, ref.pis) and torch.equal(ex.planes, ref.planes) and torch.equal(ex.vs, ref.vs)
