@@ -68,6 +68,7 @@ SIGNATURES = [
     ("azg_conv3x3_variant", ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
     ("azg_game_info", ctypes.c_int, [_I32, _I32, _VP]),
     ("azg_winograd_layout", ctypes.c_int, [_I32, _VP, _VP]),
+    ("azg_winograd_tables", ctypes.c_int, [_I32, _VP, _VP]),
     ("azg_winograd_in_nhwc", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
     ("azg_winograd_out_nhwc", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, ctypes.c_float, _VP]),
     ("azg_winograd_out_split", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, ctypes.c_float, _I32, _VP, _VP]),

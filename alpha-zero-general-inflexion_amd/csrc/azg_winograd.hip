@@ -1,19 +1,20 @@
 // azg_winograd.hip -- the leaf network's 3x3 convolutions as Winograd convolutions
-// over mixed F(3,3) / F(2,3) tiles.
+// over mixed F(4,3) / F(3,3) / F(2,3) tiles.
 //
 // conv2-4 of InflexionNNet.forward (InflexionNNet.py:39-45, BN folded) are
 // y = relu(bias + conv3x3(x, w)).  Winograd F(m,3) along one axis turns m outputs
 // into n = m + 2 transformed points; the 2-D transform is separable, so a tile may
 // use F(ma,3) down its rows and F(mb,3) across its columns:
 //     Y = A_ma^T [ U (.) V ] A_mb,  U = G_ma g G_mb^T (per (c, k)),  V = B_ma^T d B_mb.
-// An h-long output axis is cut into p = ceil(h/3) tiles, as many of side 3 as fit
-// and the rest of side 2 (h = 7: 3+2+2; 5: 3+2; 3: 3; 8: 3+3+2; 6: 3+3; 4: 2+2), the
-// fewest transformed points that cover it exactly: 13^2 instead of uniform F(3,3)'s
-// 15^2 for a 7x7 output, 9^2 instead of 10^2 for 5x5.
+// An h-long output axis is cut into the fewest tiles of sides 4, 3, 2 (at most two
+// sides per axis; h = 7: 4+3; 5: 3+2; 3: 3; 8: 4+4; 6: 3+3; 4: 4), the fewest
+// transformed points that cover it exactly: 11^2 instead of 13^2 (3+2+2) for a 7x7
+// output, 9^2 for 5x5.
 //
 // Summed over input channels c, each transformed point e of a tile type
 // g = (ma, mb) is one GEMM  M_e[T_g x K] = V_e[T_g x C] x U_e[C x K].  Layout of V
-// (and M, with K for C): the groups (3,3), (3,2), (2,3), (2,2) one after another
+// (and M, with K for C): the groups (big,big), (big,small), (small,big), (small,small)
+// (big = 4 or 3, small = big - 1, per layer: WSeq) one after another
 // (absent types skipped), group g as [P_g][batch * n_g][row] with P_g = (ma+2)(mb+2)
 // points and n_g tiles of that type per image, tiles row-major within the image.
 // The GEMMs (hipBLASLt through torch.bmm) are the caller's; these kernels are the
@@ -27,8 +28,8 @@
 //                     one pass (the activation stays on chip)
 //   * winograd_first: conv1 + bias + ReLU from the NCHW planes + conv2's input
 //                     transform in one pass
-// B and A have small integer entries (F(2,3): 0, +-1; F(3,3): up to 4); U is formed
-// in f64 by the caller (G has entries 1/2, 1/3, 1/6).
+// B and A have small entries (B^T integers up to 5; A^T up to 8, F(4,3)'s -1/2 point
+// powers 1/2..1/8 exact); U is formed in f64 by the caller (G entries like 1/6, 1/15).
 //
 // V is written in one of three formats (vfmt):
 //   AZG_WINO_F32  : f32 rows of C;
@@ -44,6 +45,8 @@
 //                   |v| > 65504 or NaN sets *overflow.
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "../../include/azg.h"
 
 namespace {
@@ -53,21 +56,32 @@ struct IC {
     static constexpr int value = V;
 };
 
-// tile sequence of an h-long output axis: p tiles, the first n3 of side 3, the rest 2
+// Tile sequence of an h-long output axis: the fewest tiles, p = ceil(h / 4), of sides
+// in {4, 3, 2} summing to h with at most two distinct sides (big = small + 1, the big
+// ones first): r = h - 2p extra units over all-2 tiles; r <= p: r 3-tiles + (p - r)
+// 2-tiles, else (r - p) 4-tiles + (2p - r) 3-tiles.  h = 1: one 2-tile, cropped.
 struct WSeq {
-    int h, p, n3;
+    int h, p, big, nbig;
+    __host__ __device__ static constexpr int tiles(int h_) { return h_ <= 4 ? 1 : (h_ + 3) / 4; }
+    __host__ __device__ static constexpr int extra(int h_) {
+        return h_ - 2 * tiles(h_) > 0 ? h_ - 2 * tiles(h_) : 0;
+    }
     __host__ __device__ constexpr explicit WSeq(int h_)
-        : h(h_), p((h_ + 2) / 3), n3(h_ - 2 * ((h_ + 2) / 3) > 0 ? h_ - 2 * ((h_ + 2) / 3) : 0) {}
-    __host__ __device__ constexpr int m(int i) const { return i < n3 ? 3 : 2; }
-    __host__ __device__ constexpr int off(int i) const { return i < n3 ? 3 * i : 3 * n3 + 2 * (i - n3); }
-    __host__ __device__ constexpr int cnt(int mm) const { return mm == 3 ? n3 : p - n3; }
-    __host__ __device__ constexpr int idx(int i) const { return i < n3 ? i : i - n3; }  // index among its type
-    // rows of V (or M) before group (ma, mb); group order (3,3) (3,2) (2,3) (2,2)
+        : h(h_), p(tiles(h_)), big(extra(h_) > tiles(h_) ? 4 : 3),
+          nbig(extra(h_) > tiles(h_) ? extra(h_) - tiles(h_) : extra(h_)) {}
+    __host__ __device__ constexpr int small() const { return big - 1; }
+    __host__ __device__ constexpr int m(int i) const { return i < nbig ? big : big - 1; }
+    __host__ __device__ constexpr int off(int i) const {
+        return i < nbig ? big * i : big * nbig + (big - 1) * (i - nbig);
+    }
+    __host__ __device__ constexpr int cnt(int mm) const { return mm == big ? nbig : p - nbig; }
+    __host__ __device__ constexpr int idx(int i) const { return i < nbig ? i : i - nbig; }  // index among its type
+    // rows of V (or M) before group (ma, mb); group order (big,big) (big,small) (small,big) (small,small)
     __host__ __device__ constexpr long long base(int ma, int mb, long long B) const {
-        const int g = (ma == 3 ? 0 : 2) + (mb == 3 ? 0 : 1);
+        const int g = (ma == big ? 0 : 2) + (mb == big ? 0 : 1);
         long long r = 0;
         for (int q = 0; q < g; ++q) {
-            const int qa = q < 2 ? 3 : 2, qb = (q & 1) ? 2 : 3;
+            const int qa = q < 2 ? big : big - 1, qb = (q & 1) ? big - 1 : big;
             r += (long long)(qa + 2) * (qb + 2) * B * cnt(qa) * cnt(qb);
         }
         return r;
@@ -85,13 +99,44 @@ struct WSeq {
 // run f(IC<ma>, IC<mb>): the tile bodies are compiled per type; with constant
 // ma, mb (unrolled compile-time sequences) the branches fold away
 template <class F>
+__device__ __forceinline__ void with_type_b(int ma, int mb, F&& f) {
+    if (mb == 4) f(IC<4>{});
+    else if (mb == 3) f(IC<3>{});
+    else f(IC<2>{});
+}
+template <class F>
 __device__ __forceinline__ void with_types(int ma, int mb, F&& f) {
-    if (ma == 3) {
-        if (mb == 3) f(IC<3>{}, IC<3>{});
-        else f(IC<3>{}, IC<2>{});
+    if (ma == 4) with_type_b(ma, mb, [&](auto B_) { f(IC<4>{}, B_); });
+    else if (ma == 3) with_type_b(ma, mb, [&](auto B_) { f(IC<3>{}, B_); });
+    else with_type_b(ma, mb, [&](auto B_) { f(IC<2>{}, B_); });
+}
+
+template <int... Is, class F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, F&& f) {
+    (f(IC<Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+// f(IC<ma>, IC<mb>, i, j) for every tile (i, j) of an axis sequence S, row-major.
+// With a compile-time side HC (S == WSeq(HC)) the tiles are expanded at compile time,
+// so every index into a lane's register plane is a constant (no scratch);
+// otherwise a runtime loop over the types.
+template <int HC, class F>
+__device__ __forceinline__ void for_tiles(const WSeq& S, F&& f) {
+    if constexpr (HC > 0) {
+        constexpr WSeq SC(HC);
+        static_for<SC.p>([&](auto I) {
+            static_for<SC.p>([&](auto J) {
+                constexpr int i = decltype(I)::value, j = decltype(J)::value;
+                f(IC<SC.m(i)>{}, IC<SC.m(j)>{}, i, j);
+            });
+        });
     } else {
-        if (mb == 3) f(IC<2>{}, IC<3>{});
-        else f(IC<2>{}, IC<2>{});
+        for (int i = 0; i < S.p; ++i)
+            for (int j = 0; j < S.p; ++j) with_types(S.m(i), S.m(j), [&](auto A_, auto B_) { f(A_, B_, i, j); });
     }
 }
 
@@ -109,6 +154,16 @@ struct WinoT<3> {
     static constexpr float BT[5][5] = {
         {2, -1, -2, 1, 0}, {0, -2, -1, 1, 0}, {0, 2, -3, 1, 0}, {0, -1, 0, 1, 0}, {0, 2, -1, -2, 1}};
     static constexpr float AT[3][5] = {{1, 1, 1, 1, 0}, {0, 1, -1, 2, 0}, {0, 1, 1, 4, 1}};
+};
+template <>
+struct WinoT<4> {
+    // F(4,3): interpolation points 0, 1, -1, 2, -1/2, inf (-1/2 rather than -2 keeps the
+    // error at F(3,3)'s); B^T's rows scaled to small integers, their inverse scales in G
+    // (nnet.WINOGRAD_G, applied to the weights in f64)
+    static constexpr float BT[6][6] = {{2, 3, -4, -3, 2, 0},  {0, -2, -5, -1, 2, 0}, {0, 2, 1, -5, 2, 0},
+                                       {0, -1, -2, 1, 2, 0}, {0, 2, -1, -2, 1, 0},  {0, 2, 3, -4, -3, 2}};
+    static constexpr float AT[4][6] = {
+        {1, 1, 1, 1, 1, 0}, {0, 1, -1, 2, -0.5f, 0}, {0, 1, 1, 4, 0.25f, 0}, {0, 1, -1, 8, -0.125f, 1}};
 };
 
 __device__ __forceinline__ float vadd(float a, float b) { return a + b; }
@@ -351,54 +406,35 @@ struct Plane {
     }
 };
 
-// The next layer's input transform (pad `pad`) of the lane's h x h plane: V out.
-// Loop bounds are compile-time for HC > 0 (p <= (HC + 4) / 3), 3 otherwise (h <= 9).
-template <int HC, int FMT, class P>
-__device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, int pad, long long b, int c, int C, long long B,
+// The next layer's input transform (pad PAD) of the lane's h x h plane: V out.
+template <int HC, int FMT, int PAD, class P>
+__device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, long long b, int c, int C, long long B,
                                            void* __restrict__ Vout, int* overflow) {
-    constexpr int PMAX = HC > 0 ? (HC + 4) / 3 : 3;
     const int h = HC > 0 ? HC : h_rt;
-    const WSeq S(h + 2 * pad - 2);
+    const WSeq S(h + 2 * PAD - 2);
+    constexpr int HO = HC > 0 ? HC + 2 * PAD - 2 : 0;
+    for_tiles<HO>(S, [&](auto A_, auto B_, int i, int j) {
+        constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+        const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
+        const int y0 = S.off(i) - PAD, x0 = S.off(j) - PAD;
+        float d[MA + 2][MB + 2];
 #pragma unroll
-    for (int i = 0; i < PMAX; ++i) {
-        if (i >= S.p) break;
+        for (int u = 0; u < MA + 2; ++u)
 #pragma unroll
-        for (int j = 0; j < PMAX; ++j) {
-            if (j >= S.p) break;
-            const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
-            const int y0 = S.off(i) - pad, x0 = S.off(j) - pad;
-            with_types(S.m(i), S.m(j), [&](auto A_, auto B_) {
-                constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
-                float d[MA + 2][MB + 2];
+            for (int v = 0; v < MB + 2; ++v) {
+                const int iy = y0 + u, ix = x0 + v;
+                d[u][v] = (iy >= 0 && iy < h && ix >= 0 && ix < h) ? ys.get(iy * h + ix) : 0.f;
+            }
+        float Vt[MA + 2][MB + 2];
+        in_tile<MA, MB>(d, Vt);
 #pragma unroll
-                for (int u = 0; u < MA + 2; ++u)
-#pragma unroll
-                    for (int v = 0; v < MB + 2; ++v) {
-                        const int iy = y0 + u, ix = x0 + v;
-                        d[u][v] = (iy >= 0 && iy < h && ix >= 0 && ix < h) ? ys.get(iy * h + ix) : 0.f;
-                    }
-                float Vt[MA + 2][MB + 2];
-                in_tile<MA, MB>(d, Vt);
-#pragma unroll
-                for (int e = 0; e < (MA + 2) * (MB + 2); ++e) {
-#ifdef AZG_PROBE_OLD_V_LAYOUT  // timing probe only (tools/mid_probe.py): the earlier [hi(C) | lo(C)] rows
-                    if constexpr (FMT == AZG_WINO_SPLIT2) {
-                        const float x = Vt[e / (MB + 2)][e % (MB + 2)];
-                        const _Float16 hi = (_Float16)x, lo = (_Float16)(x - (float)hi);
-                        _Float16* r = (_Float16*)Vout + (row + e * ps) * 2 * C;
-                        r[c] = hi;
-                        r[C + c] = lo;
-                    } else
-#endif
-                    if constexpr (FMT == AZG_WINO_SPLIT2)  // the wave's lanes are channels c & ~63 ..
-                        store_v2_wave(Vout, row + e * ps, C, c & ~63, c & 63, Vt[e / (MB + 2)][e % (MB + 2)],
-                                      overflow);
-                    else
-                        store_v<FMT>(Vout, row + e * ps, C, c, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
-                }
-            });
+        for (int e = 0; e < (MA + 2) * (MB + 2); ++e) {
+            if constexpr (FMT == AZG_WINO_SPLIT2)  // the wave's lanes are channels c & ~63 ..
+                store_v2_wave(Vout, row + e * ps, C, c & ~63, c & 63, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
+            else
+                store_v<FMT>(Vout, row + e * ps, C, c, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
         }
-    }
+    });
 }
 
 // Layer i's output transform fused with layer i+1's input transform (pad 0
@@ -411,7 +447,6 @@ template <int HC, int FMT>
 __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restrict__ Min, const float* __restrict__ bias,
                                                           void* __restrict__ Vout, int h_rt, int C, long long B,
                                                           float mscale, int* overflow) {
-    constexpr int PMAX = HC > 0 ? (HC + 2) / 3 : 3;
     extern __shared__ float ys_raw[];  // [h * h][64] when HC == 0
     const int h = HC > 0 ? HC : h_rt;
     const int lane = threadIdx.x;
@@ -423,31 +458,23 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
     Plane<HC> ys;
     ys.lds = ys_raw;
     ys.lane = lane;
+    for_tiles<HC>(S, [&](auto A_, auto B_, int i, int j) {
+        constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+        const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
+        const int y0 = S.off(i), x0 = S.off(j);
+        float mm[MA + 2][MB + 2];
 #pragma unroll
-    for (int i = 0; i < PMAX; ++i) {
-        if (i >= S.p) break;
+        for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
+            mm[e / (MB + 2)][e % (MB + 2)] = mscale * Min[(row + e * ps) * C + c];
+        float y[MA][MB];
+        out_tile<MA, MB>(mm, y);
 #pragma unroll
-        for (int j = 0; j < PMAX; ++j) {
-            if (j >= S.p) break;
-            const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
-            const int y0 = S.off(i), x0 = S.off(j);
-            with_types(S.m(i), S.m(j), [&](auto A_, auto B_) {
-                constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
-                float mm[MA + 2][MB + 2];
+        for (int a = 0; a < MA; ++a)
 #pragma unroll
-                for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
-                    mm[e / (MB + 2)][e % (MB + 2)] = mscale * Min[(row + e * ps) * C + c];
-                float y[MA][MB];
-                out_tile<MA, MB>(mm, y);
-#pragma unroll
-                for (int a = 0; a < MA; ++a)
-#pragma unroll
-                    for (int q = 0; q < MB; ++q)
-                        if (y0 + a < h && x0 + q < h) ys.put((y0 + a) * h + x0 + q, fmaxf(y[a][q] + bc, 0.f));
-            });
-        }
-    }
-    plane_to_V<HC, FMT>(ys, h, 0, b, c, C, B, Vout, overflow);
+            for (int q = 0; q < MB; ++q)
+                if (y0 + a < h && x0 + q < h) ys.put((y0 + a) * h + x0 + q, fmaxf(y[a][q] + bc, 0.f));
+    });
+    plane_to_V<HC, FMT, 0>(ys, h, b, c, C, B, Vout, overflow);
 }
 
 // The network's first two layers' front end in one pass: conv1 (depth -> C
@@ -501,7 +528,7 @@ __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restr
             }
             ys.put(y * n + x, fmaxf(acc + bk, 0.f));
         }
-    plane_to_V<NC, FMT>(ys, n, 1, b, k, C, B, Vout, overflow);
+    plane_to_V<NC, FMT, 1>(ys, n, b, k, C, B, Vout, overflow);
 }
 
 // one thread per work item, rounded up to whole groups of 8 blocks (xcd_item)
@@ -520,9 +547,22 @@ extern "C" int azg_winograd_layout(int32_t h_out, int32_t* seq, int32_t* groups)
     const WSeq S(h_out);
     if (seq)
         for (int i = 0; i < S.p; ++i) seq[i] = S.m(i);
-    if (groups)  // tiles per image of each group (3,3) (3,2) (2,3) (2,2)
-        for (int g = 0; g < 4; ++g) groups[g] = S.cnt(g < 2 ? 3 : 2) * S.cnt((g & 1) ? 2 : 3);
+    if (groups)  // tiles per image of each group (big,big) (big,small) (small,big) (small,small)
+        for (int g = 0; g < 4; ++g) groups[g] = S.cnt(g < 2 ? S.big : S.small()) * S.cnt((g & 1) ? S.small() : S.big);
     return S.p;
+}
+
+extern "C" int azg_winograd_tables(int32_t m, float* bt, float* at) {
+    if (m < 2 || m > 4 || !bt || !at) return AZG_ERR_ARG;
+    const int n = m + 2;
+    auto copy = [&](const auto& BT, const auto& AT) {
+        for (int i = 0; i < n * n; ++i) bt[i] = BT[i / n][i % n];
+        for (int i = 0; i < m * n; ++i) at[i] = AT[i / n][i % n];
+    };
+    if (m == 2) copy(WinoT<2>::BT, WinoT<2>::AT);
+    if (m == 3) copy(WinoT<3>::BT, WinoT<3>::AT);
+    if (m == 4) copy(WinoT<4>::BT, WinoT<4>::AT);
+    return 0;
 }
 
 extern "C" int azg_winograd_in_nhwc(const float* x, const float* in_bias, void* V, int32_t batch, int32_t h_in,

@@ -90,29 +90,47 @@ def _azg_conv3x3(x, wt, b, pad):
     return y
 
 
-# Winograd F(m, 3) weight transforms G [m+2][3] (azg_winograd.hip holds B^T, A^T)
+# Winograd F(m, 3) weight transforms G [m+2][3] (azg_winograd.hip holds B^T, A^T;
+# azg_winograd_tables copies them out).  F(2,3): points 0, 1, -1; F(3,3): 0, 1, -1, 2;
+# F(4,3): 0, 1, -1, 2, -1/2 with B^T's rows scaled to small integers (their inverse
+# scales are in G, which is applied to the weights in f64).  Points -1/2 instead of
+# the usual -2 keep F(4,3)'s error at F(3,3)'s (tools/wino_error_sim.py).
 WINOGRAD_G = {2: [[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]],
               3: [[0.5, 0.0, 0.0], [-0.5, -0.5, -0.5], [-1 / 6, 1 / 6, -1 / 6], [1 / 6, 1 / 3, 2 / 3],
-                  [0.0, 0.0, 1.0]]}
+                  [0.0, 0.0, 1.0]],
+              4: [[0.5, 0.0, 0.0], [-1 / 6, -1 / 6, -1 / 6], [1 / 6, -1 / 6, 1 / 6], [1 / 30, 1 / 15, 2 / 15],
+                  [-16 / 15, 8 / 15, -4 / 15], [0.0, 0.0, 0.5]]}
 
 
 def winograd_seq(h_out):
     """Tile sides along an h_out-long output axis (azg_winograd.hip WSeq, mirrored by
-    azg_winograd_layout): p = ceil(h/3) tiles, as many of side 3 as fit, the rest 2 --
-    7: [3, 2, 2], 5: [3, 2], 3: [3], 8: [3, 3, 2], 4: [2, 2]."""
-    p = (h_out + 2) // 3
-    n3 = max(h_out - 2 * p, 0)
-    return [3] * n3 + [2] * (p - n3)
+    azg_winograd_layout): the fewest tiles, p = ceil(h/4), of sides in {4, 3, 2} summing
+    to h with at most two sides (big first), i.e. the fewest transformed points
+    h + 2p -- 7: [4, 3], 5: [3, 2], 3: [3], 8: [4, 4], 6: [3, 3], 4: [4]; h = 1: one
+    2-tile, cropped."""
+    p = max(1, (h_out + 3) // 4)
+    r = max(h_out - 2 * p, 0)
+    if r > p:
+        return [4] * (r - p) + [3] * (2 * p - r)
+    return [3] * r + [2] * (p - r)
+
+
+def winograd_types(h_out):
+    """(big, small) tile sides of an axis (kernel group order (big,big) (big,small)
+    (small,big) (small,small))."""
+    p = max(1, (h_out + 3) // 4)
+    return (4, 3) if max(h_out - 2 * p, 0) > p else (3, 2)
 
 
 def winograd_groups(h_out):
-    """Tile types of an h_out x h_out output in the kernels' order (3,3) (3,2) (2,3) (2,2),
-    present ones only: [(ma, mb, points (ma+2)(mb+2), tiles per image)]."""
+    """Tile types of an h_out x h_out output in the kernels' order (big,big) (big,small)
+    (small,big) (small,small), present ones only: [(ma, mb, points (ma+2)(mb+2), tiles
+    per image)]."""
     seq = winograd_seq(h_out)
-    cnt = {3: seq.count(3), 2: seq.count(2)}
+    big, small = winograd_types(h_out)
     out = []
-    for ma, mb in ((3, 3), (3, 2), (2, 3), (2, 2)):
-        n = cnt[ma] * cnt[mb]
+    for ma, mb in ((big, big), (big, small), (small, big), (small, small)):
+        n = seq.count(ma) * seq.count(mb)
         if n:
             out.append((ma, mb, (ma + 2) * (mb + 2), n))
     return out
@@ -126,7 +144,7 @@ def winograd_points(h_out):
 def _winograd_u(w, h_out):
     """Winograd weights of a layer with an h_out x h_out output, the groups of
     winograd_groups one after another: U[e = (ma+2) a + b][c][k] = (G_ma g_kc G_mb^T)[a][b],
-    formed in f64 and rounded once (G has entries 1/2, 1/3, 1/6).  [points][C][K]."""
+    formed in f64 and rounded once (G has entries like 1/6, 1/15).  [points][C][K]."""
     us = []
     for ma, mb, P, _ in winograd_groups(h_out):
         Ga = torch.tensor(WINOGRAD_G[ma], dtype=torch.float64, device=w.device)

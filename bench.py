@@ -61,9 +61,9 @@ def net_flops(n, depth, A, c=512):
 
 
 def winograd_flops(n, c=512):
-    """GEMM FLOPs per leaf of conv2-4 as mixed F(3,3)/F(2,3) Winograd (nnet.winograd_points:
-    (sum of tile sides + 2)^2 transformed points per image x 2 C K): 7x7 board
-    (13^2 + 9^2 + 5^2) x 2 x 512^2 = 144.2 M vs 391.6 M direct."""
+    """GEMM FLOPs per leaf of conv2-4 as mixed F(4,3)/F(3,3)/F(2,3) Winograd
+    (nnet.winograd_points: (sum of tile sides + 2)^2 transformed points per image x 2 C K):
+    7x7 board (11^2 + 9^2 + 5^2) x 2 x 512^2 = 119.0 M vs 391.6 M direct."""
     from azg_amd.nnet import winograd_points
     return sum(winograd_points(h) * 2 * c * c for h in (n, n - 2, n - 4))
 
@@ -347,8 +347,10 @@ def main():
             g = {"split": "split-fp16 GEMMs (3 fp16 MFMA products, f32 accumulate; libazg azg_split_gemm)",
                  "split_blas": "split-fp16 GEMMs (3 fp16 MFMA products, f32 accumulate; hipBLASLt)",
                  "f32": "f32 GEMMs (hipBLASLt)"}[ev.gemm]
-            seq = "+".join(map(str, winograd_seq(ev.h_out[i])))
-            return (f"Winograd {seq} tiles per axis (F(3,3)/F(2,3)): libazg fused transforms + "
+            sides = winograd_seq(ev.h_out[i])
+            seq = "+".join(map(str, sides))
+            fm = "/".join(f"F({m},3)" for m in sorted(set(sides), reverse=True))
+            return (f"Winograd {seq} tiles per axis ({fm}): libazg fused transforms + "
                     f"{winograd_points(ev.h_out[i])}-point {g}")
         conv_kernel_desc = ("conv2-4 per forward: " + "; ".join(f"conv{i} {name(i, m)}" for i, m in impls.items())
                             if impls else "whole forward (no conv hook)")

@@ -151,12 +151,14 @@ int  azg_conv3x3_bias_relu_nhwc(const float* x, const float* wt, const float* bi
 int  azg_conv3x3_variant(int variant, const float* x, const float* wt, const float* bias, float* y, int32_t batch,
                          int32_t h_in, int32_t pad, int32_t c_in, int32_t c_out, void* stream);
 
-/* Leaf-network 3x3 convolutions as Winograd convolutions over mixed F(3,3) /
- * F(2,3) tiles (azg_winograd.hip).  They replace the convolutions of
+/* Leaf-network 3x3 convolutions as Winograd convolutions over mixed F(4,3) /
+ * F(3,3) / F(2,3) tiles (azg_winograd.hip).  They replace the convolutions of
  * InflexionNNet.forward (InflexionNNet.py:39-45, BN folded).  An h-long output axis
- * is cut into p = ceil(h/3) tiles, as many of side 3 as fit, the rest of side 2
- * (7 = 3+2+2, 5 = 3+2); azg_winograd_layout returns p, writes the sides to seq[p]
- * and the tiles per image of the groups (3,3) (3,2) (2,3) (2,2) to groups[4].
+ * is cut into the fewest tiles, p = ceil(h/4), of sides 4/3/2 with at most two sides,
+ * big = small + 1 (7 = 4+3, 5 = 3+2, 3 = 3, 8 = 4+4); azg_winograd_layout returns p,
+ * writes the sides to seq[p] and the tiles per image of the groups (big,big)
+ * (big,small) (small,big) (small,small) to groups[4].  azg_winograd_tables copies
+ * F(m,3)'s B^T [(m+2)^2] and A^T [m(m+2)] (row-major; m = 2, 3, 4) to bt, at.
  * V and M hold the groups one after another, group g = (ma, mb) as
  * [P_g = (ma+2)(mb+2) points][batch * tiles_g][row], tiles row-major per image.
  *   azg_winograd_in_nhwc : x NHWC [batch, h_in, h_in, c] (zero padding `pad`) ->
@@ -176,6 +178,7 @@ int  azg_conv3x3_variant(int variant, const float* x, const float* wt, const flo
  * c % 4 == 0, k % 4 == 0, 16-B aligned pointers, h_out <= 64. */
 enum { AZG_WINO_F32 = 0, AZG_WINO_SPLIT = 1, AZG_WINO_SPLIT2 = 2 };
 int  azg_winograd_layout(int32_t h_out, int32_t* seq, int32_t* groups);
+int  azg_winograd_tables(int32_t m, float* bt, float* at);
 int  azg_winograd_in_nhwc(const float* x, const float* in_bias, void* V, int32_t batch, int32_t h_in, int32_t pad,
                           int32_t c, int32_t vfmt, int32_t* overflow, void* stream);
 int  azg_winograd_out_nhwc(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,

@@ -7,6 +7,7 @@ import hashlib
 import os
 
 import numpy as np
+import pytest
 import torch
 
 import azg_amd  # noqa: F401
@@ -70,19 +71,46 @@ def test_winograd_layout_matches_libazg():
     the kernels' own (azg_winograd_layout), and covers each axis exactly."""
     import ctypes
     from azg_amd import _lib
-    from azg_amd.nnet import winograd_groups, winograd_points, winograd_seq
+    from azg_amd.nnet import winograd_groups, winograd_points, winograd_seq, winograd_types
     L = _lib.lib()
-    assert winograd_seq(7) == [3, 2, 2] and winograd_seq(5) == [3, 2] and winograd_seq(3) == [3]
-    assert winograd_points(7) == 169 and winograd_points(5) == 81 and winograd_points(3) == 25
+    assert winograd_seq(7) == [4, 3] and winograd_seq(5) == [3, 2] and winograd_seq(3) == [3]
+    assert winograd_seq(8) == [4, 4] and winograd_seq(6) == [3, 3] and winograd_seq(4) == [4]
+    assert winograd_points(7) == 121 and winograd_points(5) == 81 and winograd_points(3) == 25
     for h in range(1, 30):
         seq = (ctypes.c_int32 * 16)()
         groups = (ctypes.c_int32 * 4)()
         p = L.azg_winograd_layout(h, seq, groups)
         assert list(seq[:p]) == winograd_seq(h), h
         assert sum(winograd_seq(h)) == max(h, 2), h  # exact cover (h = 1 pads to one 2-tile)
+        assert p == max(1, -(-h // 4)), h  # the fewest tiles of side <= 4
+        big, small = winograd_types(h)
+        assert set(winograd_seq(h)) <= {big, small} and big == small + 1, h
         want = {(ma, mb): n for ma, mb, _, n in winograd_groups(h)}
-        for g, (ma, mb) in enumerate(((3, 3), (3, 2), (2, 3), (2, 2))):
+        for g, (ma, mb) in enumerate(((big, big), (big, small), (small, big), (small, small))):
             assert groups[g] == want.get((ma, mb), 0), (h, g)
+
+
+@pytest.mark.parametrize("m", [2, 3, 4])
+def test_winograd_tables_are_exact(m):
+    """The kernels' B^T, A^T (azg_winograd_tables) with nnet.WINOGRAD_G compute the 3-tap
+    correlation: A^T [(G g) * (B^T d)] = sum_k g_k d_{i+k}, in f64, for every basis g, d."""
+    import ctypes
+    from azg_amd import _lib
+    from azg_amd.nnet import WINOGRAD_G
+    n = m + 2
+    bt = (ctypes.c_float * (n * n))()
+    at = (ctypes.c_float * (m * n))()
+    assert _lib.lib().azg_winograd_tables(m, bt, at) == 0
+    BT = np.array(bt[:], np.float64).reshape(n, n)
+    AT = np.array(at[:], np.float64).reshape(m, n)
+    G = np.array(WINOGRAD_G[m], np.float64)
+    for k in range(3):
+        for l in range(n):
+            g = np.eye(3)[k]
+            d = np.eye(n)[l]
+            y = AT @ ((G @ g) * (BT @ d))
+            want = np.array([1.0 if l == i + k else 0.0 for i in range(m)])
+            np.testing.assert_allclose(y, want, atol=1e-12)
 
 
 def test_split2_operand_blocks():
