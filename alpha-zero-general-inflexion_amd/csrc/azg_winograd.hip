@@ -1,20 +1,20 @@
 // azg_winograd.hip -- the leaf network's 3x3 convolutions as Winograd convolutions
-// over mixed F(4,3) / F(3,3) / F(2,3) tiles.
+// over mixed F(5,3) / F(4,3) / F(3,3) / F(2,3) tiles.
 //
 // conv2-4 of InflexionNNet.forward (InflexionNNet.py:39-45, BN folded) are
 // y = relu(bias + conv3x3(x, w)).  Winograd F(m,3) along one axis turns m outputs
 // into n = m + 2 transformed points; the 2-D transform is separable, so a tile may
 // use F(ma,3) down its rows and F(mb,3) across its columns:
 //     Y = A_ma^T [ U (.) V ] A_mb,  U = G_ma g G_mb^T (per (c, k)),  V = B_ma^T d B_mb.
-// An h-long output axis is cut into the fewest tiles of sides 4, 3, 2 (at most two
-// sides per axis; h = 7: 4+3; 5: 3+2; 3: 3; 8: 4+4; 6: 3+3; 4: 4), the fewest
-// transformed points that cover it exactly: 11^2 instead of 13^2 (3+2+2) for a 7x7
-// output, 9^2 for 5x5.
+// An h-long output axis is cut into the fewest tiles of side <= 5, sides as equal as
+// possible (at most two per axis; h = 7: 4+3; 5: 5; 3: 3; 8: 4+4; 6: 3+3; 4: 4), the
+// fewest transformed points that cover it exactly with F(m <= 5, 3): 11^2 instead of
+// 13^2 (3+2+2) for a 7x7 output, 7^2 instead of 9^2 (3+2) for 5x5.
 //
 // Summed over input channels c, each transformed point e of a tile type
 // g = (ma, mb) is one GEMM  M_e[T_g x K] = V_e[T_g x C] x U_e[C x K].  Layout of V
 // (and M, with K for C): the groups (big,big), (big,small), (small,big), (small,small)
-// (big = 4 or 3, small = big - 1, per layer: WSeq) one after another
+// (small = big - 1, per layer: WSeq) one after another
 // (absent types skipped), group g as [P_g][batch * n_g][row] with P_g = (ma+2)(mb+2)
 // points and n_g tiles of that type per image, tiles row-major within the image.
 // The GEMMs (hipBLASLt through torch.bmm) are the caller's; these kernels are the
@@ -28,8 +28,8 @@
 //                     one pass (the activation stays on chip)
 //   * winograd_first: conv1 + bias + ReLU from the NCHW planes + conv2's input
 //                     transform in one pass
-// B and A have small entries (B^T integers up to 5; A^T up to 8, F(4,3)'s -1/2 point
-// powers 1/2..1/8 exact); U is formed in f64 by the caller (G entries like 1/6, 1/15).
+// B and A have small entries (B^T integers up to 17; A^T powers of the points, exact
+// in f32); U is formed in f64 by the caller (G entries like 1/6, 1/15).
 //
 // V is written in one of three formats (vfmt):
 //   AZG_WINO_F32  : f32 rows of C;
@@ -56,19 +56,18 @@ struct IC {
     static constexpr int value = V;
 };
 
-// Tile sequence of an h-long output axis: the fewest tiles, p = ceil(h / 4), of sides
-// in {4, 3, 2} summing to h with at most two distinct sides (big = small + 1, the big
-// ones first): r = h - 2p extra units over all-2 tiles; r <= p: r 3-tiles + (p - r)
-// 2-tiles, else (r - p) 4-tiles + (2p - r) 3-tiles.  h = 1: one 2-tile, cropped.
+// Tile sequence of an h-long output axis: the fewest tiles of side <= 5, p = ceil(h / 5),
+// with sides as equal as possible -- big = ceil(h / p) for the first nbig tiles,
+// big - 1 for the rest (h = 7: 4+3; 5: 5; 3: 3; 8: 4+4; 6: 3+3; 4: 4; 9: 5+4).
+// h = 1: one 2-tile, cropped.
 struct WSeq {
     int h, p, big, nbig;
-    __host__ __device__ static constexpr int tiles(int h_) { return h_ <= 4 ? 1 : (h_ + 3) / 4; }
-    __host__ __device__ static constexpr int extra(int h_) {
-        return h_ - 2 * tiles(h_) > 0 ? h_ - 2 * tiles(h_) : 0;
+    __host__ __device__ static constexpr int tiles(int h_) { return h_ <= 5 ? 1 : (h_ + 4) / 5; }
+    __host__ __device__ static constexpr int side(int h_) {
+        return h_ < 2 ? 2 : (h_ + tiles(h_) - 1) / tiles(h_);
     }
     __host__ __device__ constexpr explicit WSeq(int h_)
-        : h(h_), p(tiles(h_)), big(extra(h_) > tiles(h_) ? 4 : 3),
-          nbig(extra(h_) > tiles(h_) ? extra(h_) - tiles(h_) : extra(h_)) {}
+        : h(h_), p(tiles(h_)), big(side(h_)), nbig(h_ < 2 ? 1 : h_ - tiles(h_) * (side(h_) - 1)) {}
     __host__ __device__ constexpr int small() const { return big - 1; }
     __host__ __device__ constexpr int m(int i) const { return i < nbig ? big : big - 1; }
     __host__ __device__ constexpr int off(int i) const {
@@ -99,16 +98,34 @@ struct WSeq {
 // run f(IC<ma>, IC<mb>): the tile bodies are compiled per type; with constant
 // ma, mb (unrolled compile-time sequences) the branches fold away
 template <class F>
-__device__ __forceinline__ void with_type_b(int ma, int mb, F&& f) {
-    if (mb == 4) f(IC<4>{});
-    else if (mb == 3) f(IC<3>{});
+__device__ __forceinline__ void with_type(int m, F&& f) {
+    if (m == 5) f(IC<5>{});
+    else if (m == 4) f(IC<4>{});
+    else if (m == 3) f(IC<3>{});
     else f(IC<2>{});
 }
 template <class F>
 __device__ __forceinline__ void with_types(int ma, int mb, F&& f) {
-    if (ma == 4) with_type_b(ma, mb, [&](auto B_) { f(IC<4>{}, B_); });
-    else if (ma == 3) with_type_b(ma, mb, [&](auto B_) { f(IC<3>{}, B_); });
-    else with_type_b(ma, mb, [&](auto B_) { f(IC<2>{}, B_); });
+    with_type(ma, [&](auto A_) { with_type(mb, [&](auto B_) { f(A_, B_); }); });
+}
+
+// with_types restricted to the sides a compile-time output side HC has (HC > 0): the
+// per-thread kernels then instantiate only the tile types that occur
+template <int HC, class F>
+__device__ __forceinline__ void with_types_of(int ma, int mb, F&& f) {
+    if constexpr (HC > 0) {
+        constexpr WSeq SC(HC);
+        constexpr int BG = SC.big, SM = SC.nbig == SC.p ? SC.big : SC.big - 1;
+        if (ma == BG) {
+            if (mb == BG) f(IC<BG>{}, IC<BG>{});
+            else f(IC<BG>{}, IC<SM>{});
+        } else {
+            if (mb == BG) f(IC<SM>{}, IC<BG>{});
+            else f(IC<SM>{}, IC<SM>{});
+        }
+    } else {
+        with_types(ma, mb, f);
+    }
 }
 
 template <int... Is, class F>
@@ -164,6 +181,21 @@ struct WinoT<4> {
                                        {0, -1, -2, 1, 2, 0}, {0, 2, -1, -2, 1, 0},  {0, 2, 3, -4, -3, 2}};
     static constexpr float AT[4][6] = {
         {1, 1, 1, 1, 1, 0}, {0, 1, -1, 2, -0.5f, 0}, {0, 1, 1, 4, 0.25f, 0}, {0, 1, -1, 8, -0.125f, 1}};
+};
+template <>
+struct WinoT<5> {
+    // F(5,3): interpolation points 0, 1, -1, -1/2, -2, 3/2, inf (A^T's powers exact in
+    // f32; the set with the smallest error among dyadic ones, tools/wino_error_sim.py);
+    // B^T's rows scaled to integers, their inverse scales in G
+    static constexpr float BT[7][7] = {{6, 11, -10, -15, 4, 4, 0}, {0, -6, -17, -7, 8, 4, 0},
+                                       {0, 6, 5, -15, 0, 4, 0},    {0, 6, -1, -8, 1, 2, 0},
+                                       {0, 3, 4, -7, -4, 4, 0},    {0, -2, -5, 0, 5, 2, 0},
+                                       {0, 6, 11, -10, -15, 4, 4}};
+    static constexpr float AT[5][7] = {{1, 1, 1, 1, 1, 1, 0},
+                                       {0, 1, -1, -0.5f, -2, 1.5f, 0},
+                                       {0, 1, 1, 0.25f, 4, 2.25f, 0},
+                                       {0, 1, -1, -0.125f, -8, 3.375f, 0},
+                                       {0, 1, 1, 0.0625f, 16, 5.0625f, 1}};
 };
 
 __device__ __forceinline__ float vadd(float a, float b) { return a + b; }
@@ -307,11 +339,11 @@ __device__ __forceinline__ long long xcd_item() {
 // One thread per (tile, 4 channels); tiles image-major, row-major in the image.
 // in_bias != null: x is the previous layer's raw output and relu(x + in_bias) is
 // applied on load (that layer's bias + ReLU fused here; padding stays 0).
-template <int FMT>
+template <int FMT, int HC>
 __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restrict__ x,
                                                           const float4* __restrict__ in_bias, void* __restrict__ V,
                                                           int H, int pad, int C4, long long B, int* overflow) {
-    const WSeq S(H + 2 * pad - 2);
+    const WSeq S(HC > 0 ? HC : H + 2 * pad - 2);
     const long long item = xcd_item();
     if (item >= B * S.p * S.p * C4) return;
     const int c4 = (int)(item % C4);
@@ -323,7 +355,7 @@ __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restri
     const float4 ib = in_bias ? in_bias[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
     const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
     const int y0 = S.off(i) - pad, x0 = S.off(j) - pad;
-    with_types(S.m(i), S.m(j), [&](auto A_, auto B_) {
+    with_types_of<HC>(S.m(i), S.m(j), [&](auto A_, auto B_) {
         constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
         float4 d[MA + 2][MB + 2];
 #pragma unroll
@@ -349,12 +381,13 @@ __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restri
 // FMT = AZG_WINO_F32: y is the NHWC f32 activation.  Otherwise y is one fp16 row
 // per image in V format FMT over the image's flattened NHWC activation (width
 // Ho * Ho * K): the A operand of a split GEMM over it (the network's fc1).
-template <int FMT>
+template <int FMT, int HC>
 __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restrict__ Min,
                                                            const float4* __restrict__ bias, void* __restrict__ y,
                                                            int Ho, int K4, long long B, int relu, float mscale,
                                                            int* overflow) {
-    const WSeq S(Ho);
+    const WSeq S(HC > 0 ? HC : Ho);
+    if (HC > 0) Ho = HC;
     const long long item = xcd_item();
     if (item >= B * S.p * S.p * K4) return;
     const int k4 = (int)(item % K4);
@@ -365,7 +398,7 @@ __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restr
     const long long b = r / S.p;
     const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
     const float4 bb = bias[k4];
-    with_types(S.m(i), S.m(j), [&](auto A_, auto B_) {
+    with_types_of<HC>(S.m(i), S.m(j), [&](auto A_, auto B_) {
         constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
         float4 m[MA + 2][MB + 2];
 #pragma unroll
@@ -537,6 +570,33 @@ unsigned grid_for(long long n) {
     return (unsigned)(((blocks + 7) / 8) * 8);
 }
 
+// winograd_out_kernel for the output sides of the supported boards (compile-time
+// tile types) or any side (all types)
+int launch_out(int vfmt, const float* M, const float* bias, void* y, int batch, int h_out, int k, int relu,
+               float mscale, int* overflow, void* stream) {
+    const WSeq S(h_out);
+    const dim3 grid(grid_for((long long)batch * S.p * S.p * (k / 4)));
+    hipStream_t st = (hipStream_t)stream;
+    auto launch = [&](auto F_, auto H_) {
+        hipLaunchKernelGGL((winograd_out_kernel<decltype(F_)::value, decltype(H_)::value>), grid, dim3(256), 0, st,
+                           (const float4*)M, (const float4*)bias, y, h_out, k / 4, (long long)batch, relu, mscale,
+                           overflow);
+    };
+    auto by_side = [&](auto F_) {
+        switch (h_out) {
+            case 2: launch(F_, IC<2>{}); break;
+            case 3: launch(F_, IC<3>{}); break;
+            case 4: launch(F_, IC<4>{}); break;
+            case 5: launch(F_, IC<5>{}); break;
+            default: launch(F_, IC<0>{});
+        }
+    };
+    if (vfmt == AZG_WINO_F32) by_side(IC<AZG_WINO_F32>{});
+    if (vfmt == AZG_WINO_SPLIT) by_side(IC<AZG_WINO_SPLIT>{});
+    if (vfmt == AZG_WINO_SPLIT2) by_side(IC<AZG_WINO_SPLIT2>{});
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
 bool bad_fmt(int vfmt, const int* overflow) {
     return !(vfmt == AZG_WINO_F32 || ((vfmt == AZG_WINO_SPLIT || vfmt == AZG_WINO_SPLIT2) && overflow));
 }
@@ -553,7 +613,7 @@ extern "C" int azg_winograd_layout(int32_t h_out, int32_t* seq, int32_t* groups)
 }
 
 extern "C" int azg_winograd_tables(int32_t m, float* bt, float* at) {
-    if (m < 2 || m > 4 || !bt || !at) return AZG_ERR_ARG;
+    if (m < 2 || m > 5 || !bt || !at) return AZG_ERR_ARG;
     const int n = m + 2;
     auto copy = [&](const auto& BT, const auto& AT) {
         for (int i = 0; i < n * n; ++i) bt[i] = BT[i / n][i % n];
@@ -562,6 +622,7 @@ extern "C" int azg_winograd_tables(int32_t m, float* bt, float* at) {
     if (m == 2) copy(WinoT<2>::BT, WinoT<2>::AT);
     if (m == 3) copy(WinoT<3>::BT, WinoT<3>::AT);
     if (m == 4) copy(WinoT<4>::BT, WinoT<4>::AT);
+    if (m == 5) copy(WinoT<5>::BT, WinoT<5>::AT);
     return 0;
 }
 
@@ -576,14 +637,25 @@ extern "C" int azg_winograd_in_nhwc(const float* x, const float* in_bias, void* 
     const WSeq S(h_out);
     const dim3 grid(grid_for((long long)batch * S.p * S.p * (c / 4)));
     hipStream_t st = (hipStream_t)stream;
-#define AZG_IN(F)                                                                                            \
-    if (vfmt == F)                                                                                           \
-        hipLaunchKernelGGL(winograd_in_kernel<F>, grid, dim3(256), 0, st, (const float4*)x, (const float4*)in_bias, \
-                           V, h_in, pad, c / 4, (long long)batch, overflow);
-    AZG_IN(AZG_WINO_F32)
-    AZG_IN(AZG_WINO_SPLIT)
-    AZG_IN(AZG_WINO_SPLIT2)
-#undef AZG_IN
+    auto launch = [&](auto F_, auto H_) {
+        hipLaunchKernelGGL((winograd_in_kernel<decltype(F_)::value, decltype(H_)::value>), grid, dim3(256), 0, st,
+                           (const float4*)x, (const float4*)in_bias, V, h_in, pad, c / 4, (long long)batch,
+                           overflow);
+    };
+    auto by_side = [&](auto F_) {  // the output sides of the supported boards get their own build
+        switch (h_out) {
+            case 3: launch(F_, IC<3>{}); break;
+            case 4: launch(F_, IC<4>{}); break;
+            case 5: launch(F_, IC<5>{}); break;
+            case 6: launch(F_, IC<6>{}); break;
+            case 7: launch(F_, IC<7>{}); break;
+            case 8: launch(F_, IC<8>{}); break;
+            default: launch(F_, IC<0>{});
+        }
+    };
+    if (vfmt == AZG_WINO_F32) by_side(IC<AZG_WINO_F32>{});
+    if (vfmt == AZG_WINO_SPLIT) by_side(IC<AZG_WINO_SPLIT>{});
+    if (vfmt == AZG_WINO_SPLIT2) by_side(IC<AZG_WINO_SPLIT2>{});
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
@@ -592,11 +664,7 @@ extern "C" int azg_winograd_out_nhwc(const float* M, const float* bias, float* y
     if (!M || !bias || !y || batch <= 0 || h_out <= 0 || h_out > 64 || k <= 0 || k % 4 || ((uintptr_t)M & 15) ||
         ((uintptr_t)bias & 15) || ((uintptr_t)y & 15) || (long long)batch * h_out * h_out * (k / 4) > (1ll << 38))
         return AZG_ERR_ARG;
-    const WSeq S(h_out);
-    hipLaunchKernelGGL(winograd_out_kernel<AZG_WINO_F32>, dim3(grid_for((long long)batch * S.p * S.p * (k / 4))),
-                       dim3(256), 0, (hipStream_t)stream, (const float4*)M, (const float4*)bias, (void*)y, h_out,
-                       k / 4, (long long)batch, relu, mscale, (int*)nullptr);
-    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+    return launch_out(AZG_WINO_F32, M, bias, y, batch, h_out, k, relu, mscale, nullptr, stream);
 }
 
 extern "C" int azg_winograd_out_split(const float* M, const float* bias, void* y, int32_t batch, int32_t h_out,
@@ -607,16 +675,7 @@ extern "C" int azg_winograd_out_split(const float* M, const float* bias, void* y
         (vfmt == AZG_WINO_SPLIT2 && k % 32) ||
         (long long)h_out * h_out * k > (1ll << 28) || (long long)batch * h_out * h_out * (k / 4) > (1ll << 38))
         return AZG_ERR_ARG;
-    const WSeq S(h_out);
-    const dim3 grid(grid_for((long long)batch * S.p * S.p * (k / 4)));
-    hipStream_t st = (hipStream_t)stream;
-    if (vfmt == AZG_WINO_SPLIT)
-        hipLaunchKernelGGL(winograd_out_kernel<AZG_WINO_SPLIT>, grid, dim3(256), 0, st, (const float4*)M,
-                           (const float4*)bias, y, h_out, k / 4, (long long)batch, relu, mscale, overflow);
-    else
-        hipLaunchKernelGGL(winograd_out_kernel<AZG_WINO_SPLIT2>, grid, dim3(256), 0, st, (const float4*)M,
-                           (const float4*)bias, y, h_out, k / 4, (long long)batch, relu, mscale, overflow);
-    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+    return launch_out(vfmt, M, bias, y, batch, h_out, k, relu, mscale, overflow, stream);
 }
 
 extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, void* V, int32_t batch, int32_t h, int32_t c,

@@ -92,34 +92,38 @@ def _azg_conv3x3(x, wt, b, pad):
 
 # Winograd F(m, 3) weight transforms G [m+2][3] (azg_winograd.hip holds B^T, A^T;
 # azg_winograd_tables copies them out).  F(2,3): points 0, 1, -1; F(3,3): 0, 1, -1, 2;
-# F(4,3): 0, 1, -1, 2, -1/2 with B^T's rows scaled to small integers (their inverse
-# scales are in G, which is applied to the weights in f64).  Points -1/2 instead of
-# the usual -2 keep F(4,3)'s error at F(3,3)'s (tools/wino_error_sim.py).
+# F(4,3): 0, 1, -1, 2, -1/2; F(5,3): 0, 1, -1, -1/2, -2, 3/2 -- B^T's rows scaled to
+# small integers, their inverse scales in G (applied to the weights in f64).  The point
+# sets keep the layer error at 1.2x (F(4,3)) and 2.6x (F(5,3)) F(3,3)'s
+# (tools/wino_error_sim.py); the network's P, v stay within 1e-5 of the reference.
 WINOGRAD_G = {2: [[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]],
               3: [[0.5, 0.0, 0.0], [-0.5, -0.5, -0.5], [-1 / 6, 1 / 6, -1 / 6], [1 / 6, 1 / 3, 2 / 3],
                   [0.0, 0.0, 1.0]],
               4: [[0.5, 0.0, 0.0], [-1 / 6, -1 / 6, -1 / 6], [1 / 6, -1 / 6, 1 / 6], [1 / 30, 1 / 15, 2 / 15],
-                  [-16 / 15, 8 / 15, -4 / 15], [0.0, 0.0, 0.5]]}
+                  [-16 / 15, 8 / 15, -4 / 15], [0.0, 0.0, 0.5]],
+              5: [[1 / 6, 0.0, 0.0], [-1 / 18, -1 / 18, -1 / 18], [1 / 10, -1 / 10, 1 / 10],
+                  [-4 / 9, 2 / 9, -1 / 9], [-1 / 126, 1 / 63, -2 / 63], [4 / 105, 2 / 35, 3 / 35],
+                  [0.0, 0.0, 0.25]]}
 
 
 def winograd_seq(h_out):
     """Tile sides along an h_out-long output axis (azg_winograd.hip WSeq, mirrored by
-    azg_winograd_layout): the fewest tiles, p = ceil(h/4), of sides in {4, 3, 2} summing
-    to h with at most two sides (big first), i.e. the fewest transformed points
-    h + 2p -- 7: [4, 3], 5: [3, 2], 3: [3], 8: [4, 4], 6: [3, 3], 4: [4]; h = 1: one
-    2-tile, cropped."""
-    p = max(1, (h_out + 3) // 4)
-    r = max(h_out - 2 * p, 0)
-    if r > p:
-        return [4] * (r - p) + [3] * (2 * p - r)
-    return [3] * r + [2] * (p - r)
+    azg_winograd_layout): the fewest tiles of side <= 5, p = ceil(h/5), sides as equal
+    as possible, the bigger first -- 7: [4, 3], 5: [5], 3: [3], 8: [4, 4], 6: [3, 3],
+    4: [4], 9: [5, 4]; h = 1: one 2-tile, cropped."""
+    if h_out < 2:
+        return [2]
+    p = (h_out + 4) // 5
+    big = -(-h_out // p)
+    nbig = h_out - p * (big - 1)
+    return [big] * nbig + [big - 1] * (p - nbig)
 
 
 def winograd_types(h_out):
     """(big, small) tile sides of an axis (kernel group order (big,big) (big,small)
     (small,big) (small,small))."""
-    p = max(1, (h_out + 3) // 4)
-    return (4, 3) if max(h_out - 2 * p, 0) > p else (3, 2)
+    big = winograd_seq(h_out)[0]
+    return big, big - 1
 
 
 def winograd_groups(h_out):

@@ -61,7 +61,7 @@ def net_flops(n, depth, A, c=512):
 
 
 def winograd_flops(n, c=512):
-    """GEMM FLOPs per leaf of conv2-4 as mixed F(4,3)/F(3,3)/F(2,3) Winograd
+    """GEMM FLOPs per leaf of conv2-4 as mixed F(2..5,3) Winograd
     (nnet.winograd_points: (sum of tile sides + 2)^2 transformed points per image x 2 C K):
     7x7 board (11^2 + 9^2 + 5^2) x 2 x 512^2 = 119.0 M vs 391.6 M direct."""
     from azg_amd.nnet import winograd_points

@@ -100,10 +100,11 @@ def test_azg_conv3x3_variants(variant, B, H, pad):
 @pytest.mark.parametrize("B,H,pad", [(1, 7, 1), (37, 7, 1), (300, 7, 0), (129, 5, 0), (64, 8, 1), (5, 6, 0),
                                      (3, 4, 1), (7, 9, 1), (2, 11, 0), (3, 3, 1)])
 def test_winograd_conv3x3_matches_torch(B, H, pad, gemm):
-    """Winograd layer (mixed F(4,3)/F(3,3)/F(2,3) tiles: every tile-type group; libazg
-    transforms + split-fp16 or f32 bmm) vs torch conv2d + bias + ReLU, and against an f64
-    convolution within 1e-5 of the layer's largest pre-activation (f32-level error:
-    F(4,3)'s points 0, 1, -1, 2, -1/2 keep it at F(3,3)'s, tools/wino_error_sim.py)."""
+    """Winograd layer (mixed F(5,3)/F(4,3)/F(3,3)/F(2,3) tiles: every tile-type group;
+    libazg transforms + split-fp16 or f32 bmm) vs torch conv2d + bias + ReLU, and against
+    an f64 convolution within 2e-5 of the layer's largest pre-activation.  Measured
+    (tools/wino_layer_error.py, profiles/r02_wino_layer_error.json): split 3.4-8.4e-6,
+    split_blas / f32 GEMMs up to 1.6e-5 (F(5,3)); torch's direct f32 conv 0.3-1e-6."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
     torch.manual_seed(3)
@@ -122,7 +123,7 @@ def test_winograd_conv3x3_matches_torch(B, H, pad, gemm):
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
     pre64 = torch.nn.functional.conv2d(x.double(), w.cuda().double(), None, padding=pad)
     want64 = torch.relu(pre64 + b.double().view(1, -1, 1, 1))
-    assert (got.double() - want64).abs().max().item() <= 1e-5 * pre64.abs().max().item()
+    assert (got.double() - want64).abs().max().item() <= 2e-5 * pre64.abs().max().item()
 
 
 @pytest.mark.parametrize("gemm", ["split", "split_blas", "f32"])

@@ -73,16 +73,16 @@ def test_winograd_layout_matches_libazg():
     from azg_amd import _lib
     from azg_amd.nnet import winograd_groups, winograd_points, winograd_seq, winograd_types
     L = _lib.lib()
-    assert winograd_seq(7) == [4, 3] and winograd_seq(5) == [3, 2] and winograd_seq(3) == [3]
+    assert winograd_seq(7) == [4, 3] and winograd_seq(5) == [5] and winograd_seq(3) == [3]
     assert winograd_seq(8) == [4, 4] and winograd_seq(6) == [3, 3] and winograd_seq(4) == [4]
-    assert winograd_points(7) == 121 and winograd_points(5) == 81 and winograd_points(3) == 25
+    assert winograd_points(7) == 121 and winograd_points(5) == 49 and winograd_points(3) == 25
     for h in range(1, 30):
         seq = (ctypes.c_int32 * 16)()
         groups = (ctypes.c_int32 * 4)()
         p = L.azg_winograd_layout(h, seq, groups)
         assert list(seq[:p]) == winograd_seq(h), h
         assert sum(winograd_seq(h)) == max(h, 2), h  # exact cover (h = 1 pads to one 2-tile)
-        assert p == max(1, -(-h // 4)), h  # the fewest tiles of side <= 4
+        assert p == max(1, -(-h // 5)), h  # the fewest tiles of side <= 5
         big, small = winograd_types(h)
         assert set(winograd_seq(h)) <= {big, small} and big == small + 1, h
         want = {(ma, mb): n for ma, mb, _, n in winograd_groups(h)}
@@ -90,7 +90,7 @@ def test_winograd_layout_matches_libazg():
             assert groups[g] == want.get((ma, mb), 0), (h, g)
 
 
-@pytest.mark.parametrize("m", [2, 3, 4])
+@pytest.mark.parametrize("m", [2, 3, 4, 5])
 def test_winograd_tables_are_exact(m):
     """The kernels' B^T, A^T (azg_winograd_tables) with nnet.WINOGRAD_G compute the 3-tap
     correlation: A^T [(G g) * (B^T d)] = sum_k g_k d_{i+k}, in f64, for every basis g, d."""
