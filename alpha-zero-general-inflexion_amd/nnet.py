@@ -309,9 +309,16 @@ class InferenceNet(nn.Module):
             self.overflow.zero_()
             raise FloatingPointError("Winograd split-GEMM operand out of fp16 range; use InferenceNet(gemm='f32')")
 
-    # optional hook: callable(layer_index, "start"|"stop") used by bench.py to
-    # bracket each convolution with HIP events on the current stream
+    # optional hooks used by bench.py to bracket work with HIP events on the current
+    # stream: conv_hook(layer_index, "start"|"stop") around each convolution,
+    # kernel_hook(kind, layer_index, "start"|"stop") around each libazg launch of kind
+    # "gemm" (azg_split_gemm) or "transform" (the Winograd transforms)
     conv_hook = None
+    kernel_hook = None
+
+    def _khook(self, kind, i, what):
+        if self.kernel_hook is not None:
+            self.kernel_hook(kind, i, what)
 
     def _conv_miopen(self, x, i, pad):
         # MIOpen conv without bias, then one HIP pass: bias + ReLU in place (azg_nn.hip)
@@ -358,9 +365,11 @@ class InferenceNet(nn.Module):
         self._ensure_ws(self._wino_need(2, B, C, True), s.device)
         st = ctypes.c_void_p(torch.cuda.current_stream(s.device).cuda_stream)
         fmt, ovf = self._vfmt()
+        self._khook("transform", 1, "start")
         _lib.check(_lib.lib().azg_winograd_first_nchw(
             ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(self.w1c.data_ptr()), ctypes.c_void_p(self.b1.data_ptr()),
             ctypes.c_void_p(self._ws[0].data_ptr()), B, self.depth, self.n, C, fmt, ctypes.c_void_p(ovf), st))
+        self._khook("transform", 1, "stop")
 
     def _winograd_gemms(self, i, B, C, K):
         """M = V x U for every transformed point of layer i, by runs of tile groups with
@@ -377,10 +386,12 @@ class InferenceNet(nn.Module):
             from . import _lib
             pts = (ctypes.c_int32 * len(runs))(*[P for P, _ in runs])
             rows = (ctypes.c_int32 * len(runs))(*[B * n for _, n in runs])
+            self._khook("gemm", i, "start")
             _lib.check(_lib.lib().azg_split_gemm(
                 ctypes.c_void_p(self._ws[0].data_ptr()), ctypes.c_void_p(getattr(self, f"us_{i}").data_ptr()),
                 ctypes.c_void_p(self._ws[1].data_ptr()), len(runs), pts, rows, C, K,
                 ctypes.c_void_p(torch.cuda.current_stream(self._ws[0].device).cuda_stream)))
+            self._khook("gemm", i, "stop")
             return
         split = self.gemm == "split_blas"
         W = 3 * C if split else C
@@ -436,13 +447,17 @@ class InferenceNet(nn.Module):
                                               ctypes.c_void_p(ovf), s))
         self._winograd_gemms(i, B, C, K)
         if fuse_next:
+            self._khook("transform", i, "start")
             _lib.check(L.azg_winograd_mid_nhwc(M, bias, V, B, Ho, K, mscale, fmt, ctypes.c_void_p(ovf), s))
+            self._khook("transform", i, "stop")
             return None
         if split_out:
             # the flattened NHWC activation as one [hi | lo | hi] fp16 row per image (fc1's A operand)
             y = torch.empty((B, 3 * Ho * Ho * K), device=dev, dtype=torch.float16)
+            self._khook("transform", i, "start")
             _lib.check(L.azg_winograd_out_split(M, bias, ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, mscale, 1,
                                                 ctypes.c_void_p(self.overflow.data_ptr()), s))
+            self._khook("transform", i, "stop")
             return y
         y = torch.empty((B, K, Ho, Ho), device=dev, dtype=torch.float32, memory_format=torch.channels_last)
         _lib.check(L.azg_winograd_out_nhwc(M, bias, ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, mscale, s))

@@ -36,11 +36,10 @@ F32_MFMA_PEAK_TF = 157.3         # MI355X_MICROARCH.md: f32 matrix peak (dense)
 F16_MFMA_PEAK_TF = 2500.0        # MI355X_MICROARCH.md: BF16/FP16 MFMA peak (dense)
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E spec peak
 EXPANSIONS_PER_GAME_REF = 8555   # reference random-init Inflexion episodes
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_G4096.json")
-GEMM_PMC_FILE = os.path.join(ROOT, "profiles", "r01_split_gemm_pmc_v4.json")  # the azg_split_gemm default
-PMC_FILE_WINOGRAD = {"f32": os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd.json"),
-                     "split_blas": os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd_split_blas.json"),
-                     "split": os.path.join(ROOT, "profiles", "r01_pmc_G4096_winograd_split.json")}
+GEMM_PMC_FILE = os.path.join(ROOT, "profiles", "r02_split_gemm_pmc_v4.json")  # the azg_split_gemm default
+# PMC passes of the current Winograd tiling (F(4,3)+F(3,3) / F(5,3) / F(3,3)); the r01 files
+# were measured on the earlier F(3,3)/F(2,3) tiling and are kept for the record only
+PMC_FILE_WINOGRAD = {"split": os.path.join(ROOT, "profiles", "r02_pmc_G4096_winograd_split.json")}
 
 PRESETS = {
     "C1": dict(game="othello", n=6, games=1, sims=25),
@@ -60,10 +59,25 @@ def net_flops(n, depth, A, c=512):
     return conv1 + conv234 + fc, conv234
 
 
+def transform_bytes(n, depth, c=512, split=True):
+    """Algorithmic HBM bytes per leaf of the fused Winograd transforms (azg_winograd.hip),
+    each operand read or written once at its stored width: winograd_first reads the planes
+    and writes conv2's V; each winograd_mid reads layer i's M (f32) and writes layer i+1's
+    V; winograd_out reads conv4's M and writes the flattened activation ([hi|lo|hi] fp16
+    rows for fc1 in the split form, else f32).  V is 4 B per element (split hi + lo, or
+    f32), M 4 B.  7x7 Inflexion, split: 0.247 + 0.348 + 0.151 + 0.079 = 0.826 MB."""
+    from azg_amd.nnet import winograd_points
+    h = [n, n - 2, n - 4]
+    first = depth * n * n * 4 + winograd_points(h[0]) * c * 4
+    mids = [winograd_points(h[i]) * c * 4 + winograd_points(h[i + 1]) * c * 4 for i in range(2)]
+    out = winograd_points(h[2]) * c * 4 + h[2] * h[2] * c * (6 if split else 4)
+    return {"first": first, "mid": sum(mids), "out": out, "total": first + sum(mids) + out}
+
+
 def winograd_flops(n, c=512):
     """GEMM FLOPs per leaf of conv2-4 as mixed F(2..5,3) Winograd
     (nnet.winograd_points: (sum of tile sides + 2)^2 transformed points per image x 2 C K):
-    7x7 board (11^2 + 9^2 + 5^2) x 2 x 512^2 = 119.0 M vs 391.6 M direct."""
+    7x7 board (11^2 + 7^2 + 5^2) x 2 x 512^2 = 102.2 M vs 391.6 M direct."""
     from azg_amd.nnet import winograd_points
     return sum(winograd_points(h) * 2 * c * c for h in (n, n - 2, n - 4))
 
@@ -83,29 +97,27 @@ def tree_bytes_per_exp(A, planes_bytes, valid=87.0, d=1.33):
 
 
 def load_pmc(G, game, impl, gemm="split"):
-    """HBM-side bytes per launch from the committed PMC passes (tools/pmc_summary.py:
-    rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs, FETCH doubled
-    per the gfx950 correction).  Only valid for the workload and convolution
-    implementation it was measured on."""
-    path = {"miopen": PMC_FILE, "winograd": PMC_FILE_WINOGRAD[gemm]}.get(impl)
+    """HBM-side bytes from the committed PMC passes (tools/pmc_summary.py: rocprofv3
+    --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs, FETCH doubled per the gfx950
+    correction): per split-GEMM launch, per forward of the transforms, per simulation
+    step of the tree kernels.  Only valid for the workload and network form it was
+    measured on (G = 4096 Inflexion 7x7, Winograd + libazg split GEMM)."""
+    path = PMC_FILE_WINOGRAD.get(gemm) if impl == "winograd" else None
     if G != 4096 or game != "inflexion" or not path or not os.path.exists(path):
         return None
     d = json.load(open(path))
-    def tot(k):
-        if k not in d:
-            return 0.0
-        return d[k].get("hbm_bytes_per_forward") or d[k]["hbm_bytes_sum_over_shapes"]
-    if impl == "winograd":
-        conv = sum(tot(k) for k in ("winograd_first", "winograd_mid", "winograd_in", "winograd_out",
-                                      "split_gemm", "gemm (hipBLASLt)"))
-        what = "Winograd transforms + the GEMM batches (and the FC GEMMs, ~2%)"
-    else:
-        conv = tot("conv2-4 igemm")
-        what = "conv2+3+4 igemm"
-    tree = tot("select_kernel") + tot("expand_backup_kernel")
-    return {"conv": conv, "tree": tree,
-            "note": f"{os.path.relpath(path, ROOT)}: FETCH_SIZE x2 + WRITE_SIZE per forward ({what}); "
-                    "counts L2 misses incl. Infinity-Cache hits"}
+
+    def per_fwd(k):
+        return (d.get(k) or {}).get("hbm_bytes_per_forward") or 0.0
+
+    out = {"transforms": sum(per_fwd(k) for k in ("winograd_first", "winograd_mid", "winograd_out")),
+           "tree": per_fwd("select_kernel") + per_fwd("expand_backup_kernel"),
+           "note": f"{os.path.relpath(path, ROOT)}: FETCH_SIZE x2 + WRITE_SIZE (split GEMM: per launch; "
+                   "transforms: per forward; tree: per simulation step); counts L2 misses incl. Infinity-Cache hits"}
+    sg = d.get("split_gemm")
+    if sg and sg.get("dispatches"):
+        out["split_gemm"] = (sg["fetch_bytes_corrected_total"] + sg["write_bytes_total"]) / sg["dispatches"]
+    return out
 
 
 def parse():
@@ -241,6 +253,19 @@ def main():
 
     if hasattr(ev, "conv_hook"):
         ev.conv_hook = conv_hook
+    # HIP events around every libazg launch of the network (split GEMM, transforms), on the
+    # stream they are launched on (the current stream)
+    t_kern = {"gemm": Timer(), "transform": Timer()}
+    kpending = {}
+
+    def kernel_hook(kind, i, what):
+        if what == "start":
+            kpending[kind] = t_kern[kind].start()
+        else:
+            t_kern[kind].stop(kpending.pop(kind))
+
+    if hasattr(ev, "kernel_hook"):
+        ev.kernel_hook = kernel_hook
 
     def timed_move():
         for _ in range(eng.sims):
@@ -259,12 +284,16 @@ def main():
 
     step = timed_move
     if args.graph:
-        hook = getattr(ev, "conv_hook", None)
+        hook, khook = getattr(ev, "conv_hook", None), getattr(ev, "kernel_hook", None)
         if hook is not None:
             ev.conv_hook = None  # no event records inside the capture
+        if khook is not None:
+            ev.kernel_hook = None
         eng.capture_move()
         if hook is not None:
             ev.conv_hook = hook
+        if khook is not None:
+            ev.kernel_hook = khook
         step = eng.move
     if world > 1:
         dist.barrier()
@@ -389,7 +418,8 @@ def main():
                                  "reference); bench.py --full-games measures it directly"),
             "expansions": exp,
             "simulations": sims_run,
-            "roofline": {"bound": "mfma",
+            "roofline": None,  # the dominant kernel's (set below)
+            "roofline_conv_span": {"bound": "mfma",
                          "kernel": conv_kernel_desc,
                          "achieved": mfma_mult * conv_tflops, "peak": mfma_peak, "unit": "TFLOP/s",
                          "frac": mfma_mult * conv_tflops / mfma_peak, "traffic": None,
@@ -411,17 +441,52 @@ def main():
                            "wall_ms": elapsed * 1e3, "graph": bool(args.graph)},
             "iteration_sync_bytes": sync_bytes,
         }
+        # the dominant kernel: libazg's split GEMM (about half of the step's GPU time), its
+        # launches timed with HIP events on their stream; algorithmic FLOPs = the Winograd
+        # GEMM work (transformed points x 2 C K per leaf) x 3 fp16 products
+        g_pairs, t_pairs = t_kern["gemm"].pairs, t_kern["transform"].pairs
+        if g_pairs:
+            g_ms = t_kern["gemm"].total_ms()
+            n_launch = len(g_pairs)
+            per_fwd = n_launch / n_forwards
+            flops_launch = 3 * leaves * algo_conv_leaf / per_fwd
+            ach = flops_launch / (g_ms / n_launch / 1e3) / 1e12
+            out["roofline"] = {
+                "bound": "mfma", "kernel": "split_gemm_persist_kernel (libazg azg_split_gemm, Winograd GEMMs of "
+                                           "conv2-4, one launch per layer)",
+                "achieved": ach, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TF,
+                "traffic": None, "mfma_dtype": "fp16 (split, 3 products per f32 multiply-add, f32 accumulation)",
+                "avg_launch_us": g_ms / n_launch * 1e3, "launches": n_launch,
+                "per_launch": f"{leaves} leaves x {algo_conv_leaf / 1e6:.1f} MFLOP x 3 products / {per_fwd:.0f} "
+                              f"launches per forward = {flops_launch / 1e9:.1f} GFLOP per launch (avg over the 3 "
+                              f"layers' shapes) / {g_ms / n_launch * 1e3:.1f} us (HIP events)",
+                "share_of_forward": g_ms / nn_ms if nn_ms > 0 else None}
+        if t_pairs and impl == "winograd" and getattr(ev, "gemm", "") == "split":
+            tb = transform_bytes(args.n, depth, split=True)
+            t_ms = t_kern["transform"].total_ms()
+            gbs = leaves * tb["total"] * n_forwards / (t_ms / 1e3) / 1e9
+            out["roofline_transforms"] = {
+                "bound": "hbm", "kernel": "winograd_first + winograd_mid x2 + winograd_out (fused Winograd transforms)",
+                "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                "bytes_per_leaf": tb, "us_per_forward": t_ms / n_forwards * 1e3}
+        if out["roofline"] is None:  # no libazg GEMM in this configuration: the conv span is the figure
+            out["roofline"] = out.pop("roofline_conv_span")
         pmc = load_pmc(G, args.game, impl, getattr(ev, "gemm", "f32"))
         if pmc:
-            out["roofline"]["traffic"] = pmc["conv"]
-            out["roofline"]["traffic_note"] = pmc["note"]
+            if "split_gemm" in pmc and out["roofline"].get("launches"):
+                out["roofline"]["traffic"] = pmc["split_gemm"]
+            if "roofline_transforms" in out:
+                out["roofline_transforms"]["traffic"] = pmc["transforms"]
+            for k in ("roofline", "roofline_transforms"):
+                if k in out:
+                    out[k]["traffic_note"] = pmc["note"]
             out["roofline_tree"]["traffic"] = pmc["tree"]
         if split and getattr(ev, "gemm", "") == "split" and os.path.exists(GEMM_PMC_FILE):
             d = json.load(open(GEMM_PMC_FILE))
             out["roofline"]["mfma_busy_frac"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * d["GRBM_GUI_ACTIVE"] / 8)
             out["roofline"]["mfma_busy_note"] = (
                 f"{os.path.relpath(GEMM_PMC_FILE, ROOT)}: SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 "
-                "XCDs) of the default split GEMM alone on conv2's shape (tools/split_gemm_pmc.py); the MFMA pipes' "
+                "XCDs) of the split GEMM alone on conv2's shape (tools/split_gemm_pmc.py); the MFMA pipes' "
                 "busy share at the clock the chip holds under this load")
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, depth, A)

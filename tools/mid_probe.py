@@ -23,8 +23,10 @@ def main():
             getattr(L, name).restype, getattr(L, name).argtypes = res, args
     C = K = 512
     B, H = 4096, 7
-    runs = [(25, 4096), (40, 8192), (16, 16384)]
-    rows = sum(p * t for p, t in runs)  # conv2's 169 points
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from split_gemm_bench import layer_runs
+    runs = layer_runs(7)  # conv2
+    rows = sum(p * t for p, t in runs)
     P = sum(p for p, _ in runs)
     A = torch.randn(rows, 2 * C, device="cuda").half()
     Bt = torch.randn(P, K, 2 * C, device="cuda").half()

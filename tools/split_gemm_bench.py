@@ -18,7 +18,21 @@ from azg_amd import _lib  # noqa: E402
 
 # AZG_SG_VARIANTS="4,6,15,16" times the probes instead (6/15/16 give wrong results by design)
 VARIANTS = tuple(int(v) for v in os.environ.get("AZG_SG_VARIANTS", "0,4,7,12").split(","))
-LAYERS = {"conv2": [(25, 4096), (40, 8192), (16, 16384)], "conv3": [(81, 4096)], "conv4": [(25, 4096)]}
+
+
+def layer_runs(h_out, B=4096):
+    """(points, rows) runs of one layer's GEMMs as InferenceNet._winograd_gemms forms them."""
+    from azg_amd.nnet import winograd_groups
+    runs = []
+    for _, _, P, n in winograd_groups(h_out):
+        if runs and runs[-1][1] == B * n:
+            runs[-1][0] += P
+        else:
+            runs.append([P, B * n])
+    return [tuple(r) for r in runs]
+
+
+LAYERS = {"conv2": layer_runs(7), "conv3": layer_runs(5), "conv4": layer_runs(3)}
 
 
 def timeit(fn, reps=10):

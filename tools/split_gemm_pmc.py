@@ -15,10 +15,12 @@ from collections import defaultdict
 def run(variant, reps):
     import torch
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import azg_amd  # noqa: F401
     from azg_amd import _lib
+    from split_gemm_bench import layer_runs
     C = K = 512
-    runs = [(25, 4096), (40, 8192), (16, 16384)]
+    runs = layer_runs(7)  # conv2
     P = sum(p for p, _ in runs)
     rows = sum(p * t for p, t in runs)
     A = torch.randn(rows, 2 * C, device="cuda").half()

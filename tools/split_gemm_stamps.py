@@ -21,7 +21,9 @@ SEGMENTS = ["reads+dma_issue (reads landed)", "mfma_issue", "vmcnt_wait", "barri
 
 def main():
     C = K = 512
-    runs = [(25, 4096), (40, 8192), (16, 16384)]
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from split_gemm_bench import layer_runs
+    runs = layer_runs(7)  # conv2
     P = sum(p for p, _ in runs)
     rows = sum(p * t for p, t in runs)
     A = torch.randn(rows, 2 * C, device="cuda").half()
