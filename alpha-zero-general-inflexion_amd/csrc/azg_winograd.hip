@@ -282,17 +282,17 @@ __device__ __forceinline__ void store_v(void* V, long long row, int C, int c, fl
 // c0 + lane (c0 % 64 == 0), in AZG_WINO_SPLIT2: one v_permlane32_swap turns (hi, lo)
 // into the two 32-channel blocks [hi(32) | lo(32)] as they lie in the row, so each of
 // the two stores writes one whole 128-B line (per-lane stores would write each line
-// in two 64-B halves from two instructions).
-__device__ __forceinline__ void store_v2_wave(void* V, long long row, int C, int c0, int lane, float v,
-                                              int* overflow) {
+// in two 64-B halves from two instructions).  rowp = the row's halves at channel c0,
+// wave-uniform, so the stores take a scalar base and a 32-bit lane offset.  Returns
+// whether v is out of fp16 range (the caller raises the flag once).
+__device__ __forceinline__ bool store_v2_wave(unsigned short* rowp, unsigned lane, float v) {
     const _Float16 hi = (_Float16)v;  // round to nearest even
     const _Float16 lo = (_Float16)(v - (float)hi);
     const auto sw = __builtin_amdgcn_permlane32_swap((unsigned)__builtin_bit_cast(unsigned short, hi),
                                                      (unsigned)__builtin_bit_cast(unsigned short, lo), false, false);
-    unsigned short* r = (unsigned short*)V + row * 2 * C + 2 * c0 + lane;
-    r[0] = (unsigned short)sw[0];   // lanes 0-31: hi of c0 + lane; 32-63: lo of c0 + lane - 32
-    r[64] = (unsigned short)sw[1];  // the same for channels c0 + 32 ..
-    if (!(fabsf(v) <= 65504.f)) atomicOr(overflow, 1);
+    rowp[lane] = (unsigned short)sw[0];       // lanes 0-31: hi of c0 + lane; 32-63: lo of c0 + lane - 32
+    rowp[64 + lane] = (unsigned short)sw[1];  // the same for channels c0 + 32 ..
+    return !(fabsf(v) <= 65504.f);
 }
 
 // Four consecutive channels (c4 = c / 4) of one V row.
@@ -334,6 +334,16 @@ __device__ __forceinline__ long long xcd_item() {
     const unsigned per = gridDim.x / 8;  // the grid is a multiple of 8 blocks
     const unsigned vb = (blockIdx.x % 8) * per + blockIdx.x / 8;
     return (long long)vb * blockDim.x + threadIdx.x;
+}
+
+// Work item of a one-wave block (grids of one wave per (image, 64 channels)): the
+// items of each XCD are one contiguous range (blocks are dealt to the 8 XCDs
+// round-robin), so an image's channel blocks run side by side on one XCD and its
+// V / M rows are read and written there together; the identity when the grid is not
+// a multiple of 8.
+__device__ __forceinline__ unsigned xcd_block() {
+    if (gridDim.x % 8) return blockIdx.x;
+    return (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
 }
 
 // One thread per (tile, 4 channels); tiles image-major, row-major in the image.
@@ -439,13 +449,16 @@ struct Plane {
     }
 };
 
-// The next layer's input transform (pad PAD) of the lane's h x h plane: V out.
+// The next layer's input transform (pad PAD) of the lane's h x h plane: V out.  The
+// wave's lanes hold channels c0 + lane (c0 wave-uniform, a multiple of 64).
 template <int HC, int FMT, int PAD, class P>
-__device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, long long b, int c, int C, long long B,
-                                           void* __restrict__ Vout, int* overflow) {
+__device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, long long b, int c0, unsigned lane, int C,
+                                           long long B, void* __restrict__ Vout, int* overflow) {
     const int h = HC > 0 ? HC : h_rt;
+    const int c = c0 + (int)lane;
     const WSeq S(h + 2 * PAD - 2);
     constexpr int HO = HC > 0 ? HC + 2 * PAD - 2 : 0;
+    bool bad = false;
     for_tiles<HO>(S, [&](auto A_, auto B_, int i, int j) {
         constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
         const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
@@ -462,12 +475,14 @@ __device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, long long b, i
         in_tile<MA, MB>(d, Vt);
 #pragma unroll
         for (int e = 0; e < (MA + 2) * (MB + 2); ++e) {
-            if constexpr (FMT == AZG_WINO_SPLIT2)  // the wave's lanes are channels c & ~63 ..
-                store_v2_wave(Vout, row + e * ps, C, c & ~63, c & 63, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
+            if constexpr (FMT == AZG_WINO_SPLIT2)
+                bad |= store_v2_wave((unsigned short*)Vout + (row + e * ps) * 2 * C + 2 * c0, lane,
+                                     Vt[e / (MB + 2)][e % (MB + 2)]);
             else
                 store_v<FMT>(Vout, row + e * ps, C, c, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
         }
     });
+    if (bad) atomicOr(overflow, 1);
 }
 
 // Layer i's output transform fused with layer i+1's input transform (pad 0
@@ -482,10 +497,11 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
                                                           float mscale, int* overflow) {
     extern __shared__ float ys_raw[];  // [h * h][64] when HC == 0
     const int h = HC > 0 ? HC : h_rt;
-    const int lane = threadIdx.x;
+    const unsigned lane = threadIdx.x;
     const int cblocks = C / 64;
-    const long long b = blockIdx.x / cblocks;
-    const int c = (blockIdx.x % cblocks) * 64 + lane;
+    const unsigned blk = xcd_block();
+    const long long b = blk / cblocks;
+    const int c0 = (blk % cblocks) * 64, c = c0 + (int)lane;
     const float bc = bias[c];
     const WSeq S(h);
     Plane<HC> ys;
@@ -497,8 +513,8 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
         const int y0 = S.off(i), x0 = S.off(j);
         float mm[MA + 2][MB + 2];
 #pragma unroll
-        for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
-            mm[e / (MB + 2)][e % (MB + 2)] = mscale * Min[(row + e * ps) * C + c];
+        for (int e = 0; e < (MA + 2) * (MB + 2); ++e)  // uniform row base + lane
+            mm[e / (MB + 2)][e % (MB + 2)] = mscale * (Min + (row + e * ps) * C + c0)[lane];
         float y[MA][MB];
         out_tile<MA, MB>(mm, y);
 #pragma unroll
@@ -507,16 +523,97 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
             for (int q = 0; q < MB; ++q)
                 if (y0 + a < h && x0 + q < h) ys.put((y0 + a) * h + x0 + q, fmaxf(y[a][q] + bc, 0.f));
     });
-    plane_to_V<HC, FMT, 0>(ys, h, b, c, C, B, Vout, overflow);
+    plane_to_V<HC, FMT, 0>(ys, h, b, c0, lane, C, B, Vout, overflow);
+}
+
+// conv1 of one image for the lane's output channel k into acc[NC * NC] (no bias),
+// compile-time side NC, the image's planes read as wave-uniform scalars (every lane
+// reads the same cells).  Exact restructuring of the 3x3 zero-padded convolution
+// (InflexionNNet.py:39, conv1) for leaf planes, which are mostly constant planes and
+// sparse 0/1 planes (InflexionGame.py:84-91: turn and can_spawn planes are constant,
+// own/opponent planes disjoint): per input plane c,
+//   * constant value x (all cells equal): out(y, x') += x * S_c(class(y), class(x')),
+//     S_c the sum of the taps that stay inside the board for that border class
+//     (first / inner / last row and column) -- one multiply-add per output;
+//   * otherwise: each nonzero input cell adds w[dy][dx] * x to the <= 9 outputs it
+//     reaches (a zero cell contributes exactly nothing: skipped on a uniform branch).
+// Any plane values are handled; only the work depends on them (at most 361 multiply-
+// adds per plane, as the gather).  The sums are in a different order than the gather.
+template <int NC>
+__device__ __forceinline__ void conv1_sparse(const float* __restrict__ pb, const float* __restrict__ wk, int depth,
+                                             unsigned lane, float (&acc)[NC * NC]) {
+    constexpr int DMAX = 4, NN = NC * NC;
+#pragma unroll
+    for (int q = 0; q < NN; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int c = 0; c < DMAX; ++c) {
+        if (c >= depth) break;
+        const float* __restrict__ pc = pb + c * NN;
+        float w[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) w[t] = wk[c * 9 + t];
+        const float x0 = pc[0];
+        const bool cst = __all(pc[lane < NN ? lane : 0] == x0);
+        if (cst) {
+            if (x0 != 0.f) {
+                // row sums of the taps valid in each column class, then the 3x3 classes
+                float rs[3][3];  // [dy][column class]
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy) {
+                    rs[dy][0] = w[dy * 3 + 1] + w[dy * 3 + 2];  // first column: dx = 0 falls outside
+                    rs[dy][1] = w[dy * 3 + 0] + w[dy * 3 + 1] + w[dy * 3 + 2];
+                    rs[dy][2] = w[dy * 3 + 0] + w[dy * 3 + 1];  // last column
+                }
+                float S[3][3];  // [row class][column class]
+#pragma unroll
+                for (int cx = 0; cx < 3; ++cx) {
+                    S[0][cx] = rs[1][cx] + rs[2][cx];
+                    S[1][cx] = rs[0][cx] + rs[1][cx] + rs[2][cx];
+                    S[2][cx] = rs[0][cx] + rs[1][cx];
+                }
+#pragma unroll
+                for (int y = 0; y < NC; ++y)
+#pragma unroll
+                    for (int x = 0; x < NC; ++x) {
+                        const int cy = y == 0 ? 0 : (y == NC - 1 ? 2 : 1), cx = x == 0 ? 0 : (x == NC - 1 ? 2 : 1);
+                        acc[y * NC + x] = fmaf(x0, S[cy][cx], acc[y * NC + x]);
+                    }
+            }
+        } else {
+            unsigned xb[NN];  // the plane's bits, wave-uniform (scalar loads, issued together)
+#pragma unroll
+            for (int q = 0; q < NN; ++q) xb[q] = __builtin_amdgcn_readfirstlane(__float_as_uint(pc[q]));
+#pragma unroll
+            for (int q = 0; q < NN; ++q) {
+                const float xq = __uint_as_float(xb[q]);
+                if (xb[q] << 1) {  // nonzero (either zero skips)
+                    asm volatile("");  // a real (uniform) branch, not a select over the multiply-adds
+                    const int iy = q / NC, ix = q % NC;
+#pragma unroll
+                    for (int dy = 0; dy < 3; ++dy) {
+                        const int oy = iy - dy + 1;
+                        if (oy < 0 || oy >= NC) continue;
+#pragma unroll
+                        for (int dx = 0; dx < 3; ++dx) {
+                            const int ox = ix - dx + 1;
+                            if (ox < 0 || ox >= NC) continue;
+                            acc[oy * NC + ox] = fmaf(w[dy * 3 + dx], xq, acc[oy * NC + ox]);
+                        }
+                    }
+                }
+            }
+        }
+    }
 }
 
 // The network's first two layers' front end in one pass: conv1 (depth -> C
 // channels, 3x3, pad 1) + bias + ReLU computed directly from the NCHW leaf
 // planes, then conv2's Winograd input transform (pad 1) -- conv1's activation
 // never leaves the chip.  One wave per (image, 64 output channels of conv1),
-// one channel per lane: the image's planes are shared through LDS, the lane's
-// depth*9 weights and its n x n output plane sit in registers (compile-time
-// side NC) or its own LDS column.
+// one channel per lane: with a compile-time side NC the planes are read as
+// wave-uniform scalars and conv1 runs as conv1_sparse, the lane's output plane in
+// registers; otherwise the image's planes are shared through LDS and each output
+// is gathered, the plane in the lane's own LDS column.
 template <int NC, int FMT>
 __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restrict__ planes,
                                                             const float* __restrict__ w1,
@@ -524,44 +621,51 @@ __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restr
                                                             int depth, int n_rt, int C, long long B, int* overflow) {
     constexpr int DMAX = 4;
     extern __shared__ float lds[];
-    float* xs = lds;  // [depth][n][n], then (NC == 0) the lanes' planes [n * n][64]
     const int n = NC > 0 ? NC : n_rt;
-    const int lane = threadIdx.x;
+    const unsigned lane = threadIdx.x;
     const int cblocks = C / 64;
+    // (blocks in dispatch order: the XCD-contiguous mapping of the mid kernels measured
+    // 7% slower here, where nothing is read back)
     const long long b = blockIdx.x / cblocks;
-    const int k = (blockIdx.x % cblocks) * 64 + lane;
-    for (int i = lane; i < depth * n * n; i += 64) xs[i] = planes[b * depth * n * n + i];
-    float w[DMAX * 9];
-#pragma unroll
-    for (int j = 0; j < DMAX * 9; ++j) w[j] = j < depth * 9 ? w1[(size_t)k * depth * 9 + j] : 0.f;
+    const int k0 = (blockIdx.x % cblocks) * 64, k = k0 + (int)lane;
     const float bk = b1[k];
-    __syncthreads();
     Plane<NC> ys;
-    ys.lds = lds + DMAX * 81;
-    ys.lane = lane;
+    if constexpr (NC > 0) {
+        float acc[NC * NC];
+        conv1_sparse<NC>(planes + b * depth * NC * NC, w1 + (size_t)k * depth * 9, depth, lane, acc);
 #pragma unroll
-    for (int y = 0; y < n; ++y)
+        for (int q = 0; q < NC * NC; ++q) ys.put(q, fmaxf(acc[q] + bk, 0.f));
+    } else {
+        float* xs = lds;  // [depth][n][n], then the lanes' planes [n * n][64]
+        for (int i = lane; i < depth * n * n; i += 64) xs[i] = planes[b * depth * n * n + i];
+        float w[DMAX * 9];
 #pragma unroll
-        for (int x = 0; x < n; ++x) {
-            float acc = 0.f;
+        for (int j = 0; j < DMAX * 9; ++j) w[j] = j < depth * 9 ? w1[(size_t)k * depth * 9 + j] : 0.f;
+        __syncthreads();
+        ys.lds = lds + DMAX * 81;
+        ys.lane = lane;
+        for (int y = 0; y < n; ++y)
+            for (int x = 0; x < n; ++x) {
+                float acc = 0.f;
 #pragma unroll
-            for (int c = 0; c < DMAX; ++c) {
-                if (c >= depth) break;
+                for (int c = 0; c < DMAX; ++c) {
+                    if (c >= depth) break;
 #pragma unroll
-                for (int dy = 0; dy < 3; ++dy) {
-                    const int iy = y + dy - 1;
-                    if (iy < 0 || iy >= n) continue;
+                    for (int dy = 0; dy < 3; ++dy) {
+                        const int iy = y + dy - 1;
+                        if (iy < 0 || iy >= n) continue;
 #pragma unroll
-                    for (int dx = 0; dx < 3; ++dx) {
-                        const int ix = x + dx - 1;
-                        if (ix < 0 || ix >= n) continue;
-                        acc = fmaf(w[c * 9 + dy * 3 + dx], xs[(c * n + iy) * n + ix], acc);
+                        for (int dx = 0; dx < 3; ++dx) {
+                            const int ix = x + dx - 1;
+                            if (ix < 0 || ix >= n) continue;
+                            acc = fmaf(w[c * 9 + dy * 3 + dx], xs[(c * n + iy) * n + ix], acc);
+                        }
                     }
                 }
+                ys.put(y * n + x, fmaxf(acc + bk, 0.f));
             }
-            ys.put(y * n + x, fmaxf(acc + bk, 0.f));
-        }
-    plane_to_V<NC, FMT, 1>(ys, n, b, k, C, B, Vout, overflow);
+    }
+    plane_to_V<NC, FMT, 1>(ys, n, b, k0, lane, C, B, Vout, overflow);
 }
 
 // one thread per work item, rounded up to whole groups of 8 blocks (xcd_item)
@@ -719,7 +823,7 @@ extern "C" int azg_winograd_first_nchw(const float* planes, const float* w1, con
         c % 64 || bad_fmt(vfmt, overflow))
         return AZG_ERR_ARG;
     const dim3 grid((unsigned)(batch * (c / 64)));
-    const size_t lds_reg = 4 * 81 * sizeof(float), lds = (4 * 81 + (size_t)n * n * 64) * sizeof(float);
+    const size_t lds_reg = 0, lds = (4 * 81 + (size_t)n * n * 64) * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
     const long long B = batch;
 #define AZG_FIRST(N, SP, L)                                                                                       \

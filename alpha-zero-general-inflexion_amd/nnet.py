@@ -289,6 +289,14 @@ class InferenceNet(nn.Module):
         # fc3 and fc4 read the same activation: one GEMM over their stacked rows
         self.register_buffer("fw34", torch.cat([self.fw3, self.fw4], dim=0).contiguous())
         self.register_buffer("fb34", torch.cat([self.fb3, self.fb4]).contiguous())
+        # with the split form, fc2 and [fc3 | fc4] are split GEMMs too: each layer's bias +
+        # ReLU epilogue writes the next layer's [hi | lo | hi] rows (azg_fc_act_split), and
+        # one kernel turns the stacked fc3 | fc4 output into P and v (azg_policy_value)
+        if self.fc1_split:
+            whi, wlo, self.fc2_scale = _split_u(w2.t().unsqueeze(0))
+            self.register_buffer("fw2_s", torch.cat([whi, whi, wlo], dim=1).contiguous())
+            whi, wlo, self.fc34_scale = _split_u(self.fw34.t().unsqueeze(0))
+            self.register_buffer("fw34_s", torch.cat([whi, whi, wlo], dim=1).contiguous())
         # sticky device flag: a split-GEMM operand fp16 could not hold (checked by check_range)
         self.register_buffer("overflow", torch.zeros(1, dtype=torch.int32))
 
@@ -489,9 +497,39 @@ class InferenceNet(nn.Module):
         self._choices[key] = best[0]
         return best[0]
 
+    def _fc_split(self, a):
+        """The FC tail on split-fp16 GEMMs (azg_heads.hip): fc1 (+ folded fc_bn1) + ReLU,
+        fc2 (+ fc_bn2) + ReLU, [fc3 | fc4] as hi.Wh + lo.Wh + hi.Wl on the fp16 MFMA
+        (hipBLASLt, f32 accumulation), each epilogue writing the next GEMM's [hi | lo | hi]
+        rows; then P = softmax(fc3), v = tanh(fc4).  a: conv4's flattened activation as
+        [B, 3 * 4608] fp16 rows (azg_winograd_out_split)."""
+        import ctypes
+        from . import _lib
+        L = _lib.lib()
+        B, dev = a.shape[0], a.device
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        ovf = ctypes.c_void_p(self.overflow.data_ptr())
+        for w, b, scale in ((self.fw1_s, self.fb1, self.fc1_scale), (self.fw2_s, self.fb2, self.fc2_scale)):
+            n = w.shape[2]
+            m = torch.empty((1, B, n), device=dev, dtype=torch.float32)
+            torch.bmm(a.unsqueeze(0), w, out_dtype=torch.float32, out=m)
+            a = torch.empty((B, 3 * n), device=dev, dtype=torch.float16)
+            _lib.check(L.azg_fc_act_split(ctypes.c_void_p(m.data_ptr()), ctypes.c_void_p(b.data_ptr()), scale,
+                                          ctypes.c_void_p(a.data_ptr()), B, n, 1, ovf, st))
+        n = self.fw34_s.shape[2]
+        m = torch.empty((1, B, n), device=dev, dtype=torch.float32)
+        torch.bmm(a.unsqueeze(0), self.fw34_s, out_dtype=torch.float32, out=m)
+        A = n - 1
+        p = torch.empty((B, A), device=dev, dtype=torch.float32)
+        v = torch.empty((B, 1), device=dev, dtype=torch.float32)
+        _lib.check(L.azg_policy_value(ctypes.c_void_p(m.data_ptr()), n, ctypes.c_void_p(self.fb34.data_ptr()),
+                                      self.fc34_scale, ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()),
+                                      B, A, st))
+        return p, v
+
     def forward(self, s):
         planes = s.view(-1, self.depth, self.n, self.n)
-        x = planes.contiguous(memory_format=torch.channels_last)
+        x = planes
         hook = self.conv_hook
         fused = x.is_cuda
         impls = []
@@ -505,6 +543,8 @@ class InferenceNet(nn.Module):
         B, H = x.shape[0], self.n
         first_fused = (fused and self.fuse_transforms and impls[1] == "winograd" and self.pads == [1, 1, 0, 0]
                        and self.depth <= 4 and 3 <= self.n <= 9 and self.w1c.shape[0] % 64 == 0)
+        if not first_fused:  # the fused front end reads the NCHW planes as they are
+            x = planes.contiguous(memory_format=torch.channels_last)
         for i, pad in enumerate(self.pads, start=1):
             impl = impls[i - 1]
             h_out = H + 2 * pad - 2
@@ -539,11 +579,7 @@ class InferenceNet(nn.Module):
                 hook(i, "stop")
             H = h_out
         if isinstance(x, tuple):
-            # fc1 + folded fc_bn1 + ReLU: hi.Wh + lo.Wh + hi.Wl on the fp16 MFMA (hipBLASLt), f32 accumulation
-            a3 = x[1]
-            m1 = torch.empty((1, a3.shape[0], self.fw1_s.shape[2]), device=a3.device, dtype=torch.float32)
-            torch.bmm(a3.unsqueeze(0), self.fw1_s, out_dtype=torch.float32, out=m1)
-            x = torch.relu_(torch.add(self.fb1, m1[0], alpha=self.fc1_scale))
+            return self._fc_split(x[1])
         else:
             x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten, no copy
             x = torch.relu_(torch.addmm(self.fb1, x, self.fw1.t()))

@@ -151,14 +151,14 @@ int  azg_conv3x3_bias_relu_nhwc(const float* x, const float* wt, const float* bi
 int  azg_conv3x3_variant(int variant, const float* x, const float* wt, const float* bias, float* y, int32_t batch,
                          int32_t h_in, int32_t pad, int32_t c_in, int32_t c_out, void* stream);
 
-/* Leaf-network 3x3 convolutions as Winograd convolutions over mixed F(4,3) /
- * F(3,3) / F(2,3) tiles (azg_winograd.hip).  They replace the convolutions of
- * InflexionNNet.forward (InflexionNNet.py:39-45, BN folded).  An h-long output axis
- * is cut into the fewest tiles, p = ceil(h/4), of sides 4/3/2 with at most two sides,
- * big = small + 1 (7 = 4+3, 5 = 3+2, 3 = 3, 8 = 4+4); azg_winograd_layout returns p,
- * writes the sides to seq[p] and the tiles per image of the groups (big,big)
- * (big,small) (small,big) (small,small) to groups[4].  azg_winograd_tables copies
- * F(m,3)'s B^T [(m+2)^2] and A^T [m(m+2)] (row-major; m = 2, 3, 4) to bt, at.
+/* Leaf-network 3x3 convolutions as Winograd convolutions over mixed F(5,3) /
+ * F(4,3) / F(3,3) / F(2,3) tiles (azg_winograd.hip).  They replace the convolutions
+ * of InflexionNNet.forward (InflexionNNet.py:39-45, BN folded).  An h-long output axis
+ * is cut into the fewest tiles of side <= 5, p = ceil(h/5), sides as equal as possible
+ * (big = small + 1: 7 = 4+3, 5 = 5, 3 = 3, 8 = 4+4, 6 = 3+3); azg_winograd_layout
+ * returns p, writes the sides to seq[p] and the tiles per image of the groups
+ * (big,big) (big,small) (small,big) (small,small) to groups[4].  azg_winograd_tables
+ * copies F(m,3)'s B^T [(m+2)^2] and A^T [m(m+2)] (row-major; m = 2..5) to bt, at.
  * V and M hold the groups one after another, group g = (ma, mb) as
  * [P_g = (ma+2)(mb+2) points][batch * tiles_g][row], tiles row-major per image.
  *   azg_winograd_in_nhwc : x NHWC [batch, h_in, h_in, c] (zero padding `pad`) ->
@@ -230,6 +230,24 @@ int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, floa
  * the kernel's: read the shares. */
 int  azg_split_gemm_stamps(const void* a, const void* bt, float* m, int32_t nruns, const int32_t* points,
                            const int32_t* rows, int32_t c, int32_t k, uint64_t* stamps, int64_t cap, void* stream);
+
+/* The fully connected tail of the leaf network (InflexionNNet.py:47-54, BN folded)
+ * around split-fp16 GEMMs (azg_heads.hip; the GEMMs are the caller's: one fp16
+ * hipBLASLt GEMM with f32 accumulation per layer, A rows [hi | lo | hi] times the
+ * weights stacked [hi; hi; lo] and pre-scaled by a power of two that `scale` undoes).
+ *   azg_fc_act_split: y = bias + scale * m ([rows][n] f32), ReLU if relu != 0, written
+ *                     as the next GEMM's A operand: fp16 rows [hi(n) | lo(n) | hi(n)]
+ *                     (AZG_WINO_SPLIT); |y| > 65504 or NaN sets *overflow.
+ *                     n % 4 == 0; m, bias 16-B and out 8-B aligned.
+ *   azg_policy_value: P[r][a] = softmax_a(bias[a] + scale * m[r][a]) (a < actions,
+ *                     = exp(log_softmax), NNet.py:94) and v[r] = tanh(bias[actions] +
+ *                     scale * m[r][actions]) from the stacked [fc3 | fc4] output m
+ *                     (row stride ldm >= actions + 1); P [rows][actions], v [rows].
+ *                     actions <= 512. */
+int  azg_fc_act_split(const float* m, const float* bias, float scale, void* out, int32_t rows, int32_t n,
+                      int32_t relu, int32_t* overflow, void* stream);
+int  azg_policy_value(const float* m, int32_t ldm, const float* bias, float scale, float* P, float* v,
+                      int32_t rows, int32_t actions, void* stream);
 
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active

@@ -240,9 +240,10 @@ def test_split_gemm_kernel_matches_reference(variant, runs, C, K):
 
 
 def test_fc1_split_form_matches_reference():
-    """At >= FC1_SPLIT_MIN_BATCH leaves fc1 runs as the split-fp16 GEMM over conv4's
-    [hi|lo|hi] output rows (azg_winograd_out_split): P, v against the reference
-    module within the north_star's 1e-5, and equal to the f32-fc1 form within it."""
+    """At >= FC1_SPLIT_MIN_BATCH leaves the FC tail runs as split-fp16 GEMMs: fc1 over
+    conv4's [hi|lo|hi] output rows (azg_winograd_out_split), fc2 and [fc3 | fc4] over the
+    rows azg_fc_act_split writes, P and v from azg_policy_value: against the reference
+    module within the north_star's 1e-5, and equal to the f32 FC tail within it."""
     import azg_amd  # noqa: F401
     from azg_amd import nnet as nn_mod
     from azg_amd.nnet import InferenceNet, InflexionNNet
@@ -260,3 +261,47 @@ def test_fc1_split_form_matches_reference():
     torch.testing.assert_close(p, torch.exp(logp), rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(v.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(p, p32, rtol=1e-5, atol=1e-7)
+
+
+def test_fc_act_split_kernel():
+    """azg_fc_act_split against the torch f32 expression relu(b + s m): hi = fp16(y),
+    lo = fp16(y - hi), rows [hi | lo | hi]; an out-of-range value sets the flag."""
+    import ctypes
+    from azg_amd import _lib
+    B, n, scale = 300, 1024, 2.0 ** -7
+    m = torch.randn(B, n, device="cuda") * 300
+    b = torch.randn(n, device="cuda")
+    out = torch.empty(B, 3 * n, device="cuda", dtype=torch.float16)
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(_lib.lib().azg_fc_act_split(ctypes.c_void_p(m.data_ptr()), ctypes.c_void_p(b.data_ptr()), scale,
+                                           ctypes.c_void_p(out.data_ptr()), B, n, 1, ctypes.c_void_p(ovf.data_ptr()),
+                                           st))
+    y = torch.relu(b + scale * m)
+    hi = y.half()
+    lo = (y - hi.float()).half()
+    assert torch.equal(out[:, :n], hi) and torch.equal(out[:, n:2 * n], lo) and torch.equal(out[:, 2 * n:], hi)
+    assert int(ovf.item()) == 0
+    m[7, 5] = 1e9
+    _lib.check(_lib.lib().azg_fc_act_split(ctypes.c_void_p(m.data_ptr()), ctypes.c_void_p(b.data_ptr()), scale,
+                                           ctypes.c_void_p(out.data_ptr()), B, n, 1, ctypes.c_void_p(ovf.data_ptr()),
+                                           st))
+    assert int(ovf.item()) == 1
+
+
+@pytest.mark.parametrize("A", [343, 65, 36, 512])
+def test_policy_value_kernel(A):
+    """azg_policy_value against torch f32 softmax / tanh of the stacked [fc3 | fc4] output."""
+    import ctypes
+    from azg_amd import _lib
+    B, ld, scale = 777, A + 3, 0.5
+    m = torch.randn(B, ld, device="cuda") * 8
+    b = torch.randn(A + 1, device="cuda")
+    P = torch.empty(B, A, device="cuda")
+    v = torch.empty(B, 1, device="cuda")
+    _lib.check(_lib.lib().azg_policy_value(ctypes.c_void_p(m.data_ptr()), ld, ctypes.c_void_p(b.data_ptr()), scale,
+                                           ctypes.c_void_p(P.data_ptr()), ctypes.c_void_p(v.data_ptr()), B, A,
+                                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    logits = b + scale * m[:, :A + 1]
+    torch.testing.assert_close(P, torch.softmax(logits[:, :A], dim=1), rtol=2e-6, atol=1e-9)
+    torch.testing.assert_close(v, torch.tanh(logits[:, A:]), rtol=2e-6, atol=1e-7)
