@@ -71,11 +71,12 @@ SIGNATURES = [
     ("azg_winograd_tables", ctypes.c_int, [_I32, _VP, _VP]),
     ("azg_winograd_in_nhwc", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
     ("azg_winograd_out_nhwc", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, ctypes.c_float, _VP]),
-    ("azg_winograd_out_split", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, ctypes.c_float, _I32, _VP, _VP]),
+    ("azg_winograd_out_split", ctypes.c_int,
+     [_VP, _VP, _VP, _I32, _I32, _I32, _I32, ctypes.c_float, _I32, _I32, _VP, _VP]),
     ("azg_winograd_mid_nhwc", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, ctypes.c_float, _I32, _VP, _VP]),
     ("azg_winograd_first_nchw", ctypes.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
     ("azg_split_gemm", ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
-    ("azg_fc_act_split", ctypes.c_int, [_VP, _VP, ctypes.c_float, _VP, _I32, _I32, _I32, _VP, _VP]),
+    ("azg_fc_act_split", ctypes.c_int, [_VP, _I32, _I64, _VP, ctypes.c_float, _VP, _I32, _I32, _I32, _VP, _VP]),
     ("azg_policy_value", ctypes.c_int, [_VP, _I32, _VP, ctypes.c_float, _VP, _VP, _I32, _I32, _VP]),
     ("azg_split_gemm_variant", ctypes.c_int, [_I32, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
     ("azg_split_gemm_stamps", ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP, _I64, _VP]),

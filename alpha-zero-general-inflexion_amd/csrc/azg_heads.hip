@@ -6,7 +6,8 @@
 //   [hi; hi; lo] (= hi Wh + lo Wh + hi Wl, f32-accurate products as the Winograd GEMMs,
 //   DESIGN.md 4.1); the weights are pre-scaled by a power of two that `scale` undoes.
 //
-//  * fc_act_split: y = relu(bias + scale * m) of one FC layer written straight as the
+//  * fc_act_split: y = relu(bias + scale * m) of one FC layer (m summed over the parts
+//    of a split-K GEMM first, fc1 on libazg's split GEMM) written straight as the
 //    next layer's A operand, one fp16 row [hi | lo | hi] per leaf (AZG_WINO_SPLIT), so
 //    the activation never exists in f32; |y| > 65504 or NaN sets *overflow (the
 //    InferenceNet range flag).  HBM-bound: 4 values per lane, float4 loads.
@@ -20,14 +21,20 @@
 
 namespace {
 
-__global__ __launch_bounds__(256) void fc_act_split_kernel(const float4* __restrict__ m, const float4* __restrict__ bias,
+__global__ __launch_bounds__(256) void fc_act_split_kernel(const float4* __restrict__ m, int parts,
+                                                           long long pstride4, const float4* __restrict__ bias,
                                                            float scale, ushort4* __restrict__ out, long long rows,
                                                            int n4, int relu, int* overflow) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= rows * n4) return;
     const long long r = i / n4;
     const int c4 = (int)(i - r * n4);
-    const float4 x = m[i], b = bias[c4];
+    float4 x = m[i];
+    for (int p = 1; p < parts; ++p) {  // split-K parts, summed in order
+        const float4 t = m[p * pstride4 + i];
+        x = make_float4(x.x + t.x, x.y + t.y, x.z + t.z, x.w + t.w);
+    }
+    const float4 b = bias[c4];
     float y[4] = {b.x + scale * x.x, b.y + scale * x.y, b.z + scale * x.z, b.w + scale * x.w};
     unsigned short hi[4], lo[4];
     bool bad = false;
@@ -88,15 +95,16 @@ __global__ __launch_bounds__(256) void policy_value_kernel(const float* __restri
 
 }  // namespace
 
-extern "C" int azg_fc_act_split(const float* m, const float* bias, float scale, void* out, int32_t rows, int32_t n,
-                                int32_t relu, int32_t* overflow, void* stream) {
-    if (!m || !bias || !out || !overflow || rows <= 0 || n <= 0 || n % 4 || ((uintptr_t)m & 15) ||
-        ((uintptr_t)bias & 15) || ((uintptr_t)out & 7))
+extern "C" int azg_fc_act_split(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale,
+                                void* out, int32_t rows, int32_t n, int32_t relu, int32_t* overflow, void* stream) {
+    if (!m || !bias || !out || !overflow || rows <= 0 || n <= 0 || n % 4 || parts < 1 || part_stride % 4 ||
+        (parts > 1 && part_stride < (int64_t)rows * n) || ((uintptr_t)m & 15) || ((uintptr_t)bias & 15) ||
+        ((uintptr_t)out & 7))
         return AZG_ERR_ARG;
     const long long items = (long long)rows * (n / 4);
     hipLaunchKernelGGL(fc_act_split_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       (const float4*)m, (const float4*)bias, scale, (ushort4*)out, (long long)rows, n / 4, relu,
-                       overflow);
+                       (const float4*)m, parts, (long long)(part_stride / 4), (const float4*)bias, scale,
+                       (ushort4*)out, (long long)rows, n / 4, relu, overflow);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 

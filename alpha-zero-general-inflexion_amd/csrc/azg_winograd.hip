@@ -391,11 +391,14 @@ __global__ __launch_bounds__(256) void winograd_in_kernel(const float4* __restri
 // FMT = AZG_WINO_F32: y is the NHWC f32 activation.  Otherwise y is one fp16 row
 // per image in V format FMT over the image's flattened NHWC activation (width
 // Ho * Ho * K): the A operand of a split GEMM over it (the network's fc1).
+// With kparts > 1 (split formats) the row is cut into kparts equal chunks stored as
+// kparts matrices one after another, [kparts][B][chunk]: the A operands of a split-K
+// GEMM whose parts are the split GEMM's "points".
 template <int FMT, int HC>
 __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restrict__ Min,
                                                            const float4* __restrict__ bias, void* __restrict__ y,
                                                            int Ho, int K4, long long B, int relu, float mscale,
-                                                           int* overflow) {
+                                                           int* overflow, int kparts) {
     const WSeq S(HC > 0 ? HC : Ho);
     if (HC > 0) Ho = HC;
     const long long item = xcd_item();
@@ -424,10 +427,12 @@ __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restr
                 if (oy >= Ho || ox >= Ho) continue;  // h = 1: one 2-tile, cropped
                 float4 z = vadd(yt[a][q], bb);
                 if (relu) z = vrelu(z);
-                if constexpr (FMT == AZG_WINO_F32)
+                if constexpr (FMT == AZG_WINO_F32) {
                     ((float4*)y)[((b * Ho + oy) * Ho + ox) * K4 + k4] = z;
-                else
-                    store_v<FMT>(y, b, Ho * Ho * K4, (oy * Ho + ox) * K4 + k4, z, overflow);
+                } else {
+                    const int wc4 = Ho * Ho * K4 / kparts, j4 = (oy * Ho + ox) * K4 + k4, e = j4 / wc4;
+                    store_v<FMT>(y, e * B + b, wc4, j4 - e * wc4, z, overflow);
+                }
             }
     });
 }
@@ -677,14 +682,14 @@ unsigned grid_for(long long n) {
 // winograd_out_kernel for the output sides of the supported boards (compile-time
 // tile types) or any side (all types)
 int launch_out(int vfmt, const float* M, const float* bias, void* y, int batch, int h_out, int k, int relu,
-               float mscale, int* overflow, void* stream) {
+               float mscale, int* overflow, int kparts, void* stream) {
     const WSeq S(h_out);
     const dim3 grid(grid_for((long long)batch * S.p * S.p * (k / 4)));
     hipStream_t st = (hipStream_t)stream;
     auto launch = [&](auto F_, auto H_) {
         hipLaunchKernelGGL((winograd_out_kernel<decltype(F_)::value, decltype(H_)::value>), grid, dim3(256), 0, st,
                            (const float4*)M, (const float4*)bias, y, h_out, k / 4, (long long)batch, relu, mscale,
-                           overflow);
+                           overflow, kparts);
     };
     auto by_side = [&](auto F_) {
         switch (h_out) {
@@ -768,18 +773,19 @@ extern "C" int azg_winograd_out_nhwc(const float* M, const float* bias, float* y
     if (!M || !bias || !y || batch <= 0 || h_out <= 0 || h_out > 64 || k <= 0 || k % 4 || ((uintptr_t)M & 15) ||
         ((uintptr_t)bias & 15) || ((uintptr_t)y & 15) || (long long)batch * h_out * h_out * (k / 4) > (1ll << 38))
         return AZG_ERR_ARG;
-    return launch_out(AZG_WINO_F32, M, bias, y, batch, h_out, k, relu, mscale, nullptr, stream);
+    return launch_out(AZG_WINO_F32, M, bias, y, batch, h_out, k, relu, mscale, nullptr, 1, stream);
 }
 
 extern "C" int azg_winograd_out_split(const float* M, const float* bias, void* y, int32_t batch, int32_t h_out,
-                                      int32_t k, int32_t relu, float mscale, int32_t vfmt, int32_t* overflow,
-                                      void* stream) {
+                                      int32_t k, int32_t relu, float mscale, int32_t vfmt, int32_t kparts,
+                                      int32_t* overflow, void* stream) {
+    const long long width = (long long)h_out * h_out * k;
     if (!M || !bias || !y || batch <= 0 || h_out <= 0 || h_out > 64 || k <= 0 || k % 4 || ((uintptr_t)M & 15) ||
         ((uintptr_t)bias & 15) || ((uintptr_t)y & 15) || vfmt == AZG_WINO_F32 || bad_fmt(vfmt, overflow) ||
-        (vfmt == AZG_WINO_SPLIT2 && k % 32) ||
-        (long long)h_out * h_out * k > (1ll << 28) || (long long)batch * h_out * h_out * (k / 4) > (1ll << 38))
+        kparts < 1 || width % kparts || (width / kparts) % (vfmt == AZG_WINO_SPLIT2 ? 32 : 4) ||
+        width > (1ll << 28) || (long long)batch * h_out * h_out * (k / 4) > (1ll << 38))
         return AZG_ERR_ARG;
-    return launch_out(vfmt, M, bias, y, batch, h_out, k, relu, mscale, overflow, stream);
+    return launch_out(vfmt, M, bias, y, batch, h_out, k, relu, mscale, overflow, kparts, stream);
 }
 
 extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, void* V, int32_t batch, int32_t h, int32_t c,

@@ -29,6 +29,7 @@ DEFAULT_ARGS = dict(lr=0.001, dropout=0.3, epochs=10, batch_size=512, num_channe
                     fused_adam=False, train_dtype="f32")
 WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C1: 1 game)
 FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
+FC1_KPARTS = 4  # split-K parts of fc1 on libazg's split GEMM (4608 = 4 x 1152 for the 7x7 board)
 
 
 class InflexionNNet(nn.Module):
@@ -275,9 +276,20 @@ class InferenceNet(nn.Module):
         # writes the flattened activation as [hi | lo | hi] rows, fc1's weights are
         # stacked [hi; hi; lo] (scaled by a power of two, undone with the bias)
         self.fc1_split = gemm != "f32"
+        # fc1 on libazg's split GEMM as a split-K GEMM of FC1_KPARTS parts (the parts are
+        # the GEMM's "points": ~256 output tiles at 4096 leaves instead of 64), its A
+        # operand written by conv4's output transform in [parts][leaves][chunk] blocks
+        width = w1.shape[1]
+        self.fc1_kparts = FC1_KPARTS if (gemm == "split" and width % (64 * FC1_KPARTS) == 0
+                                         and w1.shape[0] % 256 == 0) else 0
         if self.fc1_split:
             whi, wlo, self.fc1_scale = _split_u(w1.t().unsqueeze(0))
             self.register_buffer("fw1_s", torch.cat([whi, whi, wlo], dim=1).contiguous())
+            if self.fc1_kparts:
+                kp, n1 = self.fc1_kparts, w1.shape[0]
+                hp = whi[0].t().reshape(n1, kp, width // kp).transpose(0, 1)
+                lp = wlo[0].t().reshape(n1, kp, width // kp).transpose(0, 1)
+                self.register_buffer("fw1_sk", split2_rows(hp, lp))  # [parts][N][2 chunk]
         self.register_buffer("fb1", b1)
         w2, b2 = _fold_bn(net.fc2.weight.detach(), net.fc2.bias.detach(), net.fc_bn2)
         self.register_buffer("fw2", w2.contiguous())
@@ -319,14 +331,16 @@ class InferenceNet(nn.Module):
 
     # optional hooks used by bench.py to bracket work with HIP events on the current
     # stream: conv_hook(layer_index, "start"|"stop") around each convolution,
-    # kernel_hook(kind, layer_index, "start"|"stop") around each libazg launch of kind
-    # "gemm" (azg_split_gemm) or "transform" (the Winograd transforms)
+    # kernel_hook(kind, layer_index, "start"|"stop", flops) around each libazg launch of
+    # kind "gemm" (azg_split_gemm: conv2-4 and fc1, with the launch's executed fp16 MFMA
+    # FLOPs, 3 products per f32 multiply-add) or "transform" (the Winograd transforms)
     conv_hook = None
     kernel_hook = None
 
-    def _khook(self, kind, i, what):
+    def _khook(self, kind, i, what, flops=0.0):
+        """flops (on "stop"): the executed MFMA FLOPs of a GEMM launch."""
         if self.kernel_hook is not None:
-            self.kernel_hook(kind, i, what)
+            self.kernel_hook(kind, i, what, flops)
 
     def _conv_miopen(self, x, i, pad):
         # MIOpen conv without bias, then one HIP pass: bias + ReLU in place (azg_nn.hip)
@@ -399,7 +413,7 @@ class InferenceNet(nn.Module):
                 ctypes.c_void_p(self._ws[0].data_ptr()), ctypes.c_void_p(getattr(self, f"us_{i}").data_ptr()),
                 ctypes.c_void_p(self._ws[1].data_ptr()), len(runs), pts, rows, C, K,
                 ctypes.c_void_p(torch.cuda.current_stream(self._ws[0].device).cuda_stream)))
-            self._khook("gemm", i, "stop")
+            self._khook("gemm", i, "stop", 3.0 * 2 * C * K * sum(P * B * n for P, n in runs))
             return
         split = self.gemm == "split_blas"
         W = 3 * C if split else C
@@ -460,10 +474,13 @@ class InferenceNet(nn.Module):
             self._khook("transform", i, "stop")
             return None
         if split_out:
-            # the flattened NHWC activation as one [hi | lo | hi] fp16 row per image (fc1's A operand)
-            y = torch.empty((B, 3 * Ho * Ho * K), device=dev, dtype=torch.float16)
+            # the flattened NHWC activation as fc1's A operand: [parts][B][chunk] split2 blocks
+            # for libazg's split-K GEMM, else one [hi | lo | hi] fp16 row per image (hipBLASLt)
+            kp = self.fc1_kparts
+            y = torch.empty((B, (2 if kp else 3) * Ho * Ho * K), device=dev, dtype=torch.float16)
             self._khook("transform", i, "start")
-            _lib.check(L.azg_winograd_out_split(M, bias, ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, mscale, 1,
+            _lib.check(L.azg_winograd_out_split(M, bias, ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, mscale,
+                                                2 if kp else 1, max(kp, 1),
                                                 ctypes.c_void_p(self.overflow.data_ptr()), s))
             self._khook("transform", i, "stop")
             return y
@@ -501,21 +518,34 @@ class InferenceNet(nn.Module):
         """The FC tail on split-fp16 GEMMs (azg_heads.hip): fc1 (+ folded fc_bn1) + ReLU,
         fc2 (+ fc_bn2) + ReLU, [fc3 | fc4] as hi.Wh + lo.Wh + hi.Wl on the fp16 MFMA
         (hipBLASLt, f32 accumulation), each epilogue writing the next GEMM's [hi | lo | hi]
-        rows; then P = softmax(fc3), v = tanh(fc4).  a: conv4's flattened activation as
-        [B, 3 * 4608] fp16 rows (azg_winograd_out_split)."""
+        rows; then P = softmax(fc3), v = tanh(fc4).  fc1 runs on libazg's split GEMM as a
+        split-K GEMM (fc1_kparts > 0) or on hipBLASLt.  a: conv4's flattened activation
+        (azg_winograd_out_split) as [parts][B][chunk] split2 blocks or [B, 3 * 4608] fp16 rows."""
         import ctypes
         from . import _lib
         L = _lib.lib()
         B, dev = a.shape[0], a.device
         st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         ovf = ctypes.c_void_p(self.overflow.data_ptr())
-        for w, b, scale in ((self.fw1_s, self.fb1, self.fc1_scale), (self.fw2_s, self.fb2, self.fc2_scale)):
+        for layer, (w, b, scale) in enumerate(((self.fw1_s, self.fb1, self.fc1_scale),
+                                               (self.fw2_s, self.fb2, self.fc2_scale))):
             n = w.shape[2]
-            m = torch.empty((1, B, n), device=dev, dtype=torch.float32)
-            torch.bmm(a.unsqueeze(0), w, out_dtype=torch.float32, out=m)
+            kp = self.fc1_kparts if layer == 0 else 0
+            if kp:  # fc1: libazg split GEMM, the K parts as points, partial products summed below
+                m = torch.empty((kp, B, n), device=dev, dtype=torch.float32)
+                chunk = a.shape[1] // (2 * kp)
+                pts, rows = (ctypes.c_int32 * 1)(kp), (ctypes.c_int32 * 1)(B)
+                self._khook("gemm", 5, "start")
+                _lib.check(L.azg_split_gemm(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(self.fw1_sk.data_ptr()),
+                                            ctypes.c_void_p(m.data_ptr()), 1, pts, rows, chunk, n, st))
+                self._khook("gemm", 5, "stop", 3.0 * 2 * kp * chunk * n * B)
+            else:
+                m = torch.empty((1, B, n), device=dev, dtype=torch.float32)
+                torch.bmm(a.unsqueeze(0), w, out_dtype=torch.float32, out=m)
             a = torch.empty((B, 3 * n), device=dev, dtype=torch.float16)
-            _lib.check(L.azg_fc_act_split(ctypes.c_void_p(m.data_ptr()), ctypes.c_void_p(b.data_ptr()), scale,
-                                          ctypes.c_void_p(a.data_ptr()), B, n, 1, ovf, st))
+            _lib.check(L.azg_fc_act_split(ctypes.c_void_p(m.data_ptr()), max(kp, 1), B * n,
+                                          ctypes.c_void_p(b.data_ptr()), scale, ctypes.c_void_p(a.data_ptr()), B, n,
+                                          1, ovf, st))
         n = self.fw34_s.shape[2]
         m = torch.empty((1, B, n), device=dev, dtype=torch.float32)
         torch.bmm(a.unsqueeze(0), self.fw34_s, out_dtype=torch.float32, out=m)

@@ -257,12 +257,16 @@ def main():
     # stream they are launched on (the current stream)
     t_kern = {"gemm": Timer(), "transform": Timer()}
     kpending = {}
+    kflops = {"gemm": 0.0, "gemm_layers": set()}
 
-    def kernel_hook(kind, i, what):
+    def kernel_hook(kind, i, what, flops=0.0):
         if what == "start":
             kpending[kind] = t_kern[kind].start()
         else:
             t_kern[kind].stop(kpending.pop(kind))
+            if kind == "gemm":
+                kflops["gemm"] += flops
+                kflops["gemm_layers"].add(i)
 
     if hasattr(ev, "kernel_hook"):
         ev.kernel_hook = kernel_hook
@@ -441,25 +445,28 @@ def main():
                            "wall_ms": elapsed * 1e3, "graph": bool(args.graph)},
             "iteration_sync_bytes": sync_bytes,
         }
-        # the dominant kernel: libazg's split GEMM (about half of the step's GPU time), its
-        # launches timed with HIP events on their stream; algorithmic FLOPs = the Winograd
-        # GEMM work (transformed points x 2 C K per leaf) x 3 fp16 products
+        # the dominant kernel: libazg's split GEMM (over half of the step's GPU time), its
+        # launches timed with HIP events on their stream; algorithmic FLOPs = the GEMM work
+        # (Winograd: transformed points x 2 C K per leaf; fc1: 2 x 4608 x 1024 per leaf) x 3
+        # fp16 products, as InferenceNet reports it per launch
         g_pairs, t_pairs = t_kern["gemm"].pairs, t_kern["transform"].pairs
         if g_pairs:
             g_ms = t_kern["gemm"].total_ms()
             n_launch = len(g_pairs)
             per_fwd = n_launch / n_forwards
-            flops_launch = 3 * leaves * algo_conv_leaf / per_fwd
+            flops_launch = kflops["gemm"] / n_launch
             ach = flops_launch / (g_ms / n_launch / 1e3) / 1e12
+            layers = sorted(kflops["gemm_layers"])
+            names = ", ".join(f"conv{i}" if i < 5 else "fc1 (split-K)" for i in layers)
             out["roofline"] = {
-                "bound": "mfma", "kernel": "split_gemm_persist_kernel (libazg azg_split_gemm, Winograd GEMMs of "
-                                           "conv2-4, one launch per layer)",
+                "bound": "mfma", "kernel": f"split_gemm_persist_kernel (libazg azg_split_gemm: {names}; one launch "
+                                           "per layer)",
                 "achieved": ach, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TF,
                 "traffic": None, "mfma_dtype": "fp16 (split, 3 products per f32 multiply-add, f32 accumulation)",
                 "avg_launch_us": g_ms / n_launch * 1e3, "launches": n_launch,
-                "per_launch": f"{leaves} leaves x {algo_conv_leaf / 1e6:.1f} MFLOP x 3 products / {per_fwd:.0f} "
-                              f"launches per forward = {flops_launch / 1e9:.1f} GFLOP per launch (avg over the 3 "
-                              f"layers' shapes) / {g_ms / n_launch * 1e3:.1f} us (HIP events)",
+                "per_launch": f"{kflops['gemm'] / n_forwards / 1e9:.1f} GFLOP per forward ({leaves} leaves; 3 fp16 "
+                              f"products) / {per_fwd:.0f} launches = {flops_launch / 1e9:.1f} GFLOP per launch (avg "
+                              f"over the layers' shapes) / {g_ms / n_launch * 1e3:.1f} us (HIP events)",
                 "share_of_forward": g_ms / nn_ms if nn_ms > 0 else None}
         if t_pairs and impl == "winograd" and getattr(ev, "gemm", "") == "split":
             tb = transform_bytes(args.n, depth, split=True)

@@ -184,12 +184,15 @@ int  azg_winograd_in_nhwc(const float* x, const float* in_bias, void* V, int32_t
 int  azg_winograd_out_nhwc(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,
                            int32_t relu, float mscale, void* stream);
 /* The output transform writing, instead of the NHWC activation, one row per image of
- * the flattened NHWC activation (width h_out*h_out*k) in split format vfmt
- * (AZG_WINO_SPLIT [hi|lo|hi] or AZG_WINO_SPLIT2 [hi|lo]): the A operand of a split
- * GEMM over it (the network's fc1, InflexionNNet.py:47).  Same checks as above;
- * out-of-range values set *overflow. */
+ * the flattened NHWC activation (width w = h_out*h_out*k) in split format vfmt
+ * (AZG_WINO_SPLIT [hi|lo|hi] or AZG_WINO_SPLIT2 [hi|lo] blocks): the A operand of a
+ * split GEMM over it (the network's fc1, InflexionNNet.py:47).  kparts > 1 cuts each
+ * row into kparts chunks of w / kparts stored as kparts matrices [kparts][batch][chunk]
+ * (the parts of a split-K GEMM; chunk % 32 == 0 for AZG_WINO_SPLIT2, % 4 otherwise).
+ * Same checks as above; out-of-range values set *overflow. */
 int  azg_winograd_out_split(const float* M, const float* bias, void* y, int32_t batch, int32_t h_out, int32_t k,
-                            int32_t relu, float mscale, int32_t vfmt, int32_t* overflow, void* stream);
+                            int32_t relu, float mscale, int32_t vfmt, int32_t kparts, int32_t* overflow,
+                            void* stream);
 /* Between two Winograd layers with no padding on the second (conv2->conv3->conv4):
  * M of layer i (h x h outputs, c channels) -> relu(A^T (mscale M) A + bias) -> V of
  * layer i+1 (input h x h, format vfmt) in one pass; the activation stays on chip.
@@ -235,17 +238,19 @@ int  azg_split_gemm_stamps(const void* a, const void* bt, float* m, int32_t nrun
  * around split-fp16 GEMMs (azg_heads.hip; the GEMMs are the caller's: one fp16
  * hipBLASLt GEMM with f32 accumulation per layer, A rows [hi | lo | hi] times the
  * weights stacked [hi; hi; lo] and pre-scaled by a power of two that `scale` undoes).
- *   azg_fc_act_split: y = bias + scale * m ([rows][n] f32), ReLU if relu != 0, written
- *                     as the next GEMM's A operand: fp16 rows [hi(n) | lo(n) | hi(n)]
+ *   azg_fc_act_split: y = bias + scale * sum_p m[p] (parts >= 1 partial products
+ *                     [rows][n] f32, part p at m + p * part_stride floats: the parts of a
+ *                     split-K GEMM, summed in order), ReLU if relu != 0, written as the
+ *                     next GEMM's A operand: fp16 rows [hi(n) | lo(n) | hi(n)]
  *                     (AZG_WINO_SPLIT); |y| > 65504 or NaN sets *overflow.
- *                     n % 4 == 0; m, bias 16-B and out 8-B aligned.
+ *                     n % 4 == 0, part_stride % 4 == 0; m, bias 16-B and out 8-B aligned.
  *   azg_policy_value: P[r][a] = softmax_a(bias[a] + scale * m[r][a]) (a < actions,
  *                     = exp(log_softmax), NNet.py:94) and v[r] = tanh(bias[actions] +
  *                     scale * m[r][actions]) from the stacked [fc3 | fc4] output m
  *                     (row stride ldm >= actions + 1); P [rows][actions], v [rows].
  *                     actions <= 512. */
-int  azg_fc_act_split(const float* m, const float* bias, float scale, void* out, int32_t rows, int32_t n,
-                      int32_t relu, int32_t* overflow, void* stream);
+int  azg_fc_act_split(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale, void* out,
+                      int32_t rows, int32_t n, int32_t relu, int32_t* overflow, void* stream);
 int  azg_policy_value(const float* m, int32_t ldm, const float* bias, float scale, float* P, float* v,
                       int32_t rows, int32_t actions, void* stream);
 

@@ -204,11 +204,12 @@ def test_split_gemm_error_not_above_f32():
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 8, 11, 12])
 @pytest.mark.parametrize("runs,C,K", [([(25, 4096)], 512, 512), ([(3, 300), (5, 37), (2, 513)], 512, 512),
                                       ([(1, 1)], 512, 512), ([(2, 77), (1, 256)], 64, 256),
-                                      ([(4, 129)], 128, 768)])
+                                      ([(4, 129)], 128, 768), ([(17, 4000)], 64, 512), ([(11, 3000)], 64, 512)])
 def test_split_gemm_kernel_matches_reference(variant, runs, C, K):
     """libazg azg_split_gemm (hand-written fp16 MFMA, LDS-DMA): M = Ah.Bh + Al.Bh + Ah.Bl
     for every point of every run, against the same products in f64 (ragged row counts,
-    the smallest channel counts, both kernel schedules)."""
+    the smallest channel counts, every kernel schedule; the last three shapes leave a
+    partial last round of the persistent grid, ragged ones included)."""
     import ctypes
     import azg_amd  # noqa: F401
     from azg_amd import _lib
@@ -242,8 +243,9 @@ def test_split_gemm_kernel_matches_reference(variant, runs, C, K):
 def test_fc1_split_form_matches_reference():
     """At >= FC1_SPLIT_MIN_BATCH leaves the FC tail runs as split-fp16 GEMMs: fc1 over
     conv4's [hi|lo|hi] output rows (azg_winograd_out_split), fc2 and [fc3 | fc4] over the
-    rows azg_fc_act_split writes, P and v from azg_policy_value: against the reference
-    module within the north_star's 1e-5, and equal to the f32 FC tail within it."""
+    rows azg_fc_act_split writes, P and v from azg_policy_value (fc1 on libazg's split
+    GEMM as a split-K GEMM, or on hipBLASLt): against the reference module within the
+    north_star's 1e-5, and equal to the f32 FC tail within it."""
     import azg_amd  # noqa: F401
     from azg_amd import nnet as nn_mod
     from azg_amd.nnet import InferenceNet, InflexionNNet
@@ -252,41 +254,52 @@ def test_fc1_split_form_matches_reference():
     fast = InferenceNet(net).cuda()
     assert fast.fc1_split
     x = (torch.rand(nn_mod.FC1_SPLIT_MIN_BATCH, 4, 7, 7, device="cuda") < 0.3).float()
+    assert fast.fc1_kparts == nn_mod.FC1_KPARTS
     with torch.no_grad():
-        p, v = fast(x)
+        p, v = fast(x)                  # fc1 as libazg's split-K split GEMM
         logp, v_ref = net(x)
+        fast.fc1_kparts = 0
+        pb, vb = fast(x)                # fc1 as the hipBLASLt split GEMM
         fast.fc1_split = False
-        p32, v32 = fast(x)
+        p32, v32 = fast(x)              # f32 FC tail
     fast.check_range()
-    torch.testing.assert_close(p, torch.exp(logp), rtol=1e-5, atol=1e-7)
-    torch.testing.assert_close(v.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(p, p32, rtol=1e-5, atol=1e-7)
+    for pp, vv in ((p, v), (pb, vb)):
+        torch.testing.assert_close(pp, torch.exp(logp), rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(vv.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(pp, p32, rtol=1e-5, atol=1e-7)
 
 
 def test_fc_act_split_kernel():
-    """azg_fc_act_split against the torch f32 expression relu(b + s m): hi = fp16(y),
-    lo = fp16(y - hi), rows [hi | lo | hi]; an out-of-range value sets the flag."""
+    """azg_fc_act_split against the torch f32 expression relu(b + s sum_p m_p): hi =
+    fp16(y), lo = fp16(y - hi), rows [hi | lo | hi]; one part and four split-K parts
+    (summed in order); an out-of-range value sets the flag."""
     import ctypes
     from azg_amd import _lib
     B, n, scale = 300, 1024, 2.0 ** -7
-    m = torch.randn(B, n, device="cuda") * 300
-    b = torch.randn(n, device="cuda")
-    out = torch.empty(B, 3 * n, device="cuda", dtype=torch.float16)
-    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    _lib.check(_lib.lib().azg_fc_act_split(ctypes.c_void_p(m.data_ptr()), ctypes.c_void_p(b.data_ptr()), scale,
-                                           ctypes.c_void_p(out.data_ptr()), B, n, 1, ctypes.c_void_p(ovf.data_ptr()),
-                                           st))
-    y = torch.relu(b + scale * m)
-    hi = y.half()
-    lo = (y - hi.float()).half()
-    assert torch.equal(out[:, :n], hi) and torch.equal(out[:, n:2 * n], lo) and torch.equal(out[:, 2 * n:], hi)
-    assert int(ovf.item()) == 0
-    m[7, 5] = 1e9
-    _lib.check(_lib.lib().azg_fc_act_split(ctypes.c_void_p(m.data_ptr()), ctypes.c_void_p(b.data_ptr()), scale,
-                                           ctypes.c_void_p(out.data_ptr()), B, n, 1, ctypes.c_void_p(ovf.data_ptr()),
-                                           st))
-    assert int(ovf.item()) == 1
+    for parts in (1, 4):
+        m = torch.randn(parts, B, n, device="cuda") * 300
+        b = torch.randn(n, device="cuda")
+        out = torch.empty(B, 3 * n, device="cuda", dtype=torch.float16)
+        ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+        def run():
+            _lib.check(_lib.lib().azg_fc_act_split(ctypes.c_void_p(m.data_ptr()), parts, B * n,
+                                                   ctypes.c_void_p(b.data_ptr()), scale,
+                                                   ctypes.c_void_p(out.data_ptr()), B, n, 1,
+                                                   ctypes.c_void_p(ovf.data_ptr()), st))
+        run()
+        acc = m[0].clone()
+        for p in range(1, parts):
+            acc = acc + m[p]
+        y = torch.relu(b + scale * acc)
+        hi = y.half()
+        lo = (y - hi.float()).half()
+        assert torch.equal(out[:, :n], hi) and torch.equal(out[:, n:2 * n], lo) and torch.equal(out[:, 2 * n:], hi)
+        assert int(ovf.item()) == 0
+        m[0, 7, 5] = 1e9
+        run()
+        assert int(ovf.item()) == 1
 
 
 @pytest.mark.parametrize("A", [343, 65, 36, 512])
@@ -305,3 +318,32 @@ def test_policy_value_kernel(A):
     logits = b + scale * m[:, :A + 1]
     torch.testing.assert_close(P, torch.softmax(logits[:, :A], dim=1), rtol=2e-6, atol=1e-9)
     torch.testing.assert_close(v, torch.tanh(logits[:, A:]), rtol=2e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("kind", ["dense", "mixed", "board6", "board8"])
+def test_first_layer_any_planes(kind):
+    """winograd_first's conv1 takes per-plane shortcuts (constant planes by border
+    class, zero cells skipped); any plane values must give the reference module's
+    P, v: dense random floats (no shortcut applies), and a mix of constant, all-zero,
+    sparse and dense planes, on 7x7 and on the Othello board sides."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    n, depth, A = {"board6": (6, 2, 37), "board8": (8, 2, 65)}.get(kind, (7, 4, 343))
+    torch.manual_seed(3)
+    net = InflexionNNet(n=n, depth=depth, action_size=A).cuda().eval()
+    fast = InferenceNet(net).cuda()
+    B = 96
+    if kind == "dense":
+        x = torch.randn(B, depth, n, n, device="cuda")
+    else:
+        x = (torch.rand(B, depth, n, n, device="cuda") < 0.2).float()
+        x[: B // 3, -1] = 3.5                                             # constant plane
+        x[B // 3: 2 * B // 3, 0] = 0.0                                    # all-zero plane
+        x[2 * B // 3:, 0] = torch.randn(B - 2 * B // 3, n, n, device="cuda")  # dense plane
+        x[5, :, 2, 3] = -0.0                                              # a negative zero
+    with torch.no_grad():
+        p, v = fast(x)
+        logp, v_ref = net(x)
+    fast.check_range()
+    torch.testing.assert_close(p, torch.exp(logp), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(v.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
