@@ -144,6 +144,10 @@ def parse():
     p.add_argument("--cpu-moves", type=int, default=200, help="cpu_baseline sample: first moves of one game")
     p.add_argument("--full-games", action="store_true",
                    help="time complete games (restart after warmup, play until every game ends): measured games/s")
+    p.add_argument("--timer-every", type=int, default=25,
+                   help="record the per-kernel HIP events (roofline, time split) on every N-th simulation of the "
+                        "timed region only: each event record costs ~10 us of GPU idle time, which would otherwise "
+                        "be charged to the throughput (1 = every simulation)")
     p.add_argument("--graph", action="store_true",
                    help="replay each move from a captured HIP graph (roofline fields then come from one extra "
                         "eager move after the timed region)")
@@ -242,9 +246,12 @@ def main():
     t_nn, t_sel, t_exp, t_end = Timer(), Timer(), Timer(), Timer()
     t_conv = {i: Timer() for i in (2, 3, 4)}
     pending = {}
+    # instrumented simulations: every args.timer_every-th one (HIP event records stall
+    # the stream ~10 us each, so the others run unobserved)
+    inst = {"on": False, "sims": 0, "count": 0}
 
     def conv_hook(i, what):
-        if i not in t_conv:
+        if i not in t_conv or not inst["on"]:
             return
         if what == "start":
             pending[i] = t_conv[i].start()
@@ -260,6 +267,8 @@ def main():
     kflops = {"gemm": 0.0, "gemm_layers": set()}
 
     def kernel_hook(kind, i, what, flops=0.0):
+        if not inst["on"]:
+            return
         if what == "start":
             kpending[kind] = t_kern[kind].start()
         else:
@@ -271,8 +280,18 @@ def main():
     if hasattr(ev, "kernel_hook"):
         ev.kernel_hook = kernel_hook
 
-    def timed_move():
+    def timed_move(every=None):
+        every = every or max(args.timer_every, 1)
         for _ in range(eng.sims):
+            on = inst["count"] % every == 0
+            inst["count"] += 1
+            if not on:
+                azg_amd._lib.check(eng.L.azg_sim_begin(eng.h, eng.planes.data_ptr(), eng._stream()))
+                P, v = eng.evaluate()
+                azg_amd._lib.check(eng.L.azg_sim_end(eng.h, P.data_ptr(), P.stride(0), v.data_ptr(), eng._stream()))
+                continue
+            inst["on"] = True
+            inst["sims"] += 1
             s = t_sel.start()
             azg_amd._lib.check(eng.L.azg_sim_begin(eng.h, eng.planes.data_ptr(), eng._stream()))
             t_sel.stop(s)
@@ -282,6 +301,7 @@ def main():
             s = t_exp.start()
             azg_amd._lib.check(eng.L.azg_sim_end(eng.h, P.data_ptr(), P.stride(0), v.data_ptr(), eng._stream()))
             t_exp.stop(s)
+            inst["on"] = False
         s = t_end.start()
         eng.move_end()
         t_end.stop(s)
@@ -334,7 +354,7 @@ def main():
         eng.drop_graph()
         if args.full_games:
             eng.reset()
-        timed_move()
+        timed_move(every=1)
         n_timed = 1
     nn_ms, sel_ms, exp_ms, end_ms = t_nn.total_ms(), t_sel.total_ms(), t_exp.total_ms(), t_end.total_ms()
     if st1["error"]:
@@ -350,7 +370,7 @@ def main():
 
     if rank == 0:
         value = exp / elapsed
-        n_forwards = max(n_timed * args.sims, 1)
+        n_forwards = max(inst["sims"], 1)  # instrumented simulations (one forward each)
         nn_avg = nn_ms / n_forwards / 1e3
         leaves = G  # the forward is evaluated on the full [G, planes, n, n] batch
         nn_tflops = None  # set below, from the FLOPs the chosen convolution performs
@@ -391,7 +411,9 @@ def main():
         mfma_mult, mfma_peak = (3, F16_MFMA_PEAK_TF) if split else (1, F32_MFMA_PEAK_TF)
         tree_s = (sel_ms + exp_ms) / 1e3
         b_exp = tree_bytes_per_exp(A, depth * args.n * args.n * 4, VALID_ACTIONS.get((args.game, args.n), 87.0))
-        tree_gbs = (exp / world) * b_exp / tree_s / 1e9 if tree_s > 0 else 0.0
+        # expansions of the instrumented simulations (the per-simulation mean of the timed region)
+        exp_inst = (exp / world) * n_forwards / max(sims_run / world / max(G, 1), 1)
+        tree_gbs = exp_inst * b_exp / tree_s / 1e9 if tree_s > 0 else 0.0
         gname = f"{args.n}x{args.n} {'Inflexion' if args.game == 'inflexion' else 'Othello'}"
         out = {
             "metric": f"node-expansions/s ({gname} self-play, {args.sims} sims/move); games/s in games_per_s",
@@ -441,7 +463,10 @@ def main():
                               "bytes_per_expansion": b_exp,
                               "select_ms_per_sim": sel_ms / n_forwards, "expand_ms_per_sim": exp_ms / n_forwards,
                               "move_end_ms_per_move": end_ms / max(n_timed, 1)},
-            "time_split": {"nn_ms": nn_ms, "select_ms": sel_ms, "expand_backup_ms": exp_ms, "move_end_ms": end_ms,
+            "time_split": {"instrumented_sims": n_forwards, "timer_every": args.timer_every,
+                           "nn_ms_per_sim": nn_ms / n_forwards, "select_ms_per_sim": sel_ms / n_forwards,
+                           "expand_backup_ms_per_sim": exp_ms / n_forwards,
+                           "nn_ms": nn_ms, "select_ms": sel_ms, "expand_backup_ms": exp_ms, "move_end_ms": end_ms,
                            "wall_ms": elapsed * 1e3, "graph": bool(args.graph)},
             "iteration_sync_bytes": sync_bytes,
         }
