@@ -355,6 +355,17 @@ class InferenceNet(nn.Module):
         """f32 words of a V with `rows` rows: f32 rows of C, fp16 rows of 2C (split) or 3C (split_blas)."""
         return rows * C if self.gemm in ("f32", "split") else (3 * rows * C + 1) // 2
 
+    def _gemm_runs(self, i):
+        """[points, tiles per image] runs of layer i's GEMMs (tile groups with equal tiles
+        per image merged): 7x7 output: 1 run, 5x5: 1, 3x3: 1."""
+        runs = []
+        for _, _, P, n in winograd_groups(self.h_out[i]):
+            if runs and runs[-1][1] == n:
+                runs[-1][0] += P
+            else:
+                runs.append([P, n])
+        return runs
+
     def _wino_need(self, i, B, C, fuse_next):
         """Workspace words layer i needs: (its V, or the next layer's V when larger and fused; its M)."""
         K = getattr(self, f"u{i}").shape[2]
@@ -395,14 +406,9 @@ class InferenceNet(nn.Module):
 
     def _winograd_gemms(self, i, B, C, K):
         """M = V x U for every transformed point of layer i, by runs of tile groups with
-        equal tiles per image (7x7: 3 runs, 5x5: 1, 3x3: 1): one libazg azg_split_gemm
+        equal tiles per image (7x7: 1 run, 5x5: 1, 3x3: 1): one libazg azg_split_gemm
         launch for all runs ("split"), or one torch.bmm (hipBLASLt) per run."""
-        runs = []
-        for _, _, P, n in winograd_groups(self.h_out[i]):
-            if runs and runs[-1][1] == n:
-                runs[-1][0] += P
-            else:
-                runs.append([P, n])
+        runs = self._gemm_runs(i)
         if self.gemm == "split":
             import ctypes
             from . import _lib
@@ -612,13 +618,23 @@ class InferenceNet(nn.Module):
             return self._fc_split(x[1])
         else:
             x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten, no copy
-            x = torch.relu_(torch.addmm(self.fb1, x, self.fw1.t()))
-        x = torch.relu_(torch.addmm(self.fb2, x, self.fw2.t()))
-        pv = torch.addmm(self.fb34, x, self.fw34.t())  # [B, A + 1]: fc3 logits | fc4
+            # f32 FC tail (small batches): bias + ReLU in the GEMMs' epilogue
+            x = torch._addmm_activation(self.fb1, x, self.fw1.t())
+        x = torch._addmm_activation(self.fb2, x, self.fw2.t())
         A = self.fw3.shape[0]
-        p = torch.softmax(pv[:, :A], dim=1)
-        v = torch.tanh(pv[:, A:])
-        return p, v
+        if x.is_cuda and A <= 512:  # [fc3 | fc4] then P, v in one libazg kernel (azg_policy_value)
+            import ctypes
+            from . import _lib
+            pv = torch.mm(x, self.fw34.t())  # [B, A + 1]; the bias is added by the kernel
+            p = torch.empty((x.shape[0], A), device=x.device, dtype=torch.float32)
+            v = torch.empty((x.shape[0], 1), device=x.device, dtype=torch.float32)
+            _lib.check(_lib.lib().azg_policy_value(
+                ctypes.c_void_p(pv.data_ptr()), A + 1, ctypes.c_void_p(self.fb34.data_ptr()), 1.0,
+                ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()), x.shape[0], A,
+                ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)))
+            return p, v
+        pv = torch.addmm(self.fb34, x, self.fw34.t())  # [B, A + 1]: fc3 logits | fc4
+        return torch.softmax(pv[:, :A], dim=1), torch.tanh(pv[:, A:])
 
 
 class NNetWrapper:
