@@ -60,6 +60,15 @@ class InflexionNNet(nn.Module):
         return F.log_softmax(self.fc3(x), dim=1), torch.tanh(self.fc4(x))
 
 
+def _addmm_relu(b, x, w):
+    """relu(b + x w): one hipBLASLt GEMM with the bias and ReLU in its epilogue where
+    torch has the fused op (torch._addmm_activation), else addmm + relu."""
+    fused = getattr(torch, "_addmm_activation", None)
+    if fused is not None:
+        return fused(b, x, w)
+    return torch.relu_(torch.addmm(b, x, w))
+
+
 def _bias_relu_(x, b):
     """x = relu(x + b) in place on a channels_last CUDA tensor (libazg, one pass)."""
     import ctypes
@@ -619,8 +628,8 @@ class InferenceNet(nn.Module):
         else:
             x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten, no copy
             # f32 FC tail (small batches): bias + ReLU in the GEMMs' epilogue
-            x = torch._addmm_activation(self.fb1, x, self.fw1.t())
-        x = torch._addmm_activation(self.fb2, x, self.fw2.t())
+            x = _addmm_relu(self.fb1, x, self.fw1.t())
+        x = _addmm_relu(self.fb2, x, self.fw2.t())
         A = self.fw3.shape[0]
         if x.is_cuda and A <= 512:  # [fc3 | fc4] then P, v in one libazg kernel (azg_policy_value)
             import ctypes
