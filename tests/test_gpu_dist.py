@@ -93,3 +93,40 @@ def test_two_ranks_gather_and_learn():
     assert len(res[0]["hist"]) == 2 and all(n > 0 for n in res[0]["hist"]) and res[1]["hist"] == []
     for k in res[0]["w"]:
         assert (res[0]["w"][k] == res[1]["w"][k]).all(), k
+
+
+def _nccl_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        import azg_amd  # noqa: F401
+        from azg_amd import dist as ad
+        from azg_amd.engine import SelfPlayEngine
+        from azg_amd.nnet import InflexionNNet
+        eng = SelfPlayEngine(5, sims=4, max_turns=12, seed_base=9)
+        eng.play()
+        rec, sent = ad.gather_records(eng, dst=0)
+        mv, act, cnt = ad.engine_records(eng)
+        m = int(mv.max())
+        ok = (torch.equal(rec[0], mv) and torch.equal(rec[1], act[:, :m])
+              and torch.equal(rec[2].to(torch.int32), cnt[:, :m]))
+        net = InflexionNNet(num_channels=16).cuda()
+        nb = ad.iteration_sync(eng, net)
+        eng.close()
+        q.put((ok, sent, nb))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_single_rank_exchange():
+    """The per-iteration exchange over the real RCCL backend (one rank: RCCL refuses two
+    ranks on one device): the gather of move records and the weight broadcast run through
+    ProcessGroupNCCL and return this rank's own records unchanged."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    ok, sent, nb = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and ok and sent > 0 and nb > 0
