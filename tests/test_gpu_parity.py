@@ -175,3 +175,30 @@ def test_refill_games_match_oracle(azg, game, n, max_turns, kind):
     assert e.active() == 0
     if game == "othello":
         assert len(lengths) > 1  # the slots did refill out of step
+
+
+def test_no_valid_action_is_flagged_not_crashed(azg):
+    """SURVEY hard part 7: a mover with no pieces and total power > 48 has no valid action
+    (MCTS.py:116,131 leave best_act = -1 and the reference crashes on it).  The engine flags
+    the slot with AZG_ERR_NO_ACTION and reports it (active() raises); the other slot's
+    search is unaffected and bit-identical to an engine without the bad slot."""
+    from azg_amd._lib import AzgError
+    from azg_amd.engine import SelfPlayEngine
+    cfg = dict(sims=6, cpuct=1, temp_threshold=30, max_turns=30, evaluator="stub")
+    e = SelfPlayEngine(2, first_game=40, **cfg)
+    board = -np.ones((7, 7), np.int8)  # 49 opponent cells of power 1: no spread, no spawn for RED
+    e.set_root(0, board, turn=12, player=1)
+    e.simulate()  # expands the root (all priors masked: the uniform fallback over no action)
+    assert e.stats()["error"] == 0
+    e.simulate()  # selects at the root: no valid action
+    assert e.stats()["error"] == -5
+    with pytest.raises(AzgError, match="no valid action"):
+        e.active()
+    for _ in range(e.sims - 2):
+        e.simulate()
+    ref = SelfPlayEngine(2, first_game=40, **cfg)
+    for _ in range(ref.sims):
+        ref.simulate()
+    assert np.array_equal(e.root_counts(1), ref.root_counts(1))
+    e.close()
+    ref.close()
