@@ -55,8 +55,9 @@ __global__ __launch_bounds__(256) void fc_act_split_kernel(const float4* __restr
     if (bad) atomicOr(overflow, 1);
 }
 
-constexpr int PV_PER_LANE = 8;  // up to 512 actions per leaf
+constexpr int PV_MAX_PER_LANE = 16;  // up to 1024 actions per leaf (9x9 Inflexion: 567)
 
+template <int PV_PER_LANE>
 __global__ __launch_bounds__(256) void policy_value_kernel(const float* __restrict__ m, int ldm,
                                                            const float* __restrict__ bias, float scale,
                                                            float* __restrict__ P, float* __restrict__ v, int rows,
@@ -110,9 +111,14 @@ extern "C" int azg_fc_act_split(const float* m, int32_t parts, int64_t part_stri
 
 extern "C" int azg_policy_value(const float* m, int32_t ldm, const float* bias, float scale, float* P, float* v,
                                 int32_t rows, int32_t actions, void* stream) {
-    if (!m || !bias || !P || !v || rows <= 0 || actions <= 0 || actions > 64 * PV_PER_LANE || ldm < actions + 1)
+    if (!m || !bias || !P || !v || rows <= 0 || actions <= 0 || actions > 64 * PV_MAX_PER_LANE || ldm < actions + 1)
         return AZG_ERR_ARG;
-    hipLaunchKernelGGL(policy_value_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, m,
-                       ldm, bias, scale, P, v, rows, actions);
+    const dim3 grid((unsigned)((rows + 3) / 4));
+    if (actions <= 64 * 8)
+        hipLaunchKernelGGL(policy_value_kernel<8>, grid, dim3(256), 0, (hipStream_t)stream, m, ldm, bias, scale, P, v,
+                           rows, actions);
+    else
+        hipLaunchKernelGGL(policy_value_kernel<PV_MAX_PER_LANE>, grid, dim3(256), 0, (hipStream_t)stream, m, ldm,
+                           bias, scale, P, v, rows, actions);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }

@@ -631,7 +631,7 @@ class InferenceNet(nn.Module):
             x = _addmm_relu(self.fb1, x, self.fw1.t())
         x = _addmm_relu(self.fb2, x, self.fw2.t())
         A = self.fw3.shape[0]
-        if x.is_cuda and A <= 512:  # [fc3 | fc4] then P, v in one libazg kernel (azg_policy_value)
+        if x.is_cuda and A <= 1024:  # [fc3 | fc4] then P, v in one libazg kernel (azg_policy_value)
             import ctypes
             from . import _lib
             pv = torch.mm(x, self.fw34.t())  # [B, A + 1]; the bias is added by the kernel

@@ -248,7 +248,7 @@ int  azg_split_gemm_stamps(const void* a, const void* bt, float* m, int32_t nrun
  *                     = exp(log_softmax), NNet.py:94) and v[r] = tanh(bias[actions] +
  *                     scale * m[r][actions]) from the stacked [fc3 | fc4] output m
  *                     (row stride ldm >= actions + 1); P [rows][actions], v [rows].
- *                     actions <= 512. */
+ *                     actions <= 1024. */
 int  azg_fc_act_split(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale, void* out,
                       int32_t rows, int32_t n, int32_t relu, int32_t* overflow, void* stream);
 int  azg_policy_value(const float* m, int32_t ldm, const float* bias, float scale, float* P, float* v,

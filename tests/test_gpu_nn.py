@@ -146,7 +146,7 @@ def test_winograd_fused_transforms_match_unfused(gemm):
 
 
 @pytest.mark.parametrize("gemm", ["split", "split_blas", "f32"])
-@pytest.mark.parametrize("n,depth,A", [(7, 4, 343), (6, 2, 37), (8, 2, 65), (5, 4, 175), (9, 2, 82)])
+@pytest.mark.parametrize("n,depth,A", [(7, 4, 343), (6, 2, 37), (8, 2, 65), (5, 4, 175), (9, 2, 82), (9, 4, 567)])
 def test_inference_net_board_sizes(n, depth, A, gemm):
     """The inference form (fused front end, fused Winograd transforms; register
     planes for the supported boards, LDS planes otherwise) vs the reference module."""
@@ -302,7 +302,7 @@ def test_fc_act_split_kernel():
         assert int(ovf.item()) == 1
 
 
-@pytest.mark.parametrize("A", [343, 65, 36, 512])
+@pytest.mark.parametrize("A", [343, 65, 36, 512, 567, 1024])
 def test_policy_value_kernel(A):
     """azg_policy_value against torch f32 softmax / tanh of the stacked [fc3 | fc4] output."""
     import ctypes
