@@ -228,9 +228,9 @@ class InferenceNet(nn.Module):
     outputs_probs = True
 
     def __init__(self, net: InflexionNNet, conv="winograd", gemm="split"):
-        """conv (conv2-4): "winograd" (default; Winograd F(2x2,3x3): libazg input /
-        output transforms around 16 f32 GEMMs, bias + ReLU in the output transform,
-        1.6x fewer multiply-adds), "miopen" (MIOpen implicit GEMM + one fused
+        """conv (conv2-4): "winograd" (default; Winograd F(5,3)/F(4,3)/F(3,3) tiles: libazg
+        fused input / output transforms around one GEMM per transformed point, bias + ReLU
+        in the output transform, 3.8x fewer multiply-adds), "miopen" (MIOpen implicit GEMM + one fused
         bias/ReLU pass), "azg" (libazg's f32-MFMA implicit GEMM with the bias/ReLU
         in its epilogue) or "auto" (per layer and input shape, whichever measured
         faster on first use).  All within the 1e-5 tolerance of the reference
@@ -448,7 +448,7 @@ class InferenceNet(nn.Module):
 
     def _conv_winograd(self, x, i, pad, in_bias=None, carried=False, B=None, H=None, fuse_next=False,
                        split_out=False):
-        """Winograd layer i (mixed F(3,3)/F(2,3) tiles, azg_winograd.hip): libazg input
+        """Winograd layer i (F(5,3)/F(4,3)/F(3,3) tiles, azg_winograd.hip): libazg input
         transform (or, with carried=True, the V the previous layer's fused transform left
         in the workspace), the GEMMs (_winograd_gemms), then either the output transform
         with bias + ReLU (returns the NHWC activation) or, with fuse_next, the fused
