@@ -198,6 +198,13 @@ struct WinoT<5> {
                                        {0, 1, 1, 0.0625f, 16, 5.0625f, 1}};
 };
 
+// a float4 read once (non-temporal: it neither stays in nor evicts from the caches)
+__device__ __forceinline__ float4 nt_load4(const float4* p) {
+    using v4 = __attribute__((ext_vector_type(4))) float;
+    const v4 x = __builtin_nontemporal_load((const v4*)p);
+    return make_float4(x[0], x[1], x[2], x[3]);
+}
+
 __device__ __forceinline__ float vadd(float a, float b) { return a + b; }
 __device__ __forceinline__ float vmul(float c, float a) { return c * a; }
 __device__ __forceinline__ float4 vadd(float4 a, float4 b) {
@@ -415,8 +422,8 @@ __global__ __launch_bounds__(256) void winograd_out_kernel(const float4* __restr
         constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
         float4 m[MA + 2][MB + 2];
 #pragma unroll
-        for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
-            m[e / (MB + 2)][e % (MB + 2)] = vmul(mscale, Min[(row + e * ps) * K4 + k4]);
+        for (int e = 0; e < (MA + 2) * (MB + 2); ++e)  // M is read once: nt
+            m[e / (MB + 2)][e % (MB + 2)] = vmul(mscale, nt_load4(Min + (row + e * ps) * K4 + k4));
         float4 yt[MA][MB];
         out_tile<MA, MB>(m, yt);
 #pragma unroll
@@ -518,8 +525,8 @@ __global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restric
         const int y0 = S.off(i), x0 = S.off(j);
         float mm[MA + 2][MB + 2];
 #pragma unroll
-        for (int e = 0; e < (MA + 2) * (MB + 2); ++e)  // uniform row base + lane
-            mm[e / (MB + 2)][e % (MB + 2)] = mscale * (Min + (row + e * ps) * C + c0)[lane];
+        for (int e = 0; e < (MA + 2) * (MB + 2); ++e)  // uniform row base + lane; M is read once: nt
+            mm[e / (MB + 2)][e % (MB + 2)] = mscale * __builtin_nontemporal_load(Min + (row + e * ps) * C + c0 + lane);
         float y[MA][MB];
         out_tile<MA, MB>(mm, y);
 #pragma unroll
