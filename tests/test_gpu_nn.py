@@ -240,7 +240,8 @@ def test_split_gemm_kernel_matches_reference(variant, runs, C, K):
         pt += p
 
 
-def test_fc1_split_form_matches_reference():
+@pytest.mark.parametrize("extra", [0, 277])
+def test_fc1_split_form_matches_reference(extra):
     """At >= FC1_SPLIT_MIN_BATCH leaves the FC tail runs as split-fp16 GEMMs: fc1 over
     conv4's [hi|lo|hi] output rows (azg_winograd_out_split), fc2 and [fc3 | fc4] over the
     rows azg_fc_act_split writes, P and v from azg_policy_value (fc1 on libazg's split
@@ -253,7 +254,7 @@ def test_fc1_split_form_matches_reference():
     net = InflexionNNet().cuda().eval()
     fast = InferenceNet(net).cuda()
     assert fast.fc1_split
-    x = (torch.rand(nn_mod.FC1_SPLIT_MIN_BATCH, 4, 7, 7, device="cuda") < 0.3).float()
+    x = (torch.rand(nn_mod.FC1_SPLIT_MIN_BATCH + extra, 4, 7, 7, device="cuda") < 0.3).float()  # ragged tiles too
     assert fast.fc1_kparts == nn_mod.FC1_KPARTS
     with torch.no_grad():
         p, v = fast(x)                  # fc1 as libazg's split-K split GEMM
