@@ -86,9 +86,19 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 // then vmcnt(0) + barrier (reads and MFMAs of a wave do not overlap).
 // Variant 3 (ILV = true): the same, with the next stage's 8 DMA pieces issued one per
 // row block between the MFMAs instead of in one burst before them.
-template <bool ILV>
+// Variant 17 (BM = 128): variant 0 on 128 x 256 tiles (64 x 64 per wave, 48 MFMAs per
+// stage, 48 KB stage buffers): twice the tiles of the 256-row form for launches that
+// fill less than a round of the chip (a few hundred leaves: conv3 / conv4 at 256
+// leaves are 98 / 50 tiles of 256 rows on 256 CUs), at twice the A-operand bytes per
+// flop; azg_split_gemm picks it by round count (split_gemm_pick).
+template <bool ILV, int BM = SG_BM>
 __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * SG_STAGEB];
+    static_assert(BM == 256 || (BM == 128 && !ILV), "row tile");
+    constexpr int ATILEB = BM * SG_ROWB;       // A bytes per stage
+    constexpr int STAGEB = ATILEB + SG_TILEB;  // A then B (256 rows)
+    constexpr int NI = BM / 32;                // 16-row blocks per wave
+    constexpr int AP = BM / 64;                // A DMA pieces (8 rows each) per wave
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGEB];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 
     // block -> tile: each XCD (bid % 8) takes one contiguous range (bijective)
@@ -104,14 +114,15 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
     const int mt = (u / g.ntn) % g.mtiles[r];
     const int e = u / (g.ntn * g.mtiles[r]);
     const int T = g.rows[r], C = g.C, K = g.K, C2 = 2 * C;
-    const int m0 = mt * SG_BM, n0 = nt * SG_BN;
+    const int m0 = mt * BM, n0 = nt * SG_BN;
     const _Float16* Ae = g.A + g.a_off[r] + (long long)e * T * C2;
     const _Float16* Be = g.Bt + (long long)(g.b_pt0[r] + e) * K * C2;
     float* Me = g.M + g.m_off[r] + (long long)e * T * K;
 
-    // DMA sources: wave w fills tile rows 32w + 8i + lane/8 (i < 4) of A and of B;
-    // lane%8 is the physical 16-B chunk, holding logical chunk lc = phys ^ ((row>>1)&7):
-    // hi channels 8lc.. (lc < 4) or lo channels 8(lc-4).. of the stage
+    // DMA sources: wave w fills A tile rows (BM/8) w + 8i + lane/8 (i < AP) and B tile
+    // rows 32w + 8i + lane/8 (i < 4); lane%8 is the physical 16-B chunk, holding logical
+    // chunk lc = phys ^ ((row>>1)&7): hi channels 8lc.. (lc < 4) or lo channels 8(lc-4)..
+    // of the stage
     // DMA by buffer_load ... lds: two descriptors per operand (SGPRs), the second
     // based 16 rows further on with 16 rows fewer in range, serve row groups i < 2
     // and i >= 2 with the same two lane offsets (the chunk swizzle differs between
@@ -126,29 +137,28 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
     int aoff[2], boff[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+        const int RA = (BM / 8) * wid + 8 * i + (lane >> 3);
         const int R = 32 * wid + 8 * i + (lane >> 3);
-        const int lc = (lane & 7) ^ ((R >> 1) & 7);
-        const int col = 8 * lc;
-        aoff[i] = ((m0 + R) * C2 + col) * 2;
-        boff[i] = ((n0 + b_col(R)) * C2 + col) * 2;
+        aoff[i] = ((m0 + RA) * C2 + 8 * ((lane & 7) ^ ((RA >> 1) & 7))) * 2;
+        boff[i] = ((n0 + b_col(R)) * C2 + 8 * ((lane & 7) ^ ((R >> 1) & 7))) * 2;
     }
     auto issue = [&](int ks, int buf) {
-        char* base = smem + buf * SG_STAGEB + (32 * wid) * SG_ROWB;
+        char* abase = smem + buf * STAGEB + ((BM / 8) * wid) * SG_ROWB;
+        char* bbase = smem + buf * STAGEB + ATILEB + (32 * wid) * SG_ROWB;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < AP; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
-                                                     (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
+                                                     (__attribute__((address_space(3))) void*)(abase + 8 * i * SG_ROWB),
                                                      16, aoff[i & 1], ks * SG_STAGE_SOFF, 0, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
-                                                     (__attribute__((address_space(3))) void*)(base + SG_TILEB +
-                                                                                              8 * i * SG_ROWB),
+                                                     (__attribute__((address_space(3))) void*)(bbase + 8 * i * SG_ROWB),
                                                      16, boff[i & 1], ks * SG_STAGE_SOFF, 0, 0);
     };
     // DMA piece p of a stage (p < 4: A row group p, else B row group p - 4)
     auto issue_piece = [&](int ks, int buf, int p) {
-        char* base = smem + buf * SG_STAGEB + (32 * wid) * SG_ROWB;
+        char* base = smem + buf * STAGEB + (32 * wid) * SG_ROWB;
         const int q = p & 3;
         if (p < 4)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 2 ? ar0 : ar1,
@@ -156,24 +166,24 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
                                                      16, aoff[q & 1], ks * SG_STAGE_SOFF, 0, 0);
         else
             __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 2 ? br0 : br1,
-                                                     (__attribute__((address_space(3))) void*)(base + SG_TILEB +
+                                                     (__attribute__((address_space(3))) void*)(base + ATILEB +
                                                                                               8 * q * SG_ROWB),
                                                      16, boff[q & 1], ks * SG_STAGE_SOFF, 0, 0);
     };
 
-    // operand reads: wave (wm, wn) = rows 128 wm.., cols 64 wn..; lane holds row lane%16
-    // of a 16-row block, channels 8 (lane/16).. of the 32 (hi) and the same of lo
+    // operand reads: wave (wm, wn) = rows (BM/2) wm.., cols 64 wn..; lane holds row
+    // lane%16 of a 16-row block, channels 8 (lane/16).. of the 32 (hi) and the same of lo
     const int wm = wid >> 2, wn = wid & 3;
     const int lr = lane & 15, sw = lr >> 1;  // (row >> 1) & 7 of every 16-row block
     const int ch = lane >> 4;
-    const int a_hi = (wm * 128 + lr) * SG_ROWB + 16 * (ch ^ sw);
-    const int a_lo = (wm * 128 + lr) * SG_ROWB + 16 * ((4 + ch) ^ sw);
-    const int b_hi = SG_TILEB + (wn * 64 + lr) * SG_ROWB + 16 * (ch ^ sw);
-    const int b_lo = SG_TILEB + (wn * 64 + lr) * SG_ROWB + 16 * ((4 + ch) ^ sw);
+    const int a_hi = (wm * (BM / 2) + lr) * SG_ROWB + 16 * (ch ^ sw);
+    const int a_lo = (wm * (BM / 2) + lr) * SG_ROWB + 16 * ((4 + ch) ^ sw);
+    const int b_hi = ATILEB + (wn * 64 + lr) * SG_ROWB + 16 * (ch ^ sw);
+    const int b_lo = ATILEB + (wn * 64 + lr) * SG_ROWB + 16 * ((4 + ch) ^ sw);
 
-    f32x4 acc[8][4];
+    f32x4 acc[NI][4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -182,22 +192,22 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int ks = 0; ks < nks; ++ks) {
-        const char* st = smem + (ks & 1) * SG_STAGEB;
-        f16x8 ah[8], al[8], bh[4], bl[4];
+        const char* st = smem + (ks & 1) * STAGEB;
+        f16x8 ah[NI], al[NI], bh[4], bl[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             bh[j] = *(const f16x8*)(st + b_hi + 16 * j * SG_ROWB);
             bl[j] = *(const f16x8*)(st + b_lo + 16 * j * SG_ROWB);
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < NI; ++i) {
             ah[i] = *(const f16x8*)(st + a_hi + 16 * i * SG_ROWB);
             al[i] = *(const f16x8*)(st + a_lo + 16 * i * SG_ROWB);
         }
         if (!ILV && ks + 1 < nks) issue(ks + 1, (ks + 1) & 1);
         __builtin_amdgcn_sched_barrier(0);  // the DMA issue stays ahead of the MFMAs
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < NI; ++i) {
             if (ILV && ks + 1 < nks) {
                 issue_piece(ks + 1, (ks + 1) & 1, i);
                 __builtin_amdgcn_sched_barrier(0);
@@ -218,10 +228,10 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
     // epilogue: C/D map of 16x16x32: col = lane % 16, row = 4 (lane / 16) + reg; the
     // lane's four column blocks are adjacent columns (b_col): one 16-B store per row
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NI; ++i) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int row = m0 + wm * 128 + 16 * i + 4 * ch + q;
+            const int row = m0 + wm * (BM / 2) + 16 * i + 4 * ch + q;
             if (row >= T) continue;
             *(f32x4*)(Me + (long long)row * K + n0 + wn * 64 + 4 * lr) =
                 f32x4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
@@ -1198,8 +1208,9 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
                              unsigned long long* stamps = nullptr) {
     if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % (2 * SG_BK) ||
         k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
-        variant > 16 || variant == 9 || variant == 13 || variant == 14 || (variant == 10) != (stamps != nullptr))
+        variant > 17 || variant == 9 || variant == 13 || variant == 14 || (variant == 10) != (stamps != nullptr))
         return AZG_ERR_ARG;
+    const int bm = variant == 17 ? 128 : SG_BM;
     SGArgs g{};
     g.A = (const _Float16*)A;
     g.Bt = (const _Float16*)Bt;
@@ -1214,7 +1225,7 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
         if (points[r] <= 0 || rows[r] <= 0) return AZG_ERR_ARG;
         g.points[r] = points[r];
         g.rows[r] = rows[r];
-        g.mtiles[r] = (rows[r] + SG_BM - 1) / SG_BM;
+        g.mtiles[r] = (rows[r] + bm - 1) / bm;
         g.tile0[r] = tiles;
         g.a_off[r] = a;
         g.m_off[r] = m;
@@ -1231,6 +1242,8 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
     g.stamps = stamps;
     if (variant == 0)
         hipLaunchKernelGGL(split_gemm_kernel<false>, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 17)
+        hipLaunchKernelGGL((split_gemm_kernel<false, 128>), dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 3)
         hipLaunchKernelGGL(split_gemm_kernel<true>, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 1)
@@ -1269,9 +1282,27 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
+// The default schedule for a launch: variant 4 (256-row tiles, persistent) unless the
+// launch is short enough that the 128-row form (variant 17) needs fewer rounds of the
+// chip, weighting a 128-row round at SG_R128 of a 256-row one (its stage moves 3/4 of
+// the bytes for 1/2 of the MFMAs; measured, tools/split_gemm_bench.py AZG_SG_LEAVES).
+constexpr int SG_R128_NUM = 5, SG_R128_DEN = 8;
+static int split_gemm_pick(int32_t nruns, const int32_t* points, const int32_t* rows, int32_t k) {
+    if (!points || !rows || nruns < 1 || nruns > SG_MAXRUNS || k <= 0) return 4;
+    long long t256 = 0, t128 = 0;
+    for (int r = 0; r < nruns; ++r) {
+        if (points[r] <= 0 || rows[r] <= 0) return 4;
+        t256 += (long long)points[r] * ((rows[r] + 255) / 256) * (k / SG_BN);
+        t128 += (long long)points[r] * ((rows[r] + 127) / 128) * (k / SG_BN);
+    }
+    const long long cus = persistent_blocks(1 << 30);
+    const long long r256 = (t256 + cus - 1) / cus, r128 = (t128 + cus - 1) / cus;
+    return r128 * SG_R128_NUM < r256 * SG_R128_DEN ? 17 : 4;
+}
+
 extern "C" int azg_split_gemm(const void* A, const void* Bt, float* M, int32_t nruns, const int32_t* points,
                               const int32_t* rows, int32_t c, int32_t k, void* stream) {
-    return split_gemm_launch(4, A, Bt, M, nruns, points, rows, c, k, stream);
+    return split_gemm_launch(split_gemm_pick(nruns, points, rows, k), A, Bt, M, nruns, points, rows, c, k, stream);
 }
 
 extern "C" int azg_split_gemm_variant(int32_t variant, const void* A, const void* Bt, float* M, int32_t nruns,

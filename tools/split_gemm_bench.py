@@ -1,5 +1,5 @@
 """Time libazg's split GEMM (azg_split_gemm) on the leaf network's Winograd GEMM shapes
-at 4096 leaves, every kernel variant, against the same products as one hipBLASLt fp16
+at 4096 leaves (AZG_SG_LEAVES), every kernel variant, against the same products as one hipBLASLt fp16
 GEMM ([hi|lo|hi] rows) and the f32 GEMM; median (and best) of 7 round-robin rounds.
 TF/s are of the executed fp16 MFMA work (3 products per f32 multiply-add).
 
@@ -32,7 +32,9 @@ def layer_runs(h_out, B=4096):
     return [tuple(r) for r in runs]
 
 
-LAYERS = {"conv2": layer_runs(7), "conv3": layer_runs(5), "conv4": layer_runs(3)}
+# AZG_SG_LEAVES=256 times the shapes of a 256-leaf forward (C2) instead of 4096
+LEAVES = int(os.environ.get("AZG_SG_LEAVES", "4096"))
+LAYERS = {"conv2": layer_runs(7, LEAVES), "conv3": layer_runs(5, LEAVES), "conv4": layer_runs(3, LEAVES)}
 
 
 def timeit(fn, reps=10):
@@ -103,7 +105,11 @@ def main():
 
         flops16 = 3 * 2.0 * rows * C * K
         row = {"layer": name, "runs": runs}
-        fns = [("azg_v%d" % v, azg_variant(v)) for v in VARIANTS] + [("hipblaslt_split", blas),
+        def azg_default():
+            _lib.check(L.azg_split_gemm(ctypes.c_void_p(A.data_ptr()), ctypes.c_void_p(Bt.data_ptr()),
+                                        ctypes.c_void_p(M.data_ptr()), len(runs), pts, rws, C, K, st))
+
+        fns = [("azg_v%d" % v, azg_variant(v)) for v in VARIANTS] + [("azg_default", azg_default), ("hipblaslt_split", blas),
                                                                          ("hipblaslt_f32", f32)]
         for k, (med, mn) in time_all(fns).items():
             fl = flops16 if k != "hipblaslt_f32" else flops16 / 3
