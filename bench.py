@@ -112,11 +112,11 @@ def load_pmc(G, game, impl, gemm="split"):
 
     out = {"transforms": sum(per_fwd(k) for k in ("winograd_first", "winograd_mid", "winograd_out")),
            "tree": per_fwd("select_kernel") + per_fwd("expand_backup_kernel"),
-           "note": f"{os.path.relpath(path, ROOT)}: FETCH_SIZE x2 + WRITE_SIZE (split GEMM: per launch; "
+           "note": f"{os.path.relpath(path, ROOT)}: FETCH_SIZE x2 + WRITE_SIZE (split GEMM: per call; "
                    "transforms: per forward; tree: per simulation step); counts L2 misses incl. Infinity-Cache hits"}
-    sg = d.get("split_gemm")
-    if sg and sg.get("dispatches"):
-        out["split_gemm"] = (sg["fetch_bytes_corrected_total"] + sg["write_bytes_total"]) / sg["dispatches"]
+    if per_fwd("split_gemm"):
+        # per forward over the calls' launches (one per call)
+        out["split_gemm_per_forward"] = per_fwd("split_gemm")
     return out
 
 
@@ -484,14 +484,16 @@ def main():
             layers = sorted(kflops["gemm_layers"])
             names = ", ".join(f"conv{i}" if i < 5 else "fc1 (split-K)" for i in layers)
             out["roofline"] = {
-                "bound": "mfma", "kernel": f"split_gemm_persist_kernel (libazg azg_split_gemm: {names}; one launch "
-                                           "per layer)",
+                "bound": "mfma", "kernel": f"libazg azg_split_gemm ({names}; one call per layer: "
+                                           "split_gemm_persist_kernel on 256-row tiles, or split_gemm_kernel on "
+                                           "128-row tiles for short layers)",
                 "achieved": ach, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TF,
                 "traffic": None, "mfma_dtype": "fp16 (split, 3 products per f32 multiply-add, f32 accumulation)",
                 "avg_launch_us": g_ms / n_launch * 1e3, "launches": n_launch,
                 "per_launch": f"{kflops['gemm'] / n_forwards / 1e9:.1f} GFLOP per forward ({leaves} leaves; 3 fp16 "
-                              f"products) / {per_fwd:.0f} launches = {flops_launch / 1e9:.1f} GFLOP per launch (avg "
-                              f"over the layers' shapes) / {g_ms / n_launch * 1e3:.1f} us (HIP events)",
+                              f"products) / {per_fwd:.0f} calls = {flops_launch / 1e9:.1f} GFLOP per call (avg "
+                              f"over the layers' shapes) / {g_ms / n_launch * 1e3:.1f} us (HIP events around each "
+                              "call)",
                 "share_of_forward": g_ms / nn_ms if nn_ms > 0 else None}
         if t_pairs and impl == "winograd" and getattr(ev, "gemm", "") == "split":
             tb = transform_bytes(args.n, depth, split=True)
@@ -505,8 +507,8 @@ def main():
             out["roofline"] = out.pop("roofline_conv_span")
         pmc = load_pmc(G, args.game, impl, getattr(ev, "gemm", "f32"))
         if pmc:
-            if "split_gemm" in pmc and out["roofline"].get("launches"):
-                out["roofline"]["traffic"] = pmc["split_gemm"]
+            if "split_gemm_per_forward" in pmc and out["roofline"].get("launches"):
+                out["roofline"]["traffic"] = pmc["split_gemm_per_forward"] / (out["roofline"]["launches"] / n_forwards)
             if "roofline_transforms" in out:
                 out["roofline_transforms"]["traffic"] = pmc["transforms"]
             for k in ("roofline", "roofline_transforms"):

@@ -210,6 +210,19 @@ def test_split_gemm_kernel_matches_reference(variant, runs, C, K):
     for every point of every run, against the same products in f64 (ragged row counts,
     the smallest channel counts, every kernel schedule; the last three shapes leave a
     partial last round of the persistent grid, ragged ones included)."""
+    _check_split_gemm(variant, runs, C, K)
+
+
+@pytest.mark.parametrize("runs,C,K", [([(9, 4096)], 512, 512), ([(8, 2048), (8, 4096)], 512, 512),
+                                      ([(17, 4000)], 64, 512), ([(49, 256)], 512, 512), ([(25, 256)], 512, 512),
+                                      ([(121, 1024)], 64, 512)])
+def test_split_gemm_default_schedule_matches_reference(runs, C, K):
+    """azg_split_gemm's own schedule: 256-row persistent tiles, or 128-row tiles for short
+    launches (the 256-leaf shapes), ragged and multi-run shapes included."""
+    _check_split_gemm(None, runs, C, K)
+
+
+def _check_split_gemm(variant, runs, C, K):
     import ctypes
     import azg_amd  # noqa: F401
     from azg_amd import _lib
@@ -221,10 +234,12 @@ def test_split_gemm_kernel_matches_reference(variant, runs, C, K):
     M = torch.full((sum(p * t for p, t in runs) * K,), float("nan"), device="cuda")
     pts = (ctypes.c_int32 * len(runs))(*[p for p, _ in runs])
     rows = (ctypes.c_int32 * len(runs))(*[t for _, t in runs])
-    _lib.check(_lib.lib().azg_split_gemm_variant(variant, ctypes.c_void_p(A.data_ptr()),
-                                                 ctypes.c_void_p(Bt.data_ptr()), ctypes.c_void_p(M.data_ptr()),
-                                                 len(runs), pts, rows, C, K,
-                                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    ptrs = (ctypes.c_void_p(A.data_ptr()), ctypes.c_void_p(Bt.data_ptr()), ctypes.c_void_p(M.data_ptr()),
+            len(runs), pts, rows, C, K, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    if variant is None:
+        _lib.check(_lib.lib().azg_split_gemm(*ptrs))
+    else:
+        _lib.check(_lib.lib().azg_split_gemm_variant(variant, *ptrs))
     torch.cuda.synchronize()
     a_row = m_row = pt = 0
     for p, t in runs:
