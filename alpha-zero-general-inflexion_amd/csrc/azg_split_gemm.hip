@@ -90,10 +90,11 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 // stage, 48 KB stage buffers): twice the tiles of the 256-row form for launches that
 // fill less than a round of the chip (a few hundred leaves: conv3 / conv4 at 256
 // leaves are 98 / 50 tiles of 256 rows on 256 CUs), at twice the A-operand bytes per
-// flop; azg_split_gemm picks it by round count (split_gemm_pick).
+// flop; azg_split_gemm picks it by round count (split_gemm_pick).  Variant 18 (BM = 64)
+// is the same on 64 x 256 tiles (32 x 64 per wave).
 template <bool ILV, int BM = SG_BM>
 __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
-    static_assert(BM == 256 || (BM == 128 && !ILV), "row tile");
+    static_assert(BM == 256 || ((BM == 128 || BM == 64) && !ILV), "row tile");
     constexpr int ATILEB = BM * SG_ROWB;       // A bytes per stage
     constexpr int STAGEB = ATILEB + SG_TILEB;  // A then B (256 rows)
     constexpr int NI = BM / 32;                // 16-row blocks per wave
@@ -1208,9 +1209,9 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
                              unsigned long long* stamps = nullptr) {
     if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % (2 * SG_BK) ||
         k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
-        variant > 17 || variant == 9 || variant == 13 || variant == 14 || (variant == 10) != (stamps != nullptr))
+        variant > 18 || variant == 9 || variant == 13 || variant == 14 || (variant == 10) != (stamps != nullptr))
         return AZG_ERR_ARG;
-    const int bm = variant == 17 ? 128 : SG_BM;
+    const int bm = variant == 17 ? 128 : variant == 18 ? 64 : SG_BM;
     SGArgs g{};
     g.A = (const _Float16*)A;
     g.Bt = (const _Float16*)Bt;
@@ -1244,6 +1245,8 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
         hipLaunchKernelGGL(split_gemm_kernel<false>, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 17)
         hipLaunchKernelGGL((split_gemm_kernel<false, 128>), dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 18)
+        hipLaunchKernelGGL((split_gemm_kernel<false, 64>), dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 3)
         hipLaunchKernelGGL(split_gemm_kernel<true>, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 1)
@@ -1282,22 +1285,27 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
-// The default schedule for a launch: variant 4 (256-row tiles, persistent) unless the
-// launch is short enough that the 128-row form (variant 17) needs fewer rounds of the
-// chip, weighting a 128-row round at SG_R128 of a 256-row one (its stage moves 3/4 of
-// the bytes for 1/2 of the MFMAs; measured, tools/split_gemm_bench.py AZG_SG_LEAVES).
-constexpr int SG_R128_NUM = 5, SG_R128_DEN = 8;
+// The default schedule for a launch: variant 4 (256-row tiles, persistent) unless a
+// short launch needs fewer weighted rounds of the chip on 128-row (variant 17) or
+// 64-row tiles (variant 18), a round of those costing about 5/8 and 4/8 of a 256-row
+// round (tools/split_gemm_bench.py with AZG_SG_LEAVES = 128-4096,
+// profiles/r02_split_gemm_bench_smallbatch.json); ties keep the larger tile.
 static int split_gemm_pick(int32_t nruns, const int32_t* points, const int32_t* rows, int32_t k) {
     if (!points || !rows || nruns < 1 || nruns > SG_MAXRUNS || k <= 0) return 4;
-    long long t256 = 0, t128 = 0;
+    long long t[3] = {0, 0, 0};  // tiles at 256, 128, 64 rows
     for (int r = 0; r < nruns; ++r) {
         if (points[r] <= 0 || rows[r] <= 0) return 4;
-        t256 += (long long)points[r] * ((rows[r] + 255) / 256) * (k / SG_BN);
-        t128 += (long long)points[r] * ((rows[r] + 127) / 128) * (k / SG_BN);
+        for (int i = 0; i < 3; ++i) t[i] += (long long)points[r] * ((rows[r] + (255 >> i)) / (256 >> i)) * (k / SG_BN);
     }
     const long long cus = persistent_blocks(1 << 30);
-    const long long r256 = (t256 + cus - 1) / cus, r128 = (t128 + cus - 1) / cus;
-    return r128 * SG_R128_NUM < r256 * SG_R128_DEN ? 17 : 4;
+    const int weight[3] = {8, 5, 4}, variant[3] = {4, 17, 18};
+    int best = 0;
+    long long best_cost = 0;
+    for (int i = 0; i < 3; ++i) {
+        const long long cost = (t[i] + cus - 1) / cus * weight[i];
+        if (i == 0 || cost < best_cost) best = i, best_cost = cost;
+    }
+    return variant[best];
 }
 
 extern "C" int azg_split_gemm(const void* A, const void* Bt, float* M, int32_t nruns, const int32_t* points,

@@ -211,8 +211,9 @@ int  azg_winograd_first_nchw(const float* planes, const float* w1, const float* 
  *   M_e [rows x k] f32 = A_e x B_e^T,  A_e [rows][2c] fp16 rows of 32-channel
  *   [hi | lo] blocks (V in AZG_WINO_SPLIT2), B_e [k][2c] fp16 rows in the same blocks
  *   (U^T, points of all runs in order), computed as hi.hi + lo.hi + hi.lo with f32
- *   accumulation.  Schedule: 256 x 256 tiles (variant 4), or 128 x 256 tiles
- *   (variant 17) when those need fewer rounds of the chip (small leaf batches).
+ *   accumulation.  Schedule: 256 x 256 tiles (variant 4), or 128 x 256 / 64 x 256
+ *   tiles (variants 17 / 18) when those need fewer rounds of the chip (small leaf
+ *   batches).
  * c % 64 == 0, k % 256 == 0, nruns <= 4, 16-B aligned pointers. */
 int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, const int32_t* points,
                     const int32_t* rows, int32_t c, int32_t k, void* stream);
@@ -225,7 +226,8 @@ int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, cons
  * variant 4 with each accumulator's products 4 MFMAs apart; 11: variant 4 with each
  * tile's stores deferred into the next tile's first stage; 12: ping-pong with each
  * wave's own DMA and one stage stream across tiles; 17: variant 0 on 128-row tiles,
- * azg_split_gemm's pick for short launches); for tests and probes. */
+ * azg_split_gemm's pick for short launches; 18: the same on 64-row tiles); for tests
+ * and probes. */
 int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, float* m, int32_t nruns,
                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
 /* Diagnostic build of the default split GEMM with in-kernel s_memtime stamps

@@ -201,7 +201,7 @@ def test_split_gemm_error_not_above_f32():
     assert errs["split_blas"] <= 1.5 * errs["f32"], errs
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 8, 11, 12, 17])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 8, 11, 12, 17, 18])
 @pytest.mark.parametrize("runs,C,K", [([(25, 4096)], 512, 512), ([(3, 300), (5, 37), (2, 513)], 512, 512),
                                       ([(1, 1)], 512, 512), ([(2, 77), (1, 256)], 64, 256),
                                       ([(4, 129)], 128, 768), ([(17, 4000)], 64, 512), ([(11, 3000)], 64, 512)])
