@@ -296,13 +296,19 @@ __device__ __forceinline__ void store_v(void* V, long long row, int C, int c, fl
 // in two 64-B halves from two instructions).  rowp = the row's halves at channel c0,
 // wave-uniform, so the stores take a scalar base and a 32-bit lane offset.  Returns
 // whether v is out of fp16 range (the caller raises the flag once).
+template <bool NT = false>
 __device__ __forceinline__ bool store_v2_wave(unsigned short* rowp, unsigned lane, float v) {
     const _Float16 hi = (_Float16)v;  // round to nearest even
     const _Float16 lo = (_Float16)(v - (float)hi);
     const auto sw = __builtin_amdgcn_permlane32_swap((unsigned)__builtin_bit_cast(unsigned short, hi),
                                                      (unsigned)__builtin_bit_cast(unsigned short, lo), false, false);
-    rowp[lane] = (unsigned short)sw[0];       // lanes 0-31: hi of c0 + lane; 32-63: lo of c0 + lane - 32
-    rowp[64 + lane] = (unsigned short)sw[1];  // the same for channels c0 + 32 ..
+    if constexpr (NT) {
+        __builtin_nontemporal_store((unsigned short)sw[0], rowp + lane);
+        __builtin_nontemporal_store((unsigned short)sw[1], rowp + 64 + lane);
+    } else {
+        rowp[lane] = (unsigned short)sw[0];       // lanes 0-31: hi of c0 + lane; 32-63: lo of c0 + lane - 32
+        rowp[64 + lane] = (unsigned short)sw[1];  // the same for channels c0 + 32 ..
+    }
     return !(fabsf(v) <= 65504.f);
 }
 
@@ -467,7 +473,7 @@ struct Plane {
 
 // The next layer's input transform (pad PAD) of the lane's h x h plane: V out.  The
 // wave's lanes hold channels c0 + lane (c0 wave-uniform, a multiple of 64).
-template <int HC, int FMT, int PAD, class P>
+template <int HC, int FMT, int PAD, bool NT = false, class P>
 __device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, long long b, int c0, unsigned lane, int C,
                                            long long B, void* __restrict__ Vout, int* overflow) {
     const int h = HC > 0 ? HC : h_rt;
@@ -492,7 +498,7 @@ __device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, long long b, i
 #pragma unroll
         for (int e = 0; e < (MA + 2) * (MB + 2); ++e) {
             if constexpr (FMT == AZG_WINO_SPLIT2)
-                bad |= store_v2_wave((unsigned short*)Vout + (row + e * ps) * 2 * C + 2 * c0, lane,
+                bad |= store_v2_wave<NT>((unsigned short*)Vout + (row + e * ps) * 2 * C + 2 * c0, lane,
                                      Vt[e / (MB + 2)][e % (MB + 2)]);
             else
                 store_v<FMT>(Vout, row + e * ps, C, c, Vt[e / (MB + 2)][e % (MB + 2)], overflow);
@@ -681,7 +687,10 @@ __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restr
                 ys.put(y * n + x, fmaxf(acc + bk, 0.f));
             }
     }
-    plane_to_V<NC, FMT, 1>(ys, n, b, k0, lane, C, B, Vout, overflow);
+    // V2 goes out with non-temporal stores: nothing here reads it back, and the GEMM
+    // reads it only after the whole grid (241 -> 209 us at 4096 leaves, DESIGN 6b,
+    // profiles/r02_nt_store_probe)
+    plane_to_V<NC, FMT, 1, true>(ys, n, b, k0, lane, C, B, Vout, overflow);
 }
 
 // one thread per work item, rounded up to whole groups of 8 blocks (xcd_item)
