@@ -47,13 +47,15 @@ class BatchedArena:
         self.last_engine_state = None
 
     def _inference_form(self, gemm):
-        from .nnet import InferenceNet, NNetWrapper
-        return InferenceNet(self.nnet.nnet, gemm=gemm) if isinstance(self.nnet, NNetWrapper) else self.nnet
+        from .nnet import InferenceNet, NNetWrapper, replay_form
+        if not isinstance(self.nnet, NNetWrapper):
+            return self.nnet
+        return replay_form(self.nnet.nnet) if gemm == "f32" else InferenceNet(self.nnet.nnet, gemm=gemm)
 
     def playGames(self, num, verbose=False):
         """Arena.playGames (Arena.py:90-142): (MCTS player wins, baseline wins, draws).
         If the split-fp16 network met an operand out of fp16 range, the games are
-        replayed (same seeds, same result as a first run) with the f32-GEMM form."""
+        replayed (same seeds, same result as a first run) with nnet.replay_form."""
         if not (isinstance(num, int) and num >= 2):
             raise AssertionError("num must be an int >= 2")
         try:
@@ -62,7 +64,7 @@ class BatchedArena:
             f32 = self._inference_form("f32")
             if f32 is self.evaluator:
                 raise
-            log.warning("arena: split-fp16 operand out of range; replaying with InferenceNet(gemm='f32')")
+            log.warning("arena: split-fp16 operand out of range; replaying with the f32 replay form")
             self.evaluator = f32
             return self._play(num)
 

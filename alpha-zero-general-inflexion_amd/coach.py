@@ -100,16 +100,17 @@ class Coach:
     def evaluator(self, gemm="split"):
         """The leaf evaluator for the engine: an NNetWrapper's current weights as
         the inference form (BN folded, NHWC; nnet.InferenceNet), else self.nnet
-        itself (a module, or "stub")."""
-        from .nnet import InferenceNet, NNetWrapper
+        itself (a module, or "stub").  gemm="f32" gives the out-of-fp16-range
+        fallback, nnet.replay_form (direct f32 convolutions)."""
+        from .nnet import InferenceNet, NNetWrapper, replay_form
         if isinstance(self.nnet, NNetWrapper):
-            return InferenceNet(self.nnet.nnet, gemm=gemm)
+            return replay_form(self.nnet.nnet) if gemm == "f32" else InferenceNet(self.nnet.nnet, gemm=gemm)
         return self.nnet
 
     def _range_checked(self, run, evaluator):
         """run(evaluator) -> result; if the split-fp16 network met an operand out of
         fp16 range (FloatingPointError from SelfPlayEngine.check_evaluator), rerun
-        with the f32-GEMM form.  Games are seeded by their index, so the rerun's
+        with nnet.replay_form.  Games are seeded by their index, so the rerun's
         records are the ones a first f32 run would have produced."""
         ev = evaluator if evaluator is not None else self.evaluator()
         try:
@@ -117,7 +118,7 @@ class Coach:
         except FloatingPointError:
             if evaluator is not None or ev is self.nnet:
                 raise
-            log.warning("self-play: split-fp16 operand out of range; replaying with InferenceNet(gemm='f32')")
+            log.warning("self-play: split-fp16 operand out of range; replaying with the f32 replay form")
             return run(self.evaluator(gemm="f32"))
 
     def selfplay_batch(self, num_games, evaluator=None, seed_base=0, first_game=0, return_records=False):
@@ -193,11 +194,31 @@ class Coach:
                 eng.close()
                 raise
             return eng
-        # a rank whose split-fp16 net overflows replays its games in f32 before the
-        # gather, which every rank then enters exactly once
-        eng = self._range_checked(run, None)
+        # If any rank's split-fp16 net met an operand out of fp16 range, EVERY rank replays
+        # its games with nnet.replay_form, together: no rank waits in the gather while
+        # another replays (which could outlast the process group's timeout), and the
+        # iteration's records are those of an all-f32 run whatever the sharding.
+        ev = self.evaluator()
         try:
-            rec, _ = gather_records(eng, dst=0, group=group)
+            eng, overflow = run(ev), 0
+        except FloatingPointError:
+            if ev is self.nnet:
+                raise
+            eng, overflow = None, 1
+        dev = (torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl"
+               else torch.device("cpu"))
+        flag = torch.tensor([overflow], dtype=torch.int64, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if int(flag.item()):
+            log.warning("self-play: split-fp16 operand out of range on a rank; all ranks replay with "
+                        "the f32 replay form")
+            if eng is not None:
+                eng.close()
+            eng = run(self.evaluator(gemm="f32"))
+        self.last_replayed_f32 = bool(int(flag.item()))
+        try:
+            rec, self.last_sent_bytes = gather_records(eng, dst=0, group=group,
+                                                       temp_threshold=int(self.args.tempThreshold))
         finally:
             eng.close()
         if rank != 0:

@@ -10,10 +10,16 @@ iteration's examples and trains -- two collectives run over RCCL (backend
     (an all_reduce of the sizes, then gathers into the trainer only);
   * broadcast of the trainer's weights (one flat f32 buffer, ~50 MB).
 
-A compact move record is (moves made, actions, root visit counts as int16 --
-int32 if any count exceeds 32767) per game: enough to rebuild every training
-example (Coach.py:74-90) by replaying the actions from the initial position
-(examples.examples_from_records; temperatures follow from tempThreshold).
+A compact move record is (moves made, actions, root visit counts) per game:
+enough to rebuild every training example (Coach.py:74-90) by replaying the
+actions from the initial position (examples.examples_from_records; temperatures
+follow from tempThreshold).  The counts travel sparse: only the moves played at
+temperature 1 need them (a temperature-0 move's pi is the one-hot of its action,
+MCTS.py:51-56), and of a root's 343 counts only the visited actions are nonzero
+(at most sims + the subtree kept from the previous move), so each such move is
+sent as its number of visited actions plus (action, count) pairs packed in 32
+bits.  At 4096 games x 344 moves that is ~1 MB of counts per rank instead of
+0.97 GB as dense int16.
 """
 import ctypes
 
@@ -46,12 +52,14 @@ def engine_records(engine):
     return moves, actions, counts
 
 
-def gather_records(engine, dst=0, group=None):
+def gather_records(engine, dst=0, group=None, temp_threshold=None):
     """Gather compact move records of all ranks (moves made so far) to `dst`.
     Returns (moves [W*G], actions [W*G, m], counts [W*G, m, A] int16/int32) on dst, None
-    elsewhere, and the bytes this rank sent."""
+    elsewhere, and the bytes this rank sent.  temp_threshold: see gather_record_tensors
+    (default: the engine's own)."""
     moves, actions, counts = engine_records(engine)
-    return gather_record_tensors(moves, actions, counts, dst, group, actions_per_move=engine.A)
+    tt = engine.cfg.temp_threshold if temp_threshold is None else temp_threshold
+    return gather_record_tensors(moves, actions, counts, dst, group, actions_per_move=engine.A, temp_threshold=tt)
 
 
 def group_src(group, rank):
@@ -72,30 +80,108 @@ def _gather(t, dst, group):
     return None
 
 
-def gather_record_tensors(moves, actions, counts, dst=0, group=None, actions_per_move=343):
+def _pad_to(t, n):
+    if t.shape[0] == n:
+        return t.contiguous()
+    out = t.new_zeros((n,) + tuple(t.shape[1:]))
+    out[:t.shape[0]] = t
+    return out
+
+
+def sparse_counts(moves, counts, rows):
+    """Encode the first `rows` moves of every game's root counts (rows past a game's
+    end are empty): (per-(game, move) number of visited actions int16 [G*rows],
+    pairs [nnz] int32 = action | count << 16, or [nnz, 2] int32 when a count exceeds
+    65535), in (game, move, action) order."""
+    G, _, A = counts.shape
+    sub = counts[:, :rows]
+    live = torch.arange(rows, device=counts.device)[None, :] < moves.to(torch.int64)[:, None]
+    sub = sub * live[:, :, None].to(sub.dtype)
+    nz = sub != 0
+    row_nnz = nz.sum(dim=2, dtype=torch.int32).reshape(-1).to(torch.int16)
+    act = nz.reshape(-1, A).nonzero()[:, 1].to(torch.int32)
+    val = sub[nz].to(torch.int32)
+    if val.numel() and int(val.max()) > 65535:
+        return row_nnz, torch.stack([act, val], dim=1)
+    return row_nnz, act | (val << 16)
+
+
+def dense_counts(row_nnz, pairs, G, rows, m, A, dtype):
+    """Inverse of sparse_counts: [G, m, A] counts, zero outside the encoded rows."""
+    out = torch.zeros((G, m, A), dtype=dtype, device=row_nnz.device)
+    n = row_nnz.to(torch.int64)
+    if pairs.shape[0]:
+        row = torch.repeat_interleave(torch.arange(G * rows, device=n.device), n)
+        if pairs.dim() == 2:
+            act, val = pairs[:, 0].to(torch.int64), pairs[:, 1]
+        else:
+            act, val = (pairs & 0xFFFF).to(torch.int64), (pairs >> 16) & 0xFFFF
+        out.view(G, m * A)[row // rows, (row % rows) * A + act] = val.to(dtype)
+    return out
+
+
+def gather_record_tensors(moves, actions, counts, dst=0, group=None, actions_per_move=343, temp_threshold=None):
     """gather_records on plain tensors (any device the group's backend serves).
-    Only `dst` allocates and receives the other ranks' records."""
+    Only `dst` allocates and receives the other ranks' records.
+
+    temp_threshold: the counts of a move are needed only if it was played at
+    temperature 1 (episodeStep < tempThreshold, Coach.py:68), so only the first
+    tempThreshold - 1 moves' counts are sent; the others arrive as zeros (their
+    examples' pi is the one-hot of the action).  None sends every move's counts.
+    Returns ((moves [W*G], actions [W*G, m] int32, counts [W*G, m, A] int16, or
+    int32 if a count exceeds 32767) on dst, None elsewhere; the bytes this rank sent)."""
     A = counts.shape[2] if counts is not None else int(actions_per_move)
-    m_local = torch.stack([torch.max(moves).to(torch.int64),
-                           (counts.max() if counts is not None and counts.numel() else moves.new_zeros(())).to(
-                               torch.int64)])
-    m_all = m_local.clone()
-    dist.all_reduce(m_all, op=dist.ReduceOp.MAX, group=group)
-    m, cmax = (int(x) for x in m_all.tolist())
-    ctype = torch.int16 if cmax <= 32767 else torch.int32
     G = moves.shape[0]
-    act = actions[:, :m].contiguous()
-    cnt = counts[:, :m].to(ctype).contiguous() if counts is not None else torch.zeros(
-        (G, m, A), dtype=ctype, device=moves.device)
-    mv = moves.contiguous()
+    dev = moves.device
+    m_loc = int(torch.max(moves)) if G else 0
+    rows_loc = m_loc if temp_threshold is None else min(m_loc, max(int(temp_threshold) - 1, 0))
+    if counts is not None:
+        row_nnz, pairs = sparse_counts(moves, counts[:, :m_loc], rows_loc)
+    else:
+        row_nnz = torch.zeros(G * rows_loc, dtype=torch.int16, device=dev)
+        pairs = torch.zeros(0, dtype=torch.int32, device=dev)
+    cmax = int(((pairs >> 16) & 0xFFFF).max()) if pairs.dim() == 1 and pairs.numel() else (
+        int(pairs[:, 1].max()) if pairs.numel() else 0)
+    hdr = torch.tensor([m_loc, cmax, pairs.shape[0], int(pairs.dim() == 2)], dtype=torch.int64, device=dev)
+    hmax = hdr.clone()
+    dist.all_reduce(hmax, op=dist.ReduceOp.MAX, group=group)
+    m, cmax, nnz_max, wide = (int(x) for x in hmax.tolist())
+    rows = m if temp_threshold is None else min(m, max(int(temp_threshold) - 1, 0))
+    if wide and pairs.dim() == 1:
+        pairs = torch.stack([pairs & 0xFFFF, (pairs >> 16) & 0xFFFF], dim=1)
+    # every rank pads to the group's max moves / rows / pairs so the gathers are equal-shaped
+    act = actions[:, :m]
+    if act.shape[1] < m:
+        act = torch.cat([act, act.new_zeros((G, m - act.shape[1]))], dim=1)
+    act16 = act.to(torch.int16).contiguous() if A <= 32767 else act.contiguous()
+    rn = row_nnz.reshape(G, rows_loc)
+    rn = torch.cat([rn, rn.new_zeros((G, rows - rows_loc))], dim=1).reshape(-1) if rows > rows_loc else row_nnz
+    pairs_p = _pad_to(pairs, nnz_max)
+    mv = moves.to(torch.int32).contiguous()
+    out_hdr = _gather(hdr, dst, group)
     out_mv = _gather(mv, dst, group)
-    out_act = _gather(act, dst, group)
-    # moved as raw bytes (RCCL/gloo have no int16 type)
-    out_cnt = _gather(cnt.view(torch.uint8), dst, group)
-    sent = mv.numel() * 4 + act.numel() * 4 + cnt.numel() * cnt.element_size()
-    if out_mv is not None:
-        return (out_mv.reshape(-1), out_act.reshape(-1, m), out_cnt.view(ctype).reshape(-1, m, A)), sent
-    return None, sent
+    out_act = _gather(act16.view(torch.uint8), dst, group)  # raw bytes: RCCL/gloo have no int16
+    out_rn = _gather(rn.contiguous().view(torch.uint8), dst, group)
+    out_pairs = _gather(pairs_p.view(torch.uint8), dst, group)
+    sent = (hdr.numel() * 8 + mv.numel() * 4 + act16.numel() * act16.element_size() + rn.numel() * 2
+            + pairs_p.numel() * 4)
+    if out_mv is None:
+        return None, sent
+    W = out_mv.shape[0]
+    ctype = torch.int16 if cmax <= 32767 else torch.int32
+    acts = out_act.view(act16.dtype).reshape(W * G, m).to(torch.int32)
+    cnts = torch.empty((W * G, m, A), dtype=ctype, device=out_mv.device)
+    ptype_rows = 2 if wide else 1
+    for r in range(W):
+        nnz_r = int(out_hdr[r, 2])
+        pr = out_pairs[r].view(torch.int32).reshape(nnz_max, ptype_rows) if wide else out_pairs[r].view(torch.int32)
+        cnts[r * G:(r + 1) * G] = dense_counts(out_rn[r].view(torch.int16), pr[:nnz_r], G, rows, m, A, ctype)
+    return (out_mv.reshape(-1), acts, cnts), sent
+
+
+def dense_record_bytes(G, m, A):
+    """Bytes the round-2 gather sent per rank: moves i32, actions i32, dense int16 counts."""
+    return G * 4 + G * m * 4 + G * m * A * 2
 
 
 def broadcast_weights(module, src=0, group=None):

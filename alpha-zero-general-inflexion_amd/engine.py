@@ -35,10 +35,70 @@ GAMES = {"inflexion": (_lib.GAME_INFLEXION, 4, lambda n: 7 * n * n),
          "othello": (_lib.GAME_OTHELLO, 2, lambda n: n * n + 1)}
 
 
+# Game plugin classes with native rules kernels (the Game.py:8-181 surface the engine
+# takes its state from), matched on the exact class -- never on a name substring or
+# by subclass, since a subclass may override the rules.  The reference's own
+# InflexionGame (inflexion/InflexionGame.py:40) is recognised by its qualified name
+# (the reference is not importable on the GPU box).  register_game() adds a plugin
+# whose rules a builder has restated as kernels.
+_REGISTRY = {}
+_REFERENCE_CLASSES = {("inflexion.InflexionGame", "InflexionGame"): "inflexion"}
+MAX_POWER_AT_SPAWN = 48  # InflexionGame.py:69 (read by the rules at :89, :95, :278)
+
+
+def register_game(cls, name):
+    """Map a Game plugin class to an engine game (a key of GAMES)."""
+    if name not in GAMES:
+        raise ValueError(f"unknown engine game {name!r}")
+    _REGISTRY[cls] = name
+
+
+def _registered(cls):
+    if not _REGISTRY:
+        from .inflexion import InflexionGame
+        from .othello import OthelloGame
+        register_game(InflexionGame, "inflexion")
+        register_game(OthelloGame, "othello")
+    name = _REGISTRY.get(cls)
+    if name is None:
+        name = _REFERENCE_CLASSES.get((cls.__module__, cls.__qualname__))
+    return name
+
+
 def game_spec(game):
-    """(name, n, max_turns) of a Game plugin instance (duck-typed)."""
-    name = "othello" if "othello" in type(game).__name__.lower() else "inflexion"
-    return name, int(game._n), int(getattr(game, "_max_turns", 0) or 0)
+    """(name, n, max_turns) of a Game plugin instance the engine has kernels for.
+
+    Raises AzgError for any other class (an unknown plugin, or a subclass of a
+    known one) and for parameters the rules kernels do not implement, instead of
+    running some other game's rules.  Accepted as the reference plays them:
+      * first_mover / the player to move: every quantity the engine returns is
+        relative to the player to move (to_planes own/opp, the valid mask, the
+        outcome, Coach.py:89's labels), and the drop-in MCTS takes the root's
+        player from the instance (azg_set_root), so BLUE-first games give the
+        reference's results (tests/test_gpu_dropin.py);
+      * InflexionGame's max_power: stored but never read by the reference rules,
+        whose power cap is the literal 6 (InflexionGame.py:66, :288), so any
+        value plays those rules, here as there."""
+    cls = type(game)
+    name = _registered(cls)
+    if name is None:
+        raise _lib.AzgError(f"no native rules for Game plugin {cls.__module__}.{cls.__qualname__}: "
+                            "the engine runs InflexionGame(7) and OthelloGame(6|8) "
+                            "(azg_amd.engine.register_game for a plugin with its own kernels)")
+    n = int(game._n)
+    if name == "inflexion":
+        if n != 7:
+            raise _lib.AzgError(f"InflexionGame({n}): the rules kernels are built for n = 7")
+        if int(getattr(game, "_max_power_at_spawn", MAX_POWER_AT_SPAWN)) != MAX_POWER_AT_SPAWN:
+            raise _lib.AzgError("InflexionGame with _max_power_at_spawn != 48 has no native rules")
+        max_turns = int(game._max_turns)
+        if max_turns < 1:
+            raise _lib.AzgError(f"InflexionGame max_turns {max_turns}: must be >= 1")
+    else:
+        if n not in (6, 8):
+            raise _lib.AzgError(f"OthelloGame({n}): the rules kernels are built for n = 6 and 8")
+        max_turns = int(getattr(game, "_max_turns", 0) or 0)
+    return name, n, max_turns
 
 
 def _ptr(t):
@@ -173,7 +233,7 @@ class SelfPlayEngine:
         """Raise FloatingPointError if the evaluator's split-fp16 GEMMs met an operand
         fp16 cannot hold since the last check (InferenceNet.check_range): its priors and
         values would be wrong, not just inexact.  play(), play_games(), the arena and the
-        drop-in MCTS call this; callers rerun with InferenceNet(gemm="f32")."""
+        drop-in MCTS call this; callers rerun with nnet.replay_form."""
         chk = getattr(self.evaluator, "check_range", None)
         if chk is not None:
             chk()

@@ -646,6 +646,16 @@ class InferenceNet(nn.Module):
         return torch.softmax(pv[:, :A], dim=1), torch.tanh(pv[:, A:])
 
 
+def replay_form(net):
+    """The evaluator self-play and the arena fall back to when the split-fp16 form
+    meets an operand fp16 cannot hold (InferenceNet.check_range): direct f32
+    convolutions (MIOpen; per-layer error ~6.5e-7 relative, profiles/r02_wino_layer_error.json)
+    and the f32 FC tail, not the f32-GEMM Winograd form, whose F(5,3)/F(4,3) tiles
+    carry the largest error of the three (1.6e-5 at conv3) -- the fallback runs for
+    exactly the large-activation networks where that would matter."""
+    return InferenceNet(net, conv="miopen", gemm="f32")
+
+
 class NNetWrapper:
     """Reference NNetWrapper surface (NNet.py:27-120) over InflexionNNet."""
 

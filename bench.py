@@ -22,6 +22,8 @@ per-iteration RCCL example gather + weight broadcast (configs[3]).
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -151,6 +153,15 @@ def parse():
     p.add_argument("--graph", action="store_true",
                    help="replay each move from a captured HIP graph (roofline fields then come from one extra "
                         "eager move after the timed region)")
+    p.add_argument("--cpu-procs", type=int, default=0,
+                   help="cpu_baseline: host cores to use (0 = the cores this process may run on, at most "
+                        f"{CPU_BASELINE_MAX_CORES})")
+    p.add_argument("--cpu-proc-moves", type=int, default=30,
+                   help="cpu_baseline's processes x 1 thread leg: first moves of one game per process")
+    # internal: one single-threaded cpu_baseline worker (a child process, never touches the GPU)
+    p.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
+    # internal: each rank prints its rendezvous env and exits before any GPU call (tests/test_bench_cpu.py)
+    p.add_argument("--print-rank-env", action="store_true", help=argparse.SUPPRESS)
     a = p.parse_args()
     if a.config:
         for k, v in PRESETS[a.config].items():
@@ -181,14 +192,27 @@ class Timer:
         return sum(s.elapsed_time(e) for s, e in self.pairs)
 
 
-def cpu_baseline(args, depth, A):
-    """Oracle (C restatement of the reference search) + the same f32 network on
-    the host's cores, batch-1 per leaf like NNetWrapper.predict -- the
-    reference CPU path's shape -- timed on a bounded sample of the workload."""
+# The GPU box gives one GPU's job 16 host cores (os.cpu_count() there shows the whole
+# machine's); the CPU baseline uses at most that many.
+CPU_BASELINE_MAX_CORES = 16
+
+
+def host_cores():
+    """Cores this process may run on (its affinity mask), and the machine's count."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return usable, os.cpu_count() or usable
+
+
+def _cpu_episode(args, depth, A, seed, max_moves, threads):
+    """One oracle episode (the C restatement of the reference search) whose leaves
+    are evaluated by the f32 InflexionNNet batch-1 on the CPU, like
+    NNetWrapper.predict (NNet.py:78-94): (expansions, seconds, moves)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as ol
     from azg_amd.nnet import InflexionNNet
-    threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     net = InflexionNNet(n=args.n, depth=depth, action_size=A).eval()
@@ -200,27 +224,114 @@ def cpu_baseline(args, depth, A):
         return torch.exp(pi)[0].numpy(), float(v[0, 0])
 
     t = time.perf_counter()
-    o = ol.episode(args.n, args.max_turns, args.sims, 1, 30, 0, evaluator=evaluator, max_moves=args.cpu_moves,
+    o = ol.episode(args.n, args.max_turns, args.sims, 1, 30, seed, evaluator=evaluator, max_moves=max_moves,
                    kind=kind)
-    dt = time.perf_counter() - t
+    return o["expansions"], time.perf_counter() - t, o["moves"]
+
+
+def cpu_worker(args):
+    """--cpu-worker SEED: one single-threaded episode sample, one JSON line on stdout."""
+    from azg_amd.engine import GAMES
+    _, depth, actions = GAMES[args.game]
+    exp, dt, moves = _cpu_episode(args, depth, actions(args.n), args.cpu_worker, args.cpu_proc_moves, 1)
+    print(json.dumps({"expansions": exp, "seconds": dt, "moves": min(moves, args.cpu_proc_moves)}), flush=True)
+
+
+def cpu_baseline(args, depth, A):
+    """The reference CPU path's shape on the host cores: the oracle's search with
+    the same f32 network evaluated batch-1 per leaf, timed on bounded samples of
+    the workload in the two arrangements BASELINE.md:20-22 measured for the
+    reference itself: one process using every core as torch threads, and one
+    single-threaded process per core running concurrently (the aggregate; the
+    reference's best CPU arrangement, 2.2x the first).  `value` is the larger.
+    The workers are child processes started with subprocess (fork + exec of a
+    fresh interpreter that never touches the GPU)."""
+    usable, machine = host_cores()
+    cores = max(1, min(args.cpu_procs or usable, usable, CPU_BASELINE_MAX_CORES))
+    exp1, dt1, moves1 = _cpu_episode(args, depth, A, 0, args.cpu_moves, cores)
+    one = exp1 / dt1
+    # the per-core processes: seeds 0..cores-1, the first cpu_proc_moves moves of each game
+    cmd = [sys.executable, os.path.abspath(__file__), "--game", args.game, "--n", str(args.n), "--sims",
+           str(args.sims), "--max-turns", str(args.max_turns), "--cpu-proc-moves", str(args.cpu_proc_moves)]
+    env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1", HIP_VISIBLE_DEVICES="",
+               CUDA_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    t = time.perf_counter()
+    procs = [subprocess.Popen(cmd + ["--cpu-worker", str(i)], stdout=subprocess.PIPE, env=env, cwd=ROOT)
+             for i in range(cores)]
+    outs = []
+    for p in procs:
+        so, _ = p.communicate(timeout=600)
+        if p.returncode != 0:
+            raise RuntimeError(f"cpu_baseline worker exited with {p.returncode}")
+        outs.append(json.loads(so.decode().strip().splitlines()[-1]))
+    wall = time.perf_counter() - t
+    exp_n = sum(o["expansions"] for o in outs)
+    slowest = max(o["seconds"] for o in outs)
+    agg = exp_n / slowest
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as ol
+    kind = ol.OTHELLO if args.game == "othello" else ol.INFLEXION
     t2 = time.perf_counter()
     o2 = ol.episode(args.n, args.max_turns, args.sims, 1, 30, 0, kind=kind)
     dt2 = time.perf_counter() - t2
-    return {"value": o["expansions"] / dt, "unit": "node-expansions/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ C MCTS + InflexionNNet f32 batch-1 on CPU ({threads} threads), {args.game} "
-                      f"{args.n}x{args.n}, seed 0, {o['moves']} moves x {args.sims} sims = {o['expansions']} "
-                      f"expansions in {dt:.1f}s",
+    best = "processes" if agg >= one else "threads"
+    return {"value": max(one, agg), "unit": "node-expansions/s", "cores": cores, "kind": "port",
+            "host_cpu_count": machine, "usable_cores": usable, "arrangement": best,
+            "one_process_value": one,
+            "one_process_sample": f"1 process x {cores} torch threads: oracle/ C MCTS + InflexionNNet f32 batch-1, "
+                                  f"{args.game} {args.n}x{args.n}, seed 0, {min(moves1, args.cpu_moves)} moves x "
+                                  f"{args.sims} sims = {exp1} expansions in {dt1:.1f}s",
+            "processes_value": agg,
+            "processes_sample": f"{cores} processes x 1 thread, concurrently: seeds 0..{cores - 1}, first "
+                                f"{args.cpu_proc_moves} moves each = {exp_n} expansions; slowest process "
+                                f"{slowest:.1f}s (all {wall:.1f}s wall incl. interpreter start)",
+            "sample": f"max of the two arrangements ({best}); see one_process_sample / processes_sample",
             "tree_only_value": o2["expansions"] / dt2,
             "tree_only_sample": f"same search, hash evaluator, 1 thread: {o2['expansions']} expansions in {dt2:.2f}s"}
 
 
+def rank_command(n, argv, port):
+    """torchrun command for --gpus N started without a launcher: N ranks on this
+    node, rendezvous on 127.0.0.1 (the driver's own form of the command)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` with no WORLD_SIZE in the environment: start the N ranks
+    as a child torchrun (before this process makes any GPU call; it never does) and
+    exit with its status.  Rank 0 prints the JSON line."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(rank_command(n, sys.argv[1:], _free_port()), env=env)
+
+
 def main():
     args = parse()
+    if args.cpu_worker is not None:
+        return cpu_worker(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.print_rank_env:
+        print(json.dumps({"rank": rank, "local_rank": local, "world_size": world, "gpus": args.gpus,
+                          "master_addr": os.environ.get("MASTER_ADDR")}), flush=True)
+        return 0
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
+    if world != args.gpus:
+        print(f"# bench: --gpus {args.gpus} but {world} rank(s) run; n_gpus reports {world}", file=sys.stderr)
     torch.cuda.set_device(local)
 
     import azg_amd
@@ -364,9 +475,11 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor([exp, sims_run], dtype=torch.float64, device="cuda")
+        c = torch.tensor([exp, sims_run, 1], dtype=torch.float64, device="cuda")
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         exp, sims_run = int(c[0].item()), int(c[1].item())
+        if int(c[2].item()) != world:  # every rank contributed its count: the ranks that ran
+            raise RuntimeError(f"{int(c[2].item())} ranks reported, world size {world}")
 
     if rank == 0:
         value = exp / elapsed
@@ -531,4 +644,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

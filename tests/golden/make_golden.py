@@ -19,8 +19,10 @@ Fixtures written (all small, gzip'd JSON or npz):
   rules_kat.npz          random playouts: board, turn, action, valid mask, outcome
   pairwise_kat.npz       numpy f32 pairwise .sum() known answers
   mcts_<set>.json.gz     Coach.executeEpisode + MCTS traces driven by stubnet
+  mcts_realnet_*.json.gz the same driven by the reference NNetWrapper (manual_seed 0 net)
   arena_<set>.json.gz    Arena.playGame MCTSPlayer(stubnet) vs Random/Greedy players
   nnet_golden.npz        InflexionNNet(manual_seed 0) checksum + (planes -> P, v)
+  train_golden.json.gz   NNetWrapper.train (32 channels, 2 epochs): losses + weight digests
 """
 import gzip
 import hashlib
@@ -152,11 +154,17 @@ def gen_pairwise(np):
 
 
 # -------------------------------------------------------------------------- MCTS
-def gen_mcts(np, quick, othello=False):
+def gen_mcts(np, quick, othello=False, realnet=False):
     """Reference Coach.executeEpisode + MCTS traces.  With othello=True the
     reference search is driven with this repo's builder-authored OthelloGame
     plugin (the reference has no Othello): the rules are ours, the search,
-    sampling and example construction are the reference's."""
+    sampling and example construction are the reference's.
+
+    With realnet=True the evaluator is the reference's own NNetWrapper
+    (inflexion/pytorch/NNet.py:78-94: batch-1 CPU f32 predict) over the
+    512-channel InflexionNNet built under torch.manual_seed(0) -- the network
+    nnet_golden.npz pins by checksum -- so the traces pin the production
+    evaluator's search, not just the hash stub's."""
     import MCTS as mcts_mod
     from Coach import Coach
     from inflexion.InflexionGame import InflexionGame
@@ -183,6 +191,18 @@ def gen_mcts(np, quick, othello=False):
         def predict(self, board):
             self.calls += 1
             return stub_eval(board, self.n_actions)
+
+    class CountingNNet(NNetWrapper):
+        """The reference NNetWrapper itself; only counts predict calls (expansions)."""
+        def __init__(self, game):
+            super().__init__(game)
+            self.calls = 0
+
+        def predict(self, board):
+            self.calls += 1
+            return super().predict(board)
+
+    real_nets = {}
 
     class Rec:
         in_search = False
@@ -231,6 +251,15 @@ def gen_mcts(np, quick, othello=False):
     }
     if quick:
         sets = {"short": sets["short"]}
+    if realnet:
+        sets = {
+            # main.py's configuration, whole episodes: every move's counts pinned
+            "realnet_main": dict(max_turns=343, sims=25, cpuct=1, temp_threshold=30, seeds=[0, 1, 2, 3]),
+            # C3's 100 simulations per move on 40-turn games
+            "realnet_sims100": dict(max_turns=40, sims=100, cpuct=1, temp_threshold=30, seeds=[10, 11]),
+        }
+        if quick:
+            sets = {"realnet_sims100": sets["realnet_sims100"]}
     if othello:
         sets = {
             "othello6": dict(n=6, sims=25, cpuct=1, temp_threshold=15, seeds=list(range(500, 516))),
@@ -242,7 +271,15 @@ def gen_mcts(np, quick, othello=False):
         t0 = time.time()
         for seed in cfg["seeds"]:
             game = GameCls(cfg["n"]) if othello else InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
-            nnet = StubNNet(game)
+            if realnet:
+                if "net" not in real_nets:
+                    import torch
+                    torch.manual_seed(0)  # the network of nnet_golden.npz (gen_nnet)
+                    real_nets["net"] = CountingNNet(game)
+                nnet = real_nets["net"]
+                nnet.calls = 0
+            else:
+                nnet = StubNNet(game)
             args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"],
                             "tempThreshold": cfg["temp_threshold"]})
             coach = Coach(game, nnet, args)
@@ -373,6 +410,96 @@ def gen_nnet(np, InflexionGame):
     print("wrote", path, os.path.getsize(path))
 
 
+# ------------------------------------------------------------------------- train
+TRAIN_CFG = dict(max_turns=30, sims=8, cpuct=1.0, temp_threshold=10, seed=3, num_channels=32, epochs=2,
+                 batch_seed=11, torch_seed=5, init_seed=0, proj_seed=99)
+
+
+def state_digest(np, sd, proj_seed):
+    """Per tensor of a state_dict: sha256 of its bytes, its f64 sum and 4 projections
+    on fixed standard-normal vectors (tolerance checks on another device)."""
+    rs = np.random.RandomState(proj_seed)
+    out = {}
+    for k, v in sd.items():
+        a = v.detach().cpu().contiguous().numpy()
+        f = a.astype(np.float64).ravel()
+        proj = (rs.standard_normal((4, f.size)) @ f).tolist() if f.size else [0.0] * 4
+        out[k] = {"sha256": hashlib.sha256(a.tobytes()).hexdigest(), "sum": float(f.sum()), "proj": proj,
+                  "absmax": float(np.abs(f).max()) if f.size else 0.0}
+    return out
+
+
+def gen_train(np):
+    """Reference NNetWrapper.train (inflexion/pytorch/NNet.py:36-76) on the examples of
+    one reference Coach.executeEpisode (stub evaluator), with NNet.args shrunk to 32
+    channels x 2 epochs (2 batches of 512 per epoch: 4 Adam steps): the weights after
+    training (digests) and every batch's (l_pi, l_v), with dropout 0.3 (the
+    reference's) and 0.0 (comparable across devices: dropout masks come from the
+    device's generator).  One torch thread, so the CPU arithmetic is reproducible."""
+    import torch
+    import MCTS as mcts_mod
+    from Coach import Coach
+    from inflexion.InflexionGame import InflexionGame
+    import inflexion.pytorch.NNet as nn_mod
+    from inflexion.pytorch.NNet import NNetWrapper
+    from utils import dotdict
+    from stubnet import stub_eval
+    torch.set_num_threads(1)
+    c = TRAIN_CFG
+
+    class StubNNet(NNetWrapper):
+        def __init__(self, game):
+            self.n_actions = game.max_actions
+
+        def predict(self, board):
+            return stub_eval(board, self.n_actions)
+
+    class RecNNet(NNetWrapper):
+        losses = []
+
+        def loss_pi(self, targets, outputs):
+            lp = super().loss_pi(targets, outputs)
+            self.losses.append([float(lp.item()), None])
+            return lp
+
+        def loss_v(self, targets, outputs):
+            lv = super().loss_v(targets, outputs)
+            self.losses[-1][1] = float(lv.item())
+            return lv
+
+    game = InflexionGame(7, max_turns=c["max_turns"], max_power=6)
+    args = dotdict({"numMCTSSims": c["sims"], "cpuct": c["cpuct"], "tempThreshold": c["temp_threshold"]})
+    stub = StubNNet(game)
+    np.random.seed(c["seed"])
+    ex = Coach(game, stub, args).executeEpisode((game.restarted(), mcts_mod.MCTS(stub, args)))
+    ex_pol = hashlib.sha256(np.array([e[1] for e in ex], np.float64).tobytes()).hexdigest()
+    ex_brd = hashlib.sha256(np.array([e[0] for e in ex], np.int64).tobytes()).hexdigest()
+    ex_z = hashlib.sha256(np.array([e[2] for e in ex], np.float64).tobytes()).hexdigest()
+    saved = dict(nn_mod.args)
+    out = {"config": c, "n_examples": len(ex), "examples_policy_sha256": ex_pol, "examples_board_sha256": ex_brd,
+           "examples_z_sha256": ex_z, "runs": {}}
+    try:
+        for name, dropout in (("dropout", 0.3), ("nodropout", 0.0)):
+            nn_mod.args.num_channels = c["num_channels"]
+            nn_mod.args.epochs = c["epochs"]
+            nn_mod.args.dropout = dropout
+            torch.manual_seed(c["init_seed"])
+            w = RecNNet(game)
+            init = state_digest(np, w.nnet.state_dict(), c["proj_seed"])
+            RecNNet.losses = []
+            np.random.seed(c["batch_seed"])
+            torch.manual_seed(c["torch_seed"])
+            w.train(ex)
+            out["runs"][name] = {"dropout": dropout, "init": init, "losses": RecNNet.losses,
+                                 "final": state_digest(np, w.nnet.state_dict(), c["proj_seed"]),
+                                 "rng_pos": int(np.random.get_state()[2])}
+            print(f"  train {name}: {len(RecNNet.losses)} steps, losses {RecNNet.losses}", flush=True)
+    finally:
+        nn_mod.args.clear()
+        nn_mod.args.update(saved)
+    _dump("train_golden.json.gz", out)
+
+
 def main():
     _need_reference()
     import numpy as np
@@ -388,7 +515,9 @@ def main():
         "nnet": lambda: gen_nnet(np, InflexionGame),
         "mcts": lambda: gen_mcts(np, quick),
         "othello": lambda: gen_mcts(np, quick, othello=True),
+        "realnet": lambda: gen_mcts(np, quick, realnet=True),
         "arena": lambda: gen_arena(np),
+        "train": lambda: gen_train(np),
     }
     for name, fn in jobs.items():
         if only and name not in only:

@@ -36,3 +36,41 @@ def test_presets_are_the_baseline_configs():
     assert bench.PRESETS["C4"] == dict(game="inflexion", n=7, games=4096, sims=25)
     assert bench.PRESETS["C2"]["games"] == 256 and bench.PRESETS["C3"]["sims"] == 100
     assert bench.PRESETS["C5"] == dict(game="othello", n=8, games=4096, sims=200)
+
+
+def test_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` with no launcher env starts 2 ranks (a child torchrun) with
+    RANK / LOCAL_RANK / WORLD_SIZE set; each rank stops before any GPU call here."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    out = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--print-rank-env"], env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert sorted((d["rank"], d["local_rank"], d["world_size"]) for d in lines) == [(0, 0, 2), (1, 1, 2)]
+    assert all(d["master_addr"] == "127.0.0.1" and d["gpus"] == 2 for d in lines)
+
+
+def test_rank_command_is_the_drivers_form():
+    cmd = bench.rank_command(8, ["--gpus", "8", "--steps", "3"], 29500)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr" in cmd and "127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"]
+
+
+def test_cpu_baseline_core_count():
+    usable, machine = bench.host_cores()
+    assert 1 <= usable <= machine
+
+
+def test_cpu_worker_runs_a_bounded_sample():
+    """One single-threaded cpu_baseline worker (what each of the per-core processes runs)."""
+    import json
+    import subprocess
+    out = subprocess.run([sys.executable, bench.__file__, "--cpu-worker", "3", "--cpu-proc-moves", "1"],
+                         capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["moves"] == 1 and 1 <= d["expansions"] <= 25 and d["seconds"] > 0

@@ -130,3 +130,69 @@ def test_rccl_single_rank_exchange():
     ok, sent, nb = q.get(timeout=300)
     p.join(timeout=60)
     assert p.exitcode == 0 and ok and sent > 0 and nb > 0
+
+
+def _overflow_worker(rank, world, port, q):
+    """rank 1's split-fp16 evaluator trips its range flag; every rank must
+    learn of it before the gather and replay together with the f32 form."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import azg_amd  # noqa: F401
+        from azg_amd.coach import Coach
+        from azg_amd.inflexion import InflexionGame
+        from azg_amd.nnet import InferenceNet, NNetWrapper, replay_form
+        torch.cuda.set_device(0)
+        game = InflexionGame(7, max_turns=8, max_power=6)
+        torch.manual_seed(0)
+        nnet = NNetWrapper(game, dict(num_channels=64), device="cuda")
+        args = Args(numEps=4, tempThreshold=5, maxlenOfQueue=10**6, numMCTSSims=3, cpuct=1)
+        c = Coach(game, nnet, args)
+        made = []
+
+        def evaluator(gemm="split"):
+            made.append(gemm)
+            if gemm == "f32":
+                return replay_form(nnet.nnet)
+            ev = InferenceNet(nnet.nnet, gemm=gemm)
+            if rank == 1:
+                ev.overflow.fill_(1)  # as the split GEMM's range check would
+            return ev
+        c.evaluator = evaluator
+        ex = c._selfplay_iteration(1, None)
+        res = {"made": made, "replayed": c.last_replayed_f32}
+        if rank == 0:
+            res["ex"] = (ex.planes.cpu().numpy(), ex.pis.cpu().numpy(), ex.vs.cpu().numpy())
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overflow_on_one_rank_replays_all_ranks():
+    import azg_amd  # noqa: F401
+    from azg_amd.engine import SelfPlayEngine
+    from azg_amd.examples import engine_examples
+    from azg_amd.nnet import NNetWrapper, replay_form
+    from azg_amd.inflexion import InflexionGame
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overflow_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0]["made"] == ["split", "f32"] and res[1]["made"] == ["split", "f32"]
+    assert res[0]["replayed"] and res[1]["replayed"]
+    # the gathered examples = one all-f32 engine over both ranks' 8 games
+    game = InflexionGame(7, max_turns=8, max_power=6)
+    torch.manual_seed(0)
+    nnet = NNetWrapper(game, dict(num_channels=64), device="cuda")
+    eng = SelfPlayEngine(8, sims=3, max_turns=8, temp_threshold=5, evaluator=replay_form(nnet.nnet))
+    eng.play()
+    ref = engine_examples(eng, 5, maxlen=10**6)
+    planes, pis, vs = res[0]["ex"]
+    assert (planes == ref.planes.cpu().numpy()).all() and (pis == ref.pis.cpu().numpy()).all()
+    assert (vs == ref.vs.cpu().numpy()).all()

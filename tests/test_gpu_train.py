@@ -1,0 +1,72 @@
+"""The trainer on the GPU against the REFERENCE trainer's fixture.
+
+Same fixture as tests/test_train_golden.py (reference NNetWrapper.train,
+inflexion/pytorch/NNet.py:36-76), its dropout-0 run: on the GPU the dropout
+masks would come from the device's generator, so only the mask-free run is
+comparable across devices.  GPU f32 kernels (MIOpen convolutions, hipBLASLt
+GEMMs) sum in other orders than the CPU's, so this is a tolerance test, and the
+tolerance follows the optimiser:
+
+  * the first two batches' losses (the initial weights' forward, and the forward
+    after one Adam step) within 2e-5 relative;
+  * every batch's losses within 2e-3 relative.  Adam divides each gradient by its
+    own running magnitude, so elements whose gradient is pure rounding noise take
+    full +-lr steps whose sign depends on the summation order: the biases of
+    conv1-4 and fc1-fc2 (a BatchNorm right after them cancels their gradient
+    exactly, InflexionNNet.py:39-52) and conv1's weights on the planes that are
+    constant per image.  Measured on MI355X: 1e-6 relative at step 2, 1e-3 at
+    step 4.  (On the CPU the trainer is bit-identical to the reference:
+    tests/test_train_golden.py.)
+  * the training update of the weight matrices whose gradient no BatchNorm
+    cancels (conv2-4, fc1-3; projected on the fixture's fixed random vectors)
+    within 5e-2 of its size (measured: <= 1e-2 after the 4 steps).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+
+
+def _proj(sd, proj_seed):
+    rs = np.random.RandomState(proj_seed)
+    out = {}
+    for k, v in sd.items():
+        f = v.detach().cpu().double().numpy().ravel()
+        out[k] = rs.standard_normal((4, f.size)) @ f if f.size else np.zeros(4)
+    return out
+
+
+@pytest.mark.parametrize("path", ["train", "train_examples"])
+def test_trainer_gpu_within_tolerance(path):
+    import azg_amd  # noqa: F401
+    from azg_amd.examples import ExampleSet
+    from azg_amd.nnet import NNetWrapper
+    from test_train_golden import golden, reference_examples
+
+    g = golden()
+    c, r = g["config"], g["runs"]["nodropout"]
+    game, ex = reference_examples(c)
+    torch.manual_seed(c["init_seed"])
+    w = NNetWrapper(game, dict(num_channels=c["num_channels"], epochs=c["epochs"], dropout=0.0), device="cuda")
+    init = _proj(w.nnet.state_dict(), c["proj_seed"])
+    for k in init:
+        np.testing.assert_allclose(init[k], r["init"][k]["proj"], rtol=0, atol=1e-9, err_msg=f"initial {k}")
+    np.random.seed(c["batch_seed"])
+    torch.manual_seed(c["torch_seed"])
+    if path == "train":
+        w.train(ex)
+    else:
+        losses = w.train_examples(ExampleSet.from_list(ex, "cuda")).cpu().numpy().astype(np.float64)
+    assert int(np.random.get_state()[2]) == r["rng_pos"]
+    if path == "train_examples":
+        np.testing.assert_allclose(losses[:2], np.array(r["losses"][:2]), rtol=2e-5)
+        np.testing.assert_allclose(losses, np.array(r["losses"]), rtol=2e-3)
+    # the trained weights moved by the reference's amount (the update's projection)
+    final = _proj(w.nnet.state_dict(), c["proj_seed"])
+    for k in ("conv2.weight", "conv3.weight", "conv4.weight", "fc1.weight", "fc2.weight", "fc3.weight"):
+        d_ref = np.array(r["final"][k]["proj"]) - np.array(r["init"][k]["proj"])
+        d_gpu = final[k] - init[k]
+        np.testing.assert_allclose(d_gpu, d_ref, rtol=5e-2, atol=5e-2 * float(np.abs(d_ref).max()), err_msg=k)
