@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/azg.h"
+#include "azg_ptr.h"
 
 namespace {
 
@@ -98,7 +99,7 @@ __global__ __launch_bounds__(256) void policy_value_kernel(const float* __restri
 
 extern "C" int azg_fc_act_split(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale,
                                 void* out, int32_t rows, int32_t n, int32_t relu, int32_t* overflow, void* stream) {
-    if (!m || !bias || !out || !overflow || rows <= 0 || n <= 0 || n % 4 || parts < 1 || part_stride % 4 ||
+    if (!m || !bias || !out || !azg_device_writable(overflow) || rows <= 0 || n <= 0 || n % 4 || parts < 1 || part_stride % 4 ||
         (parts > 1 && part_stride < (int64_t)rows * n) || ((uintptr_t)m & 15) || ((uintptr_t)bias & 15) ||
         ((uintptr_t)out & 7))
         return AZG_ERR_ARG;

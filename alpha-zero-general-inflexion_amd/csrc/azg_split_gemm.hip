@@ -1190,6 +1190,152 @@ __global__ __launch_bounds__(256, 1) void split_gemm_w4_kernel(SGArgs g) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Variant 19: variant 4 on 384 x 256 tiles.  The operand feed (global -> LDS by
+// LDS-DMA) sets variant 4's stage time, so the lever is operand bytes per flop:
+// a tile of M x N moves (M + N) 128 B per 32-channel stage for 3 * 2 M N 32 flop,
+// 1.5 M N / (M + N) flop per byte -- 192 at 256 x 256, 230 at 384 x 256 (+20%).
+// The accumulators bound the tile (f32 acc of 384 x 256 = 384 KB of the CU's
+// 512 KB register file): 8 waves (2 x 4) of 192 x 64, 12 x 4 accumulators of 16 x 16
+// = 192 registers per lane, which two waves per SIMD (256 registers each) only
+// hold if the A fragments are not all resident: a wave keeps the stage's 4 B
+// fragments (hi, lo: 32 registers) and streams its 12 A row blocks one ahead (2 x 8
+// registers), each read issued under the previous row block's 12 MFMAs.  Stage
+// buffers are 48 KB of A + 32 KB of B, two of them fill the 160 KB of LDS.  Each wave
+// issues 10 DMA pieces per stage (6 A, 4 B), one ahead of each of its first 10 row
+// blocks' MFMAs instead of in one burst.  Accumulators, MFMA order per accumulator
+// (stage by stage, hi.hi, lo.hi, hi.lo) and so every result are variant 4's.
+constexpr int S3_BM = 384;
+constexpr int S3_ATILEB = S3_BM * SG_ROWB;      // 48 KB
+constexpr int S3_STAGEB = S3_ATILEB + SG_TILEB;  // 80 KB
+
+__global__ __launch_bounds__(512, 1) void split_gemm_384_kernel(SGArgs g) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * S3_STAGEB];
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int C = g.C, K = g.K, C2 = 2 * C;
+
+    // this block's tiles: its XCD's contiguous range, strided by the XCD's block count (variant 4)
+    const int xcd = blockIdx.x % 8, kb = blockIdx.x / 8;
+    const int nblk = ((int)gridDim.x - xcd + 7) / 8;
+    const int q8 = g.total / 8, rr = g.total % 8;
+    const int start = xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8;
+    const int cnt = q8 + (xcd < rr ? 1 : 0);
+    if (kb >= cnt) return;
+
+    auto tile_of = [&](int L) {
+        SGTile t = sg_tile(g, L);
+        int r = 0;
+        while (r + 1 < g.nruns && L >= g.tile0[r + 1]) ++r;
+        t.m0 = ((L - g.tile0[r]) / g.ntn % g.mtiles[r]) * S3_BM;
+        return t;
+    };
+
+    // DMA geometry.  A: wave w fills tile rows 48 w + 8 i + lane / 8 (i < 6); the
+    // chunk swizzle (row >> 1) & 7 depends on i's parity only, so two lane offsets
+    // serve the six pieces, with descriptors based 0 / 16 / 32 rows on (range check
+    // on the row: rows past T load zeros).  B as variant 4: rows 32 w + 8 i + lane / 8.
+    // The lane offsets are formed once per tile (4 registers: the accumulators leave
+    // few); the swizzled chunk is that of both operands' rows: (4 i + lane / 16) & 7.
+    const int wm = wid >> 2, wn = wid & 3;
+    const int lr = lane & 15, ch = lane >> 4;
+    // fragment rows: the lo chunk of a row is its hi chunk ^ 4 (ch < 4), i.e. byte ^ 64
+    const int a_hi = (wm * 192 + lr) * SG_ROWB + 16 * (ch ^ (lr >> 1));
+    const int b_hi = S3_ATILEB + (wn * 64 + lr) * SG_ROWB + 16 * (ch ^ (lr >> 1));
+    int aoff[2], boff[2];
+    auto tile_offsets = [&](const SGTile& t) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int R = 8 * i + (lane >> 3);
+            const int col = 8 * ((lane & 7) ^ ((R >> 1) & 7));
+            aoff[i] = ((t.m0 + 48 * wid + R) * C2 + col) * 2;
+            boff[i] = ((t.n0 + b_col(32 * wid + R)) * C2 + col) * 2;
+        }
+    };
+
+    // DMA piece p (< 6: A row group p, else B row group p - 6) of stage ks of tile t
+    // (offsets of that tile in aoff / boff)
+    auto piece = [&](const SGTile& t, int ks, int buf, int p) {
+        char* base = smem + buf * S3_STAGEB;
+        if (p < 6) {
+            const int d = p >> 1;  // descriptor: rows 16 d on
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(t.Ae + 16 * d * C2), 0, (t.T - 16 * d > 0 ? t.T - 16 * d : 0) * C2 * 2, 0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void*)(base + (48 * wid + 8 * p) * SG_ROWB), 16,
+                aoff[p & 1], ks * SG_STAGE_SOFF, 0, 0);
+        } else {
+            const int q = p - 6, d = q >> 1;  // descriptor: one column row on for q >= 2
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(t.Be + d * C2), 0, (K - d) * C2 * 2,
+                                                              0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void*)(base + S3_ATILEB + (32 * wid + 8 * q) * SG_ROWB), 16,
+                boff[q & 1], ks * SG_STAGE_SOFF, 0, 0);
+        }
+    };
+
+    const int nks = C / SG_BK;  // even: every tile starts in buffer 0
+    SGTile cur = tile_of(start + kb);
+    tile_offsets(cur);
+#pragma unroll
+    for (int p = 0; p < 10; ++p) piece(cur, 0, 0, p);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    f32x4 acc[12][4];
+    for (int it = kb;;) {
+        const int nx = it + nblk;
+        const bool more = nx < cnt;
+        const SGTile nxt = tile_of(start + (more ? nx : it));
+#pragma unroll
+        for (int i = 0; i < 12; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < nks; ++ks) {
+            const char* st = smem + (ks & 1) * S3_STAGEB;
+            const bool has_next = ks + 1 < nks || more;
+            const SGTile& dt = ks + 1 < nks ? cur : nxt;
+            const int dks = ks + 1 < nks ? ks + 1 : 0, dbuf = (ks + 1) & 1;
+            if (ks + 1 == nks && more) tile_offsets(nxt);  // the next tile's stage 0 goes out now
+            f16x8 bh[4], bl[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bh[j] = *(const f16x8*)(st + b_hi + 16 * j * SG_ROWB);
+                bl[j] = *(const f16x8*)(st + (b_hi ^ 64) + 16 * j * SG_ROWB);
+            }
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+                // one A fragment pair in flight: the partner wave of the SIMD covers its latency
+                const f16x8 ah = *(const f16x8*)(st + a_hi + 16 * i * SG_ROWB);
+                const f16x8 al = *(const f16x8*)(st + (a_hi ^ 64) + 16 * i * SG_ROWB);
+                if (i < 10 && has_next) piece(dt, dks, dbuf, i);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        // epilogue: rows 4 ch + q of each row block, 4 adjacent columns per lane (b_col)
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = cur.m0 + wm * 192 + 16 * i + 4 * ch + q;
+                if (row < cur.T)
+                    *(f32x4*)(cur.Me + (long long)row * K + cur.n0 + wn * 64 + 4 * lr) =
+                        f32x4{acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]};
+            }
+        }
+        if (!more) break;
+        it = nx;
+        cur = nxt;
+    }
+}
+
 }  // namespace
 
 // one workgroup per CU (a block fills a CU: 128 KB of LDS), at most one per tile
@@ -1209,9 +1355,9 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
                              unsigned long long* stamps = nullptr) {
     if (!A || !Bt || !M || !points || !rows || nruns < 1 || nruns > SG_MAXRUNS || c <= 0 || c % (2 * SG_BK) ||
         k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
-        variant > 18 || variant == 9 || variant == 13 || variant == 14 || (variant == 10) != (stamps != nullptr))
+        variant > 19 || variant == 9 || variant == 13 || variant == 14 || (variant == 10) != (stamps != nullptr))
         return AZG_ERR_ARG;
-    const int bm = variant == 17 ? 128 : variant == 18 ? 64 : SG_BM;
+    const int bm = variant == 17 ? 128 : variant == 18 ? 64 : variant == 19 ? S3_BM : SG_BM;
     SGArgs g{};
     g.A = (const _Float16*)A;
     g.Bt = (const _Float16*)Bt;
@@ -1280,6 +1426,8 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
     else if (variant == 10)
         hipLaunchKernelGGL((split_gemm_persist_kernel<8, false, false, false, true>), dim3(persistent_blocks(tiles)),
                            dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 19)
+        hipLaunchKernelGGL(split_gemm_384_kernel, dim3(persistent_blocks(tiles)), dim3(512), 0, (hipStream_t)stream, g);
     else
         hipLaunchKernelGGL(split_gemm_w4_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, g);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;

@@ -52,6 +52,7 @@
 #include <utility>
 
 #include "../../include/azg.h"
+#include "azg_ptr.h"
 
 namespace {
 
@@ -727,6 +728,7 @@ inline int launch_out(int vfmt, const float* M, const float* bias, void* y, int 
 }
 
 inline bool bad_fmt(int vfmt, const int* overflow) {
-    return !(vfmt == AZG_WINO_F32 || ((vfmt == AZG_WINO_SPLIT || vfmt == AZG_WINO_SPLIT2) && overflow));
+    return !(vfmt == AZG_WINO_F32 ||
+             ((vfmt == AZG_WINO_SPLIT || vfmt == AZG_WINO_SPLIT2) && azg_device_writable(overflow)));
 }
 }  // namespace

@@ -318,8 +318,10 @@ class InferenceNet(nn.Module):
             self.register_buffer("fw2_s", torch.cat([whi, whi, wlo], dim=1).contiguous())
             whi, wlo, self.fc34_scale = _split_u(self.fw34.t().unsqueeze(0))
             self.register_buffer("fw34_s", torch.cat([whi, whi, wlo], dim=1).contiguous())
-        # sticky device flag: a split-GEMM operand fp16 could not hold (checked by check_range)
-        self.register_buffer("overflow", torch.zeros(1, dtype=torch.int32))
+        # sticky device flag: a split-GEMM operand fp16 could not hold (checked by check_range).
+        # It lives where the kernels run: the transforms set it with a device atomic, so a
+        # host-memory flag would fault the GPU the first time an operand overflowed.
+        self.register_buffer("overflow", torch.zeros(1, dtype=torch.int32, device=self.w1.device))
 
     def set_winograd_layer(self, i, w, h_out):
         """Replace conv i's Winograd weights by w [K][C][3][3] (BN already folded) for an
@@ -395,7 +397,15 @@ class InferenceNet(nn.Module):
         """(azg.h AZG_WINO_* format of V, overflow flag pointer)."""
         if self.gemm == "f32":
             return 0, None
-        return (2 if self.gemm == "split" else 1), self.overflow.data_ptr()
+        return (2 if self.gemm == "split" else 1), self._overflow_ptr()
+
+    def _overflow_ptr(self):
+        """Device address of the range flag, on the device of the weights the kernels read."""
+        if self.overflow.device != self.w1.device:
+            self.overflow = self.overflow.to(self.w1.device)
+        if not self.overflow.is_cuda:
+            raise RuntimeError("InferenceNet's kernels need its weights on the GPU")
+        return self.overflow.data_ptr()
 
     def _first_winograd(self, s):
         """conv1 + bias + ReLU + conv2's Winograd input transform straight from the NCHW
@@ -496,7 +506,7 @@ class InferenceNet(nn.Module):
             self._khook("transform", i, "start")
             _lib.check(L.azg_winograd_out_split(M, bias, ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, mscale,
                                                 2 if kp else 1, max(kp, 1),
-                                                ctypes.c_void_p(self.overflow.data_ptr()), s))
+                                                ctypes.c_void_p(self._overflow_ptr()), s))
             self._khook("transform", i, "stop")
             return y
         y = torch.empty((B, K, Ho, Ho), device=dev, dtype=torch.float32, memory_format=torch.channels_last)
@@ -541,7 +551,7 @@ class InferenceNet(nn.Module):
         L = _lib.lib()
         B, dev = a.shape[0], a.device
         st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        ovf = ctypes.c_void_p(self.overflow.data_ptr())
+        ovf = ctypes.c_void_p(self._overflow_ptr())
         for layer, (w, b, scale) in enumerate(((self.fw1_s, self.fb1, self.fc1_scale),
                                                (self.fw2_s, self.fb2, self.fc2_scale))):
             n = w.shape[2]

@@ -584,7 +584,7 @@ def main():
             "iteration_sync_bytes": sync_bytes,
         }
         # the dominant kernel: libazg's split GEMM (over half of the step's GPU time), its
-        # launches timed with HIP events on their stream; algorithmic FLOPs = the GEMM work
+        # launches timed with HIP events on their stream; executed MFMA FLOPs = the GEMM work
         # (Winograd: transformed points x 2 C K per leaf; fc1: 2 x 4608 x 1024 per leaf) x 3
         # fp16 products, as InferenceNet reports it per launch
         g_pairs, t_pairs = t_kern["gemm"].pairs, t_kern["transform"].pairs
@@ -602,6 +602,12 @@ def main():
                                            "128-row tiles for short layers)",
                 "achieved": ach, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TF,
                 "traffic": None, "mfma_dtype": "fp16 (split, 3 products per f32 multiply-add, f32 accumulation)",
+                "flops_kind": "executed fp16 MFMA FLOPs: each f32 multiply-add of the Winograd GEMMs (already 3.8x "
+                              "fewer than the direct convolution's) runs as 3 fp16 products, hi.hi + lo.hi + hi.lo",
+                # the same launches as f32 work (one multiply-add per product of the f32 GEMM),
+                # against the f32 matrix peak -- a frac above 1 is work no f32 GEMM on this chip could do as fast
+                "f32_equivalent": {"achieved": ach / 3, "peak": F32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                                   "frac": ach / 3 / F32_MFMA_PEAK_TF},
                 "avg_launch_us": g_ms / n_launch * 1e3, "launches": n_launch,
                 "per_launch": f"{kflops['gemm'] / n_forwards / 1e9:.1f} GFLOP per forward ({leaves} leaves; 3 fp16 "
                               f"products) / {per_fwd:.0f} calls = {flops_launch / 1e9:.1f} GFLOP per call (avg "

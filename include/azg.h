@@ -174,7 +174,8 @@ int  azg_conv3x3_variant(int variant, const float* x, const float* wt, const flo
  * c % 32 == 0; the A operand of azg_split_gemm); AZG_WINO_SPLIT fp16 rows of 3c =
  * [hi | lo | hi], hi = fp16(v), lo = fp16(v - hi) -- the A operand of the
  * error-compensated GEMM [hi|lo|hi] x [Uh; Uh; Ul] (f32 accumulation); a value
- * fp16 cannot hold (|v| > 65504, NaN) sets *overflow (device int, required).
+ * fp16 cannot hold (|v| > 65504, NaN) sets *overflow (device int, required: a
+ * host pointer is rejected with AZG_ERR_ARG, the kernels set it with a device atomic).
  * c % 4 == 0, k % 4 == 0, 16-B aligned pointers, h_out <= 64. */
 enum { AZG_WINO_F32 = 0, AZG_WINO_SPLIT = 1, AZG_WINO_SPLIT2 = 2 };
 int  azg_winograd_layout(int32_t h_out, int32_t* seq, int32_t* groups);

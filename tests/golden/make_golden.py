@@ -23,6 +23,8 @@ Fixtures written (all small, gzip'd JSON or npz):
   arena_<set>.json.gz    Arena.playGame MCTSPlayer(stubnet) vs Random/Greedy players
   nnet_golden.npz        InflexionNNet(manual_seed 0) checksum + (planes -> P, v)
   train_golden.json.gz   NNetWrapper.train (32 channels, 2 epochs): losses + weight digests
+  realnet_sensitivity.json.gz  first divergent move of the reference's real-net traces under 1e-7 / 1e-6
+                         relative perturbations of its network outputs
 """
 import gzip
 import hashlib
@@ -410,6 +412,71 @@ def gen_nnet(np, InflexionGame):
     print("wrote", path, os.path.getsize(path))
 
 
+# --------------------------------------------------------------- realnet sensitivity
+def gen_realnet_sensitivity(np):
+    """How far do the reference's own real-network traces survive a perturbation of
+    its network outputs far below the north_star's 1e-5 tolerance?  The reference
+    Coach/MCTS (main.py's configuration, the seeds of mcts_realnet_main) is rerun
+    with NNetWrapper.predict's P and v multiplied by (1 + eps u), u ~ U(-1, 1) drawn
+    from a RandomState keyed on the planes (a deterministic, equally valid f32-level
+    evaluation; numpy's global stream is untouched), and each move's visit counts
+    are compared with the unperturbed trace.  Records the first move whose counts
+    differ, per seed and eps: the scale at which whole-game visit counts are a
+    property of the last bits of the network's arithmetic, not of the search."""
+    import torch
+    import MCTS as mcts_mod
+    from Coach import Coach
+    from inflexion.InflexionGame import InflexionGame
+    from inflexion.pytorch.NNet import NNetWrapper
+    from utils import dotdict
+    base = json.load(gzip.open(os.path.join(HERE, "mcts_realnet_main.json.gz"), "rt"))
+    cfg = base["config"]
+
+    class NoisyNNet(NNetWrapper):
+        eps = 0.0
+
+        def predict(self, board):
+            p, v = super().predict(board)
+            rs = np.random.RandomState(int.from_bytes(hashlib.sha256(board.tobytes()).digest()[:4], "little"))
+            u = rs.uniform(-1.0, 1.0, size=p.shape[0] + 1)
+            p = (p.astype(np.float64) * (1.0 + self.eps * u[:-1])).astype(np.float32)
+            v = (v.astype(np.float64) * (1.0 + self.eps * u[-1])).astype(np.float32)
+            return p, v
+
+    class RecMCTS(mcts_mod.MCTS):
+        counts = None
+
+        def getActionProb(self, game, temp=1):
+            probs = super().getActionProb(game, temp)
+            s = game.to_planes().tobytes()
+            self.counts.append({a: int(self.Nsa[(s, a)]) for a in range(game.max_actions) if (s, a) in self.Nsa})
+            return probs
+
+    torch.manual_seed(0)
+    game0 = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
+    net = NoisyNNet(game0)
+    out = {"config": cfg, "runs": []}
+    for eps in (1e-7, 1e-6):
+        for ep in base["episodes"]:
+            NoisyNNet.eps = eps
+            args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"], "tempThreshold": cfg["temp_threshold"]})
+            mcts = RecMCTS(net, args)
+            mcts.counts = []
+            np.random.seed(ep["seed"])
+            Coach(game0, net, args).executeEpisode((game0.restarted(), mcts))
+            first = None
+            for m, (mine, ref) in enumerate(zip(mcts.counts, ep["moves"])):
+                if mine != {a: c for a, c in ref["counts"]}:
+                    first = m
+                    break
+            if first is None and len(mcts.counts) != ep["n_moves"]:
+                first = min(len(mcts.counts), ep["n_moves"])
+            out["runs"].append({"eps": eps, "seed": ep["seed"], "first_divergent_move": first,
+                                "moves": len(mcts.counts), "reference_moves": ep["n_moves"]})
+            print(f"  eps {eps:g} seed {ep['seed']}: first divergent move {first}", flush=True)
+    _dump("realnet_sensitivity.json.gz", out)
+
+
 # ------------------------------------------------------------------------- train
 TRAIN_CFG = dict(max_turns=30, sims=8, cpuct=1.0, temp_threshold=10, seed=3, num_channels=32, epochs=2,
                  batch_seed=11, torch_seed=5, init_seed=0, proj_seed=99)
@@ -518,6 +585,7 @@ def main():
         "realnet": lambda: gen_mcts(np, quick, realnet=True),
         "arena": lambda: gen_arena(np),
         "train": lambda: gen_train(np),
+        "sensitivity": lambda: gen_realnet_sensitivity(np),
     }
     for name, fn in jobs.items():
         if only and name not in only:

@@ -201,10 +201,11 @@ def test_split_gemm_error_not_above_f32():
     assert errs["split_blas"] <= 1.5 * errs["f32"], errs
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 8, 11, 12, 17, 18])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 8, 11, 12, 17, 18, 19])
 @pytest.mark.parametrize("runs,C,K", [([(25, 4096)], 512, 512), ([(3, 300), (5, 37), (2, 513)], 512, 512),
                                       ([(1, 1)], 512, 512), ([(2, 77), (1, 256)], 64, 256),
-                                      ([(4, 129)], 128, 768), ([(17, 4000)], 64, 512), ([(11, 3000)], 64, 512)])
+                                      ([(4, 129)], 128, 768), ([(17, 4000)], 64, 512), ([(11, 3000)], 64, 512),
+                                      ([(3, 385), (2, 768), (1, 383)], 64, 512)])
 def test_split_gemm_kernel_matches_reference(variant, runs, C, K):
     """libazg azg_split_gemm (hand-written fp16 MFMA, LDS-DMA): M = Ah.Bh + Al.Bh + Ah.Bl
     for every point of every run, against the same products in f64 (ragged row counts,
@@ -222,11 +223,20 @@ def test_split_gemm_default_schedule_matches_reference(runs, C, K):
     _check_split_gemm(None, runs, C, K)
 
 
-def _check_split_gemm(variant, runs, C, K):
+@pytest.mark.parametrize("runs,C,K", [([(121, 4096)], 512, 512), ([(4, 4096)], 1152, 1024),
+                                      ([(3, 385), (2, 768), (1, 383)], 64, 512)])
+def test_split_gemm_384_rows_bit_equal_to_256_rows(runs, C, K):
+    """Variant 19 (384 x 256 tiles) runs every accumulator's MFMAs in variant 4's order
+    (stage by stage, hi.hi, lo.hi, hi.lo): the same bits, so a schedule pick between
+    the two never changes the network's outputs."""
+    outs = [_run_split_gemm(v, runs, C, K)[2] for v in (4, 19)]
+    assert torch.equal(outs[0], outs[1])
+
+
+def _run_split_gemm(variant, runs, C, K):
     import ctypes
     import azg_amd  # noqa: F401
     from azg_amd import _lib
-    from azg_amd.nnet import split2_halves
     torch.manual_seed(7)
     P = sum(p for p, _ in runs)
     A = torch.cat([torch.randn(p * t, 2 * C, device="cuda").half() for p, t in runs]).contiguous()
@@ -241,6 +251,12 @@ def _check_split_gemm(variant, runs, C, K):
     else:
         _lib.check(_lib.lib().azg_split_gemm_variant(variant, *ptrs))
     torch.cuda.synchronize()
+    return A, Bt, M
+
+
+def _check_split_gemm(variant, runs, C, K):
+    from azg_amd.nnet import split2_halves
+    A, Bt, M = _run_split_gemm(variant, runs, C, K)
     a_row = m_row = pt = 0
     for p, t in runs:
         a = A[a_row:a_row + p * t].view(p, t, 2 * C).double()
