@@ -78,7 +78,11 @@ SIGNATURES = [
     ("azg_split_gemm", ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
     ("azg_fc_act_split", ctypes.c_int, [_VP, _I32, _I64, _VP, ctypes.c_float, _VP, _I32, _I32, _I32, _VP, _VP]),
     ("azg_policy_value", ctypes.c_int, [_VP, _I32, _VP, ctypes.c_float, _VP, _VP, _I32, _I32, _VP]),
+    ("azg_fc_act", ctypes.c_int, [_VP, _I32, _I64, _VP, ctypes.c_float, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
+    ("azg_policy_value_parts", ctypes.c_int, [_VP, _I32, _I64, _I32, _VP, ctypes.c_float, _VP, _VP, _I32, _I32,
+                                              _VP]),
     ("azg_split_gemm_variant", ctypes.c_int, [_I32, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
+    ("azg_split_gemm_pick", ctypes.c_int, [_I32, _VP, _VP, _I32]),
     ("azg_split_gemm_stamps", ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP, _I64, _VP]),
     ("azg_set_arena", ctypes.c_int, [_VP, _VP, _VP, _VP]),
     ("azg_opponent_move", ctypes.c_int, [_VP, _I32, _VP]),

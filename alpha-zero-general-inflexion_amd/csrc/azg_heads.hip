@@ -15,6 +15,13 @@
 //    NNet.py:94) and v = tanh(bias[A] + scale * m[:, A]) from the stacked fc3 | fc4
 //    GEMM, one wave per leaf (max and sum as __shfl_xor butterflies), written in the
 //    [G, A] / [G] layout azg_sim_end reads.
+//
+// With fc2 and [fc3 | fc4] on libazg's split GEMM too (azg_fc_act with AZG_WINO_SPLIT2
+// output, azg_policy_value_parts), no library GEMM is left in the 4096-leaf forward:
+// fc_act writes the next layer's A operand as out_parts K-parts of 32-channel
+// [hi(32) | lo(32)] blocks ([part][rows][2 n / out_parts] fp16, the split GEMM's
+// operand layout, AZG_WINO_SPLIT2), the next split-K GEMM's parts being its "points";
+// policy_value sums that GEMM's parts in order before the softmax / tanh.
 #include <hip/hip_runtime.h>
 
 #include "../../include/azg.h"
@@ -22,10 +29,11 @@
 
 namespace {
 
+template <int FMT>
 __global__ __launch_bounds__(256) void fc_act_split_kernel(const float4* __restrict__ m, int parts,
                                                            long long pstride4, const float4* __restrict__ bias,
                                                            float scale, ushort4* __restrict__ out, long long rows,
-                                                           int n4, int relu, int* overflow) {
+                                                           int n4, int relu, int out_parts, int* overflow) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= rows * n4) return;
     const long long r = i / n4;
@@ -48,21 +56,31 @@ __global__ __launch_bounds__(256) void fc_act_split_kernel(const float4* __restr
         lo[j] = __builtin_bit_cast(unsigned short, l);
         bad |= !(fabsf(y[j]) <= 65504.f);
     }
-    ushort4* row = out + r * 3 * n4;
     const ushort4 H = {hi[0], hi[1], hi[2], hi[3]}, L = {lo[0], lo[1], lo[2], lo[3]};
-    row[c4] = H;
-    row[n4 + c4] = L;
-    row[2 * n4 + c4] = H;
+    if constexpr (FMT == AZG_WINO_SPLIT) {
+        ushort4* row = out + r * 3 * n4;
+        row[c4] = H;
+        row[n4 + c4] = L;
+        row[2 * n4 + c4] = H;
+    } else {
+        // column c = 4 c4 of part p = c / np: block (c % np) / 32 of its row, hi at
+        // 64 block + c % 32 halves, lo 32 halves on (np = n / out_parts columns per part)
+        const int np4 = n4 / out_parts, p = c4 / np4, cc4 = c4 - p * np4;
+        ushort4* row = out + ((long long)p * rows + r) * 2 * np4;
+        const int q = (cc4 >> 3) * 16 + (cc4 & 7);  // in ushort4 units: 16 per 64-half block
+        row[q] = H;
+        row[q + 8] = L;
+    }
     if (bad) atomicOr(overflow, 1);
 }
 
 constexpr int PV_MAX_PER_LANE = 16;  // up to 1024 actions per leaf (9x9 Inflexion: 567)
 
 template <int PV_PER_LANE>
-__global__ __launch_bounds__(256) void policy_value_kernel(const float* __restrict__ m, int ldm,
-                                                           const float* __restrict__ bias, float scale,
-                                                           float* __restrict__ P, float* __restrict__ v, int rows,
-                                                           int A) {
+__global__ __launch_bounds__(256) void policy_value_kernel(const float* __restrict__ m, int ldm, int parts,
+                                                           long long pstride, const float* __restrict__ bias,
+                                                           float scale, float* __restrict__ P,
+                                                           float* __restrict__ v, int rows, int A) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= rows) return;  // wave-uniform
@@ -72,7 +90,12 @@ __global__ __launch_bounds__(256) void policy_value_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < PV_PER_LANE; ++j) {
         const int a = lane + 64 * j;
-        x[j] = a < A ? bias[a] + scale * mr[a] : -INFINITY;
+        float t = 0.f;
+        if (a < A) {
+            t = mr[a];
+            for (int p = 1; p < parts; ++p) t += mr[p * pstride + a];  // split-K parts, in order
+        }
+        x[j] = a < A ? bias[a] + scale * t : -INFINITY;
         mx = fmaxf(mx, x[j]);
     }
 #pragma unroll
@@ -92,34 +115,59 @@ __global__ __launch_bounds__(256) void policy_value_kernel(const float* __restri
         const int a = lane + 64 * j;
         if (a < A) pr[a] = x[j] * inv;
     }
-    if (lane == 0) v[r] = tanhf(bias[A] + scale * mr[A]);
+    if (lane == 0) {
+        float t = mr[A];
+        for (int p = 1; p < parts; ++p) t += mr[p * pstride + A];
+        v[r] = tanhf(bias[A] + scale * t);
+    }
 }
 
 }  // namespace
 
-extern "C" int azg_fc_act_split(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale,
-                                void* out, int32_t rows, int32_t n, int32_t relu, int32_t* overflow, void* stream) {
-    if (!m || !bias || !out || !azg_device_writable(overflow) || rows <= 0 || n <= 0 || n % 4 || parts < 1 || part_stride % 4 ||
-        (parts > 1 && part_stride < (int64_t)rows * n) || ((uintptr_t)m & 15) || ((uintptr_t)bias & 15) ||
-        ((uintptr_t)out & 7))
+extern "C" int azg_fc_act(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale,
+                          void* out, int32_t rows, int32_t n, int32_t relu, int32_t fmt, int32_t out_parts,
+                          int32_t* overflow, void* stream) {
+    if (!m || !bias || !out || !azg_device_writable(overflow) || rows <= 0 || n <= 0 || n % 4 || parts < 1 ||
+        part_stride % 4 || (parts > 1 && part_stride < (int64_t)rows * n) || ((uintptr_t)m & 15) ||
+        ((uintptr_t)bias & 15) || ((uintptr_t)out & 7) || (fmt != AZG_WINO_SPLIT && fmt != AZG_WINO_SPLIT2) ||
+        (fmt == AZG_WINO_SPLIT && out_parts != 1) ||
+        (fmt == AZG_WINO_SPLIT2 && (out_parts < 1 || n % out_parts || (n / out_parts) % 32)))
         return AZG_ERR_ARG;
     const long long items = (long long)rows * (n / 4);
-    hipLaunchKernelGGL(fc_act_split_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       (const float4*)m, parts, (long long)(part_stride / 4), (const float4*)bias, scale,
-                       (ushort4*)out, (long long)rows, n / 4, relu, overflow);
+    const dim3 grid((unsigned)((items + 255) / 256));
+    if (fmt == AZG_WINO_SPLIT)
+        hipLaunchKernelGGL(fc_act_split_kernel<AZG_WINO_SPLIT>, grid, dim3(256), 0, (hipStream_t)stream,
+                           (const float4*)m, parts, (long long)(part_stride / 4), (const float4*)bias, scale,
+                           (ushort4*)out, (long long)rows, n / 4, relu, 1, overflow);
+    else
+        hipLaunchKernelGGL(fc_act_split_kernel<AZG_WINO_SPLIT2>, grid, dim3(256), 0, (hipStream_t)stream,
+                           (const float4*)m, parts, (long long)(part_stride / 4), (const float4*)bias, scale,
+                           (ushort4*)out, (long long)rows, n / 4, relu, out_parts, overflow);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+extern "C" int azg_fc_act_split(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale,
+                                void* out, int32_t rows, int32_t n, int32_t relu, int32_t* overflow, void* stream) {
+    return azg_fc_act(m, parts, part_stride, bias, scale, out, rows, n, relu, AZG_WINO_SPLIT, 1, overflow, stream);
+}
+
+extern "C" int azg_policy_value_parts(const float* m, int32_t parts, int64_t part_stride, int32_t ldm,
+                                      const float* bias, float scale, float* P, float* v, int32_t rows,
+                                      int32_t actions, void* stream) {
+    if (!m || !bias || !P || !v || rows <= 0 || actions <= 0 || actions > 64 * PV_MAX_PER_LANE ||
+        ldm < actions + 1 || parts < 1 || (parts > 1 && part_stride < (int64_t)rows * ldm))
+        return AZG_ERR_ARG;
+    const dim3 grid((unsigned)((rows + 3) / 4));
+    if (actions <= 64 * 8)
+        hipLaunchKernelGGL(policy_value_kernel<8>, grid, dim3(256), 0, (hipStream_t)stream, m, ldm, parts,
+                           (long long)part_stride, bias, scale, P, v, rows, actions);
+    else
+        hipLaunchKernelGGL(policy_value_kernel<PV_MAX_PER_LANE>, grid, dim3(256), 0, (hipStream_t)stream, m, ldm,
+                           parts, (long long)part_stride, bias, scale, P, v, rows, actions);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
 extern "C" int azg_policy_value(const float* m, int32_t ldm, const float* bias, float scale, float* P, float* v,
                                 int32_t rows, int32_t actions, void* stream) {
-    if (!m || !bias || !P || !v || rows <= 0 || actions <= 0 || actions > 64 * PV_MAX_PER_LANE || ldm < actions + 1)
-        return AZG_ERR_ARG;
-    const dim3 grid((unsigned)((rows + 3) / 4));
-    if (actions <= 64 * 8)
-        hipLaunchKernelGGL(policy_value_kernel<8>, grid, dim3(256), 0, (hipStream_t)stream, m, ldm, bias, scale, P, v,
-                           rows, actions);
-    else
-        hipLaunchKernelGGL(policy_value_kernel<PV_MAX_PER_LANE>, grid, dim3(256), 0, (hipStream_t)stream, m, ldm,
-                           bias, scale, P, v, rows, actions);
-    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+    return azg_policy_value_parts(m, 1, 0, ldm, bias, scale, P, v, rows, actions, stream);
 }

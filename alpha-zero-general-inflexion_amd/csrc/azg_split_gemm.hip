@@ -1461,6 +1461,10 @@ extern "C" int azg_split_gemm(const void* A, const void* Bt, float* M, int32_t n
     return split_gemm_launch(split_gemm_pick(nruns, points, rows, k), A, Bt, M, nruns, points, rows, c, k, stream);
 }
 
+extern "C" int azg_split_gemm_pick(int32_t nruns, const int32_t* points, const int32_t* rows, int32_t k) {
+    return split_gemm_pick(nruns, points, rows, k);
+}
+
 extern "C" int azg_split_gemm_variant(int32_t variant, const void* A, const void* Bt, float* M, int32_t nruns,
                                       const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream) {
     return split_gemm_launch(variant, A, Bt, M, nruns, points, rows, c, k, stream);

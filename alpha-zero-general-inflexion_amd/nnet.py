@@ -30,6 +30,11 @@ DEFAULT_ARGS = dict(lr=0.001, dropout=0.3, epochs=10, batch_size=512, num_channe
 WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C1: 1 game)
 FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
 FC1_KPARTS = 4  # split-K parts of fc1 on libazg's split GEMM (4608 = 4 x 1152 for the 7x7 board)
+# split-K parts of fc2 (1024 -> 512) and [fc3 | fc4] (512 -> 344, padded to 512 columns) when the whole
+# FC tail runs on libazg's split GEMM (InferenceNet.fc_tail_azg): 4 x 256 and 2 x 256 channels, the
+# fastest of 4/8/16 x 2/4 at 4096 leaves (tools/fc_tail_bench.py, profiles/r03_fc_tail_bench.json)
+FC2_KPARTS = 4
+FC34_KPARTS = 2
 
 
 class InflexionNNet(nn.Module):
@@ -318,10 +323,35 @@ class InferenceNet(nn.Module):
             self.register_buffer("fw2_s", torch.cat([whi, whi, wlo], dim=1).contiguous())
             whi, wlo, self.fc34_scale = _split_u(self.fw34.t().unsqueeze(0))
             self.register_buffer("fw34_s", torch.cat([whi, whi, wlo], dim=1).contiguous())
+        # the whole FC tail on libazg's split GEMM (fc1 split-K as above, then fc2 and the
+        # stacked [fc3 | fc4] as split-K GEMMs whose A operands the epilogues write in the
+        # split GEMM's own layout, azg_fc_act AZG_WINO_SPLIT2): no library GEMM in the forward
+        n2, n34 = w2.shape[0], self.fw34.shape[0]
+        self.fc_tail_azg = bool(self.fc1_kparts) and n2 % 256 == 0 and (w2.shape[1] // FC2_KPARTS) % 64 == 0 \
+            and (n2 // FC34_KPARTS) % 64 == 0 and w2.shape[1] % FC2_KPARTS == 0 and n2 % FC34_KPARTS == 0
+        if self.fc_tail_azg:
+            self.fc2_kparts, self.fc34_kparts = FC2_KPARTS, FC34_KPARTS
+            self.register_buffer("fw2_sk", self._split_k_weights(w2, FC2_KPARTS, self.fc2_scale))
+            n34p = -(-n34 // 256) * 256  # the split GEMM's 256-column tiles: zero weights past fc4
+            w34 = torch.zeros((n34p, self.fw34.shape[1]), dtype=self.fw34.dtype, device=self.fw34.device)
+            w34[:n34] = self.fw34
+            self.register_buffer("fw34_sk", self._split_k_weights(w34, FC34_KPARTS, self.fc34_scale))
         # sticky device flag: a split-GEMM operand fp16 could not hold (checked by check_range).
         # It lives where the kernels run: the transforms set it with a device atomic, so a
         # host-memory flag would fault the GPU the first time an operand overflowed.
         self.register_buffer("overflow", torch.zeros(1, dtype=torch.int32, device=self.w1.device))
+
+    @staticmethod
+    def _split_k_weights(w, kp, scale):
+        """[N][C] f32 weights -> the B operand of a kp-part split-K split GEMM: [kp][N][2 C / kp]
+        32-channel [hi | lo] blocks of W 2^k (the scale 2^-k _split_u picked for the same W)."""
+        us = w.detach().double().t() / scale  # [C][N], times 2^k
+        hi = us.half()
+        lo = (us - hi.double()).half()
+        n, c = w.shape
+        hp = hi.t().reshape(n, kp, c // kp).transpose(0, 1)
+        lp = lo.t().reshape(n, kp, c // kp).transpose(0, 1)
+        return split2_rows(hp, lp)
 
     def set_winograd_layer(self, i, w, h_out):
         """Replace conv i's Winograd weights by w [K][C][3][3] (BN already folded) for an
@@ -348,10 +378,19 @@ class InferenceNet(nn.Module):
     conv_hook = None
     kernel_hook = None
 
-    def _khook(self, kind, i, what, flops=0.0):
-        """flops (on "stop"): the executed MFMA FLOPs of a GEMM launch."""
+    def _khook(self, kind, i, what, flops=0.0, variant=None):
+        """flops (on "stop"): the executed MFMA FLOPs of a GEMM launch; variant: the split
+        GEMM schedule azg_split_gemm picked for it (4 persistent 256-row tiles, 17 / 18
+        128 / 64-row tiles)."""
         if self.kernel_hook is not None:
-            self.kernel_hook(kind, i, what, flops)
+            self.kernel_hook(kind, i, what, flops, variant)
+
+    @staticmethod
+    def _gemm_pick(runs_pts, runs_rows, k):
+        import ctypes
+        from . import _lib
+        n = len(runs_pts)
+        return _lib.lib().azg_split_gemm_pick(n, (ctypes.c_int32 * n)(*runs_pts), (ctypes.c_int32 * n)(*runs_rows), k)
 
     def _conv_miopen(self, x, i, pad):
         # MIOpen conv without bias, then one HIP pass: bias + ReLU in place (azg_nn.hip)
@@ -438,7 +477,8 @@ class InferenceNet(nn.Module):
                 ctypes.c_void_p(self._ws[0].data_ptr()), ctypes.c_void_p(getattr(self, f"us_{i}").data_ptr()),
                 ctypes.c_void_p(self._ws[1].data_ptr()), len(runs), pts, rows, C, K,
                 ctypes.c_void_p(torch.cuda.current_stream(self._ws[0].device).cuda_stream)))
-            self._khook("gemm", i, "stop", 3.0 * 2 * C * K * sum(P * B * n for P, n in runs))
+            self._khook("gemm", i, "stop", 3.0 * 2 * C * K * sum(P * B * n for P, n in runs),
+                        self._gemm_pick([P for P, _ in runs], [B * n for _, n in runs], K) if self.kernel_hook else None)
             return
         split = self.gemm == "split_blas"
         W = 3 * C if split else C
@@ -552,6 +592,8 @@ class InferenceNet(nn.Module):
         B, dev = a.shape[0], a.device
         st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         ovf = ctypes.c_void_p(self._overflow_ptr())
+        if self.fc_tail_azg and self.fc1_kparts:
+            return self._fc_split_azg(a, B, dev, st, ovf)
         for layer, (w, b, scale) in enumerate(((self.fw1_s, self.fb1, self.fc1_scale),
                                                (self.fw2_s, self.fb2, self.fc2_scale))):
             n = w.shape[2]
@@ -563,7 +605,8 @@ class InferenceNet(nn.Module):
                 self._khook("gemm", 5, "start")
                 _lib.check(L.azg_split_gemm(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(self.fw1_sk.data_ptr()),
                                             ctypes.c_void_p(m.data_ptr()), 1, pts, rows, chunk, n, st))
-                self._khook("gemm", 5, "stop", 3.0 * 2 * kp * chunk * n * B)
+                self._khook("gemm", 5, "stop", 3.0 * 2 * kp * chunk * n * B,
+                            self._gemm_pick([kp], [B], n) if self.kernel_hook else None)
             else:
                 m = torch.empty((1, B, n), device=dev, dtype=torch.float32)
                 torch.bmm(a.unsqueeze(0), w, out_dtype=torch.float32, out=m)
@@ -580,6 +623,48 @@ class InferenceNet(nn.Module):
         _lib.check(L.azg_policy_value(ctypes.c_void_p(m.data_ptr()), n, ctypes.c_void_p(self.fb34.data_ptr()),
                                       self.fc34_scale, ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()),
                                       B, A, st))
+        return p, v
+
+    def _fc_split_azg(self, a, B, dev, st, ovf):
+        """The FC tail as three split-K libazg split GEMMs (fc1, fc2, [fc3 | fc4] padded to 512
+        columns), each epilogue (azg_fc_act) summing the previous GEMM's parts in order,
+        adding the folded bias, applying ReLU and writing the next GEMM's split2 K-parts;
+        azg_policy_value_parts sums the last GEMM's parts into P = softmax, v = tanh."""
+        import ctypes
+        from . import _lib
+        L = _lib.lib()
+
+        def gemm(layer, A_, W, kp, n):
+            c = A_.shape[-1] // (2 * kp) if A_.dim() == 2 else A_.shape[-1] // 2
+            m = torch.empty((kp, B, n), device=dev, dtype=torch.float32)
+            pts, rows = (ctypes.c_int32 * 1)(kp), (ctypes.c_int32 * 1)(B)
+            self._khook("gemm", layer, "start")
+            _lib.check(L.azg_split_gemm(ctypes.c_void_p(A_.data_ptr()), ctypes.c_void_p(W.data_ptr()),
+                                        ctypes.c_void_p(m.data_ptr()), 1, pts, rows, c, n, st))
+            self._khook("gemm", layer, "stop", 3.0 * 2 * kp * c * n * B,
+                        self._gemm_pick([kp], [B], n) if self.kernel_hook else None)
+            return m
+
+        def act(m, kp_in, bias, scale, kp_out):
+            n = m.shape[2]
+            out = torch.empty((kp_out, B, 2 * n // kp_out), device=dev, dtype=torch.float16)
+            _lib.check(L.azg_fc_act(ctypes.c_void_p(m.data_ptr()), kp_in, B * n, ctypes.c_void_p(bias.data_ptr()),
+                                    scale, ctypes.c_void_p(out.data_ptr()), B, n, 1, 2, kp_out, ovf, st))
+            return out
+
+        kp1, kp2, kp3 = self.fc1_kparts, self.fc2_kparts, self.fc34_kparts
+        m1 = gemm(5, a, self.fw1_sk, kp1, self.fw1_sk.shape[1])
+        a2 = act(m1, kp1, self.fb1, self.fc1_scale, kp2)
+        m2 = gemm(6, a2, self.fw2_sk, kp2, self.fw2_sk.shape[1])
+        a3 = act(m2, kp2, self.fb2, self.fc2_scale, kp3)
+        m3 = gemm(7, a3, self.fw34_sk, kp3, self.fw34_sk.shape[1])
+        A = self.fw34.shape[0] - 1
+        p = torch.empty((B, A), device=dev, dtype=torch.float32)
+        v = torch.empty((B, 1), device=dev, dtype=torch.float32)
+        n3 = m3.shape[2]
+        _lib.check(L.azg_policy_value_parts(ctypes.c_void_p(m3.data_ptr()), kp3, B * n3, n3,
+                                            ctypes.c_void_p(self.fb34.data_ptr()), self.fc34_scale,
+                                            ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()), B, A, st))
         return p, v
 
     def forward(self, s):

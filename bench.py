@@ -140,6 +140,10 @@ def parse():
     p.add_argument("--gemm", default="split", choices=["split", "split_blas", "f32"],
                    help="Winograd GEMMs: split-fp16 (f32-accurate, 3 fp16 MFMA products) in libazg's kernel "
                         "or hipBLASLt, or f32 MFMA")
+    p.add_argument("--fc-tail", default="azg", choices=["azg", "blas"],
+                   help="fc2 and [fc3 | fc4] at >= 1024 leaves: libazg split-K split GEMMs (azg) or the round-2 "
+                        "hipBLASLt fp16 GEMMs (blas)")
+    p.add_argument("--fc-kparts", default=None, help="with --fc-tail azg: split-K parts of fc2,fc3|fc4 (e.g. 4,2)")
     p.add_argument("--net", default="inference", choices=["inference", "reference"],
                    help="inference: BN-folded NHWC InferenceNet; reference: InflexionNNet as written")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -344,8 +348,13 @@ def main():
     flop_leaf, conv_flop_leaf = net_flops(args.n, depth, A)
     torch.manual_seed(0)
     net = InflexionNNet(n=args.n, depth=depth, action_size=A).cuda().eval()
+    if args.fc_kparts:
+        import azg_amd.nnet as nn_mod
+        nn_mod.FC2_KPARTS, nn_mod.FC34_KPARTS = (int(x) for x in args.fc_kparts.split(","))
     ev = ((InferenceNet(net, conv=args.conv, gemm=args.gemm) if args.net == "inference" else net)
           if args.evaluator == "net" else "stub")
+    if args.fc_tail == "blas" and hasattr(ev, "fc_tail_azg"):
+        ev.fc_tail_azg = False
     G = args.games
     eng = SelfPlayEngine(G, sims=args.sims, cpuct=1, temp_threshold=30, max_turns=args.max_turns,
                          seed_base=0, first_game=rank * G, evaluator=ev, game=args.game, n=args.n)
@@ -375,9 +384,9 @@ def main():
     # stream they are launched on (the current stream)
     t_kern = {"gemm": Timer(), "transform": Timer()}
     kpending = {}
-    kflops = {"gemm": 0.0, "gemm_layers": set()}
+    gemm_meta = []  # per timed split-GEMM launch: (layer, executed FLOPs, schedule variant)
 
-    def kernel_hook(kind, i, what, flops=0.0):
+    def kernel_hook(kind, i, what, flops=0.0, variant=None):
         if not inst["on"]:
             return
         if what == "start":
@@ -385,8 +394,7 @@ def main():
         else:
             t_kern[kind].stop(kpending.pop(kind))
             if kind == "gemm":
-                kflops["gemm"] += flops
-                kflops["gemm_layers"].add(i)
+                gemm_meta.append((i, flops, variant))
 
     if hasattr(ev, "kernel_hook"):
         ev.kernel_hook = kernel_hook
@@ -585,21 +593,42 @@ def main():
         }
         # the dominant kernel: libazg's split GEMM (over half of the step's GPU time), its
         # launches timed with HIP events on their stream; executed MFMA FLOPs = the GEMM work
-        # (Winograd: transformed points x 2 C K per leaf; fc1: 2 x 4608 x 1024 per leaf) x 3
-        # fp16 products, as InferenceNet reports it per launch
+        # (Winograd: transformed points x 2 C K per leaf; fc1-fc4: the FC layers, split-K) x 3
+        # fp16 products, as InferenceNet reports it per launch.  `roofline` is the kernel the
+        # most GEMM time runs in -- the persistent 256-row schedule (conv2-4, fc1) -- so its
+        # average launch duration is the one rocprof reports for that kernel symbol; every
+        # split-GEMM launch (fc2 and [fc3 | fc4] run on the 128 / 64-row schedule) is in
+        # `roofline_gemm_all`, per layer in `gemm_layers`.
         g_pairs, t_pairs = t_kern["gemm"].pairs, t_kern["transform"].pairs
         if g_pairs:
-            g_ms = t_kern["gemm"].total_ms()
-            n_launch = len(g_pairs)
+            torch.cuda.synchronize()
+            durs = [st.elapsed_time(en) for st, en in g_pairs]  # ms per launch
+            kname = {4: "split_gemm_persist_kernel (256 x 256 tiles, persistent)",
+                     17: "split_gemm_kernel<false, 128> (128 x 256 tiles)",
+                     18: "split_gemm_kernel<false, 64> (64 x 256 tiles)",
+                     19: "split_gemm_384_kernel (384 x 256 tiles, persistent)"}
+            lname = {2: "conv2", 3: "conv3", 4: "conv4", 5: "fc1 (split-K)", 6: "fc2 (split-K)", 7: "fc3|fc4 (split-K)"}
+            by_var, by_layer = {}, {}
+            for (layer, fl, var), ms in zip(gemm_meta, durs):
+                by_var.setdefault(var, [0.0, 0.0, 0, set()])
+                by_var[var][0] += ms
+                by_var[var][1] += fl
+                by_var[var][2] += 1
+                by_var[var][3].add(lname.get(layer, str(layer)))
+                by_layer.setdefault(layer, [0.0, 0.0, 0, var])
+                by_layer[layer][0] += ms
+                by_layer[layer][1] += fl
+                by_layer[layer][2] += 1
+            dom = max(by_var, key=lambda v: by_var[v][0])
+            g_ms, g_fl, n_launch, dom_layers = by_var[dom]
             per_fwd = n_launch / n_forwards
-            flops_launch = kflops["gemm"] / n_launch
+            flops_launch = g_fl / n_launch
             ach = flops_launch / (g_ms / n_launch / 1e3) / 1e12
-            layers = sorted(kflops["gemm_layers"])
-            names = ", ".join(f"conv{i}" if i < 5 else "fc1 (split-K)" for i in layers)
+            all_ms, all_fl = sum(durs), sum(m[1] for m in gemm_meta)
+            ach_all = all_fl / (all_ms / 1e3) / 1e12
             out["roofline"] = {
-                "bound": "mfma", "kernel": f"libazg azg_split_gemm ({names}; one call per layer: "
-                                           "split_gemm_persist_kernel on 256-row tiles, or split_gemm_kernel on "
-                                           "128-row tiles for short layers)",
+                "bound": "mfma", "kernel": f"libazg azg_split_gemm, {kname.get(dom, dom)}: "
+                                           f"{', '.join(sorted(dom_layers))} (one launch per layer)",
                 "achieved": ach, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TF,
                 "traffic": None, "mfma_dtype": "fp16 (split, 3 products per f32 multiply-add, f32 accumulation)",
                 "flops_kind": "executed fp16 MFMA FLOPs: each f32 multiply-add of the Winograd GEMMs (already 3.8x "
@@ -609,11 +638,18 @@ def main():
                 "f32_equivalent": {"achieved": ach / 3, "peak": F32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                                    "frac": ach / 3 / F32_MFMA_PEAK_TF},
                 "avg_launch_us": g_ms / n_launch * 1e3, "launches": n_launch,
-                "per_launch": f"{kflops['gemm'] / n_forwards / 1e9:.1f} GFLOP per forward ({leaves} leaves; 3 fp16 "
-                              f"products) / {per_fwd:.0f} calls = {flops_launch / 1e9:.1f} GFLOP per call (avg "
-                              f"over the layers' shapes) / {g_ms / n_launch * 1e3:.1f} us (HIP events around each "
-                              "call)",
-                "share_of_forward": g_ms / nn_ms if nn_ms > 0 else None}
+                "per_launch": f"{g_fl / n_forwards / 1e9:.1f} GFLOP per forward in this kernel ({leaves} leaves; 3 "
+                              f"fp16 products) / {per_fwd:.0f} launches = {flops_launch / 1e9:.1f} GFLOP per launch "
+                              f"(avg over the layers' shapes) / {g_ms / n_launch * 1e3:.1f} us (HIP events around "
+                              "each launch)",
+                "share_of_forward": all_ms / nn_ms if nn_ms > 0 else None}
+            out["roofline_gemm_all"] = {
+                "bound": "mfma", "kernel": "every libazg azg_split_gemm launch of the forward",
+                "achieved": ach_all, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": ach_all / F16_MFMA_PEAK_TF,
+                "launches_per_forward": len(durs) / n_forwards}
+            out["gemm_layers"] = {lname.get(k, str(k)): {"us": v[0] / v[2] * 1e3, "tflops": v[1] / (v[0] / 1e3) / 1e12,
+                                                         "schedule": kname.get(v[3], v[3])}
+                                  for k, v in sorted(by_layer.items())}
         if t_pairs and impl == "winograd" and getattr(ev, "gemm", "") == "split":
             tb = transform_bytes(args.n, depth, split=True)
             t_ms = t_kern["transform"].total_ms()

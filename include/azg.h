@@ -227,10 +227,12 @@ int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, cons
  * variant 4 with each accumulator's products 4 MFMAs apart; 11: variant 4 with each
  * tile's stores deferred into the next tile's first stage; 12: ping-pong with each
  * wave's own DMA and one stage stream across tiles; 17: variant 0 on 128-row tiles,
- * azg_split_gemm's pick for short launches; 18: the same on 64-row tiles); for tests
- * and probes. */
+ * azg_split_gemm's pick for short launches; 18: the same on 64-row tiles; 19: variant 4
+ * on 384 x 256 tiles, results bit-identical to variant 4's); for tests and probes. */
 int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, float* m, int32_t nruns,
                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
+/* The schedule azg_split_gemm picks for a launch of this shape (4, 17 or 18). */
+int  azg_split_gemm_pick(int32_t nruns, const int32_t* points, const int32_t* rows, int32_t k);
 /* Diagnostic build of the default split GEMM with in-kernel s_memtime stamps
  * (results as azg_split_gemm): per wave (block b, wave w) the cycle sums of
  * [operand reads + DMA issue], [MFMA issue], [vmcnt wait], [barrier], [epilogue]
@@ -258,6 +260,18 @@ int  azg_fc_act_split(const float* m, int32_t parts, int64_t part_stride, const 
                       int32_t rows, int32_t n, int32_t relu, int32_t* overflow, void* stream);
 int  azg_policy_value(const float* m, int32_t ldm, const float* bias, float scale, float* P, float* v,
                       int32_t rows, int32_t actions, void* stream);
+/* The same epilogues for an FC tail that runs entirely on azg_split_gemm (no library
+ * GEMM): azg_fc_act writes y as fmt AZG_WINO_SPLIT ([hi | lo | hi] rows, out_parts 1,
+ * = azg_fc_act_split) or AZG_WINO_SPLIT2: out_parts K-parts of 32-channel [hi | lo]
+ * blocks, [part][rows][2 n / out_parts] fp16 -- the A operand of the next layer's
+ * split-K azg_split_gemm (its parts as the GEMM's points); (n / out_parts) % 32 == 0.
+ * azg_policy_value_parts sums `parts` partial [fc3 | fc4] products (part p at m + p *
+ * part_stride floats, in order) first; azg_policy_value = parts 1. */
+int  azg_fc_act(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale, void* out,
+                int32_t rows, int32_t n, int32_t relu, int32_t fmt, int32_t out_parts, int32_t* overflow,
+                void* stream);
+int  azg_policy_value_parts(const float* m, int32_t parts, int64_t part_stride, int32_t ldm, const float* bias,
+                            float scale, float* P, float* v, int32_t rows, int32_t actions, void* stream);
 
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active

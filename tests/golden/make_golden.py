@@ -23,8 +23,8 @@ Fixtures written (all small, gzip'd JSON or npz):
   arena_<set>.json.gz    Arena.playGame MCTSPlayer(stubnet) vs Random/Greedy players
   nnet_golden.npz        InflexionNNet(manual_seed 0) checksum + (planes -> P, v)
   train_golden.json.gz   NNetWrapper.train (32 channels, 2 epochs): losses + weight digests
-  realnet_sensitivity.json.gz  first divergent move of the reference's real-net traces under 1e-7 / 1e-6
-                         relative perturbations of its network outputs
+  realnet_sensitivity.json.gz  first divergent move of the reference's real-net traces when its network's
+                         weights, or its outputs, move by 1e-7 / 1e-6 relative
 """
 import gzip
 import hashlib
@@ -414,15 +414,19 @@ def gen_nnet(np, InflexionGame):
 
 # --------------------------------------------------------------- realnet sensitivity
 def gen_realnet_sensitivity(np):
-    """How far do the reference's own real-network traces survive a perturbation of
-    its network outputs far below the north_star's 1e-5 tolerance?  The reference
-    Coach/MCTS (main.py's configuration, the seeds of mcts_realnet_main) is rerun
-    with NNetWrapper.predict's P and v multiplied by (1 + eps u), u ~ U(-1, 1) drawn
-    from a RandomState keyed on the planes (a deterministic, equally valid f32-level
-    evaluation; numpy's global stream is untouched), and each move's visit counts
-    are compared with the unperturbed trace.  Records the first move whose counts
-    differ, per seed and eps: the scale at which whole-game visit counts are a
-    property of the last bits of the network's arithmetic, not of the search."""
+    """How far do the reference's own real-network traces survive a change of its
+    network far below the north_star's 1e-5 tolerance?  The reference Coach/MCTS
+    (main.py's configuration, the seeds of mcts_realnet_main) is rerun with
+      * "weights": every parameter of the manual_seed(0) network multiplied by
+        (1 + eps u), u ~ U(-1, 1) from a fixed generator -- an equally valid f32
+        network, its outputs moving smoothly and consistently (as a GPU's different
+        summation order moves them);
+      * "outputs": NNetWrapper.predict's P and v multiplied by (1 + eps u), u drawn
+        per call from a RandomState keyed on the planes -- independent per action,
+        so it also splits exact ties;
+    numpy's global stream untouched, and each move's visit counts compared with the
+    unperturbed trace.  Records the first move whose counts differ, per kind, eps
+    and seed."""
     import torch
     import MCTS as mcts_mod
     from Coach import Coach
@@ -437,6 +441,8 @@ def gen_realnet_sensitivity(np):
 
         def predict(self, board):
             p, v = super().predict(board)
+            if not self.eps:
+                return p, v
             rs = np.random.RandomState(int.from_bytes(hashlib.sha256(board.tobytes()).digest()[:4], "little"))
             u = rs.uniform(-1.0, 1.0, size=p.shape[0] + 1)
             p = (p.astype(np.float64) * (1.0 + self.eps * u[:-1])).astype(np.float32)
@@ -452,28 +458,36 @@ def gen_realnet_sensitivity(np):
             self.counts.append({a: int(self.Nsa[(s, a)]) for a in range(game.max_actions) if (s, a) in self.Nsa})
             return probs
 
-    torch.manual_seed(0)
     game0 = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
-    net = NoisyNNet(game0)
     out = {"config": cfg, "runs": []}
-    for eps in (1e-7, 1e-6):
-        for ep in base["episodes"]:
-            NoisyNNet.eps = eps
-            args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"], "tempThreshold": cfg["temp_threshold"]})
-            mcts = RecMCTS(net, args)
-            mcts.counts = []
-            np.random.seed(ep["seed"])
-            Coach(game0, net, args).executeEpisode((game0.restarted(), mcts))
-            first = None
-            for m, (mine, ref) in enumerate(zip(mcts.counts, ep["moves"])):
-                if mine != {a: c for a, c in ref["counts"]}:
-                    first = m
-                    break
-            if first is None and len(mcts.counts) != ep["n_moves"]:
-                first = min(len(mcts.counts), ep["n_moves"])
-            out["runs"].append({"eps": eps, "seed": ep["seed"], "first_divergent_move": first,
-                                "moves": len(mcts.counts), "reference_moves": ep["n_moves"]})
-            print(f"  eps {eps:g} seed {ep['seed']}: first divergent move {first}", flush=True)
+    for kind in ("weights", "outputs"):
+        for eps in (1e-7, 1e-6):
+            torch.manual_seed(0)
+            net = NoisyNNet(game0)
+            NoisyNNet.eps = eps if kind == "outputs" else 0.0
+            if kind == "weights":
+                g = torch.Generator().manual_seed(12345)
+                with torch.no_grad():
+                    for prm in net.nnet.parameters():
+                        prm.mul_(1.0 + eps * (2.0 * torch.rand(prm.shape, generator=g, dtype=torch.float64) - 1.0)
+                                 .to(prm.dtype))
+            for ep in base["episodes"]:
+                args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"],
+                                "tempThreshold": cfg["temp_threshold"]})
+                mcts = RecMCTS(net, args)
+                mcts.counts = []
+                np.random.seed(ep["seed"])
+                Coach(game0, net, args).executeEpisode((game0.restarted(), mcts))
+                first = None
+                for m, (mine, ref) in enumerate(zip(mcts.counts, ep["moves"])):
+                    if mine != {a: c for a, c in ref["counts"]}:
+                        first = m
+                        break
+                if first is None and len(mcts.counts) != ep["n_moves"]:
+                    first = min(len(mcts.counts), ep["n_moves"])
+                out["runs"].append({"kind": kind, "eps": eps, "seed": ep["seed"], "first_divergent_move": first,
+                                    "moves": len(mcts.counts), "reference_moves": ep["n_moves"]})
+                print(f"  {kind} eps {eps:g} seed {ep['seed']}: first divergent move {first}", flush=True)
     _dump("realnet_sensitivity.json.gz", out)
 
 

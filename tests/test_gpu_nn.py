@@ -287,15 +287,18 @@ def test_fc1_split_form_matches_reference(extra):
     assert fast.fc1_split
     x = (torch.rand(nn_mod.FC1_SPLIT_MIN_BATCH + extra, 4, 7, 7, device="cuda") < 0.3).float()  # ragged tiles too
     assert fast.fc1_kparts == nn_mod.FC1_KPARTS
+    assert fast.fc_tail_azg
     with torch.no_grad():
-        p, v = fast(x)                  # fc1 as libazg's split-K split GEMM
+        p, v = fast(x)                  # fc1, fc2, [fc3 | fc4] all as libazg split-K split GEMMs
         logp, v_ref = net(x)
+        fast.fc_tail_azg = False
+        pa, va = fast(x)                # fc1 on libazg, fc2 and [fc3 | fc4] on hipBLASLt
         fast.fc1_kparts = 0
         pb, vb = fast(x)                # fc1 as the hipBLASLt split GEMM
         fast.fc1_split = False
         p32, v32 = fast(x)              # f32 FC tail
     fast.check_range()
-    for pp, vv in ((p, v), (pb, vb)):
+    for pp, vv in ((p, v), (pa, va), (pb, vb)):
         torch.testing.assert_close(pp, torch.exp(logp), rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(vv.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(pp, p32, rtol=1e-5, atol=1e-7)
@@ -332,6 +335,59 @@ def test_fc_act_split_kernel():
         m[0, 7, 5] = 1e9
         run()
         assert int(ovf.item()) == 1
+
+
+@pytest.mark.parametrize("n,out_parts", [(1024, 8), (512, 4), (512, 1), (256, 2)])
+def test_fc_act_split2_layout(n, out_parts):
+    """azg_fc_act with AZG_WINO_SPLIT2 output: the same hi / lo values as the [hi | lo | hi]
+    form, laid out as out_parts K-parts of 32-channel [hi | lo] blocks (nnet.split2_rows of
+    each part), the A operand of the next split-K split GEMM."""
+    import ctypes
+    from azg_amd import _lib
+    from azg_amd.nnet import split2_rows
+    B, scale, parts = 257, 2.0 ** -5, 3
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    m = torch.randn(parts, B, n, device="cuda") * 50
+    b = torch.randn(n, device="cuda")
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out = torch.empty(out_parts, B, 2 * n // out_parts, device="cuda", dtype=torch.float16)
+    _lib.check(_lib.lib().azg_fc_act(ctypes.c_void_p(m.data_ptr()), parts, B * n, ctypes.c_void_p(b.data_ptr()),
+                                     scale, ctypes.c_void_p(out.data_ptr()), B, n, 1, 2, out_parts,
+                                     ctypes.c_void_p(ovf.data_ptr()), st))
+    y = torch.relu(b + scale * (m[0] + m[1] + m[2]))
+    hi = y.half()
+    lo = (y - hi.float()).half()
+    want = split2_rows(hi.reshape(B, out_parts, n // out_parts).transpose(0, 1),
+                       lo.reshape(B, out_parts, n // out_parts).transpose(0, 1))
+    assert torch.equal(out, want)
+    assert int(ovf.item()) == 0
+    # a host-memory flag is refused at the boundary (a device atomic to it would fault the GPU)
+    host_flag = torch.zeros(1, dtype=torch.int32)
+    assert _lib.lib().azg_fc_act(ctypes.c_void_p(m.data_ptr()), parts, B * n, ctypes.c_void_p(b.data_ptr()),
+                                 scale, ctypes.c_void_p(out.data_ptr()), B, n, 1, 2, out_parts,
+                                 ctypes.c_void_p(host_flag.data_ptr()), st) == -1
+
+
+@pytest.mark.parametrize("parts", [1, 4])
+def test_policy_value_parts_kernel(parts):
+    """azg_policy_value_parts: the split-K parts of [fc3 | fc4] summed in order, then softmax / tanh."""
+    import ctypes
+    from azg_amd import _lib
+    B, A, ld, scale = 333, 343, 512, 0.25
+    m = torch.randn(parts, B, ld, device="cuda") * 4
+    b = torch.randn(A + 1, device="cuda")
+    P = torch.empty(B, A, device="cuda")
+    v = torch.empty(B, device="cuda")
+    _lib.check(_lib.lib().azg_policy_value_parts(ctypes.c_void_p(m.data_ptr()), parts, B * ld, ld,
+                                                 ctypes.c_void_p(b.data_ptr()), scale, ctypes.c_void_p(P.data_ptr()),
+                                                 ctypes.c_void_p(v.data_ptr()), B, A,
+                                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    acc = m[0].clone()
+    for p in range(1, parts):
+        acc = acc + m[p]
+    x = b + scale * acc[:, :A + 1]
+    torch.testing.assert_close(P, torch.softmax(x[:, :A], dim=1), rtol=2e-6, atol=1e-8)
+    torch.testing.assert_close(v, torch.tanh(x[:, A]), rtol=2e-6, atol=1e-7)
 
 
 @pytest.mark.parametrize("A", [343, 65, 36, 512, 567, 1024])

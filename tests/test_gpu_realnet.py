@@ -24,9 +24,9 @@ What is asserted, per seed, against the reference's visit counts:
     another action (two counts differing by one).  A GPU network agrees with the
     CPU one to ~1e-6 relative (root priors here: ~5e-9 absolute), and over a whole
     344-move game the search meets PUCT ties closer than that: the reference's OWN
-    traces diverge the same way when its network outputs are perturbed by 1e-7 or
-    1e-6 relative (tests/golden/realnet_sensitivity.json.gz, first divergent moves
-    printed beside ours).  Once one decision differs the games are different games,
+    traces diverge the same way when its network's weights (or outputs) move by
+    1e-7 or 1e-6 relative (tests/golden/realnet_sensitivity.json.gz, first
+    divergent moves printed beside ours).  Once one decision differs the games are different games,
     so nothing after it is compared.  Every flip is reported with its move and the
     root's prior error and smallest prior gap; a mismatch of any other shape --
     more than one decision, or inside the first 40 moves -- fails.
@@ -84,7 +84,7 @@ def _sensitivity():
         d = ol.load_json("realnet_sensitivity.json.gz")
     except FileNotFoundError:
         return {}
-    return {(r["eps"], r["seed"]): r["first_divergent_move"] for r in d["runs"]}
+    return {(r["kind"], r["eps"], r["seed"]): r["first_divergent_move"] for r in d["runs"]}
 
 
 def _check_episode(ep, counts, actions, n_moves, where, report, whole=False):
@@ -102,9 +102,10 @@ def _check_episode(ep, counts, actions, n_moves, where, report, whole=False):
         if whole or m < MIN_PREFIX or not single_flip:
             raise AssertionError(msg + "; " + report(mv))
         sens = _sensitivity()
-        print(f"NEAR-TIE FLIP {msg}; {report(mv)}; identical through move {m - 1}; the reference's own trace under "
-              f"1e-7 / 1e-6 output perturbations first diverges at move "
-              f"{sens.get((1e-7, ep['seed']), '?')} / {sens.get((1e-6, ep['seed']), '?')}")
+        print(f"NEAR-TIE FLIP {msg}; {report(mv)}; identical through move {m - 1}; the reference's own trace with "
+              f"its weights moved by 1e-7 / 1e-6 first diverges at move "
+              f"{sens.get(('weights', 1e-7, ep['seed']), '?')} / {sens.get(('weights', 1e-6, ep['seed']), '?')} "
+              "(None: never)")
         return m
     assert n_moves == ep["n_moves"], (where, ep["seed"])
     return None
