@@ -123,3 +123,21 @@ def test_mcts_episodes_bit_exact(name):
     for ep in data["episodes"]:
         got = ol.episode(7, cfg["max_turns"], cfg["sims"], cfg["cpuct"], cfg["temp_threshold"], ep["seed"])
         _check_episode(cfg, ep, got)
+
+
+def test_realnet_fixtures_consistent():
+    """The real-network reference traces (make_golden `realnet`) and the reference's own
+    sensitivity runs (`sensitivity`) that tests/test_gpu_realnet.py certifies near-ties with."""
+    main = ol.load_json("mcts_realnet_main.json.gz")
+    assert [e["seed"] for e in main["episodes"]] == [0, 1, 2, 3]
+    for ep in main["episodes"]:
+        assert ep["n_moves"] == len(ep["moves"]) == 344
+        for m, mv in enumerate(ep["moves"]):
+            counts = ol.golden_counts(mv)
+            assert counts.sum() >= main["config"]["sims"] and counts[mv["action"]] > 0 or mv["temp"] == 1, m
+    sens = ol.load_json("realnet_sensitivity.json.gz")
+    runs = {(r["kind"], r["eps"], r["seed"]): r["first_divergent_move"] for r in sens["runs"]}
+    assert len(runs) == 16
+    # the near-ties the reference's own rounding decides (DESIGN.md 1)
+    assert runs[("weights", 1e-7, 0)] == 222 and runs[("weights", 1e-7, 3)] == 197
+    assert runs[("weights", 1e-7, 1)] is None and runs[("weights", 1e-7, 2)] is None
