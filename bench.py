@@ -162,6 +162,8 @@ def parse():
                         f"{CPU_BASELINE_MAX_CORES})")
     p.add_argument("--cpu-proc-moves", type=int, default=30,
                    help="cpu_baseline's processes x 1 thread leg: first moves of one game per process")
+    # internal: collectives over gloo with ranks sharing GPUs (rehearsing --gpus N on a one-GPU box)
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"], help=argparse.SUPPRESS)
     # internal: one single-threaded cpu_baseline worker (a child process, never touches the GPU)
     p.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     # internal: each rank prints its rendezvous env and exits before any GPU call (tests/test_bench_cpu.py)
@@ -331,8 +333,15 @@ def main():
         print(json.dumps({"rank": rank, "local_rank": local, "world_size": world, "gpus": args.gpus,
                           "master_addr": os.environ.get("MASTER_ADDR")}), flush=True)
         return 0
+    if args.dist_backend == "gloo":
+        # rehearsal of the N > 1 path on fewer GPUs than ranks (tests of this script on a
+        # one-GPU box): ranks share devices round-robin, collectives over gloo
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
         world = dist.get_world_size()
     if world != args.gpus:
         print(f"# bench: --gpus {args.gpus} but {world} rank(s) run; n_gpus reports {world}", file=sys.stderr)
