@@ -150,6 +150,10 @@ def parse():
     p.add_argument("--cpu-moves", type=int, default=200, help="cpu_baseline sample: first moves of one game")
     p.add_argument("--full-games", action="store_true",
                    help="time complete games (restart after warmup, play until every game ends): measured games/s")
+    p.add_argument("--generation", choices=["auto", "on", "off"], default="auto",
+                   help="after the timed steps, restart every game and time one whole generation (all games to "
+                        "their end): measured games/s in games_per_s.  auto: on for 7x7 Inflexion at <= 25 sims "
+                        "(C2, C4: ~16 s), off for the 100-200-sim configs")
     p.add_argument("--timer-every", type=int, default=25,
                    help="record the per-kernel HIP events (roofline, time split) on every N-th simulation of the "
                         "timed region only: each event record costs ~10 us of GPU idle time, which would otherwise "
@@ -488,6 +492,33 @@ def main():
     if st1["error"]:
         raise RuntimeError(f"engine error {st1['error']}")
 
+    # one whole generation after the timed steps: every game restarted and played to its end
+    # (random-init games all run 344 moves), all ranks at once -- games/s measured, not estimated
+    gen = None
+    if not args.full_games and (args.generation == "on" or (args.generation == "auto" and args.game == "inflexion"
+                                                             and args.sims <= 25 and args.evaluator == "net")):
+        eng.drop_graph()
+        eng.reset()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        moves = 0
+        while eng.active() > 0:
+            eng.move()
+            moves += 1
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        gen_s = time.perf_counter() - tg
+        if world > 1:
+            t = torch.tensor([gen_s], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            gen_s = float(t.item())
+        gen = {"games": G * world, "seconds": gen_s, "moves": moves}
+        if eng.stats()["error"]:
+            raise RuntimeError(f"engine error {eng.stats()['error']} in the generation pass")
+
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -568,10 +599,15 @@ def main():
                        "games_per_gpu": G, "sims_per_move": args.sims, "global_games": G * world,
                        "parallelism": f"games sharded over {world} GPU(s)", "step": "one move of every game"},
             "games_per_s": (G * world / elapsed) if args.full_games else (
-                value / EXPANSIONS_PER_GAME_REF if args.game == "inflexion" else None),
+                gen["games"] / gen["seconds"] if gen else (
+                    value / EXPANSIONS_PER_GAME_REF if args.game == "inflexion" else None)),
             "games_per_s_note": (f"measured: {G * world} complete games in {elapsed:.1f}s" if args.full_games else
+                                 f"measured after the timed steps: one generation, {gen['games']} games restarted and "
+                                 f"played to their end ({gen['moves']} moves) in {gen['seconds']:.1f}s over "
+                                 f"{world} GPU(s)" if gen else
                                  "expansions/s / 8555 expansions per random-init game (344 moves, measured on the "
-                                 "reference); bench.py --full-games measures it directly"),
+                                 "reference); bench.py --full-games or --generation on measures it"),
+            "games_per_s_estimate": value / EXPANSIONS_PER_GAME_REF if args.game == "inflexion" else None,
             "expansions": exp,
             "simulations": sims_run,
             "roofline": None,  # the dominant kernel's (set below)

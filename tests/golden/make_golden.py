@@ -268,17 +268,24 @@ def gen_mcts(np, quick, othello=False, realnet=False):
             "othello8": dict(n=8, sims=25, cpuct=1, temp_threshold=30, seeds=list(range(600, 606))),
             "othello8_s200": dict(n=8, sims=200, cpuct=1, temp_threshold=30, seeds=[700, 701]),
         }
+        if realnet:  # C1 (6x6, one episode, 25 sims) and C5 (8x8, 200 sims) with the reference NNetWrapper
+            sets = {
+                "realnet_othello6": dict(n=6, sims=25, cpuct=1, temp_threshold=15, seeds=[500, 501, 502, 503]),
+                "realnet_othello8": dict(n=8, sims=25, cpuct=1, temp_threshold=30, seeds=[600, 601]),
+                "realnet_othello8_s200": dict(n=8, sims=200, cpuct=1, temp_threshold=30, seeds=[700]),
+            }
     for name, cfg in sets.items():
         eps = []
         t0 = time.time()
         for seed in cfg["seeds"]:
             game = GameCls(cfg["n"]) if othello else InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
             if realnet:
-                if "net" not in real_nets:
+                key = (GameCls.__name__, cfg.get("n", 7))
+                if key not in real_nets:
                     import torch
-                    torch.manual_seed(0)  # the network of nnet_golden.npz (gen_nnet)
-                    real_nets["net"] = CountingNNet(game)
-                nnet = real_nets["net"]
+                    torch.manual_seed(0)  # Inflexion 7x7: the network of nnet_golden.npz (gen_nnet)
+                    real_nets[key] = CountingNNet(game)
+                nnet = real_nets[key]
                 nnet.calls = 0
             else:
                 nnet = StubNNet(game)
@@ -413,7 +420,7 @@ def gen_nnet(np, InflexionGame):
 
 
 # --------------------------------------------------------------- realnet sensitivity
-def gen_realnet_sensitivity(np):
+def gen_realnet_sensitivity(np, othello=False):
     """How far do the reference's own real-network traces survive a change of its
     network far below the north_star's 1e-5 tolerance?  The reference Coach/MCTS
     (main.py's configuration, the seeds of mcts_realnet_main) is rerun with
@@ -433,8 +440,19 @@ def gen_realnet_sensitivity(np):
     from inflexion.InflexionGame import InflexionGame
     from inflexion.pytorch.NNet import NNetWrapper
     from utils import dotdict
-    base = json.load(gzip.open(os.path.join(HERE, "mcts_realnet_main.json.gz"), "rt"))
-    cfg = base["config"]
+    if othello:  # the builder's plugin under the reference's enums, as gen_mcts drives it
+        sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+        import flags as ref_flags
+        import azg_amd  # noqa: F401
+        import azg_amd.flags as own_flags
+        own_flags.GameOutcome = ref_flags.GameOutcome
+        own_flags.PlayerColour = ref_flags.PlayerColour
+        from azg_amd.othello import OthelloGame
+        bases = ["realnet_othello6", "realnet_othello8", "realnet_othello8_s200"]
+        kinds = ("weights",)
+    else:
+        bases = ["realnet_main"]
+        kinds = ("weights", "outputs")
 
     class NoisyNNet(NNetWrapper):
         eps = 0.0
@@ -458,37 +476,44 @@ def gen_realnet_sensitivity(np):
             self.counts.append({a: int(self.Nsa[(s, a)]) for a in range(game.max_actions) if (s, a) in self.Nsa})
             return probs
 
-    game0 = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
-    out = {"config": cfg, "runs": []}
-    for kind in ("weights", "outputs"):
-        for eps in (1e-7, 1e-6):
-            torch.manual_seed(0)
-            net = NoisyNNet(game0)
-            NoisyNNet.eps = eps if kind == "outputs" else 0.0
-            if kind == "weights":
-                g = torch.Generator().manual_seed(12345)
-                with torch.no_grad():
-                    for prm in net.nnet.parameters():
-                        prm.mul_(1.0 + eps * (2.0 * torch.rand(prm.shape, generator=g, dtype=torch.float64) - 1.0)
-                                 .to(prm.dtype))
-            for ep in base["episodes"]:
-                args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"],
-                                "tempThreshold": cfg["temp_threshold"]})
-                mcts = RecMCTS(net, args)
-                mcts.counts = []
-                np.random.seed(ep["seed"])
-                Coach(game0, net, args).executeEpisode((game0.restarted(), mcts))
-                first = None
-                for m, (mine, ref) in enumerate(zip(mcts.counts, ep["moves"])):
-                    if mine != {a: c for a, c in ref["counts"]}:
-                        first = m
-                        break
-                if first is None and len(mcts.counts) != ep["n_moves"]:
-                    first = min(len(mcts.counts), ep["n_moves"])
-                out["runs"].append({"kind": kind, "eps": eps, "seed": ep["seed"], "first_divergent_move": first,
-                                    "moves": len(mcts.counts), "reference_moves": ep["n_moves"]})
-                print(f"  {kind} eps {eps:g} seed {ep['seed']}: first divergent move {first}", flush=True)
-    _dump("realnet_sensitivity.json.gz", out)
+    out = {"runs": []}
+    for bname in bases:
+        base = json.load(gzip.open(os.path.join(HERE, f"mcts_{bname}.json.gz"), "rt"))
+        cfg = base["config"]
+        game0 = OthelloGame(cfg["n"]) if othello else InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
+        for kind in kinds:
+            for eps in (1e-7, 1e-6):
+                torch.manual_seed(0)
+                net = NoisyNNet(game0)
+                NoisyNNet.eps = eps if kind == "outputs" else 0.0
+                if kind == "weights":
+                    g = torch.Generator().manual_seed(12345)
+                    with torch.no_grad():
+                        for prm in net.nnet.parameters():
+                            prm.mul_(1.0 + eps * (2.0 * torch.rand(prm.shape, generator=g, dtype=torch.float64)
+                                                  - 1.0).to(prm.dtype))
+                for ep in base["episodes"]:
+                    args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"],
+                                    "tempThreshold": cfg["temp_threshold"]})
+                    mcts = RecMCTS(net, args)
+                    mcts.counts = []
+                    np.random.seed(ep["seed"])
+                    Coach(game0, net, args).executeEpisode((game0.restarted(), mcts))
+                    first = None
+                    for m, (mine, ref) in enumerate(zip(mcts.counts, ep["moves"])):
+                        if mine != {a: c for a, c in ref["counts"]}:
+                            first = m
+                            break
+                    if first is None and len(mcts.counts) != ep["n_moves"]:
+                        first = min(len(mcts.counts), ep["n_moves"])
+                    out["runs"].append({"set": bname, "kind": kind, "eps": eps, "seed": ep["seed"],
+                                        "first_divergent_move": first, "moves": len(mcts.counts),
+                                        "reference_moves": ep["n_moves"]})
+                    print(f"  {bname} {kind} eps {eps:g} seed {ep['seed']}: first divergent move {first}",
+                          flush=True)
+    if not othello:
+        out["config"] = cfg
+    _dump("realnet_sensitivity_othello.json.gz" if othello else "realnet_sensitivity.json.gz", out)
 
 
 # ------------------------------------------------------------------------- train
@@ -597,9 +622,11 @@ def main():
         "mcts": lambda: gen_mcts(np, quick),
         "othello": lambda: gen_mcts(np, quick, othello=True),
         "realnet": lambda: gen_mcts(np, quick, realnet=True),
+        "realnet_othello": lambda: gen_mcts(np, quick, othello=True, realnet=True),
         "arena": lambda: gen_arena(np),
         "train": lambda: gen_train(np),
         "sensitivity": lambda: gen_realnet_sensitivity(np),
+        "sensitivity_othello": lambda: gen_realnet_sensitivity(np, othello=True),
     }
     for name, fn in jobs.items():
         if only and name not in only:

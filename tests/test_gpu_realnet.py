@@ -1,11 +1,13 @@
 """Search parity with the PRODUCTION evaluator: the engine driven by the real
 network reproduces the reference's visit counts with the reference's own network.
 
-Fixtures (tests/golden/make_golden.py `realnet`): the reference Coach.executeEpisode
-(Coach.py:41-90) + MCTS (MCTS.py:33-145) with the reference NNetWrapper
-(inflexion/pytorch/NNet.py:78-94, batch-1 CPU f32) over the 512-channel
-InflexionNNet built under torch.manual_seed(0) -- whole 344-move episodes at
-main.py's 25 sims (4 seeds), and 40-turn games at C3's 100 sims (2 seeds).
+Fixtures (tests/golden/make_golden.py `realnet`, `realnet_othello`): the reference
+Coach.executeEpisode (Coach.py:41-90) + MCTS (MCTS.py:33-145) with the reference
+NNetWrapper (inflexion/pytorch/NNet.py:78-94, batch-1 CPU f32) over the 512-channel
+InflexionNNet built under torch.manual_seed(0) -- whole 344-move Inflexion episodes at
+main.py's 25 sims (4 seeds), 40-turn games at C3's 100 sims (2 seeds), and whole games
+of the builder's Othello plugin: 6x6 at 25 sims (C1, 4 seeds), 8x8 at 25 sims (2) and
+at C5's 200 sims (1).
 
 Each is replayed three ways:
   * the drop-in MCTS + Coach.executeEpisode with an NNetWrapper (batch-1 forward of
@@ -17,8 +19,9 @@ pi returned by getActionProb is a function of the counts (MCTS.py:48-60), so equ
 counts give pi exactly (tolerance 0, inside the north_star's 1e-5).
 
 What is asserted, per seed, against the reference's visit counts:
-  * the first MIN_PREFIX = 40 moves identical, count for count (the 40-move traces
-    SURVEY hard part 5 measured as robust to 1e-6 perturbations of the network);
+  * the first 40 moves identical, count for count (the 40-move traces SURVEY hard
+    part 5 measured as robust to 1e-6 perturbations of the network; 16 for the
+    32-60-move Othello games; the sims100 games must match entirely);
   * every later move identical up to the first difference, if any, and that
     difference a single search decision (one simulation of the move that took
     another action: two counts differing by one) AT A MOVE WHERE THE REFERENCE'S
@@ -51,21 +54,39 @@ class Args(dict):
     __getattr__ = dict.__getitem__
 
 
-def _ref_net():
+# per fixture set: game, board side, moves that must match before a certified near-tie may flip
+SETS = {"realnet_main": ("inflexion", 7, 40), "realnet_sims100": ("inflexion", 7, None),
+        "realnet_othello6": ("othello", 6, 16), "realnet_othello8": ("othello", 8, 16),
+        "realnet_othello8_s200": ("othello", 8, 16)}
+
+
+def _ref_net(game="inflexion", n=7):
+    """The reference's network for the game, as NNetWrapper(game) builds it under manual_seed(0)."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InflexionNNet
     torch.manual_seed(0)
-    return InflexionNNet().cuda().eval()
+    if game == "inflexion":
+        return InflexionNNet().cuda().eval()
+    return InflexionNNet(n=n, depth=2, action_size=n * n + 1).cuda().eval()
 
 
-def _margin_report(net, evaluator, board, turn, player, max_turns):
+def _game(name, cfg):
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.othello import OthelloGame
+    kind, n, _ = SETS[name]
+    return InflexionGame(7, max_turns=cfg["max_turns"], max_power=6) if kind == "inflexion" else OthelloGame(n)
+
+
+def _margin_report(net, evaluator, board, turn, player, template):
     """Root priors at a failing move: the evaluator on the GPU (at the batch size
     it ran at) against the reference's arithmetic (the module on the CPU, batch 1)."""
     import copy
     from azg_amd.flags import PlayerColour
-    from azg_amd.inflexion import InflexionGame
-    g = InflexionGame(7, max_turns=max_turns, board=np.asarray(board).reshape(7, 7).astype(int), curr_turn=turn,
-                      curr_player=PlayerColour.RED if player == 1 else PlayerColour.BLUE)
+    g = template.restarted()
+    n = g._n
+    g._board = np.asarray(board).reshape(n, n).astype(int)
+    g._curr_turn = turn
+    g._player = PlayerColour.RED if player == 1 else PlayerColour.BLUE
     x = torch.as_tensor(g.to_planes(), dtype=torch.float32).unsqueeze(0)
     with torch.no_grad():
         p_ref = torch.exp(copy.deepcopy(net).cpu()(x)[0][0]).numpy()
@@ -80,21 +101,23 @@ def _margin_report(net, evaluator, board, turn, player, max_turns):
     return f"root prior error {float(np.max(np.abs(p_ev - p_ref)[valid])):.3g}, smallest prior gap {gap:.3g}"
 
 
-MIN_PREFIX = 40
-
-
-def _sensitivity():
+def _sensitivity(name):
+    fname = "realnet_sensitivity_othello.json.gz" if "othello" in name else "realnet_sensitivity.json.gz"
     try:
-        d = ol.load_json("realnet_sensitivity.json.gz")
+        d = ol.load_json(fname)
     except FileNotFoundError:
         return {}
-    return {(r["kind"], r["eps"], r["seed"]): r["first_divergent_move"] for r in d["runs"]}
+    return {(r["kind"], r["eps"], r["seed"]): r["first_divergent_move"] for r in d["runs"]
+            if r.get("set", "realnet_main") == name}
 
 
-def _check_episode(ep, counts, actions, n_moves, where, report, whole=False):
+def _check_episode(ep, counts, actions, n_moves, where, report, name):
     """Compare one episode with the reference; returns the first divergent move or None."""
+    min_prefix = SETS[name][2]
+    whole = min_prefix is None
+    A = len(counts[0]) if n_moves else 0
     for m, mv in enumerate(ep["moves"]):
-        want = ol.golden_counts(mv)
+        want = ol.golden_counts(mv, A)
         if m < n_moves and np.array_equal(counts[m], want) and actions[m] == mv["action"]:
             continue
         got = counts[m] if m < n_moves else None
@@ -103,9 +126,9 @@ def _check_episode(ep, counts, actions, n_moves, where, report, whole=False):
                f"(engine {got[diff[:8]].tolist() if got is not None else None}, reference {want[diff[:8]].tolist()})")
         single_flip = (got is not None and len(diff) == 2 and int(np.abs(got - want).sum()) == 2
                        and int(got.sum()) == int(want.sum()))
-        sens = _sensitivity()
+        sens = _sensitivity(name)
         certified = any(sens.get(("weights", eps, ep["seed"])) == m for eps in (1e-7, 1e-6))
-        if whole or m < MIN_PREFIX or not single_flip or not certified:
+        if whole or m < min_prefix or not single_flip or not certified:
             raise AssertionError(msg + "; " + report(mv) + ("" if certified else "; the reference's own trace does "
                                  "not diverge at this move when its weights move by 1e-7 or 1e-6"))
         print(f"NEAR-TIE FLIP {msg}; {report(mv)}; identical through move {m - 1}; the reference's own trace with "
@@ -117,20 +140,22 @@ def _check_episode(ep, counts, actions, n_moves, where, report, whole=False):
     return None
 
 
-@pytest.mark.parametrize("name,k", [("realnet_main", 0), ("realnet_main", 1), ("realnet_sims100", 0)])
+@pytest.mark.parametrize("name,k", [("realnet_main", 0), ("realnet_main", 1), ("realnet_sims100", 0),
+                                    ("realnet_othello6", 0), ("realnet_othello6", 1), ("realnet_othello6", 2),
+                                    ("realnet_othello6", 3)])
 def test_dropin_mcts_real_net(name, k):
-    """Drop-in MCTS + Coach.executeEpisode with an NNetWrapper, whole episodes."""
+    """Drop-in MCTS + Coach.executeEpisode with an NNetWrapper, whole episodes (for the
+    6x6 Othello sets: BASELINE configs[0], C1, the reference main.py path on one game)."""
     import hashlib
     import azg_amd  # noqa: F401
     from azg_amd.coach import Coach
-    from azg_amd.inflexion import InflexionGame
     from azg_amd.mcts import MCTS
     from azg_amd.nnet import NNetWrapper
 
     data = ol.load_json(f"mcts_{name}.json.gz")
     cfg, ep = data["config"], data["episodes"][k]
     args = Args(numMCTSSims=cfg["sims"], cpuct=cfg["cpuct"], tempThreshold=cfg["temp_threshold"])
-    game = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
+    game = _game(name, cfg)
     torch.manual_seed(0)
     wrapper = NNetWrapper(game, device="cuda")
     counts, actions = [], []
@@ -141,21 +166,22 @@ def test_dropin_mcts_real_net(name, k):
             counts.append(self._engine.root_counts(0))
             return p
 
-    orig = InflexionGame.to_next_state
+    cls = type(game)
+    orig = cls.to_next_state
 
     def tns(self, a):
         actions.append(int(a))
         return orig(self, a)
     np.random.seed(ep["seed"])
-    InflexionGame.to_next_state = tns
+    cls.to_next_state = tns
     try:
         ex = Coach(game, wrapper, args).executeEpisode((game.restarted(), RecMCTS(wrapper, args)))
     finally:
-        InflexionGame.to_next_state = orig
+        cls.to_next_state = orig
     net = wrapper.nnet.eval()
     flip = _check_episode(ep, counts, actions, len(counts), "drop-in MCTS",
                           lambda mv: _margin_report(net, None, mv["board"], mv["turn"], 1 - 2 * (mv["turn"] % 2),
-                                                    cfg["max_turns"]), whole=name == "realnet_sims100")
+                                                    game), name)
     if flip is None:  # the same game: the same examples and RNG position as the reference's
         pol = hashlib.sha256(np.array([e[1] for e in ex], np.float64).tobytes()).hexdigest()
         assert pol == ep["policy_sha256"] and len(ex) == ep["n_examples"]
@@ -163,23 +189,28 @@ def test_dropin_mcts_real_net(name, k):
 
 
 @pytest.mark.parametrize("gemm", ["split", "f32"])
-@pytest.mark.parametrize("name", ["realnet_main", "realnet_sims100"])
+@pytest.mark.parametrize("name", ["realnet_main", "realnet_sims100", "realnet_othello6", "realnet_othello8",
+                                  "realnet_othello8_s200"])
 def test_engine_real_net_4096_games(name, gemm):
     """The batched engine with the production evaluator at 4096 games: the
     fixture's seeds are game slots of a full-size run (seed = slot index +
-    first_game), the other slots are ordinary games in the same leaf batches."""
+    first_game), the other slots are ordinary games in the same leaf batches
+    (C4 / C3 shapes for Inflexion, C5's 8x8 x 200 sims for Othello)."""
     import azg_amd  # noqa: F401
     from azg_amd.engine import SelfPlayEngine
     from azg_amd.nnet import InferenceNet
 
     data = ol.load_json(f"mcts_{name}.json.gz")
     cfg, eps = data["config"], data["episodes"]
+    kind, n, _ = SETS[name]
     seeds = [ep["seed"] for ep in eps]
     assert seeds == list(range(seeds[0], seeds[0] + len(seeds)))
-    net = _ref_net()
+    net = _ref_net(kind, n)
     ev = InferenceNet(net, gemm=gemm)
+    game = _game(name, cfg)
     e = SelfPlayEngine(G_ENGINE, sims=cfg["sims"], cpuct=cfg["cpuct"], temp_threshold=cfg["temp_threshold"],
-                       max_turns=cfg["max_turns"], seed_base=0, first_game=seeds[0], evaluator=ev)
+                       max_turns=cfg.get("max_turns", 343), seed_base=0, first_game=seeds[0], evaluator=ev,
+                       game=kind, n=n)
     e.play()
     st = e.stats()
     assert st["error"] == 0
@@ -189,7 +220,7 @@ def test_engine_real_net_4096_games(name, gemm):
     for i, ep in enumerate(eps):
         flip = _check_episode(ep, rec["counts"][i], rec["actions"][i], int(rec["moves"][i]), f"engine gemm={gemm}",
                               lambda mv: _margin_report(net, ev, mv["board"], mv["turn"], 1 - 2 * (mv["turn"] % 2),
-                                                        cfg["max_turns"]), whole=name == "realnet_sims100")
+                                                        game), name)
         if flip is None:
             whole += 1
             assert state["boards"][i].tolist() == ep["final_board"]
