@@ -16,6 +16,8 @@ break (MCTS.py:48-60) run here on the host from the engine's root counts.
 the GPU, batched), a torch module returning (log_softmax, tanh), or the string
 "stub" (hash evaluator used by the parity tests).
 """
+import warnings
+
 import numpy as np
 import torch
 
@@ -53,11 +55,17 @@ def whole_game_capacity(sims, game):
 
 
 class MCTS:
-    def __init__(self, nnet, args, device=None, node_capacity=None):
+    def __init__(self, nnet, args, device=None, node_capacity=None, graph=True):
         self.nnet = nnet
         self.args = args
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.node_capacity = node_capacity  # None: whole_game_capacity
+        # graph: after one eager getActionProb, the numMCTSSims simulations of a call are
+        # captured once as a HIP graph and replayed (the search is launch-bound at one
+        # leaf per simulation); an evaluator that cannot be captured stays eager
+        self.graph = bool(graph)
+        self._sims_graph = None
+        self._warm = False
         self._engine = None
         self._max_turns = None
 
@@ -73,7 +81,40 @@ class MCTS:
                                           evaluator=_evaluator_of(self.nnet, self.device), device=self.device,
                                           node_capacity=cap, max_depth=1024, gc=False, record=False)
             self._max_turns = spec
+            self._sims_graph, self._warm = None, False
         return self._engine
+
+    def _capture(self, eng, sims):
+        """Record `sims` simulations (select, network, expand/backup) as one graph.
+        Capturing launches nothing, so the tree is unchanged."""
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.device)
+        try:
+            with torch.cuda.device(self.device), torch.cuda.graph(g):
+                for _ in range(sims):
+                    eng.simulate()
+        except RuntimeError as e:
+            warnings.warn(f"MCTS: evaluator not graph-capturable ({e}); searching eagerly")
+            self.graph = False
+            torch.cuda.synchronize(self.device)
+            return None
+        self._sims_graph = g
+        return g
+
+    def _simulate(self, eng, sims):
+        if not self.graph or sims != int(self.args.numMCTSSims):
+            for _ in range(sims):
+                eng.simulate()
+            return
+        g = self._sims_graph
+        if g is None and self._warm:
+            g = self._capture(eng, sims)
+        if g is not None:
+            g.replay()
+            return
+        for _ in range(sims):  # first call: eager, initialises the evaluator's libraries
+            eng.simulate()
+        self._warm = True
 
     def _run(self, game, sims):
         if game.outcome != GameOutcome.ONGOING:
@@ -82,8 +123,7 @@ class MCTS:
         state = np.random.get_state()
         eng.set_rng(0, state[1], state[2])
         eng.set_root(0, game._board, game._curr_turn, game.player.num)
-        for _ in range(sims):
-            eng.simulate()
+        self._simulate(eng, sims)
         # a full node pool (or any engine error) stops the slot's search: raise rather
         # than return counts from a truncated search (azg_active_games reports it)
         eng.active()
@@ -114,4 +154,4 @@ class MCTS:
         return self._engine.stats() if self._engine is not None else {}
 
     def reset(self):
-        return MCTS(self.nnet, self.args, self.device, self.node_capacity)
+        return MCTS(self.nnet, self.args, self.device, self.node_capacity, self.graph)

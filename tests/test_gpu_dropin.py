@@ -237,3 +237,44 @@ def test_blue_first_dropin_matches_red_first_reference():
         pol = hashlib.sha256(np.array([e[1] for e in ex], np.float64).tobytes()).hexdigest()
         brd = hashlib.sha256(np.array([e[0] for e in ex], np.int64).tobytes()).hexdigest()
         assert pol == ep["policy_sha256"] and brd == ep["board_sha256"] and len(ex) == ep["n_examples"]
+
+
+@pytest.mark.parametrize("game_name", ["inflexion", "othello6"])
+def test_dropin_graph_replay_matches_eager(game_name):
+    """The drop-in replays each call's numMCTSSims simulations as one captured HIP graph
+    (after one eager call): same root counts and the same numpy RNG stream as the eager
+    search, move for move, with the real network; prints the per-call times."""
+    import time
+
+    import azg_amd  # noqa: F401
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.mcts import MCTS
+    from azg_amd.nnet import NNetWrapper
+    from azg_amd.othello import OthelloGame
+
+    args = Args(numMCTSSims=25, cpuct=1, tempThreshold=15)
+    game = InflexionGame(7, max_turns=343, max_power=6) if game_name == "inflexion" else OthelloGame(6)
+    torch.manual_seed(0)
+    w = NNetWrapper(game, device="cuda")
+    runs = {}
+    for graph in (False, True):
+        np.random.seed(7)
+        mcts = MCTS(w, args, graph=graph)
+        g = game.restarted()
+        counts, times = [], []
+        for m in range(8):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            pi = mcts.getActionProb(g, temp=1)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+            counts.append(mcts._engine.root_counts(0).copy())
+            g = g.to_next_state(int(np.random.choice(len(pi), p=pi)))
+        runs[graph] = (counts, times, np.random.randint(0, 2**32, size=2, dtype=np.uint32).tolist())
+        assert (mcts._sims_graph is not None) == graph
+    for m, (a, b) in enumerate(zip(runs[False][0], runs[True][0])):
+        assert np.array_equal(a, b), m
+    assert runs[False][2] == runs[True][2]
+    eager, graphed = np.median(runs[False][1][2:]), np.median(runs[True][1][2:])
+    print(f"\n{game_name}: getActionProb eager {eager * 1e3:.2f} ms, graph {graphed * 1e3:.2f} ms "
+          f"({25 / graphed:.0f} sims/s)")
