@@ -185,11 +185,11 @@ def test_replay_form_accurate_where_split_overflows():
     from azg_amd.engine import SelfPlayEngine
     from azg_amd.nnet import InferenceNet, replay_form
     net = _overflowing_net()
-    e = SelfPlayEngine(4096, evaluator="stub", sims=3, max_turns=343)
+    e = SelfPlayEngine(1024, evaluator="stub", sims=3, max_turns=343)
     e.move()
     e.move()
     e.simulate()
-    x = e.planes.clone()  # a real 4096-leaf batch
+    x = e.planes.clone()  # a real 1024-leaf batch
     e.close()
     split = InferenceNet(net)
     with torch.no_grad():
@@ -278,3 +278,27 @@ def test_dropin_graph_replay_matches_eager(game_name):
     eager, graphed = np.median(runs[False][1][2:]), np.median(runs[True][1][2:])
     print(f"\n{game_name}: getActionProb eager {eager * 1e3:.2f} ms, graph {graphed * 1e3:.2f} ms "
           f"({25 / graphed:.0f} sims/s)")
+
+
+def test_arena_replays_with_f32_form_where_split_overflows():
+    """BatchedArena.playGames with a network that trips the split form's
+    range flag replays the games with nnet.replay_form -- the same results and moves
+    as an arena run on the replay form from the start."""
+    import azg_amd  # noqa: F401
+    from azg_amd.arena import BatchedArena
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.nnet import InferenceNet, NNetWrapper, replay_form
+
+    net = _overflowing_net()
+    game = InflexionGame(7, max_turns=12, max_power=6)
+    args = Args(numMCTSSims=3, cpuct=1)
+    wrapper = NNetWrapper(game)
+    wrapper.nnet = net
+    arena = BatchedArena(game, wrapper, args, opponent="greedy")
+    assert isinstance(arena.evaluator, InferenceNet) and arena.evaluator.gemm != "f32"
+    got = arena.playGames(128)  # 128 leaves a forward: the split-fp16 Winograd form
+    assert arena.evaluator.gemm == "f32"
+    ref_arena = BatchedArena(game, wrapper, args, opponent="greedy", evaluator=replay_form(net))
+    assert got == ref_arena.playGames(128)
+    assert np.array_equal(arena.last_moves["actions"], ref_arena.last_moves["actions"])
+    assert np.array_equal(arena.last_engine_state["boards"], ref_arena.last_engine_state["boards"])

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 3: the whole GPU suite (as the driver runs it) + smoke; stop at the first abnormal exit
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -v -m gpu --timeout 400 --timeout-method thread > gpurun_out/r03_pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -v -m gpu --timeout 400 --timeout-method thread --durations=40 > gpurun_out/r03_pytest_gpu.log 2>&1
 rc=$?
 echo "gpu tests rc=$rc"
 tail -3 gpurun_out/r03_pytest_gpu.log
