@@ -83,6 +83,7 @@ SIGNATURES = [
                                               _VP]),
     ("azg_split_gemm_variant", ctypes.c_int, [_I32, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
     ("azg_split_gemm_pick", ctypes.c_int, [_I32, _VP, _VP, _I32]),
+    ("azg_set_gemm_blocks", ctypes.c_int, [_I32]),
     ("azg_split_gemm_stamps", ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP, _I64, _VP]),
     ("azg_set_arena", ctypes.c_int, [_VP, _VP, _VP, _VP]),
     ("azg_opponent_move", ctypes.c_int, [_VP, _I32, _VP]),

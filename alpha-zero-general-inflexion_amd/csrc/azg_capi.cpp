@@ -51,13 +51,16 @@ struct azg_engine {
     size_t bytes;
 };
 
+// Zeroed on the caller's stream, ahead of azg_reset's kernels on that stream: a plain
+// hipMemset runs on the null stream, which a non-blocking stream (every torch side
+// stream) does not wait for, so the reset kernels could run first and be zeroed after.
 template <typename T>
-static int dalloc(azg_engine* e, T** p, size_t n) {
+static int dalloc(azg_engine* e, T** p, size_t n, hipStream_t st) {
     void* q = nullptr;
     size_t b = n * sizeof(T);
     if (b == 0) b = 16;
     HIP_TRY(hipMalloc(&q, b));
-    HIP_TRY(hipMemset(q, 0, b));
+    HIP_TRY(hipMemsetAsync(q, 0, b, st));
     e->allocs.push_back(q);
     e->bytes += b;
     *p = (T*)q;
@@ -66,7 +69,7 @@ static int dalloc(azg_engine* e, T** p, size_t n) {
 
 #define ALLOC(ptr, n)                          \
     do {                                       \
-        int _r = dalloc(e, &(ptr), (size_t)(n)); \
+        int _r = dalloc(e, &(ptr), (size_t)(n), (hipStream_t)stream); \
         if (_r) {                              \
             azg_destroy(e);                    \
             return _r;                         \

@@ -1338,6 +1338,9 @@ __global__ __launch_bounds__(512, 1) void split_gemm_384_kernel(SGArgs g) {
 
 }  // namespace
 
+// cap on the persistent grid (azg_set_gemm_blocks; 0: one block per CU)
+static int g_block_cap = 0;
+
 // one workgroup per CU (a block fills a CU: 128 KB of LDS), at most one per tile
 static unsigned persistent_blocks(int tiles) {
     static int cus = 0;
@@ -1347,7 +1350,17 @@ static unsigned persistent_blocks(int tiles) {
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
     }
-    return (unsigned)(tiles < cus ? tiles : cus);
+    const int n = g_block_cap > 0 && g_block_cap < cus ? g_block_cap : cus;
+    return (unsigned)(tiles < n ? tiles : n);
+}
+
+// Persistent split-GEMM launches use at most `blocks` workgroups (CUs) from now on, leaving
+// the other CUs to kernels of another stream (two half-batches on two streams: one's GEMM
+// beside the other's HBM-bound transforms); 0 restores one block per CU.  Process-wide.
+extern "C" int azg_set_gemm_blocks(int32_t blocks) {
+    if (blocks < 0) return AZG_ERR_ARG;
+    g_block_cap = blocks;
+    return 0;
 }
 
 static int split_gemm_launch(int variant, const void* A, const void* Bt, float* M, int32_t nruns,

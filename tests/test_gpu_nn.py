@@ -233,6 +233,24 @@ def test_split_gemm_384_rows_bit_equal_to_256_rows(runs, C, K):
     assert torch.equal(outs[0], outs[1])
 
 
+def test_split_gemm_grid_cap_bit_equal():
+    """azg_set_gemm_blocks caps the persistent grid (fewer CUs, more tiles per block):
+    each tile's arithmetic is unchanged, so the results are the uncapped launch's bits;
+    a negative cap is rejected."""
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    L = _lib.lib()
+    runs = [(3, 385), (2, 768)]
+    ref = _run_split_gemm(4, runs, 64, 512)[2]
+    try:
+        for cap in (1, 7, 100):
+            _lib.check(L.azg_set_gemm_blocks(cap))
+            assert torch.equal(_run_split_gemm(4, runs, 64, 512)[2], ref), cap
+    finally:
+        _lib.check(L.azg_set_gemm_blocks(0))
+    assert L.azg_set_gemm_blocks(-1) == -1
+
+
 def _run_split_gemm(variant, runs, C, K):
     import ctypes
     import azg_amd  # noqa: F401

@@ -85,6 +85,40 @@ def test_random_seeds_vs_oracle(azg):
         assert np.array_equal(rec["counts"][i, :m], o["counts"])
 
 
+def test_engines_on_side_streams_match_golden(azg):
+    """Engines created and driven on torch side streams (non-blocking HIP streams), two
+    at once, their simulations interleaved: the golden traces bit for bit.  azg_create
+    zeroes its buffers on the caller's stream (a null-stream memset could land after the
+    reset kernels on a non-blocking stream: every game's node pool then reads full)."""
+    data = ol.load_json("mcts_short.json.gz")
+    cfg, eps = data["config"], data["episodes"]
+    half = len(eps) // 2
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    engs = []
+    for k, s in enumerate(streams):
+        with torch.cuda.stream(s):
+            engs.append(azg.SelfPlayEngine(half, sims=cfg["sims"], cpuct=cfg["cpuct"],
+                                           temp_threshold=cfg["temp_threshold"], max_turns=cfg["max_turns"],
+                                           seed_base=0, first_game=eps[k * half]["seed"], evaluator="stub"))
+    for _ in range(cfg["max_turns"] + 1):
+        for _ in range(cfg["sims"]):
+            for e, s in zip(engs, streams):
+                with torch.cuda.stream(s):
+                    e.simulate()
+        for e, s in zip(engs, streams):
+            with torch.cuda.stream(s):
+                e.move_end()
+    torch.cuda.synchronize()
+    for k, e in enumerate(engs):
+        assert e.stats()["error"] == 0
+        rec = e.read_moves()
+        for i, ep in enumerate(eps[k * half:(k + 1) * half]):
+            assert rec["moves"][i] == ep["n_moves"]
+            for m, mv in enumerate(ep["moves"]):
+                assert np.array_equal(rec["counts"][i, m], ol.golden_counts(mv)), (ep["seed"], m)
+        e.close()
+
+
 @pytest.mark.parametrize("name", ["othello6", "othello8", "othello8_s200"])
 def test_othello_golden_traces_bit_exact(azg, name):
     """Othello (builder-authored plugin) searched on the GPU vs the reference
