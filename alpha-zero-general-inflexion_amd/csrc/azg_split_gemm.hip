@@ -1357,9 +1357,11 @@ static unsigned persistent_blocks(int tiles) {
 // Persistent split-GEMM launches use at most `blocks` workgroups (CUs) from now on, leaving
 // the other CUs to kernels of another stream (two half-batches on two streams: one's GEMM
 // beside the other's HBM-bound transforms); 0 restores one block per CU.  Process-wide.
+// Rounded down to a multiple of 8 (at least 8): the persistent kernels deal each XCD
+// (blockIdx % 8) a contiguous tile range, so every XCD needs a block.
 extern "C" int azg_set_gemm_blocks(int32_t blocks) {
     if (blocks < 0) return AZG_ERR_ARG;
-    g_block_cap = blocks;
+    g_block_cap = blocks == 0 ? 0 : (blocks < 8 ? 8 : blocks & ~7);
     return 0;
 }
 

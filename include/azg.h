@@ -233,9 +233,10 @@ int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, floa
                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
 /* The schedule azg_split_gemm picks for a launch of this shape (4, 17 or 18). */
 int  azg_split_gemm_pick(int32_t nruns, const int32_t* points, const int32_t* rows, int32_t k);
-/* Cap the persistent split GEMM's grid at `blocks` workgroups (one per CU; 0 = every CU),
- * process-wide, so that a second stream's kernels (the other half-batch's transforms)
- * find CUs free beside it.  Results do not depend on it. */
+/* Cap the persistent split GEMM's grid at `blocks` workgroups (one per CU; 0 = every CU;
+ * rounded down to a multiple of 8, at least 8: one per XCD tile range), process-wide, so
+ * that a second stream's kernels (the other half-batch's transforms) find CUs free
+ * beside it.  Results do not depend on it. */
 int  azg_set_gemm_blocks(int32_t blocks);
 /* Diagnostic build of the default split GEMM with in-kernel s_memtime stamps
  * (results as azg_split_gemm): per wave (block b, wave w) the cycle sums of

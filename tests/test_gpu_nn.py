@@ -243,7 +243,7 @@ def test_split_gemm_grid_cap_bit_equal():
     runs = [(3, 385), (2, 768)]
     ref = _run_split_gemm(4, runs, 64, 512)[2]
     try:
-        for cap in (1, 7, 100):
+        for cap in (1, 7, 8, 100, 200):
             _lib.check(L.azg_set_gemm_blocks(cap))
             assert torch.equal(_run_split_gemm(4, runs, 64, 512)[2], ref), cap
     finally:
