@@ -49,8 +49,10 @@ def group(name):
         return "winograd_in"
     if "winograd_out" in name:
         return "winograd_out"
-    if "split_gemm" in name:
+    if "split_gemm_persist" in name:  # the 256-row persistent schedule: conv2-4, fc1 (bench's `roofline`)
         return "split_gemm"
+    if "split_gemm" in name:  # 128 / 64-row schedules: fc2, [fc3 | fc4] at 4096 leaves
+        return "split_gemm_small"
     if name.startswith("Cijk_"):
         return "gemm (hipBLASLt)"
     return None
