@@ -256,7 +256,7 @@ def gen_mcts(np, quick, othello=False, realnet=False):
     if realnet:
         sets = {
             # main.py's configuration, whole episodes: every move's counts pinned
-            "realnet_main": dict(max_turns=343, sims=25, cpuct=1, temp_threshold=30, seeds=[0, 1, 2, 3]),
+            "realnet_main": dict(max_turns=343, sims=25, cpuct=1, temp_threshold=30, seeds=list(range(8))),
             # C3's 100 simulations per move on 40-turn games
             "realnet_sims100": dict(max_turns=40, sims=100, cpuct=1, temp_threshold=30, seeds=[10, 11]),
         }
