@@ -230,3 +230,33 @@ def test_engine_real_net_4096_games(name, gemm):
             assert e.get_rng(i)[1] == ep["rng_pos"]
     print(f"{name} gemm={gemm}: {whole} of {len(eps)} games identical to the reference move for move")
     e.close()
+
+
+@pytest.mark.parametrize("G", [4093, 1500, 1024])
+def test_real_net_batch_composition_invariance(G):
+    """Every leaf's evaluation depends on its own planes only: the production evaluator's
+    GEMMs, transforms and split-K FC tail never mix rows, whatever the batch size and
+    whichever GEMM schedule (persistent 256-row tiles, 128 / 64-row tiles) the size picks.
+    So the games a G-game run shares with the 4096-game run -- ragged last tiles and the
+    highest slots included -- have the same visit counts and actions bit for bit.  (At
+    least 1024 leaves: below FC1_SPLIT_MIN_BATCH the FC tail is the f32 one, other bits.)"""
+    import azg_amd  # noqa: F401
+    from azg_amd.engine import SelfPlayEngine
+    from azg_amd.nnet import InferenceNet
+
+    net = _ref_net()
+    ev = InferenceNet(net)
+    recs = {}
+    for g in (G_ENGINE, G):
+        e = SelfPlayEngine(g, sims=25, cpuct=1, temp_threshold=30, max_turns=343, seed_base=0, first_game=0,
+                           evaluator=ev)
+        for _ in range(3):
+            e.move()
+        e.check_evaluator()
+        assert e.stats()["error"] == 0
+        recs[g] = e.read_moves()
+        e.close()
+    a, b = recs[G_ENGINE], recs[G]
+    assert np.array_equal(a["moves"][:G], b["moves"])
+    assert np.array_equal(a["actions"][:G, :3], b["actions"][:, :3])
+    assert np.array_equal(a["counts"][:G, :3], b["counts"][:, :3])
