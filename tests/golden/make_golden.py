@@ -270,9 +270,9 @@ def gen_mcts(np, quick, othello=False, realnet=False):
         }
         if realnet:  # C1 (6x6, one episode, 25 sims) and C5 (8x8, 200 sims) with the reference NNetWrapper
             sets = {
-                "realnet_othello6": dict(n=6, sims=25, cpuct=1, temp_threshold=15, seeds=[500, 501, 502, 503]),
-                "realnet_othello8": dict(n=8, sims=25, cpuct=1, temp_threshold=30, seeds=[600, 601]),
-                "realnet_othello8_s200": dict(n=8, sims=200, cpuct=1, temp_threshold=30, seeds=[700]),
+                "realnet_othello6": dict(n=6, sims=25, cpuct=1, temp_threshold=15, seeds=list(range(500, 508))),
+                "realnet_othello8": dict(n=8, sims=25, cpuct=1, temp_threshold=30, seeds=[600, 601, 602, 603]),
+                "realnet_othello8_s200": dict(n=8, sims=200, cpuct=1, temp_threshold=30, seeds=[700, 701, 702]),
             }
     for name, cfg in sets.items():
         eps = []

@@ -140,9 +140,8 @@ def _check_episode(ep, counts, actions, n_moves, where, report, name):
     return None
 
 
-@pytest.mark.parametrize("name,k", [("realnet_main", 0), ("realnet_main", 1), ("realnet_sims100", 0),
-                                    ("realnet_othello6", 0), ("realnet_othello6", 1), ("realnet_othello6", 2),
-                                    ("realnet_othello6", 3)])
+@pytest.mark.parametrize("name,k", [("realnet_main", 0), ("realnet_main", 1), ("realnet_sims100", 0)]
+                         + [("realnet_othello6", i) for i in range(8)] + [("realnet_othello8", 0)])
 def test_dropin_mcts_real_net(name, k):
     """Drop-in MCTS + Coach.executeEpisode with an NNetWrapper, whole episodes (for the
     6x6 Othello sets: BASELINE configs[0], C1, the reference main.py path on one game)."""
