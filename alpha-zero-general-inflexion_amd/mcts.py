@@ -65,6 +65,7 @@ class MCTS:
         # leaf per simulation); an evaluator that cannot be captured stays eager
         self.graph = bool(graph)
         self._sims_graph = None
+        self._graph_sims = 0
         self._warm = False
         self._engine = None
         self._max_turns = None
@@ -98,7 +99,7 @@ class MCTS:
             self.graph = False
             torch.cuda.synchronize(self.device)
             return None
-        self._sims_graph = g
+        self._sims_graph, self._graph_sims = g, sims
         return g
 
     def _simulate(self, eng, sims):
@@ -107,6 +108,8 @@ class MCTS:
                 eng.simulate()
             return
         g = self._sims_graph
+        if g is not None and self._graph_sims != sims:  # args.numMCTSSims changed since the capture
+            g = self._sims_graph = None
         if g is None and self._warm:
             g = self._capture(eng, sims)
         if g is not None:
