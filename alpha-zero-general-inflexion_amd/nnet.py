@@ -28,6 +28,10 @@ DEFAULT_ARGS = dict(lr=0.001, dropout=0.3, epochs=10, batch_size=512, num_channe
                     # (profiles/r01_train_probe.json)
                     fused_adam=False, train_dtype="f32")
 WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C1: 1 game)
+# below WINOGRAD_MIN_BATCH: the whole forward on libazg's small f32 GEMMs (azg_small.hip) instead of
+# MIOpen / hipBLASLt.  Off by default: correct (tests/test_gpu_nn.py) but measured slower at one leaf
+# (3.8 vs 3.1 ms per 25-simulation getActionProb, profiles/r03_small_path.json)
+SMALL_PATH = False
 FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
 FC1_KPARTS = 4  # split-K parts of fc1 on libazg's split GEMM (4608 = 4 x 1152 for the 7x7 board)
 # split-K parts of fc2 (1024 -> 512) and [fc3 | fc4] (512 -> 344, padded to 512 columns) when the whole
@@ -232,7 +236,7 @@ class InferenceNet(nn.Module):
 
     outputs_probs = True
 
-    def __init__(self, net: InflexionNNet, conv="winograd", gemm="split"):
+    def __init__(self, net: InflexionNNet, conv="winograd", gemm="split", small=None):
         """conv (conv2-4): "winograd" (default; Winograd F(5,3)/F(4,3)/F(3,3) tiles: libazg
         fused input / output transforms around one GEMM per transformed point, bias + ReLU
         in the output transform, 3.8x fewer multiply-adds), "miopen" (MIOpen implicit GEMM + one fused
@@ -245,7 +249,10 @@ class InferenceNet(nn.Module):
         fp16 hi + lo, hi*hi + lo*hi + hi*lo on the fp16 MFMA with f32 accumulation in
         libazg's hand-written GEMM: f32-accurate products -- measured error at or below
         the f32 GEMM's), "split_blas" (the same products as one hipBLASLt fp16 GEMM
-        over [hi | lo | hi] rows) or "f32" (f32 MFMA GEMMs, hipBLASLt)."""
+        over [hi | lo | hi] rows) or "f32" (f32 MFMA GEMMs, hipBLASLt).
+
+        small: below WINOGRAD_MIN_BATCH leaves, run the whole forward on libazg's small f32
+        GEMMs (azg_small.hip) instead of MIOpen / hipBLASLt (None: SMALL_PATH)."""
         super().__init__()
         if conv not in ("miopen", "azg", "auto", "winograd"):
             raise ValueError(f"unknown conv implementation {conv!r}")
@@ -258,6 +265,10 @@ class InferenceNet(nn.Module):
         self.mscale = {}  # Winograd layer -> 2^-k undoing the split operand's scale
         self._choices = {}
         self._ws = None  # Winograd V / M workspace, grown to the largest layer seen
+        # below WINOGRAD_MIN_BATCH leaves: the whole forward on libazg's small f32 GEMMs
+        # (azg_small.hip) instead of MIOpen / hipBLASLt; conv="miopen" keeps the library
+        self.small_path = conv in ("winograd", "auto") and (SMALL_PATH if small is None else bool(small))
+        self._small_plans = {}
         self.h_out = {}  # output side per conv layer
         self.fuse_transforms = True  # conv2->3->4: output + next input transform in one pass
         self.n, self.depth, c = net.n, net.depth, net.num_channels
@@ -667,8 +678,77 @@ class InferenceNet(nn.Module):
                                             ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()), B, A, st))
         return p, v
 
+    @staticmethod
+    def _small_plan(Cin, taps, tiles):
+        """(kc, ksplit) for one small GEMM: K = taps x Cin in slabs of kc (the largest power
+        of two <= 64 dividing Cin, so a slab lies in one tap), split into ksplit ranges so
+        that tiles x ksplit blocks fill about one round of the chip (the largest divisor of
+        the slab count up to that target)."""
+        target = max(1, -(-256 // tiles))
+        kc = 64
+        while Cin % kc:  # the largest slab: a slab's loads are one round trip, so fewer, fuller slabs
+            kc //= 2
+        slabs = taps * Cin // kc
+        return kc, max(d for d in range(1, min(slabs, target) + 1) if slabs % d == 0)
+
+    def _small_gemm(self, key, x, strides, B, H, pad, taps, w, Cin, Cout, bias, relu):
+        """One layer on azg_small_gemm_partial + azg_small_gemm_reduce; returns the
+        [B * Ho * Ho, Cout] f32 output (NHWC rows)."""
+        import ctypes
+        from . import _lib
+        L = _lib.lib()
+        Ho = H + 2 * pad - 2 if taps == 9 else H
+        npx = B * Ho * Ho
+        plan = self._small_plans.get((key, B))
+        if plan is None:
+            plan = self._small_plans[(key, B)] = self._small_plan(Cin, taps, -(-Cout // 128) * -(-npx // 64))
+        kc, ks = plan
+        dev = x.device
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        part = torch.empty(ks * npx * Cout, device=dev, dtype=torch.float32)
+        y = torch.empty((npx, Cout), device=dev, dtype=torch.float32)
+        sB, sY, sX, sC = strides
+        _lib.check(L.azg_small_gemm_partial(ctypes.c_void_p(x.data_ptr()), sB, sY, sX, sC, B, H, H, pad, taps,
+                                            ctypes.c_void_p(w.data_ptr()), Cin, Cout, kc, ks,
+                                            ctypes.c_void_p(part.data_ptr()), st))
+        _lib.check(L.azg_small_gemm_reduce(ctypes.c_void_p(part.data_ptr()), ks, npx, Cout,
+                                           ctypes.c_void_p(bias.data_ptr()) if bias is not None else None, int(relu),
+                                           ctypes.c_void_p(y.data_ptr()), Cout, st))
+        return y
+
+    def _forward_small(self, planes):
+        """The forward below WINOGRAD_MIN_BATCH leaves on libazg's small f32 GEMMs:
+        conv1-4 (+ folded BN, bias, ReLU) from the NCHW leaf planes to NHWC activations,
+        fc1 / fc2 (+ ReLU), [fc3 | fc4] and azg_policy_value's softmax / tanh."""
+        import ctypes
+        from . import _lib
+        planes = planes.contiguous()
+        B, n, C = planes.shape[0], self.n, self.w1.shape[0]
+        x, strides, H = planes, (self.depth * n * n, n, 1, n * n), n
+        cin = self.depth
+        for i, pad in enumerate(self.pads, start=1):
+            w = getattr(self, f"w{i}")  # channels_last: [co][ky][kx][ci] in memory
+            x = self._small_gemm(f"conv{i}", x, strides, B, H, pad, 9, w, cin, C, getattr(self, f"b{i}"), True)
+            H = H + 2 * pad - 2
+            strides, cin = (H * H * C, H * C, C, 1), C
+        feat = H * H * C  # NHWC flatten (fw1's column order)
+        x = self._small_gemm("fc1", x, (feat, 0, 0, 1), B, 1, 0, 1, self.fw1, feat, self.fw1.shape[0], self.fb1, True)
+        n1 = self.fw1.shape[0]
+        x = self._small_gemm("fc2", x, (n1, 0, 0, 1), B, 1, 0, 1, self.fw2, n1, self.fw2.shape[0], self.fb2, True)
+        n2, A = self.fw2.shape[0], self.fw3.shape[0]
+        pv = self._small_gemm("fc34", x, (n2, 0, 0, 1), B, 1, 0, 1, self.fw34, n2, A + 1, None, False)
+        p = torch.empty((B, A), device=planes.device, dtype=torch.float32)
+        v = torch.empty((B, 1), device=planes.device, dtype=torch.float32)
+        _lib.check(_lib.lib().azg_policy_value(
+            ctypes.c_void_p(pv.data_ptr()), A + 1, ctypes.c_void_p(self.fb34.data_ptr()), 1.0,
+            ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()), B, A,
+            ctypes.c_void_p(torch.cuda.current_stream(planes.device).cuda_stream)))
+        return p, v
+
     def forward(self, s):
         planes = s.view(-1, self.depth, self.n, self.n)
+        if self.small_path and planes.is_cuda and planes.shape[0] < WINOGRAD_MIN_BATCH and self.fw3.shape[0] <= 1024:
+            return self._forward_small(planes)
         x = planes
         hook = self.conv_hook
         fused = x.is_cuda

@@ -231,6 +231,19 @@ int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, cons
  * on 384 x 256 tiles, results bit-identical to variant 4's); for tests and probes. */
 int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, float* m, int32_t nruns,
                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
+/* The leaf network at a few leaves (below the Winograd path's 64): one 3x3 conv
+ * (taps 9, zero padding pad) or FC layer (taps 1, H = W = 1) as a small f32 GEMM
+ * out[px][co] = sum_k w[co][k] x[k][px], k = tap * Cin + ci, w [Cout][taps][Cin] (a
+ * channels_last conv weight, BN folded; an FC weight [Cout][Cin]), x any layout given by
+ * its element strides (sB per leaf, sY, sX, sC), px = (leaf, y, x) of the Ho x Wo output.
+ * partial: K in slabs of kc (a power of two <= 64 dividing Cin), split into ksplit equal ranges
+ * (dividing the slab count), part [ksplit][px][Cout] f32; reduce: y[px * ldy + co] = (sum
+ * of the ksplit parts in order) + bias, ReLU if relu. */
+int  azg_small_gemm_partial(const float* x, int64_t sB, int32_t sY, int32_t sX, int32_t sC, int32_t batch,
+                            int32_t H, int32_t W, int32_t pad, int32_t taps, const float* w, int32_t Cin,
+                            int32_t Cout, int32_t kc, int32_t ksplit, float* part, void* stream);
+int  azg_small_gemm_reduce(const float* part, int32_t ksplit, int32_t npx, int32_t Cout, const float* bias,
+                           int32_t relu, float* y, int32_t ldy, void* stream);
 /* The schedule azg_split_gemm picks for a launch of this shape (4, 17 or 18). */
 int  azg_split_gemm_pick(int32_t nruns, const int32_t* points, const int32_t* rows, int32_t k);
 /* Cap the persistent split GEMM's grid at `blocks` workgroups (one per CU; 0 = every CU;

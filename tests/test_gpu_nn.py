@@ -453,3 +453,76 @@ def test_first_layer_any_planes(kind):
     fast.check_range()
     torch.testing.assert_close(p, torch.exp(logp), rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(v.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,H,pad,cin,cout", [(1, 7, 1, 4, 512), (1, 7, 1, 512, 512), (3, 7, 0, 512, 512),
+                                              (1, 5, 0, 512, 512), (63, 7, 1, 512, 512), (2, 8, 1, 2, 512),
+                                              (5, 6, 0, 64, 96), (1, 1, 0, 4608, 1024), (17, 1, 0, 1024, 512),
+                                              (7, 1, 0, 512, 344)])
+def test_small_gemm_matches_torch(B, H, pad, cin, cout):
+    """azg_small_gemm_partial + reduce (the forward below 64 leaves): a 3x3 conv (or an
+    FC layer, H = 1 and taps 1) + bias + ReLU against torch in f64, NCHW and NHWC inputs,
+    ragged pixel and channel counts, every K split the planner picks."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    from azg_amd.nnet import InferenceNet
+    torch.manual_seed(3)
+    taps = 9 if H > 1 else 1
+    x = torch.randn(B, cin, H, H, device="cuda")
+    w = torch.randn(cout, cin, 3, 3, device="cuda") / (cin * taps) ** 0.5 if taps == 9 else \
+        torch.randn(cout, cin, device="cuda") / cin ** 0.5
+    b = torch.randn(cout, device="cuda")
+    if taps == 9:
+        want = torch.relu(torch.nn.functional.conv2d(x.double(), w.double(), b.double(), padding=pad))
+        want = want.permute(0, 2, 3, 1).reshape(-1, cout)
+        wk = w.contiguous(memory_format=torch.channels_last)
+    else:
+        want = torch.relu(x.double().reshape(B, cin) @ w.double().t() + b.double())
+        wk = w.contiguous()
+    Ho = H + 2 * pad - 2 if taps == 9 else 1
+    for layout in ("nchw", "nhwc"):
+        if layout == "nchw":
+            xin, strides = x.contiguous(), (cin * H * H, H, 1, H * H)
+        else:
+            xin = x.permute(0, 2, 3, 1).contiguous()
+            strides = (H * H * cin, H * cin, cin, 1)
+        kc, ks = InferenceNet._small_plan(cin, taps, -(-cout // 128) * -(-(B * Ho * Ho) // 64))
+        npx = B * Ho * Ho
+        part = torch.full((ks * npx * cout,), float("nan"), device="cuda")
+        y = torch.full((npx, cout), float("nan"), device="cuda")
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        L = _lib.lib()
+        _lib.check(L.azg_small_gemm_partial(ctypes.c_void_p(xin.data_ptr()), *strides, B, H, H, pad, taps,
+                                            ctypes.c_void_p(wk.data_ptr()), cin, cout, kc, ks,
+                                            ctypes.c_void_p(part.data_ptr()), st))
+        _lib.check(L.azg_small_gemm_reduce(ctypes.c_void_p(part.data_ptr()), ks, npx, cout,
+                                           ctypes.c_void_p(b.data_ptr()), 1, ctypes.c_void_p(y.data_ptr()), cout, st))
+        torch.cuda.synchronize()
+        err = ((y.double() - want).abs() / (want.abs() + 1.0)).max().item()
+        assert err < 1e-5, (layout, err)
+
+
+@pytest.mark.parametrize("n,depth,A,B", [(7, 4, 343, 1), (7, 4, 343, 5), (7, 4, 343, 63), (6, 2, 37, 1),
+                                         (8, 2, 65, 3)])
+def test_small_forward_matches_reference(n, depth, A, B):
+    """Below 64 leaves InferenceNet(small=True) runs on libazg's small GEMMs (no MIOpen /
+    hipBLASLt): P and v within the north_star's 1e-5 of the reference module, and of the
+    MIOpen form."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    torch.manual_seed(0)
+    net = InflexionNNet(n=n, depth=depth, action_size=A).cuda().eval()
+    x = (torch.rand(B, depth, n, n, device="cuda") < 0.3).float()
+    if depth > 2:
+        x[:, 2] = 17.0
+    small = InferenceNet(net, small=True)
+    lib_form = InferenceNet(net, conv="miopen")
+    assert small.small_path and not lib_form.small_path
+    with torch.no_grad():
+        p, v = small(x)
+        p2, v2 = lib_form(x)
+        logp, v_ref = net(x)
+    torch.testing.assert_close(p, torch.exp(logp), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(v.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p, p2, rtol=1e-5, atol=1e-7)
