@@ -506,6 +506,31 @@ __device__ __forceinline__ size_t node_row(const Dev& E, int g, int id) {
     return ((size_t)g * E.M + id) * R::AP;
 }
 
+// Compact edge slots.  A node's row holds its edges (P, N, Q) only for the valid
+// actions of its key, packed in action order: the edge of valid action a sits at
+// slot ci = #(valid actions < a).  The valid set is a function of the key, which
+// every kernel that addresses a row already holds, so the mapping costs a ballot
+// and a popcount per 64 actions and no memory; a wave's reads of a row are then
+// nv contiguous elements (87 at a mean 7x7 Inflexion node: 3 + 3 + 6 lines of P, N,
+// Q) instead of scattered elements of all 12 + 12 + 24 lines of the 384-wide row.
+// Edge order equals action order, so first-index tie-breaks are unchanged.
+// Lane's action lane + 64 j gets slot ci[j] (-1: not valid); returns nv.
+template <class R>
+__device__ __forceinline__ int edge_slots(const typename R::VCtx& vc, int (&ci)[R::AJ]) {
+    const int lane = lane_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+    int base = 0;
+#pragma unroll
+    for (int j = 0; j < R::AJ; ++j) {
+        const int a = lane + WAVE * j;
+        const bool v = a < R::A && R::valid(a, vc);
+        const uint64_t b = __ballot(v);
+        ci[j] = v ? base + __popcll(b & below) : -1;
+        base += __popcll(b);
+    }
+    return base;
+}
+
 template <class R>
 __device__ __forceinline__ Pos load_root(const Dev& E, int g) {
     Pos p;
@@ -551,25 +576,28 @@ __device__ int table_lookup(const Dev& E, int g, uint64_t own, uint64_t opp, int
 }
 
 // PUCT argmax (MCTS.py:114-131): strict '>' scan in action order == max u,
-// ties to the lowest action; NaN never wins.
+// ties to the lowest action; NaN never wins.  Returns the action; *edge gets its
+// compact edge slot (edge_slots).
 template <class R>
-__device__ int puct_select(const Dev& E, int g, int id, const typename R::VCtx& vc) {
+__device__ int puct_select(const Dev& E, int g, int id, const typename R::VCtx& vc, int* edge) {
     const int lane = lane_id();
     const size_t row = node_row<R>(E, g, id);
     const int Ns = E.node_Ns[(size_t)g * E.M + id];
     const float sq_edge = (float)sqrt((double)Ns);
     const float sq_new = (float)sqrt((double)Ns + 1e-8);
+    int ci[R::AJ];
+    edge_slots<R>(vc, ci);
     float best = -INFINITY;
-    int besta = 0x7fffffff;
+    int besta = 0x7fffffff, besti = -1;
 #pragma unroll
     for (int j = 0; j < R::AJ; ++j) {
         const int a = lane + WAVE * j;
-        if (a < R::A && R::valid(a, vc)) {
-            const float cp = E.cpuct_f * E.node_P[row + a];
-            const uint32_t nr = E.node_N[row + a];
+        if (ci[j] >= 0) {
+            const float cp = E.cpuct_f * E.node_P[row + ci[j]];
+            const uint32_t nr = E.node_N[row + ci[j]];
             // Q loaded with P and N (not after N says the edge exists): one dependent
             // round trip less per level; the value is used only where N > 0
-            const double qv = E.node_Q[row + a];
+            const double qv = E.node_Q[row + ci[j]];
             const int n = (int)(nr & 0x7fffffffu);
             float u;
             if (n > 0) {
@@ -581,6 +609,7 @@ __device__ int puct_select(const Dev& E, int g, int id, const typename R::VCtx& 
             if (u > best) {
                 best = u;
                 besta = a;
+                besti = ci[j];
             }
         }
     }
@@ -588,11 +617,14 @@ __device__ int puct_select(const Dev& E, int g, int id, const typename R::VCtx& 
     for (int o = 32; o >= 1; o >>= 1) {
         const float ou = __shfl_xor(best, o);
         const int oa = __shfl_xor(besta, o);
+        const int oi = __shfl_xor(besti, o);
         if (ou > best || (ou == best && oa < besta)) {
             best = ou;
             besta = oa;
+            besti = oi;
         }
     }
+    *edge = besti;
     return besta == 0x7fffffff ? -1 : besta;
 }
 
@@ -645,7 +677,8 @@ __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__
             kind = slot < 0 ? LEAF_NONE : LEAF_EXPAND;
             break;
         }
-        const int a = puct_select<R>(E, g, id, R::vctx(own, opp, cs));
+        int ei;
+        const int a = puct_select<R>(E, g, id, R::vctx(own, opp, cs), &ei);
         if (a < 0) {
             set_err(E, g, -5);
             kind = LEAF_NONE;
@@ -656,7 +689,7 @@ __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__
             kind = LEAF_NONE;
             break;
         }
-        if (lane == 0) path[depth] = (id << 10) | a;
+        if (lane == 0) path[depth] = (id << 10) | ei;  // the edge's slot in the node's row
         depth++;
         R::apply(p, a, E.max_turns);
     }
@@ -735,10 +768,12 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
         const typename R::VCtx vc = R::vctx(own, opp, cs);
         float pv[R::AJ];
         bool vv[R::AJ];
+        int ci[R::AJ];
+        edge_slots<R>(vc, ci);
 #pragma unroll
         for (int j = 0; j < R::AJ; ++j) {
             const int a = lane + WAVE * j;
-            vv[j] = a < R::A && R::valid(a, vc);
+            vv[j] = ci[j] >= 0;
             float x = a < R::A ? Pin[(size_t)g * p_stride + a] : 0.0f;
             x = vv[j] ? x : x * 0.0f;  // policies *= valids
             pv[j] = x;
@@ -778,11 +813,14 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
             return;
         }
         const size_t ni = (size_t)g * E.M + id, row = ni * R::AP;
+        // the valid actions' edges only, in their compact slots (edge_slots); Q is read
+        // only where N > 0: no init
 #pragma unroll
         for (int j = 0; j < R::AJ; ++j) {
-            const int a = lane + WAVE * j;
-            E.node_P[row + a] = a < R::A ? pv[j] : 0.0f;
-            E.node_N[row + a] = 0u;  // Q is read only where N > 0: no init (3 KB less per expansion)
+            if (ci[j] >= 0) {
+                E.node_P[row + ci[j]] = pv[j];
+                E.node_N[row + ci[j]] = 0u;
+            }
         }
         if (lane == 0) {
             if (depth == 0) E.root_id[g] = id;
@@ -908,11 +946,12 @@ __global__ __launch_bounds__(WAVE) void move_end_kernel(Dev E) {
     int cs, kt, slot;
     R::key(p, own, opp, kt, cs);
     const int id = table_lookup(E, g, own, opp, kt, cs, &slot);
-    int cnt[R::AJ];
+    int cnt[R::AJ], ci[R::AJ];
+    edge_slots<R>(R::vctx(own, opp, cs), ci);
 #pragma unroll
     for (int j = 0; j < R::AJ; ++j) {
         const int a = lane + WAVE * j;
-        cnt[j] = (id >= 0 && a < R::A) ? (int)(E.node_N[node_row<R>(E, g, id) + a] & 0x7fffffffu) : 0;
+        cnt[j] = (id >= 0 && ci[j] >= 0) ? (int)(E.node_N[node_row<R>(E, g, id) + ci[j]] & 0x7fffffffu) : 0;
         s_cnt[a] = cnt[j];
     }
     const int m = E.moves[g];
@@ -1068,8 +1107,14 @@ __global__ __launch_bounds__(WAVE) void root_counts_kernel(Dev E, int g, int32_t
     int cs, kt, slot;
     R::key(p, own, opp, kt, cs);
     const int id = table_lookup(E, g, own, opp, kt, cs, &slot);
-    for (int a = lane; a < R::A; a += WAVE)
-        out[a] = id >= 0 ? (int)(E.node_N[node_row<R>(E, g, id) + a] & 0x7fffffffu) : 0;
+    int ci[R::AJ];
+    edge_slots<R>(R::vctx(own, opp, cs), ci);
+#pragma unroll
+    for (int j = 0; j < R::AJ; ++j) {
+        const int a = lane + WAVE * j;
+        if (a < R::A)
+            out[a] = (id >= 0 && ci[j] >= 0) ? (int)(E.node_N[node_row<R>(E, g, id) + ci[j]] & 0x7fffffffu) : 0;
+    }
 }
 
 // A fresh game in slot g (Coach.py:110-111): initial board, RED to move, numpy
