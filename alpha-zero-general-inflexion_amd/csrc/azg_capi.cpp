@@ -123,11 +123,8 @@ int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
     ALLOC(d.root_id, G);
     ALLOC(d.mt, G * azg::MT_N);
     ALLOC(d.mt_pos, G);
-    ALLOC(d.node_own, GM);
-    ALLOC(d.node_opp, GM);
+    ALLOC(d.node_key, GM);
     ALLOC(d.node_turn, GM);
-    ALLOC(d.node_cs, GM);
-    ALLOC(d.node_Ns, GM);
     ALLOC(d.node_P, GM * ROW);
     ALLOC(d.node_N, GM * ROW);
     ALLOC(d.node_Q, GM * ROW);

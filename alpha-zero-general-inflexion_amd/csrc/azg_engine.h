@@ -18,6 +18,14 @@ constexpr int MAX_POWER_AT_SPAWN = 48;   // InflexionGame.py:69
 enum Outcome : int { ONGOING = 0, DRAW = 1, WON = 2, LOST = 3 };
 enum LeafKind : int { LEAF_NONE = 0, LEAF_EXPAND = 1, LEAF_TERMINAL = 2 };
 
+// A node's key (own-pieces mask, opponent mask, turn, can_spawn) and visit count
+// Ns in one 32-B record: a lookup's key compare, an expansion's key writes and a
+// backup step's Ns update each touch one 32-B sector instead of one per field.
+struct alignas(32) NodeKey {
+    uint64_t own, opp;
+    int32_t turn, cs, Ns, pad;
+};
+
 // Game-specific sizes (cells, actions A, row stride = A rounded up to 64,
 // planes) are compile-time constants of the game traits in azg_kernels.hip;
 // the host sees them through GameOps (azg_launch.h).
@@ -38,11 +46,8 @@ struct Dev {
     int32_t* mt_pos;     // [G]
 
     // node pool [G*M]
-    uint64_t* node_own;
-    uint64_t* node_opp;
-    int32_t* node_turn;  // -1 = free
-    int32_t* node_cs;
-    int32_t* node_Ns;
+    NodeKey* node_key;   // key + Ns, one 32-B record per node
+    int32_t* node_turn;  // -1 = free (the node GC's scan reads this dense array)
     float* node_P;       // [G*M*AP]
     uint32_t* node_N;    // [G*M*AP]  bit31: Q is f32-typed
     double* node_Q;      // [G*M*AP]
@@ -52,7 +57,7 @@ struct Dev {
     uint64_t* table;     // [G*H] (tag << 32) | (id + 1), 0 = empty
 
     // search path / leaf
-    int32_t* path;       // [G*DMAX] (node << 10) | action
+    int32_t* path;       // [G*DMAX] (node << 10) | edge slot (compact, azg_kernels.hip edge_slots)
     int32_t* leaf_kind;  // [G]
     int32_t* leaf_depth; // [G]
     double* leaf_value;  // [G]

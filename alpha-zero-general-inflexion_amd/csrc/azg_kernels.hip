@@ -551,17 +551,21 @@ __device__ int table_lookup(const Dev& E, int g, uint64_t own, uint64_t opp, int
     const uint64_t* T = E.table + (size_t)g * E.H;
     const uint32_t hm = (uint32_t)E.H - 1;
     const uint32_t base = (uint32_t)h & hm;
-    for (int probe = 0; probe < E.H; probe += WAVE) {
+    // The first probe covers 16 slots (128 B: the table is at most half full, so a
+    // lookup almost always ends there), later ones 64; slots are visited in the same
+    // order either way, so the first match-or-empty is the same.
+    for (int probe = 0, width = 16; probe < E.H; probe += width, width = WAVE) {
+        const bool in = lane < width;
         const uint32_t s = (base + (uint32_t)probe + (uint32_t)lane) & hm;
-        const uint64_t e = T[s];
+        const uint64_t e = in ? T[s] : ~0ull;
         const bool empty = e == 0;
         int id = -1;
         bool match = false;
-        if (!empty && (uint32_t)(e >> 32) == tag) {
+        if (in && !empty && (uint32_t)(e >> 32) == tag) {
             id = (int)(uint32_t)e - 1;
             const size_t ni = (size_t)g * E.M + id;
-            match = E.node_own[ni] == own && E.node_opp[ni] == opp && E.node_turn[ni] == turn &&
-                    E.node_cs[ni] == cs;
+            const NodeKey& k = E.node_key[ni];
+            match = k.own == own && k.opp == opp && k.turn == turn && k.cs == cs;
         }
         const uint64_t stop = __ballot(match || empty);
         if (stop) {
@@ -582,7 +586,7 @@ template <class R>
 __device__ int puct_select(const Dev& E, int g, int id, const typename R::VCtx& vc, int* edge) {
     const int lane = lane_id();
     const size_t row = node_row<R>(E, g, id);
-    const int Ns = E.node_Ns[(size_t)g * E.M + id];
+    const int Ns = E.node_key[(size_t)g * E.M + id].Ns;
     const float sq_edge = (float)sqrt((double)Ns);
     const float sq_new = (float)sqrt((double)Ns + 1e-8);
     int ci[R::AJ];
@@ -824,11 +828,8 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
         }
         if (lane == 0) {
             if (depth == 0) E.root_id[g] = id;
-            E.node_own[ni] = own;
-            E.node_opp[ni] = opp;
+            E.node_key[ni] = NodeKey{own, opp, kt, cs, 0, 0};
             E.node_turn[ni] = kt;
-            E.node_cs[ni] = cs;
-            E.node_Ns[ni] = 0;
             const uint64_t h = key_hash(own, opp, kt, cs);
             E.table[(size_t)g * E.H + E.leaf_slot[g]] = ((h >> 32) << 32) | (uint64_t)(uint32_t)(id + 1);
             E.st_exp[g] += 1;
@@ -864,7 +865,7 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
         }
         E.node_Q[row] = q;
         E.node_N[row] = (uint32_t)(n + 1) | (nf ? 0x80000000u : 0u);
-        E.node_Ns[ni] += 1;
+        E.node_key[ni].Ns += 1;
     }
 }
 
@@ -925,8 +926,8 @@ __device__ void commit_move(const Dev& E, int g, Pos p, int action, int m) {
     for (int b = 0; b < E.M; b += WAVE) {
         const int i = b + lane;
         if (i < E.M && E.node_turn[nb0 + i] >= 0) {
-            const uint64_t h = key_hash(E.node_own[nb0 + i], E.node_opp[nb0 + i], E.node_turn[nb0 + i],
-                                        E.node_cs[nb0 + i]);
+            const NodeKey& k = E.node_key[nb0 + i];
+            const uint64_t h = key_hash(k.own, k.opp, k.turn, k.cs);
             const unsigned long long ent = ((h >> 32) << 32) | (uint64_t)(uint32_t)(i + 1);
             uint32_t s = (uint32_t)h & hm;
             while (atomicCAS((unsigned long long*)&T64[s], 0ull, ent) != 0ull) s = (s + 1) & hm;
