@@ -85,6 +85,8 @@ SIGNATURES = [
     ("azg_small_gemm_partial", ctypes.c_int, [_VP, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _I32,
                                               _I32, _I32, _I32, _VP, _VP]),
     ("azg_small_gemm_reduce", ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _I32, _VP, _I32, _VP]),
+    ("azg_small_layer", ctypes.c_int, [_VP, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _I32, _I32,
+                                       _VP, _I32, _VP, _I32, _VP]),
     ("azg_split_gemm_pick", ctypes.c_int, [_I32, _VP, _VP, _I32]),
     ("azg_set_gemm_blocks", ctypes.c_int, [_I32]),
     ("azg_split_gemm_stamps", ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP, _I64, _VP]),

@@ -153,7 +153,182 @@ __global__ __launch_bounds__(256) void small_gemm_reduce_kernel(const float* __r
     y[(long long)px * ldy + co] = s;
 }
 
+// ---------------------------------------------------------------------------
+// small_layer: one whole layer per launch, no partial sums in HBM (one leaf to a few).
+// The partial + reduce pair above spreads a layer over the chip by splitting K, which at
+// one leaf writes and re-reads K-split x 49 x 512 partials and costs two launches.  Here
+// block (co group of COB, pixel group) owns its outputs outright: its 512 threads split
+// K (thread t: k pairs 2t, 2t + 1024, ...; 128 consecutive k of a wave lie in one tap),
+// each keeps NPG x COB accumulators in registers, and the block sums the 512 partials of
+// each output through LDS.  Per leaf the whole input activation (H x W x Cin f32, 100 KB
+// for 7 x 7 x 512) is copied into LDS by LDS-DMA (no registers, every piece in flight at
+// once) and read as float2 -- an input value feeds COB = 8 co -- while all of a thread's
+// weight pairs (at most MAXM per co) are loaded into registers up front, under that copy.
+// At one leaf conv2-4 are 64 co groups x ceil(49 / 13) pixel groups = 256 / 128 / 64
+// blocks; an FC layer (H = W = 1, taps 1) is ceil(Cout / COB) blocks of one pixel.  f32
+// fmaf in a fixed order (per thread k in order; the upper half's partials added to the
+// lower's, then four quarter sums combined pairwise): deterministic.
+constexpr int SL_THREADS = 512;
+constexpr int SL_LDS = 32768 + 1024;  // floats: an 8 x 8 x 512 input, or the 256 x (13 x 8 + 1) partials
+
+template <int NPG, int COB, int MAXM>
+__global__ __launch_bounds__(SL_THREADS) void small_layer_kernel(const float* __restrict__ x, long long sB, int sY,
+                                                                 int sX, int sC, int H, int W, int pad, int taps,
+                                                                 int Ho, int Wo, const float* __restrict__ w, int Cin,
+                                                                 int Cout, const float* __restrict__ bias, int relu,
+                                                                 float* __restrict__ y, int ldy, int B, int npg) {
+    __shared__ __attribute__((aligned(16))) float smem[SL_LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int co0 = blockIdx.x * COB, g = blockIdx.y;
+    const int NP = Ho * Wo, K = taps * Cin, KP = K >> 1;
+    // pixel group g: [p0, p0 + npb), groups as equal as possible
+    const int base = NP / npg, extra = NP % npg;
+    const int p0 = g * base + (g < extra ? g : extra), npb = base + (g < extra ? 1 : 0);
+    int oy[NPG], ox[NPG];
+#pragma unroll
+    for (int i = 0; i < NPG; ++i) {
+        const int p = p0 + (i < npb ? i : 0);
+        oy[i] = p / Wo;
+        ox[i] = p - (p / Wo) * Wo;
+    }
+    const int nin = H * W * Cin;
+    constexpr int R = NPG * COB + 1;  // partials row pitch (odd: conflict-free)
+    // a leaf's input is one contiguous [iy][ix][ci] block for NHWC activations and FC rows
+    const bool dense = sC == 1 && sX == Cin && sY == W * Cin && ((uintptr_t)x & 15) == 0 && (sB & 3) == 0;
+    for (int b = 0; b < B; ++b) {
+        const float* xb = x + (long long)b * sB;
+        if (dense) {  // LDS-DMA: 1 KB per wave-instruction, bytes past the input read as 0
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)xb, 0, nin * 4, 0x00020000);
+            const int nq = (nin * 4 + 1023) >> 10;
+            for (int q = wid; q < nq; q += SL_THREADS / 64)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)((char*)smem + (q << 10)), 16, (q << 10) + 16 * lane,
+                    0, 0, 0);
+        } else {
+            for (int e = tid; e < nin; e += SL_THREADS) {
+                const int pix = e / Cin, ci = e - pix * Cin;
+                const int iy = pix / W, ix = pix - (pix / W) * W;
+                smem[e] = xb[(long long)iy * sY + (long long)ix * sX + (long long)ci * sC];
+            }
+        }
+        float acc[NPG][COB];
+#pragma unroll
+        for (int i = 0; i < NPG; ++i)
+#pragma unroll
+            for (int c = 0; c < COB; ++c) acc[i][c] = 0.f;
+        for (int m0 = 0; m0 * SL_THREADS < KP; m0 += MAXM) {
+            // the thread's weight pairs of MAXM k pairs, all loads in flight together
+            float2 wv[MAXM][COB];
+#pragma unroll
+            for (int m = 0; m < MAXM; ++m) {
+                const int j = tid + SL_THREADS * (m0 + m);
+#pragma unroll
+                for (int c = 0; c < COB; ++c)
+                    wv[m][c] = j < KP && co0 + c < Cout ? *(const float2*)(w + (long long)(co0 + c) * K + 2 * j)
+                                                        : make_float2(0.f, 0.f);
+            }
+            if (m0 == 0) {  // the input copy has landed (this thread's pieces, then everyone's)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
+#pragma unroll
+            for (int m = 0; m < MAXM; ++m) {
+                const int j = tid + SL_THREADS * (m0 + m);
+                if (j >= KP) break;
+                const int k = 2 * j, tap = k / Cin, ci = k - tap * Cin;
+                const int dy = taps == 9 ? tap / 3 - pad : 0, dx = taps == 9 ? tap % 3 - pad : 0;
+                // the pair's inputs at the block's pixels, all LDS reads issued before the
+                // multiply-adds; a pixel outside the image or the group reads word 0, zeroed
+                float2 v[NPG];
+#pragma unroll
+                for (int i = 0; i < NPG; ++i) {
+                    const int iy = oy[i] + dy, ix = ox[i] + dx;
+                    const bool ok = i < npb && iy >= 0 && iy < H && ix >= 0 && ix < W;
+                    v[i] = *(const float2*)(smem + (ok ? (iy * W + ix) * Cin + ci : 0));
+                    if (!ok) v[i] = make_float2(0.f, 0.f);
+                }
+#pragma unroll
+                for (int i = 0; i < NPG; ++i)
+#pragma unroll
+                    for (int c = 0; c < COB; ++c) {
+                        acc[i][c] = fmaf(wv[m][c].x, v[i].x, acc[i][c]);
+                        acc[i][c] = fmaf(wv[m][c].y, v[i].y, acc[i][c]);
+                    }
+            }
+        }
+        __syncthreads();  // every thread is done with the input: the partials reuse its LDS
+        const int row = tid & 255;
+        if (tid >= 256) {
+#pragma unroll
+            for (int i = 0; i < NPG; ++i)
+#pragma unroll
+                for (int c = 0; c < COB; ++c)
+                    if (i < npb) smem[row * R + i * COB + c] = acc[i][c];
+        }
+        __syncthreads();
+        if (tid < 256) {
+#pragma unroll
+            for (int i = 0; i < NPG; ++i)
+#pragma unroll
+                for (int c = 0; c < COB; ++c)
+                    if (i < npb) smem[row * R + i * COB + c] = acc[i][c] + smem[row * R + i * COB + c];
+        }
+        __syncthreads();
+        // output o = (i, c): four threads sum 64 rows each in row order, combined pairwise
+        const int o = tid >> 2, qt = tid & 3;
+        float s = 0.f;
+        if (o < npb * COB)
+            for (int t0 = 64 * qt; t0 < 64 * qt + 64; t0 += 16) {
+                float q[16];  // 16 independent LDS reads in flight, then the adds in order
+#pragma unroll
+                for (int u = 0; u < 16; ++u) q[u] = smem[(t0 + u) * R + o];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) s += q[u];
+            }
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        if (qt == 0 && o < npb * COB) {
+            const int i = o / COB, c = o - (o / COB) * COB, co = co0 + c;
+            if (co < Cout) {
+                float r = s;
+                if (bias) r += bias[co];
+                if (relu) r = fmaxf(r, 0.f);
+                y[((long long)b * NP + p0 + i) * ldy + co] = r;
+            }
+        }
+        __syncthreads();  // the partials are read before the next leaf's input lands
+    }
+}
+
 }  // namespace
+
+// One layer (3x3 conv, taps 9, or FC, taps 1; + bias, ReLU) on small_layer_kernel:
+// batch leaves, input x with element strides (sB, sY, sX, sC), weights [Cout][taps * Cin]
+// (k = tap * Cin + ci), output rows y[(leaf * Ho * Wo + pixel) * ldy + co].  Needs Cin even,
+// the input of one leaf (H * W * Cin floats) in 128 KB of LDS and w 8-B aligned.
+extern "C" int azg_small_layer(const float* x, int64_t sB, int32_t sY, int32_t sX, int32_t sC, int32_t batch,
+                               int32_t H, int32_t W, int32_t pad, int32_t taps, const float* w, int32_t Cin,
+                               int32_t Cout, const float* bias, int32_t relu, float* y, int32_t ldy, void* stream) {
+    if (!x || !w || !y || batch <= 0 || H <= 0 || W <= 0 || (taps != 1 && taps != 9) || Cin <= 0 || (Cin & 1) ||
+        Cout <= 0 || ldy < Cout || pad < 0 || (taps == 1 && (pad || H != 1 || W != 1)) || ((uintptr_t)w & 7))
+        return AZG_ERR_ARG;
+    const int Ho = taps == 9 ? H + 2 * pad - 2 : 1, Wo = taps == 9 ? W + 2 * pad - 2 : 1;
+    if (Ho <= 0 || Wo <= 0 || (long long)H * W * Cin > 32768 || (long long)taps * Cin > (1 << 24)) return AZG_ERR_ARG;
+    const hipStream_t st = (hipStream_t)stream;
+    if (taps == 9) {
+        constexpr int NPG = 13, COB = 8;
+        const int np = Ho * Wo, npg = (np + NPG - 1) / NPG;
+        const dim3 grid((unsigned)((Cout + COB - 1) / COB), (unsigned)npg);
+        hipLaunchKernelGGL((small_layer_kernel<NPG, COB, 3>), grid, dim3(SL_THREADS), 0, st, x, (long long)sB, sY, sX, sC,
+                           H, W, pad, taps, Ho, Wo, w, Cin, Cout, bias, relu, y, ldy, batch, npg);
+    } else {
+        constexpr int COB = 4;
+        const dim3 grid((unsigned)((Cout + COB - 1) / COB), 1u);
+        hipLaunchKernelGGL((small_layer_kernel<1, COB, 8>), grid, dim3(SL_THREADS), 0, st, x, (long long)sB, sY, sX, sC, H,
+                           W, pad, taps, Ho, Wo, w, Cin, Cout, bias, relu, y, ldy, batch, 1);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
 
 extern "C" int azg_small_gemm_partial(const float* x, int64_t sB, int32_t sY, int32_t sX, int32_t sC, int32_t batch,
                                       int32_t H, int32_t W, int32_t pad, int32_t taps, const float* w, int32_t Cin,

@@ -32,6 +32,7 @@ WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C
 # MIOpen / hipBLASLt.  Off by default: correct (tests/test_gpu_nn.py) but measured slower at one leaf
 # (3.8 vs 3.1 ms per 25-simulation getActionProb, profiles/r03_small_path.json)
 SMALL_PATH = False
+SMALL_LAYER_MAX_B = 4  # up to this many leaves a small-path layer is one azg_small_layer launch
 FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
 FC1_KPARTS = 4  # split-K parts of fc1 on libazg's split GEMM (4608 = 4 x 1152 for the 7x7 board)
 # split-K parts of fc2 (1024 -> 512) and [fc3 | fc4] (512 -> 344, padded to 512 columns) when the whole
@@ -692,22 +693,30 @@ class InferenceNet(nn.Module):
         return kc, max(d for d in range(1, min(slabs, target) + 1) if slabs % d == 0)
 
     def _small_gemm(self, key, x, strides, B, H, pad, taps, w, Cin, Cout, bias, relu):
-        """One layer on azg_small_gemm_partial + azg_small_gemm_reduce; returns the
+        """One layer on azg_small_layer (up to SMALL_LAYER_MAX_B leaves: one launch, no
+        partial sums) or azg_small_gemm_partial + azg_small_gemm_reduce; returns the
         [B * Ho * Ho, Cout] f32 output (NHWC rows)."""
         import ctypes
         from . import _lib
         L = _lib.lib()
         Ho = H + 2 * pad - 2 if taps == 9 else H
         npx = B * Ho * Ho
+        dev = x.device
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        sB, sY, sX, sC = strides
+        if B <= SMALL_LAYER_MAX_B and Cin % 2 == 0 and H * H * Cin <= 32768 and w.data_ptr() % 8 == 0:
+            y = torch.empty((npx, Cout), device=dev, dtype=torch.float32)
+            _lib.check(L.azg_small_layer(ctypes.c_void_p(x.data_ptr()), sB, sY, sX, sC, B, H, H, pad, taps,
+                                         ctypes.c_void_p(w.data_ptr()), Cin, Cout,
+                                         ctypes.c_void_p(bias.data_ptr()) if bias is not None else None, int(relu),
+                                         ctypes.c_void_p(y.data_ptr()), Cout, st))
+            return y
         plan = self._small_plans.get((key, B))
         if plan is None:
             plan = self._small_plans[(key, B)] = self._small_plan(Cin, taps, -(-Cout // 128) * -(-npx // 64))
         kc, ks = plan
-        dev = x.device
-        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         part = torch.empty(ks * npx * Cout, device=dev, dtype=torch.float32)
         y = torch.empty((npx, Cout), device=dev, dtype=torch.float32)
-        sB, sY, sX, sC = strides
         _lib.check(L.azg_small_gemm_partial(ctypes.c_void_p(x.data_ptr()), sB, sY, sX, sC, B, H, H, pad, taps,
                                             ctypes.c_void_p(w.data_ptr()), Cin, Cout, kc, ks,
                                             ctypes.c_void_p(part.data_ptr()), st))

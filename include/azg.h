@@ -244,6 +244,13 @@ int  azg_small_gemm_partial(const float* x, int64_t sB, int32_t sY, int32_t sX, 
                             int32_t Cout, int32_t kc, int32_t ksplit, float* part, void* stream);
 int  azg_small_gemm_reduce(const float* part, int32_t ksplit, int32_t npx, int32_t Cout, const float* bias,
                            int32_t relu, float* y, int32_t ldy, void* stream);
+/* The same layer in one launch with no partial sums (one leaf to a few): y[px * ldy + co] =
+ * sum_k w[co][k] x[k][px] + bias, ReLU if relu; blocks own (8 co, <= 13 pixels) of a conv
+ * or 4 co of an FC layer, their 256 threads split K and sum their partials through LDS.
+ * Needs Cin even, H * W * Cin <= 32768 (one leaf's input in LDS) and w 8-B aligned. */
+int  azg_small_layer(const float* x, int64_t sB, int32_t sY, int32_t sX, int32_t sC, int32_t batch, int32_t H,
+                     int32_t W, int32_t pad, int32_t taps, const float* w, int32_t Cin, int32_t Cout,
+                     const float* bias, int32_t relu, float* y, int32_t ldy, void* stream);
 /* The schedule azg_split_gemm picks for a launch of this shape (4, 17 or 18). */
 int  azg_split_gemm_pick(int32_t nruns, const int32_t* points, const int32_t* rows, int32_t k);
 /* Cap the persistent split GEMM's grid at `blocks` workgroups (one per CU; 0 = every CU;

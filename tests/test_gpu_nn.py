@@ -503,8 +503,51 @@ def test_small_gemm_matches_torch(B, H, pad, cin, cout):
         assert err < 1e-5, (layout, err)
 
 
-@pytest.mark.parametrize("n,depth,A,B", [(7, 4, 343, 1), (7, 4, 343, 5), (7, 4, 343, 63), (6, 2, 37, 1),
-                                         (8, 2, 65, 3)])
+@pytest.mark.parametrize("B,H,pad,cin,cout", [(1, 7, 1, 4, 512), (1, 7, 1, 512, 512), (3, 7, 0, 512, 512),
+                                              (1, 5, 0, 512, 512), (2, 8, 1, 2, 512), (1, 8, 1, 512, 512),
+                                              (4, 6, 0, 64, 96), (1, 1, 0, 4608, 1024), (3, 1, 0, 1024, 512),
+                                              (2, 1, 0, 512, 344), (1, 1, 0, 8192, 1024)])
+def test_small_layer_matches_torch(B, H, pad, cin, cout):
+    """azg_small_layer (one launch per layer, no partial sums; the small path up to
+    SMALL_LAYER_MAX_B leaves): a 3x3 conv or an FC layer + bias + ReLU against torch in f64,
+    NCHW and NHWC inputs, ragged pixel groups (49 = 13 + 12 + 12 + 12, 64, 36, 25) and
+    channel counts not a multiple of the 8-co block."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    torch.manual_seed(5)
+    taps = 9 if H > 1 else 1
+    x = torch.randn(B, cin, H, H, device="cuda")
+    w = torch.randn(cout, cin, 3, 3, device="cuda") / (cin * taps) ** 0.5 if taps == 9 else \
+        torch.randn(cout, cin, device="cuda") / cin ** 0.5
+    b = torch.randn(cout, device="cuda")
+    if taps == 9:
+        want = torch.relu(torch.nn.functional.conv2d(x.double(), w.double(), b.double(), padding=pad))
+        want = want.permute(0, 2, 3, 1).reshape(-1, cout)
+        wk = w.contiguous(memory_format=torch.channels_last)
+    else:
+        want = torch.relu(x.double().reshape(B, cin) @ w.double().t() + b.double())
+        wk = w.contiguous()
+    Ho = H + 2 * pad - 2 if taps == 9 else 1
+    L = _lib.lib()
+    for layout in ("nchw", "nhwc"):
+        if layout == "nchw":
+            xin, strides = x.contiguous(), (cin * H * H, H, 1, H * H)
+        else:
+            xin = x.permute(0, 2, 3, 1).contiguous()
+            strides = (H * H * cin, H * cin, cin, 1)
+        y = torch.full((B * Ho * Ho, cout), float("nan"), device="cuda")
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        _lib.check(L.azg_small_layer(ctypes.c_void_p(xin.data_ptr()), *strides, B, H, H, pad, taps,
+                                     ctypes.c_void_p(wk.data_ptr()), cin, cout, ctypes.c_void_p(b.data_ptr()), 1,
+                                     ctypes.c_void_p(y.data_ptr()), cout, st))
+        torch.cuda.synchronize()
+        err = ((y.double() - want).abs() / (want.abs() + 1.0)).max().item()
+        assert err < 1e-5, (layout, err)
+
+
+@pytest.mark.parametrize("n,depth,A,B", [(7, 4, 343, 1), (7, 4, 343, 4), (7, 4, 343, 5), (7, 4, 343, 63),
+                                         (6, 2, 37, 1), (8, 2, 65, 3)])
 def test_small_forward_matches_reference(n, depth, A, B):
     """Below 64 leaves InferenceNet(small=True) runs on libazg's small GEMMs (no MIOpen /
     hipBLASLt): P and v within the north_star's 1e-5 of the reference module, and of the

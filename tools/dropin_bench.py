@@ -53,7 +53,9 @@ def main():
         if form.startswith("module"):
             ev, graph = w, form.endswith("graph")
         else:
-            ev = InferenceNet(w.nnet.eval(), conv=form.split("-")[1], gemm="f32")
+            kind = form.split("-")[1]
+            ev = (InferenceNet(w.nnet.eval(), small=True, gemm="f32") if kind == "small" else
+                  InferenceNet(w.nnet.eval(), conv=kind, gemm="f32"))
             graph = True
         t = run(ev, game, a.sims, graph, a.moves)
         print(json.dumps({"game": a.game, "form": form, "sims": a.sims, "ms_per_call": t * 1e3,
