@@ -30,7 +30,7 @@ DEFAULT_ARGS = dict(lr=0.001, dropout=0.3, epochs=10, batch_size=512, num_channe
 WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C1: 1 game)
 # below WINOGRAD_MIN_BATCH: the whole forward on libazg's small f32 GEMMs (azg_small.hip) instead of
 # MIOpen / hipBLASLt.  Off by default: correct (tests/test_gpu_nn.py) but measured slower at one leaf
-# (3.8 vs 3.1 ms per 25-simulation getActionProb, profiles/r03_small_path.json)
+# (3.7 vs 3.0 ms per 25-simulation getActionProb with azg_small_layer, profiles/r03_small_layer.json)
 SMALL_PATH = False
 SMALL_LAYER_MAX_B = 4  # up to this many leaves a small-path layer is one azg_small_layer launch
 FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
