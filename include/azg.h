@@ -245,8 +245,9 @@ int  azg_small_gemm_partial(const float* x, int64_t sB, int32_t sY, int32_t sX, 
 int  azg_small_gemm_reduce(const float* part, int32_t ksplit, int32_t npx, int32_t Cout, const float* bias,
                            int32_t relu, float* y, int32_t ldy, void* stream);
 /* The same layer in one launch with no partial sums (one leaf to a few): y[px * ldy + co] =
- * sum_k w[co][k] x[k][px] + bias, ReLU if relu; blocks own (8 co, <= 13 pixels) of a conv
- * or 4 co of an FC layer, their 256 threads split K and sum their partials through LDS.
+ * sum_k w[co][k] x[k][px] + bias, ReLU if relu; blocks own (8 co, one output row) of a conv
+ * up to 8 wide (only the window's three input rows in LDS), (8 co, <= 13 pixels) of a wider
+ * one, or 4 co of an FC layer; their threads split K and sum their partials through LDS.
  * Needs Cin even, H * W * Cin <= 32768 (one leaf's input in LDS) and w 8-B aligned. */
 int  azg_small_layer(const float* x, int64_t sB, int32_t sY, int32_t sX, int32_t sC, int32_t batch, int32_t H,
                      int32_t W, int32_t pad, int32_t taps, const float* w, int32_t Cin, int32_t Cout,

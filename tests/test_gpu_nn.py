@@ -506,12 +506,14 @@ def test_small_gemm_matches_torch(B, H, pad, cin, cout):
 @pytest.mark.parametrize("B,H,pad,cin,cout", [(1, 7, 1, 4, 512), (1, 7, 1, 512, 512), (3, 7, 0, 512, 512),
                                               (1, 5, 0, 512, 512), (2, 8, 1, 2, 512), (1, 8, 1, 512, 512),
                                               (4, 6, 0, 64, 96), (1, 1, 0, 4608, 1024), (3, 1, 0, 1024, 512),
-                                              (2, 1, 0, 512, 344), (1, 1, 0, 8192, 1024)])
+                                              (2, 1, 0, 512, 344), (1, 1, 0, 8192, 1024), (1, 9, 1, 64, 128),
+                                              (2, 9, 0, 128, 72)])
 def test_small_layer_matches_torch(B, H, pad, cin, cout):
     """azg_small_layer (one launch per layer, no partial sums; the small path up to
-    SMALL_LAYER_MAX_B leaves): a 3x3 conv or an FC layer + bias + ReLU against torch in f64,
-    NCHW and NHWC inputs, ragged pixel groups (49 = 13 + 12 + 12 + 12, 64, 36, 25) and
-    channel counts not a multiple of the 8-co block."""
+    SMALL_LAYER_MAX_B leaves): a 3x3 conv (one output row per block up to 8 wide, pixel
+    groups of <= 13 beyond: the 9x9 cases) or an FC layer + bias + ReLU against torch in
+    f64, NCHW and NHWC inputs, padded and unpadded windows, channel counts not a multiple
+    of the 8-co block."""
     import ctypes
     import azg_amd  # noqa: F401
     from azg_amd import _lib
