@@ -300,6 +300,135 @@ __global__ __launch_bounds__(SL_THREADS) void small_layer_kernel(const float* __
     }
 }
 
+// small_row: a 3x3 conv layer at one leaf to a few with one output row per block.  The
+// block (8 co, output row oy) stages only the three input rows its window reads (<= 3 x 8
+// x 512 f32 = 48 KB, by LDS-DMA) and its LDS (<= 66.5 KB with the partials) lets two
+// blocks share a CU, so one block's weight and input round trips run under the other's
+// multiply-adds; 256 threads split K as small_layer's, accumulators for the row's Wo <= 8
+// pixels x 8 co in registers, the 256 partials summed through LDS in a fixed order.
+constexpr int SR_THREADS = 256;
+constexpr int SR_LDS = 256 * (8 * 8 + 1);  // floats: the partials, or three input rows at a 1-KB multiple pitch
+
+template <int NPG, int COB, int MAXM>
+__global__ __launch_bounds__(SR_THREADS, 2) void small_row_kernel(const float* __restrict__ x, long long sB, int sY,
+                                                                  int sX, int sC, int H, int W, int pad, int Ho,
+                                                                  int Wo, const float* __restrict__ w, int Cin,
+                                                                  int Cout, const float* __restrict__ bias, int relu,
+                                                                  float* __restrict__ y, int ldy, int B) {
+    __shared__ __attribute__((aligned(16))) float smem[SR_LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int co0 = blockIdx.x * COB, oy = blockIdx.y;
+    const int K = 9 * Cin, KP = K >> 1, iy0 = oy - pad, rowf = W * Cin;
+    const int nq = (rowf * 4 + 1023) >> 10, rpf = nq << 8;  // 1-KB DMA pieces per row; LDS row pitch (floats)
+    constexpr int R = NPG * COB + 1;
+    const bool dense = sC == 1 && sX == Cin && sY == W * Cin && ((uintptr_t)x & 15) == 0 && (sB & 3) == 0 &&
+                       (rowf & 3) == 0;
+    for (int b = 0; b < B; ++b) {
+        const float* xb = x + (long long)b * sB;
+        // window rows r = 0..2 (input row iy0 + r; rows outside the image are never read)
+        if (dense) {  // a piece writes a whole KB (zeros past the row): rows rpf apart
+            for (int t = wid; t < 3 * nq; t += SR_THREADS / 64) {
+                const int r = t / nq, q = t - r * nq, iy = iy0 + r;
+                if (iy < 0 || iy >= H) continue;
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(xb + (long long)iy * sY), 0, rowf * 4,
+                                                                  0x00020000);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)((char*)smem + r * rpf * 4 + (q << 10)), 16,
+                    (q << 10) + 16 * lane, 0, 0, 0);
+            }
+        } else {
+            for (int e = tid; e < 3 * rowf; e += SR_THREADS) {
+                const int r = e / rowf, rem = e - r * rowf, ix = rem / Cin, ci = rem - ix * Cin, iy = iy0 + r;
+                if (iy >= 0 && iy < H)
+                    smem[r * rpf + rem] = xb[(long long)iy * sY + (long long)ix * sX + (long long)ci * sC];
+            }
+        }
+        float acc[NPG][COB];
+#pragma unroll
+        for (int i = 0; i < NPG; ++i)
+#pragma unroll
+            for (int c = 0; c < COB; ++c) acc[i][c] = 0.f;
+        // weight chunks of MAXM k pairs, double-buffered: chunk n + 1's loads are issued
+        // before chunk n's multiply-adds, so each round trip runs under the previous chunk
+        auto wload = [&](int m0, float2 (&wv)[MAXM][COB]) {
+#pragma unroll
+            for (int m = 0; m < MAXM; ++m) {
+                const int j = tid + SR_THREADS * (m0 + m);
+#pragma unroll
+                for (int c = 0; c < COB; ++c)
+                    wv[m][c] = j < KP && co0 + c < Cout ? *(const float2*)(w + (long long)(co0 + c) * K + 2 * j)
+                                                        : make_float2(0.f, 0.f);
+            }
+        };
+        auto compute = [&](int m0, const float2 (&wv)[MAXM][COB]) {
+#pragma unroll
+            for (int m = 0; m < MAXM; ++m) {
+                const int j = tid + SR_THREADS * (m0 + m);
+                if (j >= KP) break;
+                const int k = 2 * j, tap = k / Cin, ci = k - tap * Cin, ky = tap / 3, kx = tap - ky * 3;
+                const bool rok = iy0 + ky >= 0 && iy0 + ky < H;
+                float2 v[NPG];
+#pragma unroll
+                for (int i = 0; i < NPG; ++i) {
+                    const int ix = i + kx - pad;
+                    const bool ok = rok && i < Wo && ix >= 0 && ix < W;
+                    v[i] = *(const float2*)(smem + (ok ? ky * rpf + ix * Cin + ci : 0));
+                    if (!ok) v[i] = make_float2(0.f, 0.f);
+                }
+#pragma unroll
+                for (int i = 0; i < NPG; ++i)
+#pragma unroll
+                    for (int c = 0; c < COB; ++c) {
+                        acc[i][c] = fmaf(wv[m][c].x, v[i].x, acc[i][c]);
+                        acc[i][c] = fmaf(wv[m][c].y, v[i].y, acc[i][c]);
+                    }
+            }
+        };
+        const int nchunk = (KP + SR_THREADS * MAXM - 1) / (SR_THREADS * MAXM);
+        float2 wa[MAXM][COB], wb[MAXM][COB];
+        wload(0, wa);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows and chunk 0 have landed
+        __syncthreads();
+        for (int n = 0; n < nchunk; n += 2) {
+            if (n + 1 < nchunk) wload((n + 1) * MAXM, wb);
+            compute(n * MAXM, wa);
+            if (n + 1 >= nchunk) break;
+            if (n + 2 < nchunk) wload((n + 2) * MAXM, wa);
+            compute((n + 1) * MAXM, wb);
+        }
+        __syncthreads();  // the input rows are read: the partials reuse the LDS
+#pragma unroll
+        for (int i = 0; i < NPG; ++i)
+#pragma unroll
+            for (int c = 0; c < COB; ++c)
+                if (i < Wo) smem[tid * R + i * COB + c] = acc[i][c];
+        __syncthreads();
+        // output o = (i, c): four threads sum 64 partials each in thread order, combined pairwise
+        const int o = tid >> 2, qt = tid & 3, nout = Wo * COB;
+        float s = 0.f;
+        if (o < nout)
+            for (int t0 = 64 * qt; t0 < 64 * qt + 64; t0 += 16) {
+                float q[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) q[u] = smem[(t0 + u) * R + o];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) s += q[u];
+            }
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        if (qt == 0 && o < nout) {
+            const int i = o / COB, c = o - (o / COB) * COB, co = co0 + c;
+            if (co < Cout) {
+                float r = s;
+                if (bias) r += bias[co];
+                if (relu) r = fmaxf(r, 0.f);
+                y[((long long)b * Ho * Wo + oy * Wo + i) * ldy + co] = r;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 // One layer (3x3 conv, taps 9, or FC, taps 1; + bias, ReLU) on small_layer_kernel:
@@ -315,7 +444,11 @@ extern "C" int azg_small_layer(const float* x, int64_t sB, int32_t sY, int32_t s
     const int Ho = taps == 9 ? H + 2 * pad - 2 : 1, Wo = taps == 9 ? W + 2 * pad - 2 : 1;
     if (Ho <= 0 || Wo <= 0 || (long long)H * W * Cin > 32768 || (long long)taps * Cin > (1 << 24)) return AZG_ERR_ARG;
     const hipStream_t st = (hipStream_t)stream;
-    if (taps == 9) {
+    if (taps == 9 && Wo <= 8 && W <= 8 && 3LL * ((W * Cin * 4LL + 1023) / 1024) * 256 <= SR_LDS) {  // one row per block
+        const dim3 grid((unsigned)((Cout + 7) / 8), (unsigned)Ho);
+        hipLaunchKernelGGL((small_row_kernel<8, 8, 2>), grid, dim3(SR_THREADS), 0, st, x, (long long)sB, sY, sX, sC, H,
+                           W, pad, Ho, Wo, w, Cin, Cout, bias, relu, y, ldy, batch);
+    } else if (taps == 9) {
         constexpr int NPG = 13, COB = 8;
         const int np = Ho * Wo, npg = (np + NPG - 1) / NPG;
         const dim3 grid((unsigned)((Cout + COB - 1) / COB), (unsigned)npg);
