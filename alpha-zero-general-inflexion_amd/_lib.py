@@ -89,7 +89,6 @@ SIGNATURES = [
                                        _VP, _I32, _VP, _I32, _VP]),
     ("azg_split_gemm_pick", ctypes.c_int, [_I32, _VP, _VP, _I32]),
     ("azg_set_gemm_blocks", ctypes.c_int, [_I32]),
-    ("azg_split_gemm_stamps", ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP, _I64, _VP]),
     ("azg_set_arena", ctypes.c_int, [_VP, _VP, _VP, _VP]),
     ("azg_opponent_move", ctypes.c_int, [_VP, _I32, _VP]),
     ("azg_examples", ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _I32, _I32, _I64, _VP, _VP,
@@ -123,6 +122,33 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+_probes = None
+PROBES_PATH = os.path.join(os.path.dirname(HERE), "tools", "libazg_probes.so")
+
+
+def probes():
+    """tools/libazg_probes.so: the split GEMM built with its probe-only schedules
+    (azg_split_gemm_variant for every variant, azg_split_gemm_stamps).  Tools and the
+    probe tests only; the product never loads it."""
+    global _probes
+    if _probes is None:
+        if not os.path.exists(PROBES_PATH):
+            subprocess.check_call(["make", "-s", "-C", os.path.dirname(PROBES_PATH)])
+        L = ctypes.CDLL(PROBES_PATH)
+        for name, res, args in (
+                ("azg_split_gemm_variant", ctypes.c_int, [_I32, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
+                ("azg_split_gemm_stamps", ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP, _I64, _VP]),
+                ("azg_split_gemm_pick", ctypes.c_int, [_I32, _VP, _VP, _I32]),
+                ("azg_split_gemm", ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
+                ("azg_last_error", ctypes.c_char_p, [])):
+            if hasattr(L, name):
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+        _probes = L
+    return _probes
 
 
 def check(rc):

@@ -173,8 +173,19 @@ class Coach:
                 eng.close()
         return self._range_checked(run, evaluator)
 
-    def _selfplay_iteration(self, i, group):
-        """Self-play of iteration i over all ranks; examples land on the trainer (rank 0)."""
+    def _dp_train(self):
+        """Multi-rank training mode: "ddp" (default: every rank builds the iteration's
+        examples from all-gathered records and trains its slice of every batch,
+        ddp.train_examples_dp) or "rank0" (rank 0 alone trains on gathered records and
+        broadcasts its weights; the round-3 arrangement)."""
+        mode = (self.args.get("distributedTrain", "ddp") if hasattr(self.args, "get") else "ddp") or "ddp"
+        if mode not in ("ddp", "rank0"):
+            raise ValueError(f"distributedTrain must be 'ddp' or 'rank0', got {mode!r}")
+        return mode == "ddp"
+
+    def _selfplay_iteration(self, i, group, all_ranks=False):
+        """Self-play of iteration i over all ranks; examples land on the trainer (rank 0),
+        or on every rank with all_ranks (data-parallel training)."""
         import torch.distributed as dist
         from .dist import broadcast_weights, gather_records
         from .engine import game_spec
@@ -183,7 +194,8 @@ class Coach:
         if group is None and not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
             return self.selfplay_examples(eps, first_game=(i - 1) * eps)
         rank, world = dist.get_rank(group), dist.get_world_size(group)
-        broadcast_weights(self.nnet.nnet, src=0, group=group)
+        if not all_ranks:  # data-parallel training keeps the ranks' weights equal by construction
+            broadcast_weights(self.nnet.nnet, src=0, group=group)
         first = ((i - 1) * world + rank) * eps
 
         def run(ev):
@@ -194,34 +206,45 @@ class Coach:
                 eng.close()
                 raise
             return eng
-        # If any rank's split-fp16 net met an operand out of fp16 range, EVERY rank replays
-        # its games with nnet.replay_form, together: no rank waits in the gather while
-        # another replays (which could outlast the process group's timeout), and the
-        # iteration's records are those of an all-f32 run whatever the sharding.
+        # The ranks agree on how self-play went before any of them enters the record
+        # exchange (flag: 0 ok, 1 a split-fp16 operand out of fp16 range, 2 any other
+        # error).  On 1 EVERY rank replays its games with nnet.replay_form, together: no
+        # rank waits in the gather while another replays (which could outlast the process
+        # group's timeout), and the iteration's records are those of an all-f32 run
+        # whatever the sharding.  On 2 every rank raises, instead of the healthy ranks
+        # blocking in the gather until the timeout.
         ev = self.evaluator()
+        eng, flag_v, err = None, 0, None
         try:
-            eng, overflow = run(ev), 0
-        except FloatingPointError:
-            if ev is self.nnet:
-                raise
-            eng, overflow = None, 1
+            eng = run(ev)
+        except FloatingPointError as e:
+            flag_v, err = (2, e) if ev is self.nnet else (1, None)
+        except Exception as e:  # noqa: BLE001 -- reported to every rank, re-raised below
+            flag_v, err = 2, e
         dev = (torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl"
                else torch.device("cpu"))
-        flag = torch.tensor([overflow], dtype=torch.int64, device=dev)
+        flag = torch.tensor([flag_v], dtype=torch.int64, device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-        if int(flag.item()):
+        flag_v = int(flag.item())
+        if flag_v == 2:
+            if eng is not None:
+                eng.close()
+            if err is not None:
+                raise err
+            raise RuntimeError("self-play failed on another rank; this rank stops with it")
+        if flag_v == 1:
             log.warning("self-play: split-fp16 operand out of range on a rank; all ranks replay with "
                         "the f32 replay form")
             if eng is not None:
                 eng.close()
             eng = run(self.evaluator(gemm="f32"))
-        self.last_replayed_f32 = bool(int(flag.item()))
+        self.last_replayed_f32 = flag_v == 1
         try:
-            rec, self.last_sent_bytes = gather_records(eng, dst=0, group=group,
+            rec, self.last_sent_bytes = gather_records(eng, dst=None if all_ranks else 0, group=group,
                                                        temp_threshold=int(self.args.tempThreshold))
         finally:
             eng.close()
-        if rank != 0:
+        if rec is None:
             return None
         name, n, max_turns = game_spec(self.game)
         mv, act, cnt = rec
@@ -231,41 +254,64 @@ class Coach:
     def learn(self, group=None, pit=True):
         """Coach.learn (Coach.py:92-165): per iteration, numEps self-play games
         (on every rank when torch.distributed is initialised: the engine plays
-        numEps games per rank, records are gathered to rank 0 and the weights
-        broadcast back), the example history window, the examples file, training
-        (NNetWrapper.train_examples), temp.pth.tar and, every pitInterval
-        iterations, the arena against the baselines."""
+        numEps games per rank), the example history window, the examples file,
+        training (NNetWrapper.train_examples), temp.pth.tar and, every pitInterval
+        iterations, the arena against the baselines.
+
+        With several ranks and args.distributedTrain "ddp" (the default) every rank
+        receives all ranks' records (all-gather), builds the same examples and history,
+        and trains data-parallel (ddp.train_examples_dp: the reference's batches split
+        over the ranks, one gradient all-reduce per step), so all GPUs train and the
+        weights need no broadcast; "rank0" gathers the records to rank 0, which trains
+        alone and broadcasts its weights at the start of the next iteration."""
         import torch.distributed as dist
         from .examples import ExampleSet
         distributed = group is not None or (dist.is_available() and dist.is_initialized()
                                             and dist.get_world_size() > 1)
         trainer = not distributed or dist.get_rank(group) == 0
+        ddp = distributed and self._dp_train()
+        dp_group = (group if group is not None else dist.group.WORLD) if ddp else None
         if distributed:
             self.agree_skip_first(group)
+        if ddp:
+            from .dist import broadcast_weights
+            from .ddp import broadcast_example_sets
+            broadcast_weights(self.nnet.nnet, src=0, group=group)  # one start for every rank
+            if self.skipFirstSelfPlay:  # loadTrainExamples ran on the trainer only
+                dev = self.nnet.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+                hist = broadcast_example_sets(self.trainExamplesHistory if trainer else None, 0, group, dev)
+                self.trainExamplesHistory = [ExampleSet(h.planes.to(self.nnet.device), h.pis.to(self.nnet.device),
+                                                        h.vs.to(self.nnet.device)) for h in hist]
         pit_interval = 5
         for i in range(1, int(self.args.numIters) + 1):
             log.info("Starting Iter #%d ...", i)
             if not self.skipFirstSelfPlay or i > 1:
-                ex = self._selfplay_iteration(i, group)
-                if trainer:
+                ex = self._selfplay_iteration(i, group, all_ranks=ddp)
+                if trainer or ddp:
                     self.trainExamplesHistory.append(ex)
-            if not trainer:
+            if not (trainer or ddp):
                 continue
             if len(self.trainExamplesHistory) > int(self.args.numItersForTrainExamplesHistory):
                 log.warning("Removing the oldest entry in trainExamples. len(trainExamplesHistory) = %d",
                             len(self.trainExamplesHistory))
                 self.trainExamplesHistory.pop(0)
-            if self.args.get("saveExamples", True):
+            if trainer and self.args.get("saveExamples", True):
                 self.saveTrainExamples(i - 1)
             train = ExampleSet.cat(self.trainExamplesHistory)
             perm = list(range(len(train)))
-            random.shuffle(perm)  # shuffle(trainExamples), Coach.py:149
+            if trainer:
+                random.shuffle(perm)  # shuffle(trainExamples), Coach.py:149
+            if ddp:  # the trainer's shuffle on every rank
+                from .ddp import broadcast_perm
+                dev = self.nnet.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+                perm = broadcast_perm(perm, 0, group, dev)
             self.last_losses = self.nnet.train_examples(
-                train.index(torch.as_tensor(perm, dtype=torch.long, device=train.vs.device)))
-            self.nnet.save_checkpoint(folder=self.args.checkpoint, filename="temp.pth.tar")
-            if pit and i % pit_interval == 0:
-                self.pit_baselines()
-        if distributed:
+                train.index(torch.as_tensor(perm, dtype=torch.long, device=train.vs.device)), group=dp_group)
+            if trainer:
+                self.nnet.save_checkpoint(folder=self.args.checkpoint, filename="temp.pth.tar")
+                if pit and i % pit_interval == 0:
+                    self.pit_baselines()
+        if distributed and not ddp:
             from .dist import broadcast_weights
             broadcast_weights(self.nnet.nnet, src=0, group=group)
 

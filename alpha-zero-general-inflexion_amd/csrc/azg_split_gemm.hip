@@ -556,6 +556,11 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
     }
 }
 
+#ifdef AZG_SG_PROBES
+// ---------------------------------------------------------------------------
+// Probe-only schedules (variants 1, 2, 3, 5-8, 10-12, 15, 16, 19): measured, recorded in
+// DESIGN.md 4.1 / 6b, none faster than variant 4.  Built only into tools/libazg_probes.so
+// (tools/Makefile, -DAZG_SG_PROBES), never into the product libazg.so.
 // Variant 12: ping-pong with the DMA split evenly and one stage stream across tiles.
 // Waves 0-3 (X, rows 0-127 of the tile, one per SIMD) and 4-7 (Y, rows 128-255) run
 // half a stage apart, one barrier per half-step: while one wave of a SIMD reads its
@@ -1336,6 +1341,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_384_kernel(SGArgs g) {
     }
 }
 
+#endif  // AZG_SG_PROBES
 }  // namespace
 
 // cap on the persistent grid (azg_set_gemm_blocks; 0: one block per CU)
@@ -1372,7 +1378,14 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
         k <= 0 || k % SG_BN || ((uintptr_t)A & 15) || ((uintptr_t)Bt & 15) || ((uintptr_t)M & 15) || variant < 0 ||
         variant > 19 || variant == 9 || variant == 13 || variant == 14 || (variant == 10) != (stamps != nullptr))
         return AZG_ERR_ARG;
+#ifndef AZG_SG_PROBES
+    // the product schedules: 0 (one tile per workgroup), 4 (persistent, default), 17 / 18
+    // (128 / 64-row tiles for short launches); the others exist in the probe build only
+    if (variant != 0 && variant != 4 && variant != 17 && variant != 18) return AZG_ERR_ARG;
+    const int bm = variant == 17 ? 128 : variant == 18 ? 64 : SG_BM;
+#else
     const int bm = variant == 17 ? 128 : variant == 18 ? 64 : variant == 19 ? S3_BM : SG_BM;
+#endif
     SGArgs g{};
     g.A = (const _Float16*)A;
     g.Bt = (const _Float16*)Bt;
@@ -1408,13 +1421,14 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
         hipLaunchKernelGGL((split_gemm_kernel<false, 128>), dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 18)
         hipLaunchKernelGGL((split_gemm_kernel<false, 64>), dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
+    else if (variant == 4)
+        hipLaunchKernelGGL(split_gemm_persist_kernel<8>, dim3(persistent_blocks(tiles)), dim3(512), 0,
+                           (hipStream_t)stream, g);
+#ifdef AZG_SG_PROBES
     else if (variant == 3)
         hipLaunchKernelGGL(split_gemm_kernel<true>, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
     else if (variant == 1)
         hipLaunchKernelGGL(split_gemm_pipe_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, g);
-    else if (variant == 4)
-        hipLaunchKernelGGL(split_gemm_persist_kernel<8>, dim3(persistent_blocks(tiles)), dim3(512), 0,
-                           (hipStream_t)stream, g);
     else if (variant == 5)
         hipLaunchKernelGGL(split_gemm_persist_kernel<4>, dim3(persistent_blocks(tiles)), dim3(512), 0,
                            (hipStream_t)stream, g);
@@ -1445,6 +1459,7 @@ static int split_gemm_launch(int variant, const void* A, const void* Bt, float* 
         hipLaunchKernelGGL(split_gemm_384_kernel, dim3(persistent_blocks(tiles)), dim3(512), 0, (hipStream_t)stream, g);
     else
         hipLaunchKernelGGL(split_gemm_w4_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, g);
+#endif
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
@@ -1485,9 +1500,12 @@ extern "C" int azg_split_gemm_variant(int32_t variant, const void* A, const void
     return split_gemm_launch(variant, A, Bt, M, nruns, points, rows, c, k, stream);
 }
 
+#ifdef AZG_SG_PROBES
+// probe build only (tools/split_gemm_stamps.py): per-wave phase stamps of variant 4
 extern "C" int azg_split_gemm_stamps(const void* A, const void* Bt, float* M, int32_t nruns, const int32_t* points,
                                      const int32_t* rows, int32_t c, int32_t k, uint64_t* stamps, int64_t cap,
                                      void* stream) {
     if (!stamps || cap < (int64_t)persistent_blocks(1 << 30) * 8 * 5) return AZG_ERR_ARG;
     return split_gemm_launch(10, A, Bt, M, nruns, points, rows, c, k, stream, (unsigned long long*)stamps);
 }
+#endif  // AZG_SG_PROBES

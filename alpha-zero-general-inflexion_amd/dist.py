@@ -56,8 +56,9 @@ def engine_records(engine):
 def gather_records(engine, dst=0, group=None, temp_threshold=None):
     """Gather compact move records of all ranks (moves made so far) to `dst`.
     Returns (moves [W*G], actions [W*G, m], counts [W*G, m, A] int16/int32) on dst, None
-    elsewhere, and the bytes this rank sent.  temp_threshold: see gather_record_tensors
-    (default: the engine's own)."""
+    elsewhere (dst=None: on every rank), and the bytes this rank sent.  temp_threshold:
+    see gather_record_tensors (default: the engine's own) -- the counts of moves at or
+    past tempThreshold - 1 come back as zeros."""
     moves, actions, counts = engine_records(engine)
     tt = engine.cfg.temp_threshold if temp_threshold is None else temp_threshold
     return gather_record_tensors(moves, actions, counts, dst, group, actions_per_move=engine.A, temp_threshold=tt)
@@ -71,8 +72,13 @@ def group_src(group, rank):
 
 
 def _gather(t, dst, group):
-    """dist.gather of equal-shaped tensors into one [ws, ...] tensor on dst only."""
+    """dist.gather of equal-shaped tensors into one [ws, ...] tensor on dst only
+    (dst None: dist.all_gather, every rank receives)."""
     ws = dist.get_world_size(group)
+    if dst is None:
+        out = torch.empty((ws,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather(list(out.unbind(0)), t.contiguous(), group=group)
+        return out
     if dist.get_rank(group) == dst:
         out = torch.empty((ws,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         dist.gather(t, list(out.unbind(0)), dst=group_src(group, dst), group=group)
@@ -123,14 +129,20 @@ def dense_counts(row_nnz, pairs, G, rows, m, A, dtype):
 
 def gather_record_tensors(moves, actions, counts, dst=0, group=None, actions_per_move=343, temp_threshold=None):
     """gather_records on plain tensors (any device the group's backend serves).
-    Only `dst` allocates and receives the other ranks' records.
+    Only `dst` allocates and receives the other ranks' records; dst=None gives every
+    rank all records (all_gather: the data-parallel trainer, where every rank builds
+    the iteration's examples itself).
 
     temp_threshold: the counts of a move are needed only if it was played at
     temperature 1 (episodeStep < tempThreshold, Coach.py:68), so only the first
     tempThreshold - 1 moves' counts are sent; the others arrive as zeros (their
     examples' pi is the one-hot of the action).  None sends every move's counts.
     Returns ((moves [W*G], actions [W*G, m] int32, counts [W*G, m, A] int16, or
-    int32 if a count exceeds 32767) on dst, None elsewhere; the bytes this rank sent)."""
+    int32 if a count exceeds 32767) on dst, None elsewhere; the bytes this rank sent).
+    With temp_threshold set, the returned counts are TRUNCATED: every move from
+    tempThreshold - 1 on reads as zero counts -- exactly what
+    examples_from_records needs, but not the full records (statistics or saving records
+    need temp_threshold=None)."""
     A = counts.shape[2] if counts is not None else int(actions_per_move)
     G = moves.shape[0]
     dev = moves.device

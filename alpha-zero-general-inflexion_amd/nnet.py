@@ -905,12 +905,22 @@ class NNetWrapper:
                 (l_pi + l_v).backward()
                 opt.step()
 
-    def train_examples(self, ex):
+    def train_examples(self, ex, group=None):
         """NNet.py:36-76 on an ExampleSet already resident on the device: the same
         Adam, epochs and batch draws (np.random.randint on numpy's global stream,
         so the sampled batches are the reference's), with the batch gathered on
         the GPU instead of converted from Python lists.  Returns per-batch
-        (l_pi, l_v) as a device tensor [batches, 2] (one host sync at the end)."""
+        (l_pi, l_v) as a device tensor [batches, 2] (one host sync at the end).
+
+        group: a torch.distributed group of more than one rank trains data-parallel
+        (ddp.train_examples_dp: each batch split over the ranks, whole-batch
+        BatchNorm statistics, one gradient all-reduce per step); every rank of the
+        group calls this with the same examples."""
+        if group is not None:
+            import torch.distributed as dist
+            if dist.get_world_size(group) > 1:
+                from .ddp import train_examples_dp
+                return train_examples_dp(self, ex, group)
         opt = self._adam()
         bs = self.args["batch_size"]
         E = len(ex)

@@ -218,17 +218,13 @@ int  azg_winograd_first_nchw(const float* planes, const float* w1, const float* 
  * c % 64 == 0, k % 256 == 0, nruns <= 4, 16-B aligned pointers. */
 int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, const int32_t* points,
                     const int32_t* rows, int32_t c, int32_t k, void* stream);
-/* The same with an explicit kernel schedule (0: reads, then MFMAs per stage, one
- * tile per workgroup; 1: reads overlapped with MFMAs; 2: one wave per SIMD,
- * 128 x 128 per wave; 3: variant 0 with the DMA issue spread between the MFMAs;
- * 4: variant 0 persistent, the azg_split_gemm default; 5: variant 4 with the DMA
- * issued by waves 0-3; 6: timing probe of variant 4 with zero-record descriptors,
- * results WRONG; 7: ping-pong, the two waves of a SIMD half a stage apart; 8:
- * variant 4 with each accumulator's products 4 MFMAs apart; 11: variant 4 with each
- * tile's stores deferred into the next tile's first stage; 12: ping-pong with each
- * wave's own DMA and one stage stream across tiles; 17: variant 0 on 128-row tiles,
- * azg_split_gemm's pick for short launches; 18: the same on 64-row tiles; 19: variant 4
- * on 384 x 256 tiles, results bit-identical to variant 4's); for tests and probes. */
+/* The same with an explicit kernel schedule, for tests: 0 (reads, then MFMAs per stage,
+ * one tile per workgroup), 4 (variant 0 persistent, the azg_split_gemm default), 17 / 18
+ * (variant 0 on 128 / 64-row tiles, azg_split_gemm's pick for short launches).  The
+ * probe-only schedules measured in DESIGN.md (1-3, 5-8, 10-12, 15, 16, 19) are not in the
+ * product library: tools/Makefile builds them into tools/libazg_probes.so, which exports this
+ * entry point for all of them and azg_split_gemm_stamps (per-wave phase stamps of variant 4);
+ * other values return AZG_ERR_ARG here. */
 int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, float* m, int32_t nruns,
                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
 /* The leaf network at a few leaves (below the Winograd path's 64): one 3x3 conv
@@ -259,13 +255,6 @@ int  azg_split_gemm_pick(int32_t nruns, const int32_t* points, const int32_t* ro
  * that a second stream's kernels (the other half-batch's transforms) find CUs free
  * beside it.  Results do not depend on it. */
 int  azg_set_gemm_blocks(int32_t blocks);
-/* Diagnostic build of the default split GEMM with in-kernel s_memtime stamps
- * (results as azg_split_gemm): per wave (block b, wave w) the cycle sums of
- * [operand reads + DMA issue], [MFMA issue], [vmcnt wait], [barrier], [epilogue]
- * at stamps[(b * 8 + w) * 5 + i]; cap >= CUs * 40 entries.  Its run time is not
- * the kernel's: read the shares. */
-int  azg_split_gemm_stamps(const void* a, const void* bt, float* m, int32_t nruns, const int32_t* points,
-                           const int32_t* rows, int32_t c, int32_t k, uint64_t* stamps, int64_t cap, void* stream);
 
 /* The fully connected tail of the leaf network (InflexionNNet.py:47-54, BN folded)
  * around split-fp16 GEMMs (azg_heads.hip; the GEMMs are the caller's: one fp16

@@ -25,6 +25,7 @@ Fixtures written (all small, gzip'd JSON or npz):
   train_golden.json.gz   NNetWrapper.train (32 channels, 2 epochs): losses + weight digests
   realnet_sensitivity.json.gz  first divergent move of the reference's real-net traces when its network's
                          weights, or its outputs, move by 1e-7 / 1e-6 relative
+  realnet_branches.json.gz     the perturbed reference's traces past those divergent moves
 """
 import gzip
 import hashlib
@@ -516,6 +517,89 @@ def gen_realnet_sensitivity(np, othello=False):
     _dump("realnet_sensitivity_othello.json.gz" if othello else "realnet_sensitivity.json.gz", out)
 
 
+def gen_realnet_branches(np):
+    """The other side of each certified near-tie: for every (eps, seed) whose reference trace
+    diverges under the 1e-7 / 1e-6 weight perturbation of gen_realnet_sensitivity, the
+    perturbed reference's whole trace from its first divergent move on (counts, action, turn,
+    board per move; final board, outcome and RNG position).  A GPU run that flips at such a
+    move the way the perturbed reference does is then compared, move for move, against this
+    branch for the rest of the game instead of being left unchecked after the flip."""
+    import torch
+    import MCTS as mcts_mod
+    from Coach import Coach
+    from inflexion.InflexionGame import InflexionGame
+    from inflexion.pytorch.NNet import NNetWrapper
+    from utils import dotdict
+
+    base = json.load(gzip.open(os.path.join(HERE, "mcts_realnet_main.json.gz"), "rt"))
+    sens = json.load(gzip.open(os.path.join(HERE, "realnet_sensitivity.json.gz"), "rt"))
+    cfg = base["config"]
+    game0 = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
+    rec = {"actions": [], "last": None, "in_search": False}
+    orig_tns = InflexionGame.to_next_state
+
+    def tns(self, action):
+        nxt = orig_tns(self, action)
+        if not rec["in_search"]:
+            rec["actions"].append(int(action))
+            rec["last"] = nxt
+        return nxt
+
+    class RecMCTS(mcts_mod.MCTS):
+        moves = None
+
+        def getActionProb(self, game, temp=1):
+            rec["in_search"] = True
+            probs = super().getActionProb(game, temp)
+            rec["in_search"] = False
+            s = game.to_planes().tobytes()
+            self.moves.append({"turn": game._curr_turn, "temp": temp,
+                               "counts": [[a, int(self.Nsa[(s, a)])] for a in range(game.max_actions)
+                                          if (s, a) in self.Nsa],
+                               "board": game._board.astype(int).ravel().tolist()})
+            return probs
+
+    InflexionGame.to_next_state = tns
+    out = {"config": cfg, "branches": []}
+    try:
+        for eps in (1e-7, 1e-6):
+            todo = [r for r in sens["runs"] if r.get("set", "realnet_main") == "realnet_main"
+                    and r["kind"] == "weights" and r["eps"] == eps and r["first_divergent_move"] is not None]
+            if not todo:
+                continue
+            torch.manual_seed(0)
+            net = NNetWrapper(game0)
+            g = torch.Generator().manual_seed(12345)  # the perturbation of gen_realnet_sensitivity
+            with torch.no_grad():
+                for prm in net.nnet.parameters():
+                    prm.mul_(1.0 + eps * (2.0 * torch.rand(prm.shape, generator=g, dtype=torch.float64)
+                                          - 1.0).to(prm.dtype))
+            for r in todo:
+                t0 = time.time()
+                args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"],
+                                "tempThreshold": cfg["temp_threshold"]})
+                mcts = RecMCTS(net, args)
+                mcts.moves = []
+                rec["actions"] = []
+                np.random.seed(r["seed"])
+                examples = Coach(game0, net, args).executeEpisode((game0.restarted(), mcts))
+                for m, a in zip(mcts.moves, rec["actions"]):
+                    m["action"] = a
+                first = r["first_divergent_move"]
+                final = rec["last"]
+                pol = hashlib.sha256(np.array([e[1] for e in examples], np.float64).tobytes()).hexdigest()
+                out["branches"].append({"eps": eps, "seed": r["seed"], "from_move": first,
+                                        "moves": mcts.moves[first:], "n_moves": len(rec["actions"]),
+                                        "final_board": final._board.astype(int).ravel().tolist(),
+                                        "final_outcome": final.outcome.value, "n_examples": len(examples),
+                                        "policy_sha256": pol, "rng_pos": int(np.random.get_state()[2])})
+                print(f"  branch eps {eps:g} seed {r['seed']} from move {first}: {len(rec['actions'])} moves, "
+                      f"{time.time() - t0:.1f}s", flush=True)
+    finally:
+        InflexionGame.to_next_state = orig_tns
+    _dump("realnet_branches.json.gz", out)
+
+
 # ------------------------------------------------------------------------- train
 TRAIN_CFG = dict(max_turns=30, sims=8, cpuct=1.0, temp_threshold=10, seed=3, num_channels=32, epochs=2,
                  batch_seed=11, torch_seed=5, init_seed=0, proj_seed=99)
@@ -627,6 +711,7 @@ def main():
         "train": lambda: gen_train(np),
         "sensitivity": lambda: gen_realnet_sensitivity(np),
         "sensitivity_othello": lambda: gen_realnet_sensitivity(np, othello=True),
+        "branches": lambda: gen_realnet_branches(np),
     }
     for name, fn in jobs.items():
         if only and name not in only:

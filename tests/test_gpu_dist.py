@@ -8,6 +8,7 @@ one rank-free engine playing all 2G games."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -28,7 +29,7 @@ class Args(dict):
     __getattr__ = dict.__getitem__
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode="ddp"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -50,31 +51,37 @@ def _worker(rank, world, port, q):
             # numpy, not tensors: torch's queue shares tensor storage by fd with a process that exits
             res["examples"] = (ex.planes.cpu().numpy(), ex.pis.cpu().numpy(), ex.vs.cpu().numpy())
         eng.close()
-        # Coach.learn's self-play over both ranks: rank 0 trains, weights go back out
+        # Coach.learn's self-play over both ranks: "ddp" every rank builds the examples and
+        # trains its half of each batch; "rank0" rank 0 trains, weights go back out
         game = InflexionGame(7, max_turns=10, max_power=6)
         from azg_amd.nnet import NNetWrapper
         torch.manual_seed(rank)  # different weights until the broadcast
         nnet = NNetWrapper(game, dict(epochs=1, batch_size=32, num_channels=8), device="cuda")
         args = Args(numIters=2, numEps=4, tempThreshold=5, maxlenOfQueue=10**6, numMCTSSims=3, cpuct=1,
                     arenaCompare=2, checkpoint="/tmp/azg_dist_ckpt_%d" % rank, numItersForTrainExamplesHistory=5,
-                    saveExamples=False)
+                    saveExamples=False, distributedTrain=mode)
+        np.random.seed(7 + rank)  # the trainer's (rank 0's) stream drives the batch draws
         c = Coach(game, nnet, args)
         c.learn(pit=False)
         res["hist"] = [len(h) for h in c.trainExamplesHistory]
+        res["hist_data"] = [(h.planes.cpu().numpy(), h.pis.cpu().numpy(), h.vs.cpu().numpy())
+                            for h in c.trainExamplesHistory]
+        res["losses"] = c.last_losses.cpu().numpy() if getattr(c, "last_losses", None) is not None else None
         res["w"] = {k: v.cpu().numpy() for k, v in nnet.nnet.state_dict().items()}
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
 
 
-def test_two_ranks_gather_and_learn():
+@pytest.mark.parametrize("mode", ["ddp", "rank0"])
+def test_two_ranks_gather_and_learn(mode):
     import azg_amd  # noqa: F401
     from azg_amd.engine import SelfPlayEngine
     from azg_amd.examples import engine_examples
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in procs)
@@ -88,9 +95,17 @@ def test_two_ranks_gather_and_learn():
     planes, pis, vs = res[0]["examples"]
     assert (planes == ref.planes.cpu().numpy()).all() and (pis == ref.pis.cpu().numpy()).all()
     assert (vs == ref.vs.cpu().numpy()).all()
-    # learn: rank 0 holds 2 iterations of 2 x 4 games' examples; the final broadcast
-    # leaves both ranks with rank 0's trained weights
-    assert len(res[0]["hist"]) == 2 and all(n > 0 for n in res[0]["hist"]) and res[1]["hist"] == []
+    # learn: rank 0 holds 2 iterations of 2 x 4 games' examples ("ddp": every rank the same
+    # examples, trained data-parallel); both ranks end with the same weights -- "ddp" by
+    # taking the same Adam steps, "rank0" by the final broadcast of rank 0's
+    assert len(res[0]["hist"]) == 2 and all(n > 0 for n in res[0]["hist"])
+    if mode == "ddp":
+        assert res[1]["hist"] == res[0]["hist"]
+        for a, b in zip(res[0]["hist_data"], res[1]["hist_data"]):
+            assert all((x == y).all() for x, y in zip(a, b))
+        assert (res[0]["losses"] == res[1]["losses"]).all()
+    else:
+        assert res[1]["hist"] == []
     for k in res[0]["w"]:
         assert (res[0]["w"][k] == res[1]["w"][k]).all(), k
 

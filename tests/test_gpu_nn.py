@@ -1,5 +1,7 @@
 """GPU leaf network: the inference form (BN folded, NHWC, fused bias+ReLU HIP
 epilogue) against the reference module on the same planes (f32, 1e-5 rel)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -201,7 +203,12 @@ def test_split_gemm_error_not_above_f32():
     assert errs["split_blas"] <= 1.5 * errs["f32"], errs
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 8, 11, 12, 17, 18, 19])
+PROBE_VARIANTS = [1, 2, 3, 5, 7, 8, 11, 12, 19]  # tools/libazg_probes.so only
+probes = pytest.mark.skipif(not os.environ.get("AZG_PROBES"),
+                            reason="probe-only GEMM schedules: AZG_PROBES=1 (tools/Makefile builds them)")
+
+
+@pytest.mark.parametrize("variant", [0, 4, 17, 18] + [pytest.param(v, marks=probes) for v in PROBE_VARIANTS])
 @pytest.mark.parametrize("runs,C,K", [([(25, 4096)], 512, 512), ([(3, 300), (5, 37), (2, 513)], 512, 512),
                                       ([(1, 1)], 512, 512), ([(2, 77), (1, 256)], 64, 256),
                                       ([(4, 129)], 128, 768), ([(17, 4000)], 64, 512), ([(11, 3000)], 64, 512),
@@ -225,6 +232,7 @@ def test_split_gemm_default_schedule_matches_reference(runs, C, K):
 
 @pytest.mark.parametrize("runs,C,K", [([(121, 4096)], 512, 512), ([(4, 4096)], 1152, 1024),
                                       ([(3, 385), (2, 768), (1, 383)], 64, 512)])
+@probes
 def test_split_gemm_384_rows_bit_equal_to_256_rows(runs, C, K):
     """Variant 19 (384 x 256 tiles) runs every accumulator's MFMAs in variant 4's order
     (stage by stage, hi.hi, lo.hi, hi.lo): the same bits, so a schedule pick between
@@ -251,6 +259,23 @@ def test_split_gemm_grid_cap_bit_equal():
     assert L.azg_set_gemm_blocks(-1) == -1
 
 
+def test_product_library_has_no_probe_schedules():
+    """The probe-only schedules live in tools/libazg_probes.so: the product library
+    rejects them (and exports no stamp build)."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    L = _lib.lib()
+    assert not hasattr(L, "azg_split_gemm_stamps")
+    x = torch.zeros(256 * 1024, dtype=torch.float16, device="cuda")
+    m = torch.zeros(256 * 256, device="cuda")
+    pts, rows = (ctypes.c_int32 * 1)(1), (ctypes.c_int32 * 1)(256)
+    for v in PROBE_VARIANTS:
+        assert L.azg_split_gemm_variant(v, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                        ctypes.c_void_p(m.data_ptr()), 1, pts, rows, 512, 256,
+                                        ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == -1, v
+
+
 def _run_split_gemm(variant, runs, C, K):
     import ctypes
     import azg_amd  # noqa: F401
@@ -266,8 +291,10 @@ def _run_split_gemm(variant, runs, C, K):
             len(runs), pts, rows, C, K, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     if variant is None:
         _lib.check(_lib.lib().azg_split_gemm(*ptrs))
-    else:
+    elif variant in (0, 4, 17, 18):
         _lib.check(_lib.lib().azg_split_gemm_variant(variant, *ptrs))
+    else:
+        _lib.check(_lib.probes().azg_split_gemm_variant(variant, *ptrs))
     torch.cuda.synchronize()
     return A, Bt, M
 

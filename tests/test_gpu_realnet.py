@@ -77,7 +77,7 @@ def _game(name, cfg):
     return InflexionGame(7, max_turns=cfg["max_turns"], max_power=6) if kind == "inflexion" else OthelloGame(n)
 
 
-def _margin_report(net, evaluator, board, turn, player, template):
+def _margin_report(net, evaluator, board, turn, player, template, batch=G_ENGINE):
     """Root priors at a failing move: the evaluator on the GPU (at the batch size
     it ran at) against the reference's arithmetic (the module on the CPU, batch 1)."""
     import copy
@@ -93,7 +93,7 @@ def _margin_report(net, evaluator, board, turn, player, template):
         if isinstance(evaluator, str) or evaluator is None:  # the drop-in: the module, batch 1
             p_ev = torch.exp(net(x.cuda())[0][0]).cpu().numpy()
         else:
-            xb = x.cuda().expand(G_ENGINE, *x.shape[1:]).contiguous()
+            xb = x.cuda().expand(batch, *x.shape[1:]).contiguous()
             p_ev = evaluator(xb)[0][0].cpu().numpy()
     valid = g.valid_actions_mask().astype(bool)
     pv = np.sort(p_ref[valid])
@@ -111,45 +111,111 @@ def _sensitivity(name):
             if r.get("set", "realnet_main") == name}
 
 
-def _check_episode(ep, counts, actions, n_moves, where, report, name):
-    """Compare one episode with the reference; returns the first divergent move or None."""
+def _branches(name):
+    """The perturbed reference's traces past its divergent moves (make_golden.py `branches`):
+    {(seed, move): [branch, ...]}."""
+    if name != "realnet_main":
+        return {}
+    try:
+        d = ol.load_json("realnet_branches.json.gz")
+    except FileNotFoundError:
+        return {}
+    out = {}
+    for b in d["branches"]:
+        out.setdefault((b["seed"], b["from_move"]), []).append(b)
+    return out
+
+
+def _first_mismatch(moves, counts, actions, n_moves, start, A):
+    """First move index m >= start at which (counts, action) differ from `moves` (a list
+    indexed from `start`), or None if they agree through the end of `moves`."""
+    for j, mv in enumerate(moves):
+        m = start + j
+        if m < n_moves and np.array_equal(counts[m], ol.golden_counts(mv, A)) and actions[m] == mv["action"]:
+            continue
+        return m
+    return None
+
+
+def _check_episode(ep, counts, actions, n_moves, where, report, name, final=None):
+    """Compare one episode with the reference.  Returns (first divergent move from the
+    reference's own trace or None, moves compared, branch followed or None).
+
+    After a certified near-tie flip the comparison does not stop: if the flipped move's
+    counts equal those of the reference's own perturbed run that diverges at that move
+    (realnet_branches.json.gz: the same reference search with its weights moved by 1e-7 /
+    1e-6), the rest of the game is compared move for move against that branch -- the
+    game the reference plays when its arithmetic takes the other side of the tie.  A
+    mismatch on the branch fails unless it too is a single search decision (reported)."""
     min_prefix = SETS[name][2]
     whole = min_prefix is None
     A = len(counts[0]) if n_moves else 0
-    for m, mv in enumerate(ep["moves"]):
+
+    def shape(m, want_moves, off):
+        mv = want_moves[m - off]
         want = ol.golden_counts(mv, A)
-        if m < n_moves and np.array_equal(counts[m], want) and actions[m] == mv["action"]:
-            continue
         got = counts[m] if m < n_moves else None
         diff = np.nonzero(got != want)[0].tolist() if got is not None else []
         msg = (f"{where}: seed {ep['seed']} move {m} (turn {mv['turn']}): counts differ at actions {diff[:8]} "
                f"(engine {got[diff[:8]].tolist() if got is not None else None}, reference {want[diff[:8]].tolist()})")
-        single_flip = (got is not None and len(diff) == 2 and int(np.abs(got - want).sum()) == 2
-                       and int(got.sum()) == int(want.sum()))
-        sens = _sensitivity(name)
-        certified = any(sens.get(("weights", eps, ep["seed"])) == m for eps in (1e-7, 1e-6))
-        if whole or m < min_prefix or not single_flip or not certified:
-            raise AssertionError(msg + "; " + report(mv) + ("" if certified else "; the reference's own trace does "
-                                 "not diverge at this move when its weights move by 1e-7 or 1e-6"))
-        print(f"NEAR-TIE FLIP {msg}; {report(mv)}; identical through move {m - 1}; the reference's own trace with "
-              f"its weights moved by 1e-7 / 1e-6 first diverges at move "
-              f"{sens.get(('weights', 1e-7, ep['seed']), '?')} / {sens.get(('weights', 1e-6, ep['seed']), '?')} "
-              "(None: never)")
-        return m
-    assert n_moves == ep["n_moves"], (where, ep["seed"])
-    return None
+        single = (got is not None and len(diff) == 2 and int(np.abs(got - want).sum()) == 2
+                  and int(got.sum()) == int(want.sum()))
+        return msg, single, mv
+
+    m = _first_mismatch(ep["moves"], counts, actions, n_moves, 0, A)
+    if m is None:
+        assert n_moves == ep["n_moves"], (where, ep["seed"])
+        return None, n_moves, None
+    msg, single_flip, mv = shape(m, ep["moves"], 0)
+    sens = _sensitivity(name)
+    certified = any(sens.get(("weights", eps, ep["seed"])) == m for eps in (1e-7, 1e-6))
+    if whole or m < min_prefix or not single_flip or not certified:
+        raise AssertionError(msg + "; " + report(mv) + ("" if certified else "; the reference's own trace does "
+                             "not diverge at this move when its weights move by 1e-7 or 1e-6"))
+    print(f"NEAR-TIE FLIP {msg}; {report(mv)}; identical through move {m - 1}; the reference's own trace with "
+          f"its weights moved by 1e-7 / 1e-6 first diverges at move "
+          f"{sens.get(('weights', 1e-7, ep['seed']), '?')} / {sens.get(('weights', 1e-6, ep['seed']), '?')} "
+          "(None: never)")
+    for br in _branches(name).get((ep["seed"], m), []):
+        if not (m < n_moves and np.array_equal(counts[m], ol.golden_counts(br["moves"][0], A))):
+            continue
+        m2 = _first_mismatch(br["moves"], counts, actions, n_moves, m, A)
+        if m2 is None:
+            assert n_moves == br["n_moves"], (where, ep["seed"], "branch length")
+            if final is not None:
+                final(br)
+            print(f"BRANCH {where}: seed {ep['seed']} follows the reference's eps={br['eps']:g} branch from move {m} "
+                  f"to the end of the game ({n_moves} moves, final board / outcome / RNG position equal)")
+            return m, n_moves, br
+        msg2, single2, mv2 = shape(m2, br["moves"], m)
+        if not single2:
+            raise AssertionError(f"on the reference's eps={br['eps']:g} branch from move {m}: " + msg2 + "; "
+                                 + report(mv2))
+        print(f"BRANCH {where}: seed {ep['seed']} follows the reference's eps={br['eps']:g} branch from move {m} "
+              f"through move {m2 - 1}; at {m2} a second single-decision flip: {msg2}; {report(mv2)}")
+        return m, m2, br
+    print(f"BRANCH {where}: seed {ep['seed']}: no reference branch from move {m} matches the flipped counts")
+    return m, m, None
 
 
-@pytest.mark.parametrize("name,k", [("realnet_main", 0), ("realnet_main", 1), ("realnet_sims100", 0)]
-                         + [("realnet_othello6", i) for i in range(8)] + [("realnet_othello8", 0)])
-def test_dropin_mcts_real_net(name, k):
-    """Drop-in MCTS + Coach.executeEpisode with an NNetWrapper, whole episodes (for the
-    6x6 Othello sets: BASELINE configs[0], C1, the reference main.py path on one game)."""
+DROPIN_CASES = ([("realnet_main", k) for k in range(8)] + [("realnet_sims100", 0)]
+                + [("realnet_othello6", i) for i in range(8)] + [("realnet_othello8", 0)])
+
+
+@pytest.mark.parametrize("form", ["module", "inference"])
+@pytest.mark.parametrize("name,k", DROPIN_CASES)
+def test_dropin_mcts_real_net(name, k, form):
+    """Drop-in MCTS + Coach.executeEpisode, whole episodes (for the 6x6 Othello sets:
+    BASELINE configs[0], C1, the reference main.py path on one game), with the leaf
+    evaluator as the reference wires it (form="module": the NNetWrapper's own torch module,
+    batch 1 on the GPU) and in the form INTEGRATION.md recommends for the drop-in
+    (form="inference": InferenceNet(nnet.nnet, conv="miopen", gemm="f32") -- BN folded,
+    f32 direct convolutions, the f32 FC tail and libazg's policy/value kernel)."""
     import hashlib
     import azg_amd  # noqa: F401
     from azg_amd.coach import Coach
     from azg_amd.mcts import MCTS
-    from azg_amd.nnet import NNetWrapper
+    from azg_amd.nnet import InferenceNet, NNetWrapper
 
     data = ol.load_json(f"mcts_{name}.json.gz")
     cfg, ep = data["config"], data["episodes"][k]
@@ -157,6 +223,10 @@ def test_dropin_mcts_real_net(name, k):
     game = _game(name, cfg)
     torch.manual_seed(0)
     wrapper = NNetWrapper(game, device="cuda")
+    ev = None
+    if form == "inference":
+        ev = InferenceNet(wrapper.nnet.eval(), conv="miopen", gemm="f32")
+        wrapper.azg_evaluator = ev
     counts, actions = [], []
 
     class RecMCTS(MCTS):
@@ -178,23 +248,33 @@ def test_dropin_mcts_real_net(name, k):
     finally:
         cls.to_next_state = orig
     net = wrapper.nnet.eval()
-    flip = _check_episode(ep, counts, actions, len(counts), "drop-in MCTS",
-                          lambda mv: _margin_report(net, None, mv["board"], mv["turn"], 1 - 2 * (mv["turn"] % 2),
-                                                    game), name)
-    if flip is None:  # the same game: the same examples and RNG position as the reference's
-        pol = hashlib.sha256(np.array([e[1] for e in ex], np.float64).tobytes()).hexdigest()
-        assert pol == ep["policy_sha256"] and len(ex) == ep["n_examples"]
-        assert np.random.get_state()[2] == ep["rng_pos"]
+    pol = hashlib.sha256(np.array([e[1] for e in ex], np.float64).tobytes()).hexdigest()
+    rng_pos = np.random.get_state()[2]
+
+    def final(ref):  # the same game as the reference's (or its branch): same examples and RNG position
+        assert pol == ref["policy_sha256"] and len(ex) == ref["n_examples"]
+        assert rng_pos == ref["rng_pos"]
+    flip, upto, br = _check_episode(ep, counts, actions, len(counts), f"drop-in MCTS ({form})",
+                                    lambda mv: _margin_report(net, ev, mv["board"], mv["turn"],
+                                                              1 - 2 * (mv["turn"] % 2), game, batch=1),
+                                    name, final=final)
+    if flip is None:
+        final(ep)
 
 
-@pytest.mark.parametrize("gemm", ["split", "f32"])
-@pytest.mark.parametrize("name", ["realnet_main", "realnet_sims100", "realnet_othello6", "realnet_othello8",
-                                  "realnet_othello8_s200"])
-def test_engine_real_net_4096_games(name, gemm):
-    """The batched engine with the production evaluator at 4096 games: the
-    fixture's seeds are game slots of a full-size run (seed = slot index +
-    first_game), the other slots are ordinary games in the same leaf batches
-    (C4 / C3 shapes for Inflexion, C5's 8x8 x 200 sims for Othello)."""
+ENGINE_CASES = ([(name, "split", G_ENGINE) for name in SETS] + [(name, "f32", G_ENGINE // 4) for name in SETS]
+                # C2's leaf batch (and twice it): the split GEMM's 128 / 64-row schedules and the f32 FC tail
+                + [(name, "split", g) for g in (256, 512) for name in SETS])
+
+
+@pytest.mark.parametrize("name,gemm,G", ENGINE_CASES)
+def test_engine_real_net(name, gemm, G):
+    """The batched engine with the production evaluator: the fixture's seeds are game
+    slots of a G-game run (seed = slot index + first_game), the other slots are ordinary
+    games in the same leaf batches.  G = 4096 (C4 / C3 shapes, C5's 8x8 x 200 sims; the
+    split form, benchmarked), 1024 (the f32-GEMM form, a fallback: same kernels, a quarter of
+    the leaves keeps the suite short), and 256 / 512 (C2's batch: the split GEMM's 128- and
+    64-row tile schedules, and below FC1_SPLIT_MIN_BATCH the f32 hipBLASLt FC tail)."""
     import azg_amd  # noqa: F401
     from azg_amd.engine import SelfPlayEngine
     from azg_amd.nnet import InferenceNet
@@ -207,9 +287,7 @@ def test_engine_real_net_4096_games(name, gemm):
     net = _ref_net(kind, n)
     ev = InferenceNet(net, gemm=gemm)
     game = _game(name, cfg)
-    # the split form (the benchmarked one) at the full 4096 games; the f32-GEMM form, a
-    # fallback, at 1024 (same kernels, a quarter of the leaves: keeps the suite short)
-    e = SelfPlayEngine(G_ENGINE if gemm == "split" else G_ENGINE // 4, sims=cfg["sims"], cpuct=cfg["cpuct"], temp_threshold=cfg["temp_threshold"],
+    e = SelfPlayEngine(G, sims=cfg["sims"], cpuct=cfg["cpuct"], temp_threshold=cfg["temp_threshold"],
                        max_turns=cfg.get("max_turns", 343), seed_base=0, first_game=seeds[0], evaluator=ev,
                        game=kind, n=n)
     e.play()
@@ -217,17 +295,23 @@ def test_engine_real_net_4096_games(name, gemm):
     assert st["error"] == 0
     rec = e.read_moves()
     state = e.state()
-    whole = 0
+    whole = compared = total = 0
     for i, ep in enumerate(eps):
-        flip = _check_episode(ep, rec["counts"][i], rec["actions"][i], int(rec["moves"][i]), f"engine gemm={gemm}",
-                              lambda mv: _margin_report(net, ev, mv["board"], mv["turn"], 1 - 2 * (mv["turn"] % 2),
-                                                        game), name)
+        def final(ref, i=i):
+            assert state["boards"][i].tolist() == ref["final_board"]
+            assert ol.OUTCOME_VALUE[int(state["outcomes"][i])] == ref["final_outcome"]
+            assert e.get_rng(i)[1] == ref["rng_pos"]
+        flip, upto, br = _check_episode(
+            ep, rec["counts"][i], rec["actions"][i], int(rec["moves"][i]), f"engine gemm={gemm} G={G}",
+            lambda mv: _margin_report(net, ev, mv["board"], mv["turn"], 1 - 2 * (mv["turn"] % 2), game, batch=G),
+            name, final=final)
         if flip is None:
             whole += 1
-            assert state["boards"][i].tolist() == ep["final_board"]
-            assert ol.OUTCOME_VALUE[int(state["outcomes"][i])] == ep["final_outcome"]
-            assert e.get_rng(i)[1] == ep["rng_pos"]
-    print(f"{name} gemm={gemm}: {whole} of {len(eps)} games identical to the reference move for move")
+            final(ep)
+        compared += upto
+        total += int(rec["moves"][i])
+    print(f"{name} gemm={gemm} G={G}: {whole} of {len(eps)} games identical to the reference move for move; "
+          f"{compared} of {total} moves compared against the reference or its certified branch")
     e.close()
 
 

@@ -65,7 +65,7 @@ def time_all(fns, rounds=7):
 
 def main():
     C = K = 512
-    L = _lib.lib()
+    L = _lib.probes()
     out = []
     for name, runs in LAYERS.items():
         P = sum(p for p, _ in runs)

@@ -29,7 +29,7 @@ def run(variant, reps):
     pts = (ctypes.c_int32 * len(runs))(*[p for p, _ in runs])
     rws = (ctypes.c_int32 * len(runs))(*[t for _, t in runs])
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    L = _lib.lib()
+    L = _lib.probes()
     for _ in range(reps):
         _lib.check(L.azg_split_gemm_variant(variant, ctypes.c_void_p(A.data_ptr()), ctypes.c_void_p(Bt.data_ptr()),
                                             ctypes.c_void_p(M.data_ptr()), len(runs), pts, rws, C, K, st))

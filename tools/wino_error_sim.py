@@ -82,19 +82,22 @@ def split16(x):
 
 
 def wino_layer(x, w, b, pad, seq, mats):
-    """x [B,C,H,H] f32 -> relu(conv3x3(x) + b) by Winograd tiles of output sides seq."""
+    """x [B,C,H,H] f32 -> relu(conv3x3(x) + b) by Winograd tiles of output sides seq
+    (a list for both axes, or a (rows, columns) pair of lists)."""
     B, C, H, _ = x.shape
     K = w.shape[0]
     xp = F.pad(x, (pad, pad, pad, pad))
     Ho = H + 2 * pad - 2
-    assert sum(seq) == Ho
-    offs = [sum(seq[:i]) for i in range(len(seq))]
+    seqr, seqc = seq if isinstance(seq, tuple) else (seq, seq)
+    assert sum(seqr) == Ho and sum(seqc) == Ho
+    offr = [sum(seqr[:i]) for i in range(len(seqr))]
+    offc = [sum(seqc[:i]) for i in range(len(seqc))]
     y = torch.zeros((B, K, Ho, Ho), dtype=torch.float32)
-    for (i, ma), (j, mb) in itertools.product(enumerate(seq), enumerate(seq)):
+    for (i, ma), (j, mb) in itertools.product(enumerate(seqr), enumerate(seqc)):
         ATa, Ga, BTa = mats[ma]
         ATb, Gb, BTb = mats[mb]
         na, nb = ma + 2, mb + 2
-        d = xp[:, :, offs[i]:offs[i] + na, offs[j]:offs[j] + nb]  # [B,C,na,nb]
+        d = xp[:, :, offr[i]:offr[i] + na, offc[j]:offc[j] + nb]  # [B,C,na,nb]
         BTa32 = torch.tensor(BTa, dtype=torch.float32)
         BTb32 = torch.tensor(BTb, dtype=torch.float32)
         V = torch.einsum("ar,bcrs,ts->bcat", BTa32, d, BTb32)  # f32
@@ -112,7 +115,7 @@ def wino_layer(x, w, b, pad, seq, mats):
         ATa32 = torch.tensor(ATa, dtype=torch.float32)
         ATb32 = torch.tensor(ATb, dtype=torch.float32)
         Y = torch.einsum("ia,batk,jt->bkij", ATa32, M, ATb32) * float(2.0 ** -k)
-        y[:, :, offs[i]:offs[i] + ma, offs[j]:offs[j] + mb] = Y
+        y[:, :, offr[i]:offr[i] + ma, offc[j]:offc[j] + mb] = Y
     return torch.relu(y + b.view(1, -1, 1, 1))
 
 
@@ -161,15 +164,30 @@ def main():
                                (v32m.double() - v64).abs().max().item())}
         m2, m3 = cook_toom(2, [0, 1, -1]), cook_toom(3, [0, 1, -1, 2])
         m4 = cook_toom(4, [0, 1, -1, 2, -0.5], "int")
-        configs = {
-            "shipped 3+2+2 / 3+2 / 3": ({2: m2, 3: m3}, [[3, 2, 2], [3, 2], [3]]),
-            "4+3 / 3+2 / 3 (F(4,3) pts 0,1,-1,2,-1/2)": ({2: m2, 3: m3, 4: m4}, [[4, 3], [3, 2], [3]]),
-            "4+3 pts 0,1,-1,2,-2": ({2: m2, 3: m3, 4: cook_toom(4, [0, 1, -1, 2, -2])}, [[4, 3], [3, 2], [3]]),
-            "4+3 / 5 (F(5,3) 0,1,-1,2,-1/2,1/2) / 3": ({2: m2, 3: m3, 4: m4,
-                                                         5: cook_toom(5, [0, 1, -1, 2, -0.5, 0.5], "int")},
-                                                        [[4, 3], [5], [3]]),
-        }
-        for name, (mats, seqs) in configs.items():
+        m5 = cook_toom(5, [0, 1, -1, -0.5, -2, 1.5], "int")  # azg_winograd.hip's F(5,3)
+        shipped = {2: m2, 3: m3, 4: m4, 5: m5}
+        configs = {"shipped 4+3 / 5 / 3 (121 + 49 + 25 points)": (shipped, [[4, 3], [5], [3]])}
+        # conv2 as one F(7,3) tile (81 points) or F(6,3) + F(1,3)... : candidate point sets
+        for pts in ([0, 1, -1, 2, -2, 0.5, -0.5, 1.5], [0, 1, -1, 2, -2, 0.5, -0.5, -1.5],
+                    [0, 1, -1, 2, -0.5, 0.5, -2, 3], [0, 1, -1, 0.5, -0.5, 2, -2, 0.25],
+                    [0, 1, -1, 2, -2, 0.5, -0.5, 4], [0, 1, -1, 1.5, -1.5, 0.5, -0.5, 2]):
+            try:
+                m7 = cook_toom(7, pts, "int")
+            except AssertionError:
+                continue
+            mats = dict(shipped)
+            mats[7] = m7
+            configs[f"7 (F(7,3) pts {pts}) / 5 / 3"] = (mats, [[7], [5], [3]])
+            configs[f"7 x 4+3 (99 points) / 5 / 3, pts {pts}"] = (mats, [([7], [4, 3]), [5], [3]])
+        for pts in ([0, 1, -1, 2, -2, 0.5, -0.5], [0, 1, -1, 2, -0.5, 0.5, -2]):
+            m6 = cook_toom(6, pts, "int")
+            mats = dict(shipped)
+            mats[6] = m6
+            configs[f"6+1? no: F(6,3) pts {pts} as 7 = 6+1 skipped"] = None
+        for name, cfg in configs.items():
+            if cfg is None:
+                continue
+            mats, seqs = cfg
             p, v = forward(net, x, seqs, mats)
             base[name] = (((p.double() - p64).abs() / p64).max().item(), (v.double() - v64).abs().max().item())
     for k, (ep, ev) in base.items():
