@@ -28,7 +28,7 @@ from collections import deque
 import numpy as np
 import torch
 
-from .flags import GameOutcome, PlayerColour
+from .flags import PlayerColour, ongoing
 from .inflexion import InflexionGame
 
 N_SYM = 36
@@ -73,7 +73,7 @@ class Coach:
 
     def executeEpisode(self, args):
         game, mcts = args
-        if not (game._curr_turn == 0 and game.outcome == GameOutcome.ONGOING):
+        if not (game._curr_turn == 0 and ongoing(game.outcome)):
             raise AssertionError("executeEpisode needs a fresh game")
         planes, pis, players = [], [], []
         step = 0
@@ -86,7 +86,7 @@ class Coach:
             players.append(game.player.num)
             action = np.random.choice(len(pi), p=pi)
             game = game.to_next_state(action)
-            if game.outcome != GameOutcome.ONGOING:
+            if not ongoing(game.outcome):
                 return build_examples(game, planes, pis, players, game, self.label_mode)
 
     def _engine(self, num_games, evaluator, seed_base, first_game):
@@ -121,10 +121,29 @@ class Coach:
             log.warning("self-play: split-fp16 operand out of range; replaying with the f32 replay form")
             return run(self.evaluator(gemm="f32"))
 
+    def native(self):
+        """Whether the engine has rules kernels for self.game (else the generic host path)."""
+        from .mcts import MCTS
+        return MCTS.native(self.game)
+
+    def _host_selfplay(self, num_games, seed_base, first_game, evaluator=None):
+        """The generic plugin path (hostsearch.HostSelfPlay): num_games episodes of a plugin
+        without native rules, searched on the host with the leaves batched to the GPU network;
+        returns [(examples, record)] per game."""
+        from .hostsearch import HostSelfPlay
+        sp = HostSelfPlay(self.game, evaluator if evaluator is not None else self.nnet, self.args, num_games,
+                          seed_base, first_game)
+        return sp.play(self.label_mode)
+
     def selfplay_batch(self, num_games, evaluator=None, seed_base=0, first_game=0, return_records=False):
         """Play num_games complete games concurrently on the GPU engine and
-        return their examples (same format as executeEpisode)."""
+        return their examples (same format as executeEpisode).  A plugin without
+        native rules plays on the generic host path (hostsearch.py)."""
         g0 = self.game
+        if not self.native():
+            res = self._host_selfplay(num_games, seed_base, first_game, evaluator)
+            examples = [e for ex, _ in res for e in ex]
+            return (examples, [r for _, r in res]) if return_records else examples
 
         def run(ev):
             eng = self._engine(num_games, ev, seed_base, first_game)
@@ -147,8 +166,11 @@ class Coach:
         that refill as games end); the examples (last maxlen, default
         args.maxlenOfQueue) are built on the GPU and returned as a device ExampleSet."""
         from .engine import game_spec
-        from .examples import engine_examples, examples_from_records
+        from .examples import ExampleSet, engine_examples, examples_from_records
         maxlen = int(self.args.maxlenOfQueue if maxlen is None else maxlen)
+        if not self.native():
+            ex = [e for exs, _ in self._host_selfplay(num_games, seed_base, first_game, evaluator) for e in exs]
+            return ExampleSet.from_list(ex[-maxlen:], self.nnet.device)
         slots = int(self.args.get("selfplaySlots", 0) or 0)
         if 0 < slots < num_games:
             # continuous batching: num_games games through `slots` engine slots
@@ -197,6 +219,8 @@ class Coach:
         if not all_ranks:  # data-parallel training keeps the ranks' weights equal by construction
             broadcast_weights(self.nnet.nnet, src=0, group=group)
         first = ((i - 1) * world + rank) * eps
+        if not self.native():
+            return self._host_selfplay_iteration(first, eps, group, all_ranks)
 
         def run(ev):
             eng = self._engine(eps, ev, 0, first)
@@ -250,6 +274,26 @@ class Coach:
         mv, act, cnt = rec
         return examples_from_records(name, n, max_turns, int(self.args.tempThreshold), mv, act, cnt,
                                      self.label_mode, int(self.args.maxlenOfQueue))
+
+    def _host_selfplay_iteration(self, first, eps, group, all_ranks):
+        """A multi-rank iteration of a plugin without native rules: each rank plays its games
+        on the host path and the example lists travel as objects (all ranks with all_ranks,
+        else the trainer)."""
+        import torch.distributed as dist
+        from .examples import ExampleSet
+        ex = [e for exs, _ in self._host_selfplay(eps, 0, first) for e in exs]
+        world = dist.get_world_size(group)
+        if all_ranks:
+            parts = [None] * world
+            dist.all_gather_object(parts, ex, group=group)
+        else:
+            parts = [None] * world if dist.get_rank(group) == 0 else None
+            from .dist import group_src
+            dist.gather_object(ex, parts, dst=group_src(group, 0), group=group)
+            if parts is None:
+                return None
+        allex = [e for p in parts for e in p]
+        return ExampleSet.from_list(allex[-int(self.args.maxlenOfQueue):], self.nnet.device)
 
     def learn(self, group=None, pit=True):
         """Coach.learn (Coach.py:92-165): per iteration, numEps self-play games
@@ -333,6 +377,10 @@ class Coach:
         GreedyPlayer, args.arenaCompare games each (batched on the GPU)."""
         from .arena import BatchedArena
         res = {}
+        if not self.native():  # the baselines (InflexionPlayers.py) exist for the engine's games only
+            log.warning("pit_baselines: no Random/Greedy baseline players for %s; skipped", type(self.game).__name__)
+            self.last_pit = res
+            return res
         for opp in ("random", "greedy"):
             arena = BatchedArena(self.game, self.nnet, self.args, opponent=opp)
             p1, p2, draws = arena.playGames(int(self.args.arenaCompare))

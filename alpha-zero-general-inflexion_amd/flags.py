@@ -45,3 +45,10 @@ class GameOutcome(Enum):
         if self is GameOutcome.LOST:
             return GameOutcome.WON
         return self
+
+
+def ongoing(outcome):
+    """outcome == ONGOING for this module's GameOutcome or any enum with the same values (a
+    plugin written against the reference's flags.py compares with ITS enum, whose members
+    are not this one's)."""
+    return getattr(outcome, "value", outcome) == 0

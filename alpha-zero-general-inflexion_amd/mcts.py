@@ -15,14 +15,21 @@ break (MCTS.py:48-60) run here on the host from the engine's root counts.
 `nnet` may be a NNetWrapper-like object (its `.nnet` torch module is used on
 the GPU, batched), a torch module returning (log_softmax, tanh), or the string
 "stub" (hash evaluator used by the parity tests).
+
+A Game plugin the engine has no kernels for (engine.game_spec raises: a new plugin, a
+subclass of a known one, unsupported parameters) is searched by hostsearch.HostSearch
+instead: the reference's search on the host over the plugin's own methods, the leaves
+evaluated by the network on the GPU ("unknown Game subclasses fall back to a
+CPU path that calls the Python methods").
 """
 import warnings
 
 import numpy as np
 import torch
 
+from ._lib import AzgError
 from .engine import SelfPlayEngine, game_spec
-from .flags import GameOutcome
+from .flags import ongoing
 
 
 def _evaluator_of(nnet, device):
@@ -42,6 +49,23 @@ def _evaluator_of(nnet, device):
 
 
 MAX_NODE_CAPACITY = (1 << 21) - 1  # azg_create's limit
+
+# Engines (and their captured simulation graphs) of MCTS instances that are gone, for the
+# next instance with the same evaluator and configuration.  The reference's Coach builds a
+# fresh MCTS per episode (Coach.py:110) and Arena per game; each would otherwise create an
+# engine, run an eager call and capture a new graph (with its own graph memory pool).  A
+# reused engine is reset (empty tree, as a new MCTS's dicts are) before it is handed out,
+# and an entry is checked out by one live MCTS at a time.
+_POOL = {}
+_POOL_MAX = 2  # idle engines kept per key
+
+
+def clear_pool():
+    """Free the idle engines (and the evaluators and graphs they keep alive)."""
+    for idle in _POOL.values():
+        for eng, *_ in idle:
+            eng.close()
+    _POOL.clear()
 
 
 def whole_game_capacity(sims, game):
@@ -69,20 +93,63 @@ class MCTS:
         self._warm = False
         self._engine = None
         self._max_turns = None
+        self._host = None  # hostsearch.HostSearch for plugins without native rules
+
+    @staticmethod
+    def native(game):
+        """Whether the engine has rules kernels for this Game instance (engine.game_spec)."""
+        try:
+            game_spec(game)
+            return True
+        except AzgError:
+            return False
+
+    def _host_search(self):
+        if self._host is None:
+            from .hostsearch import HostSearch
+            self._host = HostSearch(self.nnet, self.args, 1, self.device)
+        return self._host
+
+    def _pool_key(self, spec, ev, cap):
+        return (id(ev), spec, int(self.args.numMCTSSims), float(self.args.cpuct), cap, str(self.device))
+
+    def _release(self):
+        """Hand this instance's engine (and graph) back to the pool."""
+        if self._engine is None:
+            return
+        entry = (self._engine, self._sims_graph, self._graph_sims, self._warm)
+        idle = _POOL.setdefault(self._key, [])
+        if len(idle) < _POOL_MAX:
+            idle.append(entry)
+        else:
+            self._engine.close()
+        self._engine, self._sims_graph, self._warm = None, None, False
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
 
     def _engine_for(self, game):
         spec = game_spec(game)
         if self._engine is None or self._max_turns != spec:
-            if self._engine is not None:
-                self._engine.close()
+            self._release()
             name, n, max_turns = spec
             cap = self.node_capacity or whole_game_capacity(self.args.numMCTSSims, game)
-            self._engine = SelfPlayEngine(1, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct,
-                                          temp_threshold=1, max_turns=max_turns, game=name, n=n,
-                                          evaluator=_evaluator_of(self.nnet, self.device), device=self.device,
-                                          node_capacity=cap, max_depth=1024, gc=False, record=False)
+            ev = _evaluator_of(self.nnet, self.device)
+            self._key = self._pool_key(spec, ev, cap)
+            idle = _POOL.get(self._key)
+            if idle:
+                self._engine, self._sims_graph, self._graph_sims, self._warm = idle.pop()
+                self._engine.reset()  # a fresh tree, as a new MCTS's empty dicts
+            else:
+                self._engine = SelfPlayEngine(1, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct,
+                                              temp_threshold=1, max_turns=max_turns, game=name, n=n,
+                                              evaluator=ev, device=self.device, node_capacity=cap, max_depth=1024,
+                                              gc=False, record=False)
+                self._sims_graph, self._warm = None, False
             self._max_turns = spec
-            self._sims_graph, self._warm = None, False
         return self._engine
 
     def _capture(self, eng, sims):
@@ -94,6 +161,8 @@ class MCTS:
             with torch.cuda.device(self.device), torch.cuda.graph(g):
                 for _ in range(sims):
                     eng.simulate()
+        except AzgError:
+            raise  # an engine error is an error, not a capture limitation
         except RuntimeError as e:
             warnings.warn(f"MCTS: evaluator not graph-capturable ({e}); searching eagerly")
             self.graph = False
@@ -120,8 +189,13 @@ class MCTS:
         self._warm = True
 
     def _run(self, game, sims):
-        if game.outcome != GameOutcome.ONGOING:
+        if not ongoing(game.outcome):
             raise ValueError("search from a finished game")
+        if not self.native(game):  # the generic plugin path: numpy's global stream, as the reference
+            hs = self._host_search()
+            for _ in range(sims):
+                hs.simulate([game])
+            return None
         eng = self._engine_for(game)
         state = np.random.get_state()
         eng.set_rng(0, state[1], state[2])
@@ -143,7 +217,7 @@ class MCTS:
         if not (isinstance(temp, (int, float)) and temp >= 0):
             raise AssertionError("temp must be a number >= 0")
         eng = self._run(game, int(self.args.numMCTSSims))
-        counts = eng.root_counts(0).astype(np.int64)
+        counts = eng.root_counts(0).astype(np.int64) if eng is not None else self._host.root_counts(0, game)
         if temp == 0:
             best = np.argwhere(counts == np.max(counts)).ravel()
             pick = np.random.choice(best)
@@ -154,6 +228,10 @@ class MCTS:
         return counts / counts.sum()
 
     def stats(self):
+        if self._host is not None:
+            h = self._host
+            return {"expansions": h.expansions, "terminal_hits": h.terminal_hits, "fallbacks": h.fallbacks,
+                    "nodes": h.nodes(0), "error": 0}
         return self._engine.stats() if self._engine is not None else {}
 
     def reset(self):

@@ -20,6 +20,7 @@ Fixtures written (all small, gzip'd JSON or npz):
   pairwise_kat.npz       numpy f32 pairwise .sum() known answers
   mcts_<set>.json.gz     Coach.executeEpisode + MCTS traces driven by stubnet
   mcts_realnet_*.json.gz the same driven by the reference NNetWrapper (manual_seed 0 net)
+  mcts_toy*.json.gz      the same for tests/golden/toygame.py, a plugin with no native rules
   arena_<set>.json.gz    Arena.playGame MCTSPlayer(stubnet) vs Random/Greedy players
   nnet_golden.npz        InflexionNNet(manual_seed 0) checksum + (planes -> P, v)
   train_golden.json.gz   NNetWrapper.train (32 channels, 2 epochs): losses + weight digests
@@ -157,7 +158,7 @@ def gen_pairwise(np):
 
 
 # -------------------------------------------------------------------------- MCTS
-def gen_mcts(np, quick, othello=False, realnet=False):
+def gen_mcts(np, quick, othello=False, realnet=False, toy=False):
     """Reference Coach.executeEpisode + MCTS traces.  With othello=True the
     reference search is driven with this repo's builder-authored OthelloGame
     plugin (the reference has no Othello): the rules are ours, the search,
@@ -175,7 +176,7 @@ def gen_mcts(np, quick, othello=False, realnet=False):
     from utils import dotdict
     from stubnet import stub_eval
     GameCls = InflexionGame
-    if othello:
+    if othello or toy:
         sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
         import flags as ref_flags
         import azg_amd  # noqa: F401
@@ -185,6 +186,9 @@ def gen_mcts(np, quick, othello=False, realnet=False):
         own_flags.PlayerColour = ref_flags.PlayerColour
         from azg_amd.othello import OthelloGame
         GameCls = OthelloGame
+        if toy:  # tests/golden/toygame.py: a plugin with no native rules (the generic host path)
+            from toygame import FourInARowGame
+            GameCls = FourInARowGame
 
     class StubNNet(NNetWrapper):
         def __init__(self, game):  # no torch model: the hash evaluator only
@@ -275,11 +279,18 @@ def gen_mcts(np, quick, othello=False, realnet=False):
                 "realnet_othello8": dict(n=8, sims=25, cpuct=1, temp_threshold=30, seeds=[600, 601, 602, 603]),
                 "realnet_othello8_s200": dict(n=8, sims=200, cpuct=1, temp_threshold=30, seeds=[700, 701, 702]),
             }
+    if toy:
+        sets = {
+            "toy": dict(n=6, sims=25, cpuct=1, temp_threshold=10, seeds=list(range(900, 916))),
+            "toy_s100": dict(n=6, sims=100, cpuct=1.0, temp_threshold=4, seeds=list(range(950, 954))),
+        }
+        if realnet:
+            sets = {"realnet_toy": dict(n=6, sims=25, cpuct=1, temp_threshold=10, seeds=list(range(920, 926)))}
     for name, cfg in sets.items():
         eps = []
         t0 = time.time()
         for seed in cfg["seeds"]:
-            game = GameCls(cfg["n"]) if othello else InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
+            game = GameCls(cfg["n"]) if (othello or toy) else InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
             if realnet:
                 key = (GameCls.__name__, cfg.get("n", 7))
                 if key not in real_nets:
@@ -707,6 +718,8 @@ def main():
         "othello": lambda: gen_mcts(np, quick, othello=True),
         "realnet": lambda: gen_mcts(np, quick, realnet=True),
         "realnet_othello": lambda: gen_mcts(np, quick, othello=True, realnet=True),
+        "toy": lambda: gen_mcts(np, quick, toy=True),
+        "realnet_toy": lambda: gen_mcts(np, quick, toy=True, realnet=True),
         "arena": lambda: gen_arena(np),
         "train": lambda: gen_train(np),
         "sensitivity": lambda: gen_realnet_sensitivity(np),

@@ -598,3 +598,33 @@ def test_small_forward_matches_reference(n, depth, A, B):
     torch.testing.assert_close(p, torch.exp(logp), rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(v.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(p, p2, rtol=1e-5, atol=1e-7)
+
+
+def test_split_form_under_expandable_segments():
+    """the range flag's device check (azg_ptr.h, hipPointerGetAttributes) must
+    accept torch's expandable-segment (VMM) allocations, or the default split evaluator
+    would fail with AZG_ERR_ARG under PYTORCH_HIP_ALLOC_CONF=expandable_segments:True."""
+    import subprocess
+    import sys
+    code = (
+        "import torch, azg_amd\n"
+        "from azg_amd.nnet import InferenceNet, InflexionNNet\n"
+        "torch.manual_seed(0)\n"
+        "net = InflexionNNet().cuda().eval()\n"
+        "x = (torch.rand(256, 4, 7, 7, device='cuda') < 0.3).float()\n"
+        "a = InferenceNet(net)\n"
+        "b = InferenceNet(net)\n"
+        "with torch.no_grad():\n"
+        "    for _ in range(2):\n"
+        "        pa, va = a(x)\n"
+        "        pb, vb = b(x)\n"
+        "    ref = torch.exp(net(x)[0])\n"
+        "torch.cuda.synchronize()\n"
+        "assert torch.equal(pa, pb)\n"
+        "assert ((pa - ref).abs() / ref).max().item() < 1e-5\n"
+        "print('ok', torch.cuda.memory._get_current_allocator if hasattr(torch.cuda.memory, '_get_current_allocator') else '')\n")
+    env = dict(os.environ, PYTORCH_HIP_ALLOC_CONF="expandable_segments:True",
+               PYTORCH_CUDA_ALLOC_CONF="expandable_segments:True")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

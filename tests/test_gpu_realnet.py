@@ -9,12 +9,15 @@ main.py's 25 sims (4 seeds), 40-turn games at C3's 100 sims (2 seeds), and whole
 of the builder's Othello plugin: 6x6 at 25 sims (C1, 4 seeds), 8x8 at 25 sims (2) and
 at C5's 200 sims (1).
 
-Each is replayed three ways:
+Each is replayed by:
   * the drop-in MCTS + Coach.executeEpisode with an NNetWrapper (batch-1 forward of
-    the reference module on the GPU);
+    the reference module on the GPU), and with InferenceNet(conv="miopen", gemm="f32")
+    as its evaluator (the form INTEGRATION.md recommends for the drop-in) -- all 8
+    realnet_main seeds;
   * SelfPlayEngine with InferenceNet(gemm="split") at 4096 concurrent games -- the
-    benchmarked path (Winograd transforms, split-fp16 MFMA GEMMs, split-K fc1);
-  * the same with InferenceNet(gemm="f32") (f32 hipBLASLt GEMMs).
+    benchmarked path (Winograd transforms, split-fp16 MFMA GEMMs, split-K fc1) -- and at
+    C2's 256 and 512 games (the split GEMM's 128 / 64-row schedules, the f32 FC tail);
+  * the same with InferenceNet(gemm="f32") (f32 hipBLASLt GEMMs) at 1024 games.
 pi returned by getActionProb is a function of the counts (MCTS.py:48-60), so equal
 counts give pi exactly (tolerance 0, inside the north_star's 1e-5).
 
@@ -31,12 +34,16 @@ What is asserted, per seed, against the reference's visit counts:
     CPU one to ~1e-6 relative (root priors here: ~5e-9 absolute), and over a whole
     344-move game the search meets PUCT ties closer than that: the reference's OWN
     traces diverge the same way when its network's weights (or outputs) move by
-    1e-7 or 1e-6 relative (tests/golden/realnet_sensitivity.json.gz, first
-    divergent moves printed beside ours).  Once one decision differs the games are different games,
-    so nothing after it is compared.  Every flip is reported with its move and the
-    root's prior error and smallest prior gap; a mismatch of any other shape --
-    more than one decision, inside the first 40 moves, or at a move the reference's
-    own perturbed runs do not certify as a near-tie -- fails.
+    1e-7 or 1e-6 relative.  Every flip is reported with its move and the root's prior
+    error and smallest prior gap; a mismatch of any other shape -- more than one
+    decision, inside the first 40 moves, or at a move the reference's own perturbed
+    runs do not certify as a near-tie -- fails;
+  * after a certified flip the game goes on being compared: the flipped move's counts
+    must equal those of the reference's own perturbed run that diverges there
+    (tests/golden/realnet_branches.json.gz), and every later move is compared with that
+    run (final board, outcome and RNG position included) -- the game the reference
+    itself plays when its rounding falls the other way.  Each test prints how many of
+    its moves were compared (all of them, on MI355X).
 The sims100 games (40 turns) must match entirely.
 """
 import numpy as np
