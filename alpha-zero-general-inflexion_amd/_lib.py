@@ -82,11 +82,9 @@ SIGNATURES = [
     ("azg_policy_value_parts", ctypes.c_int, [_VP, _I32, _I64, _I32, _VP, ctypes.c_float, _VP, _VP, _I32, _I32,
                                               _VP]),
     ("azg_split_gemm_variant", ctypes.c_int, [_I32, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
-    ("azg_small_gemm_partial", ctypes.c_int, [_VP, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _I32,
-                                              _I32, _I32, _I32, _VP, _VP]),
-    ("azg_small_gemm_reduce", ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _I32, _VP, _I32, _VP]),
-    ("azg_small_layer", ctypes.c_int, [_VP, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _I32, _I32,
-                                       _VP, _I32, _VP, _I32, _VP]),
+    ("azg_small_conv3x3", ctypes.c_int, [_VP, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _I32, _I32, _VP, _I32,
+                                         _VP, _I32, _VP]),
+    ("azg_small_fc", ctypes.c_int, [_VP, _I32, _I32, _VP, _I32, _I32, _VP, _I32, _VP, _I32, _VP]),
     ("azg_split_gemm_pick", ctypes.c_int, [_I32, _VP, _VP, _I32]),
     ("azg_set_gemm_blocks", ctypes.c_int, [_I32]),
     ("azg_set_arena", ctypes.c_int, [_VP, _VP, _VP, _VP]),

@@ -207,16 +207,18 @@ def broadcast_weights(module, src=0, group=None):
     rest = [t for t in tensors if t.dtype != torch.float32]
     flat = _flatten_dense_tensors([t.data for t in f32])
     dist.broadcast(flat, src=src, group=group)
-    for t, f in zip(f32, _unflatten_dense_tensors(flat, [t.data for t in f32])):
-        t.data.copy_(f)
+    with torch.no_grad():  # in-place copies that bump the tensors' version counters (mcts.fast_evaluator)
+        for t, f in zip(f32, _unflatten_dense_tensors(flat, [t.data for t in f32])):
+            t.copy_(f)
     nbytes = flat.numel() * 4
     if rest:
         ints = torch.cat([t.data.reshape(-1).to(torch.int64) for t in rest])
         dist.broadcast(ints, src=src, group=group)
         off = 0
-        for t in rest:
-            t.data.copy_(ints[off:off + t.numel()].reshape(t.shape).to(t.dtype))
-            off += t.numel()
+        with torch.no_grad():
+            for t in rest:
+                t.copy_(ints[off:off + t.numel()].reshape(t.shape).to(t.dtype))
+                off += t.numel()
         nbytes += ints.numel() * 8
     return nbytes
 

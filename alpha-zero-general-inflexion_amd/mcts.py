@@ -22,7 +22,9 @@ instead: the reference's search on the host over the plugin's own methods, the l
 evaluated by the network on the GPU ("unknown Game subclasses fall back to a
 CPU path that calls the Python methods").
 """
+import itertools
 import warnings
+import weakref
 
 import numpy as np
 import torch
@@ -32,7 +34,36 @@ from .engine import SelfPlayEngine, game_spec
 from .flags import ongoing
 
 
-def _evaluator_of(nnet, device):
+# InflexionNNet module -> [weights version, its InferenceNet] (fast_evaluator)
+_FAST = weakref.WeakKeyDictionary()
+
+
+def _weights_version(module):
+    """Sum of the autograd version counters of every parameter and buffer: it moves with
+    every in-place update (optimizer steps, load_state_dict, dist.broadcast_weights)."""
+    return sum(t._version for t in itertools.chain(module.parameters(), module.buffers()))
+
+
+def fast_evaluator(module, device):
+    """The drop-in's leaf evaluator for an InflexionNNet: its InferenceNet (BN folded; at the
+    drop-in's one leaf per simulation the small-batch kernels of azg_small.hip),
+    cached per module and re-folded in place whenever the module's weights have changed since
+    (training between episodes), so captured graphs stay valid."""
+    from .nnet import InferenceNet
+    ver = _weights_version(module)
+    hit = _FAST.get(module)
+    if hit is None:
+        with torch.cuda.device(device):
+            ev = InferenceNet(module.to(device), conv="miopen", gemm="f32")
+        _FAST[module] = [ver, ev]
+        return ev
+    if hit[0] != ver:
+        hit[1].refresh_from(module)
+        hit[0] = ver
+    return hit[1]
+
+
+def _evaluator_of(nnet, device, fast=True):
     if isinstance(nnet, str):
         return nnet
     ev = getattr(nnet, "azg_evaluator", None)
@@ -40,6 +71,9 @@ def _evaluator_of(nnet, device):
         return ev
     module = getattr(nnet, "nnet", nnet)
     if isinstance(module, torch.nn.Module):
+        from .nnet import InflexionNNet
+        if fast and type(module) is InflexionNNet:
+            return fast_evaluator(module, device)
         module = module.to(device)
         module.eval()
         return module
@@ -79,9 +113,12 @@ def whole_game_capacity(sims, game):
 
 
 class MCTS:
-    def __init__(self, nnet, args, device=None, node_capacity=None, graph=True):
+    def __init__(self, nnet, args, device=None, node_capacity=None, graph=True, fast=True):
         self.nnet = nnet
         self.args = args
+        # fast: an InflexionNNet (e.g. a NNetWrapper's .nnet) is evaluated through its
+        # InferenceNet (fast_evaluator); False evaluates the module itself, as the reference does
+        self.fast = bool(fast)
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.node_capacity = node_capacity  # None: whole_game_capacity
         # graph: after one eager getActionProb, the numMCTSSims simulations of a call are
@@ -137,7 +174,7 @@ class MCTS:
             self._release()
             name, n, max_turns = spec
             cap = self.node_capacity or whole_game_capacity(self.args.numMCTSSims, game)
-            ev = _evaluator_of(self.nnet, self.device)
+            ev = _evaluator_of(self.nnet, self.device, self.fast)
             self._key = self._pool_key(spec, ev, cap)
             idle = _POOL.get(self._key)
             if idle:
@@ -191,6 +228,8 @@ class MCTS:
     def _run(self, game, sims):
         if not ongoing(game.outcome):
             raise ValueError("search from a finished game")
+        if self._engine is not None and self.fast:
+            _evaluator_of(self.nnet, self.device, True)  # re-fold the weights if they were trained since
         if not self.native(game):  # the generic plugin path: numpy's global stream, as the reference
             hs = self._host_search()
             for _ in range(sims):
@@ -235,4 +274,4 @@ class MCTS:
         return self._engine.stats() if self._engine is not None else {}
 
     def reset(self):
-        return MCTS(self.nnet, self.args, self.device, self.node_capacity, self.graph)
+        return MCTS(self.nnet, self.args, self.device, self.node_capacity, self.graph, self.fast)

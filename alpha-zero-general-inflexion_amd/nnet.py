@@ -28,11 +28,10 @@ DEFAULT_ARGS = dict(lr=0.001, dropout=0.3, epochs=10, batch_size=512, num_channe
                     # (profiles/r01_train_probe.json)
                     fused_adam=False, train_dtype="f32")
 WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C1: 1 game)
-# below WINOGRAD_MIN_BATCH: the whole forward on libazg's small f32 GEMMs (azg_small.hip) instead of
-# MIOpen / hipBLASLt.  Off by default: correct (tests/test_gpu_nn.py) but measured slower at one leaf
-# (3.7 vs 3.0 ms per 25-simulation getActionProb with azg_small_layer, profiles/r03_small_layer.json)
-SMALL_PATH = False
-SMALL_LAYER_MAX_B = 4  # up to this many leaves a small-path layer is one azg_small_layer launch
+# up to SMALL_MAX_B leaves: the whole forward on libazg's small-batch kernels (azg_small.hip: one
+# launch per layer, no library) instead of MIOpen / hipBLASLt
+SMALL_PATH = True
+SMALL_MAX_B = 4
 FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
 FC1_KPARTS = 4  # split-K parts of fc1 on libazg's split GEMM (4608 = 4 x 1152 for the 7x7 board)
 # split-K parts of fc2 (1024 -> 512) and [fc3 | fc4] (512 -> 344, padded to 512 columns) when the whole
@@ -252,8 +251,8 @@ class InferenceNet(nn.Module):
         the f32 GEMM's), "split_blas" (the same products as one hipBLASLt fp16 GEMM
         over [hi | lo | hi] rows) or "f32" (f32 MFMA GEMMs, hipBLASLt).
 
-        small: below WINOGRAD_MIN_BATCH leaves, run the whole forward on libazg's small f32
-        GEMMs (azg_small.hip) instead of MIOpen / hipBLASLt (None: SMALL_PATH)."""
+        small: up to SMALL_MAX_B leaves, run the whole forward on libazg's small-batch
+        kernels (azg_small.hip) instead of MIOpen / hipBLASLt (None: SMALL_PATH)."""
         super().__init__()
         if conv not in ("miopen", "azg", "auto", "winograd"):
             raise ValueError(f"unknown conv implementation {conv!r}")
@@ -266,10 +265,10 @@ class InferenceNet(nn.Module):
         self.mscale = {}  # Winograd layer -> 2^-k undoing the split operand's scale
         self._choices = {}
         self._ws = None  # Winograd V / M workspace, grown to the largest layer seen
-        # below WINOGRAD_MIN_BATCH leaves: the whole forward on libazg's small f32 GEMMs
-        # (azg_small.hip) instead of MIOpen / hipBLASLt; conv="miopen" keeps the library
-        self.small_path = conv in ("winograd", "auto") and (SMALL_PATH if small is None else bool(small))
-        self._small_plans = {}
+        # up to SMALL_MAX_B leaves: the whole forward on libazg's small-batch kernels
+        # (azg_small.hip) instead of MIOpen / hipBLASLt
+        self.small_path = SMALL_PATH if small is None else bool(small)
+        self._init_args = (conv, gemm, small)
         self.h_out = {}  # output side per conv layer
         self.fuse_transforms = True  # conv2->3->4: output + next input transform in one pass
         self.n, self.depth, c = net.n, net.depth, net.num_channels
@@ -679,84 +678,64 @@ class InferenceNet(nn.Module):
                                             ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()), B, A, st))
         return p, v
 
-    @staticmethod
-    def _small_plan(Cin, taps, tiles):
-        """(kc, ksplit) for one small GEMM: K = taps x Cin in slabs of kc (the largest power
-        of two <= 64 dividing Cin, so a slab lies in one tap), split into ksplit ranges so
-        that tiles x ksplit blocks fill about one round of the chip (the largest divisor of
-        the slab count up to that target)."""
-        target = max(1, -(-256 // tiles))
-        kc = 64
-        while Cin % kc:  # the largest slab: a slab's loads are one round trip, so fewer, fuller slabs
-            kc //= 2
-        slabs = taps * Cin // kc
-        return kc, max(d for d in range(1, min(slabs, target) + 1) if slabs % d == 0)
+    def refresh_from(self, net):
+        """Re-fold `net`'s current weights into this form's own buffers, in place (the same
+        storage, so HIP graphs captured over this evaluator stay valid; the small-batch path
+        passes no weight-dependent scalars to its kernels)."""
+        fresh = InferenceNet(net, *self._init_args)
+        for name, buf in fresh.named_buffers():
+            if name == "overflow":
+                continue
+            getattr(self, name).copy_(buf)
+        self.mscale = dict(fresh.mscale)
+        for k in ("fc1_scale", "fc2_scale", "fc34_scale"):
+            if hasattr(fresh, k):
+                setattr(self, k, getattr(fresh, k))
 
-    def _small_gemm(self, key, x, strides, B, H, pad, taps, w, Cin, Cout, bias, relu):
-        """One layer on azg_small_layer (up to SMALL_LAYER_MAX_B leaves: one launch, no
-        partial sums) or azg_small_gemm_partial + azg_small_gemm_reduce; returns the
-        [B * Ho * Ho, Cout] f32 output (NHWC rows)."""
+    def _forward_small(self, planes):
+        """The forward at up to SMALL_MAX_B leaves on libazg's small-batch kernels
+        (azg_small.hip): conv1-4 (+ folded BN, bias, ReLU) from the NCHW leaf planes to NHWC
+        rows, fc1 / fc2 (+ ReLU), [fc3 | fc4], then azg_policy_value's softmax / tanh."""
         import ctypes
         from . import _lib
         L = _lib.lib()
-        Ho = H + 2 * pad - 2 if taps == 9 else H
-        npx = B * Ho * Ho
-        dev = x.device
-        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        sB, sY, sX, sC = strides
-        if B <= SMALL_LAYER_MAX_B and Cin % 2 == 0 and H * H * Cin <= 32768 and w.data_ptr() % 8 == 0:
-            y = torch.empty((npx, Cout), device=dev, dtype=torch.float32)
-            _lib.check(L.azg_small_layer(ctypes.c_void_p(x.data_ptr()), sB, sY, sX, sC, B, H, H, pad, taps,
-                                         ctypes.c_void_p(w.data_ptr()), Cin, Cout,
-                                         ctypes.c_void_p(bias.data_ptr()) if bias is not None else None, int(relu),
-                                         ctypes.c_void_p(y.data_ptr()), Cout, st))
-            return y
-        plan = self._small_plans.get((key, B))
-        if plan is None:
-            plan = self._small_plans[(key, B)] = self._small_plan(Cin, taps, -(-Cout // 128) * -(-npx // 64))
-        kc, ks = plan
-        part = torch.empty(ks * npx * Cout, device=dev, dtype=torch.float32)
-        y = torch.empty((npx, Cout), device=dev, dtype=torch.float32)
-        _lib.check(L.azg_small_gemm_partial(ctypes.c_void_p(x.data_ptr()), sB, sY, sX, sC, B, H, H, pad, taps,
-                                            ctypes.c_void_p(w.data_ptr()), Cin, Cout, kc, ks,
-                                            ctypes.c_void_p(part.data_ptr()), st))
-        _lib.check(L.azg_small_gemm_reduce(ctypes.c_void_p(part.data_ptr()), ks, npx, Cout,
-                                           ctypes.c_void_p(bias.data_ptr()) if bias is not None else None, int(relu),
-                                           ctypes.c_void_p(y.data_ptr()), Cout, st))
-        return y
-
-    def _forward_small(self, planes):
-        """The forward below WINOGRAD_MIN_BATCH leaves on libazg's small f32 GEMMs:
-        conv1-4 (+ folded BN, bias, ReLU) from the NCHW leaf planes to NHWC activations,
-        fc1 / fc2 (+ ReLU), [fc3 | fc4] and azg_policy_value's softmax / tanh."""
-        import ctypes
-        from . import _lib
         planes = planes.contiguous()
         B, n, C = planes.shape[0], self.n, self.w1.shape[0]
-        x, strides, H = planes, (self.depth * n * n, n, 1, n * n), n
-        cin = self.depth
+        dev = planes.device
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        x, strides, H, cin = planes, (self.depth * n * n, n, 1, n * n), n, self.depth
         for i, pad in enumerate(self.pads, start=1):
-            w = getattr(self, f"w{i}")  # channels_last: [co][ky][kx][ci] in memory
-            x = self._small_gemm(f"conv{i}", x, strides, B, H, pad, 9, w, cin, C, getattr(self, f"b{i}"), True)
-            H = H + 2 * pad - 2
-            strides, cin = (H * H * C, H * C, C, 1), C
+            Ho = H + 2 * pad - 2
+            y = torch.empty((B * Ho * Ho, C), device=dev, dtype=torch.float32)
+            _lib.check(L.azg_small_conv3x3(ctypes.c_void_p(x.data_ptr()), *strides, B, H, pad,
+                                           ctypes.c_void_p(getattr(self, f"w{i}").data_ptr()), cin, C,
+                                           ctypes.c_void_p(getattr(self, f"b{i}").data_ptr()), 1,
+                                           ctypes.c_void_p(y.data_ptr()), C, st))
+            x, H, cin = y, Ho, C
+            strides = (H * H * C, H * C, C, 1)
         feat = H * H * C  # NHWC flatten (fw1's column order)
-        x = self._small_gemm("fc1", x, (feat, 0, 0, 1), B, 1, 0, 1, self.fw1, feat, self.fw1.shape[0], self.fb1, True)
-        n1 = self.fw1.shape[0]
-        x = self._small_gemm("fc2", x, (n1, 0, 0, 1), B, 1, 0, 1, self.fw2, n1, self.fw2.shape[0], self.fb2, True)
-        n2, A = self.fw2.shape[0], self.fw3.shape[0]
-        pv = self._small_gemm("fc34", x, (n2, 0, 0, 1), B, 1, 0, 1, self.fw34, n2, A + 1, None, False)
-        p = torch.empty((B, A), device=planes.device, dtype=torch.float32)
-        v = torch.empty((B, 1), device=planes.device, dtype=torch.float32)
-        _lib.check(_lib.lib().azg_policy_value(
-            ctypes.c_void_p(pv.data_ptr()), A + 1, ctypes.c_void_p(self.fb34.data_ptr()), 1.0,
-            ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()), B, A,
-            ctypes.c_void_p(torch.cuda.current_stream(planes.device).cuda_stream)))
+
+        def fc(x, ldx, w, b, relu):
+            N, K = w.shape
+            out = torch.empty((B, N), device=dev, dtype=torch.float32)
+            _lib.check(L.azg_small_fc(ctypes.c_void_p(x.data_ptr()), ldx, B, ctypes.c_void_p(w.data_ptr()), K, N,
+                                      ctypes.c_void_p(b.data_ptr()) if b is not None else None, int(relu),
+                                      ctypes.c_void_p(out.data_ptr()), N, st))
+            return out
+        h1 = fc(x, feat, self.fw1, self.fb1, True)
+        h2 = fc(h1, h1.shape[1], self.fw2, self.fb2, True)
+        pv = fc(h2, h2.shape[1], self.fw34, None, False)  # [B, A + 1]; the heads add fb34
+        A = self.fw3.shape[0]
+        p = torch.empty((B, A), device=dev, dtype=torch.float32)
+        v = torch.empty((B, 1), device=dev, dtype=torch.float32)
+        _lib.check(L.azg_policy_value(ctypes.c_void_p(pv.data_ptr()), A + 1, ctypes.c_void_p(self.fb34.data_ptr()),
+                                      1.0, ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()), B, A, st))
         return p, v
 
     def forward(self, s):
         planes = s.view(-1, self.depth, self.n, self.n)
-        if self.small_path and planes.is_cuda and planes.shape[0] < WINOGRAD_MIN_BATCH and self.fw3.shape[0] <= 1024:
+        if (self.small_path and planes.is_cuda and planes.shape[0] <= SMALL_MAX_B and self.fw3.shape[0] <= 1024
+                and self.w1.shape[0] % 2 == 0 and planes.shape[-1] ** 2 * planes.shape[0] <= 256):
             return self._forward_small(planes)
         x = planes
         hook = self.conv_hook

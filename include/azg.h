@@ -227,27 +227,21 @@ int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, cons
  * other values return AZG_ERR_ARG here. */
 int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, float* m, int32_t nruns,
                             const int32_t* points, const int32_t* rows, int32_t c, int32_t k, void* stream);
-/* The leaf network at a few leaves (below the Winograd path's 64): one 3x3 conv
- * (taps 9, zero padding pad) or FC layer (taps 1, H = W = 1) as a small f32 GEMM
- * out[px][co] = sum_k w[co][k] x[k][px], k = tap * Cin + ci, w [Cout][taps][Cin] (a
- * channels_last conv weight, BN folded; an FC weight [Cout][Cin]), x any layout given by
- * its element strides (sB per leaf, sY, sX, sC), px = (leaf, y, x) of the Ho x Wo output.
- * partial: K in slabs of kc (a power of two <= 64 dividing Cin), split into ksplit equal ranges
- * (dividing the slab count), part [ksplit][px][Cout] f32; reduce: y[px * ldy + co] = (sum
- * of the ksplit parts in order) + bias, ReLU if relu. */
-int  azg_small_gemm_partial(const float* x, int64_t sB, int32_t sY, int32_t sX, int32_t sC, int32_t batch,
-                            int32_t H, int32_t W, int32_t pad, int32_t taps, const float* w, int32_t Cin,
-                            int32_t Cout, int32_t kc, int32_t ksplit, float* part, void* stream);
-int  azg_small_gemm_reduce(const float* part, int32_t ksplit, int32_t npx, int32_t Cout, const float* bias,
-                           int32_t relu, float* y, int32_t ldy, void* stream);
-/* The same layer in one launch with no partial sums (one leaf to a few): y[px * ldy + co] =
- * sum_k w[co][k] x[k][px] + bias, ReLU if relu; blocks own (8 co, one output row) of a conv
- * up to 8 wide (only the window's three input rows in LDS), (8 co, <= 13 pixels) of a wider
- * one, or 4 co of an FC layer; their threads split K and sum their partials through LDS.
- * Needs Cin even, H * W * Cin <= 32768 (one leaf's input in LDS) and w 8-B aligned. */
-int  azg_small_layer(const float* x, int64_t sB, int32_t sY, int32_t sX, int32_t sC, int32_t batch, int32_t H,
-                     int32_t W, int32_t pad, int32_t taps, const float* w, int32_t Cin, int32_t Cout,
-                     const float* bias, int32_t relu, float* y, int32_t ldy, void* stream);
+/* The leaf network at one to four leaves (azg_small.hip; InferenceNet's forward below
+ * SMALL_MAX_B leaves, the drop-in MCTS's batch-1 search), one launch per layer, f32 with a
+ * fixed summation order:
+ *   azg_small_conv3x3: y[px * ldy + co] = relu?(bias[co] + sum_k w[co][k] x_im2col[k][px]),
+ *     k = tap * Cin + ci, w [Cout][3][3][Cin] (a channels_last conv weight, BN folded),
+ *     px = (leaf, oy, ox) of the (H + 2 pad - 2)^2 output, x any layout given by its
+ *     element strides (sB per leaf, sY, sX, sC: the NCHW leaf planes or the NHWC rows this
+ *     writes); Cout even, at most 256 output pixels, pad 0 or 1; bias may be null;
+ *   azg_small_fc: y[b * ldy + n] = relu?(bias[n] + sum_k w[n][k] x[b * ldx + k]), b < batch <= 4,
+ *     w [N][K] row-major, K % 4 == 0, ldx % 4 == 0, x and w 16-B aligned; bias may be null. */
+int  azg_small_conv3x3(const float* x, int64_t sB, int32_t sY, int32_t sX, int32_t sC, int32_t batch, int32_t H,
+                       int32_t pad, const float* w, int32_t Cin, int32_t Cout, const float* bias, int32_t relu,
+                       float* y, int32_t ldy, void* stream);
+int  azg_small_fc(const float* x, int32_t ldx, int32_t batch, const float* w, int32_t K, int32_t N, const float* bias,
+                  int32_t relu, float* y, int32_t ldy, void* stream);
 /* The schedule azg_split_gemm picks for a launch of this shape (4, 17 or 18). */
 int  azg_split_gemm_pick(int32_t nruns, const int32_t* points, const int32_t* rows, int32_t k);
 /* Cap the persistent split GEMM's grid at `blocks` workgroups (one per CU; 0 = every CU;

@@ -302,3 +302,52 @@ def test_arena_replays_with_f32_form_where_split_overflows():
     assert got == ref_arena.playGames(128)
     assert np.array_equal(arena.last_moves["actions"], ref_arena.last_moves["actions"])
     assert np.array_equal(arena.last_engine_state["boards"], ref_arena.last_engine_state["boards"])
+
+
+def test_dropin_pools_engines_and_refolds_trained_weights():
+    """a new MCTS per episode (Coach.py:110) reuses the engine and captured graph
+    of the last one with the same network (reset: an empty tree, as a new MCTS's dicts), with
+    results equal to a fresh engine's; after the network's weights change in place (training)
+    the drop-in's evaluator is re-folded, so its counts follow the new weights."""
+    import azg_amd  # noqa: F401
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.mcts import MCTS
+    from azg_amd.nnet import InferenceNet, NNetWrapper
+
+    args = Args(numMCTSSims=25, cpuct=1, tempThreshold=30)
+    game = InflexionGame(7, max_turns=343, max_power=6)
+    torch.manual_seed(0)
+    w = NNetWrapper(game, device="cuda")
+
+    def episode(mcts, seed, moves=4):
+        np.random.seed(seed)
+        g = game.restarted()
+        out = []
+        for _ in range(moves):
+            pi = mcts.getActionProb(g, temp=1)
+            out.append(mcts._engine.root_counts(0).copy())
+            g = g.to_next_state(int(np.random.choice(len(pi), p=pi)))
+        return out
+
+    m1 = MCTS(w, args)
+    c1 = episode(m1, 11)
+    eng = m1._engine
+    assert m1._sims_graph is not None
+    del m1
+    m2 = MCTS(w, args)
+    c2 = episode(m2, 11)
+    assert m2._engine is eng and m2._sims_graph is not None  # pooled engine and graph
+    assert all(np.array_equal(a, b) for a, b in zip(c1, c2))
+    del m2
+    with torch.no_grad():  # "training": the weights move in place
+        w.nnet.fc3.weight.mul_(3.0)
+        w.nnet.conv2.weight.add_(0.01)
+    m3 = MCTS(w, args)
+    c3 = episode(m3, 11)
+    assert m3._engine is eng
+    w_ref = NNetWrapper(game, device="cuda")
+    w_ref.nnet.load_state_dict(w.nnet.state_dict())
+    w_ref.azg_evaluator = InferenceNet(w_ref.nnet.eval(), conv="miopen", gemm="f32")
+    c_ref = episode(MCTS(w_ref, args), 11)
+    assert all(np.array_equal(a, b) for a, b in zip(c3, c_ref))
+    assert not all(np.array_equal(a, b) for a, b in zip(c1, c3))

@@ -483,81 +483,26 @@ def test_first_layer_any_planes(kind):
 
 
 @pytest.mark.parametrize("B,H,pad,cin,cout", [(1, 7, 1, 4, 512), (1, 7, 1, 512, 512), (3, 7, 0, 512, 512),
-                                              (1, 5, 0, 512, 512), (63, 7, 1, 512, 512), (2, 8, 1, 2, 512),
-                                              (5, 6, 0, 64, 96), (1, 1, 0, 4608, 1024), (17, 1, 0, 1024, 512),
-                                              (7, 1, 0, 512, 344)])
-def test_small_gemm_matches_torch(B, H, pad, cin, cout):
-    """azg_small_gemm_partial + reduce (the forward below 64 leaves): a 3x3 conv (or an
-    FC layer, H = 1 and taps 1) + bias + ReLU against torch in f64, NCHW and NHWC inputs,
-    ragged pixel and channel counts, every K split the planner picks."""
-    import ctypes
-    import azg_amd  # noqa: F401
-    from azg_amd import _lib
-    from azg_amd.nnet import InferenceNet
-    torch.manual_seed(3)
-    taps = 9 if H > 1 else 1
-    x = torch.randn(B, cin, H, H, device="cuda")
-    w = torch.randn(cout, cin, 3, 3, device="cuda") / (cin * taps) ** 0.5 if taps == 9 else \
-        torch.randn(cout, cin, device="cuda") / cin ** 0.5
-    b = torch.randn(cout, device="cuda")
-    if taps == 9:
-        want = torch.relu(torch.nn.functional.conv2d(x.double(), w.double(), b.double(), padding=pad))
-        want = want.permute(0, 2, 3, 1).reshape(-1, cout)
-        wk = w.contiguous(memory_format=torch.channels_last)
-    else:
-        want = torch.relu(x.double().reshape(B, cin) @ w.double().t() + b.double())
-        wk = w.contiguous()
-    Ho = H + 2 * pad - 2 if taps == 9 else 1
-    for layout in ("nchw", "nhwc"):
-        if layout == "nchw":
-            xin, strides = x.contiguous(), (cin * H * H, H, 1, H * H)
-        else:
-            xin = x.permute(0, 2, 3, 1).contiguous()
-            strides = (H * H * cin, H * cin, cin, 1)
-        kc, ks = InferenceNet._small_plan(cin, taps, -(-cout // 128) * -(-(B * Ho * Ho) // 64))
-        npx = B * Ho * Ho
-        part = torch.full((ks * npx * cout,), float("nan"), device="cuda")
-        y = torch.full((npx, cout), float("nan"), device="cuda")
-        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        L = _lib.lib()
-        _lib.check(L.azg_small_gemm_partial(ctypes.c_void_p(xin.data_ptr()), *strides, B, H, H, pad, taps,
-                                            ctypes.c_void_p(wk.data_ptr()), cin, cout, kc, ks,
-                                            ctypes.c_void_p(part.data_ptr()), st))
-        _lib.check(L.azg_small_gemm_reduce(ctypes.c_void_p(part.data_ptr()), ks, npx, cout,
-                                           ctypes.c_void_p(b.data_ptr()), 1, ctypes.c_void_p(y.data_ptr()), cout, st))
-        torch.cuda.synchronize()
-        err = ((y.double() - want).abs() / (want.abs() + 1.0)).max().item()
-        assert err < 1e-5, (layout, err)
-
-
-@pytest.mark.parametrize("B,H,pad,cin,cout", [(1, 7, 1, 4, 512), (1, 7, 1, 512, 512), (3, 7, 0, 512, 512),
-                                              (1, 5, 0, 512, 512), (2, 8, 1, 2, 512), (1, 8, 1, 512, 512),
-                                              (4, 6, 0, 64, 96), (1, 1, 0, 4608, 1024), (3, 1, 0, 1024, 512),
-                                              (2, 1, 0, 512, 344), (1, 1, 0, 8192, 1024), (1, 9, 1, 64, 128),
-                                              (2, 9, 0, 128, 72)])
-def test_small_layer_matches_torch(B, H, pad, cin, cout):
-    """azg_small_layer (one launch per layer, no partial sums; the small path up to
-    SMALL_LAYER_MAX_B leaves): a 3x3 conv (one output row per block up to 8 wide, pixel
-    groups of <= 13 beyond: the 9x9 cases) or an FC layer + bias + ReLU against torch in
-    f64, NCHW and NHWC inputs, padded and unpadded windows, channel counts not a multiple
-    of the 8-co block."""
+                                              (1, 5, 0, 512, 512), (1, 7, 0, 512, 512), (2, 8, 1, 2, 512),
+                                              (1, 8, 1, 512, 512), (4, 8, 1, 64, 96), (4, 6, 0, 64, 96),
+                                              (1, 9, 1, 64, 128), (2, 9, 0, 128, 72), (4, 5, 0, 8, 16),
+                                              (1, 3, 1, 20, 2)])
+def test_small_conv_matches_torch(B, H, pad, cin, cout):
+    """azg_small_conv3x3 (the small path's conv, up to 256 output pixels): a 3x3 conv + bias +
+    ReLU against torch in f64, NCHW (scalar loads) and NHWC (float4) inputs, padded and
+    unpadded windows, every pixel-tile width (16-256), channel counts that leave K slices of
+    unequal length."""
     import ctypes
     import azg_amd  # noqa: F401
     from azg_amd import _lib
     torch.manual_seed(5)
-    taps = 9 if H > 1 else 1
     x = torch.randn(B, cin, H, H, device="cuda")
-    w = torch.randn(cout, cin, 3, 3, device="cuda") / (cin * taps) ** 0.5 if taps == 9 else \
-        torch.randn(cout, cin, device="cuda") / cin ** 0.5
+    w = torch.randn(cout, cin, 3, 3, device="cuda") / (cin * 9) ** 0.5
     b = torch.randn(cout, device="cuda")
-    if taps == 9:
-        want = torch.relu(torch.nn.functional.conv2d(x.double(), w.double(), b.double(), padding=pad))
-        want = want.permute(0, 2, 3, 1).reshape(-1, cout)
-        wk = w.contiguous(memory_format=torch.channels_last)
-    else:
-        want = torch.relu(x.double().reshape(B, cin) @ w.double().t() + b.double())
-        wk = w.contiguous()
-    Ho = H + 2 * pad - 2 if taps == 9 else 1
+    want = torch.relu(torch.nn.functional.conv2d(x.double(), w.double(), b.double(), padding=pad))
+    want = want.permute(0, 2, 3, 1).reshape(-1, cout)
+    wk = w.contiguous(memory_format=torch.channels_last)
+    Ho = H + 2 * pad - 2
     L = _lib.lib()
     for layout in ("nchw", "nhwc"):
         if layout == "nchw":
@@ -567,20 +512,63 @@ def test_small_layer_matches_torch(B, H, pad, cin, cout):
             strides = (H * H * cin, H * cin, cin, 1)
         y = torch.full((B * Ho * Ho, cout), float("nan"), device="cuda")
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        _lib.check(L.azg_small_layer(ctypes.c_void_p(xin.data_ptr()), *strides, B, H, H, pad, taps,
-                                     ctypes.c_void_p(wk.data_ptr()), cin, cout, ctypes.c_void_p(b.data_ptr()), 1,
-                                     ctypes.c_void_p(y.data_ptr()), cout, st))
+        _lib.check(L.azg_small_conv3x3(ctypes.c_void_p(xin.data_ptr()), *strides, B, H, pad,
+                                       ctypes.c_void_p(wk.data_ptr()), cin, cout, ctypes.c_void_p(b.data_ptr()), 1,
+                                       ctypes.c_void_p(y.data_ptr()), cout, st))
         torch.cuda.synchronize()
         err = ((y.double() - want).abs() / (want.abs() + 1.0)).max().item()
         assert err < 1e-5, (layout, err)
 
 
-@pytest.mark.parametrize("n,depth,A,B", [(7, 4, 343, 1), (7, 4, 343, 4), (7, 4, 343, 5), (7, 4, 343, 63),
-                                         (6, 2, 37, 1), (8, 2, 65, 3)])
+@pytest.mark.parametrize("B,K,N,relu,bias", [(1, 4608, 1024, 1, True), (4, 4608, 1024, 1, True),
+                                              (1, 1024, 512, 1, True), (3, 1024, 512, 1, True),
+                                              (1, 512, 344, 0, False), (2, 512, 66, 0, False),
+                                              (1, 8192, 1024, 1, True), (4, 36, 5, 1, True)])
+def test_small_fc_matches_torch(B, K, N, relu, bias):
+    """azg_small_fc (the small path's FC layers, 1-4 leaves): y = relu?(b + x W^T) against torch
+    in f64; row counts not a multiple of the 4-row block, K not a multiple of the 1024-wide
+    block stride, no bias (the [fc3 | fc4] GEMM, whose bias the policy/value kernel adds)."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    torch.manual_seed(7)
+    x = torch.randn(B, K, device="cuda")
+    w = torch.randn(N, K, device="cuda") / K ** 0.5
+    b = torch.randn(N, device="cuda") if bias else None
+    want = x.double() @ w.double().t() + (b.double() if bias else 0.0)
+    if relu:
+        want = torch.relu(want)
+    y = torch.full((B, N), float("nan"), device="cuda")
+    _lib.check(_lib.lib().azg_small_fc(ctypes.c_void_p(x.data_ptr()), K, B, ctypes.c_void_p(w.data_ptr()), K, N,
+                                       ctypes.c_void_p(b.data_ptr()) if bias else None, relu,
+                                       ctypes.c_void_p(y.data_ptr()), N,
+                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    err = ((y.double() - want).abs() / (want.abs() + 1.0)).max().item()
+    assert err < 1e-5, err
+
+
+def test_small_kernels_reject_bad_arguments():
+    """Shapes the small kernels do not serve return AZG_ERR_ARG instead of launching."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    L = _lib.lib()
+    x = torch.zeros(8 * 8 * 8 * 64, device="cuda")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = ctypes.c_void_p(x.data_ptr())
+    assert L.azg_small_conv3x3(P, 64 * 64, 64 * 8, 64, 1, 5, 8, 1, P, 64, 64, None, 1, P, 64, st) == -1  # 320 px
+    assert L.azg_small_conv3x3(P, 64 * 49, 64 * 7, 64, 1, 1, 7, 1, P, 64, 63, None, 1, P, 64, st) == -1  # odd Cout
+    assert L.azg_small_fc(P, 64, 5, P, 64, 8, None, 1, P, 8, st) == -1  # batch 5
+    assert L.azg_small_fc(P, 62, 1, P, 62, 8, None, 1, P, 8, st) == -1  # K % 4
+
+
+@pytest.mark.parametrize("n,depth,A,B", [(7, 4, 343, 1), (7, 4, 343, 2), (7, 4, 343, 4), (6, 2, 37, 1),
+                                         (6, 2, 37, 4), (8, 2, 65, 1), (8, 2, 65, 3)])
 def test_small_forward_matches_reference(n, depth, A, B):
-    """Below 64 leaves InferenceNet(small=True) runs on libazg's small GEMMs (no MIOpen /
-    hipBLASLt): P and v within the north_star's 1e-5 of the reference module, and of the
-    MIOpen form."""
+    """Up to SMALL_MAX_B leaves InferenceNet runs on libazg's small-batch kernels (no MIOpen /
+    hipBLASLt; the default): P and v within the north_star's 1e-5 of the reference module,
+    and of the MIOpen form; per leaf the same bits whatever the batch (batch invariance)."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
     torch.manual_seed(0)
@@ -588,8 +576,8 @@ def test_small_forward_matches_reference(n, depth, A, B):
     x = (torch.rand(B, depth, n, n, device="cuda") < 0.3).float()
     if depth > 2:
         x[:, 2] = 17.0
-    small = InferenceNet(net, small=True)
-    lib_form = InferenceNet(net, conv="miopen")
+    small = InferenceNet(net)
+    lib_form = InferenceNet(net, conv="miopen", small=False)
     assert small.small_path and not lib_form.small_path
     with torch.no_grad():
         p, v = small(x)

@@ -215,9 +215,9 @@ def test_dropin_mcts_real_net(name, k, form):
     """Drop-in MCTS + Coach.executeEpisode, whole episodes (for the 6x6 Othello sets:
     BASELINE configs[0], C1, the reference main.py path on one game), with the leaf
     evaluator as the reference wires it (form="module": the NNetWrapper's own torch module,
-    batch 1 on the GPU) and in the form INTEGRATION.md recommends for the drop-in
-    (form="inference": InferenceNet(nnet.nnet, conv="miopen", gemm="f32") -- BN folded,
-    f32 direct convolutions, the f32 FC tail and libazg's policy/value kernel)."""
+    batch 1 on the GPU, MCTS(fast=False)) and in the drop-in's default form (form="inference":
+    InferenceNet(nnet.nnet, conv="miopen", gemm="f32"), BN folded, which at one leaf runs on
+    libazg's small-batch kernels, azg_small.hip -- what MCTS(fast=True) builds itself)."""
     import hashlib
     import azg_amd  # noqa: F401
     from azg_amd.coach import Coach
@@ -251,7 +251,8 @@ def test_dropin_mcts_real_net(name, k, form):
     np.random.seed(ep["seed"])
     cls.to_next_state = tns
     try:
-        ex = Coach(game, wrapper, args).executeEpisode((game.restarted(), RecMCTS(wrapper, args)))
+        ex = Coach(game, wrapper, args).executeEpisode((game.restarted(),
+                                                        RecMCTS(wrapper, args, fast=form != "module")))
     finally:
         cls.to_next_state = orig
     net = wrapper.nnet.eval()

@@ -22,10 +22,10 @@ class Args(dict):
     __getattr__ = dict.__getitem__
 
 
-def run(ev, game, sims, graph, moves):
+def run(ev, game, sims, graph, moves, fast=True):
     args = Args(numMCTSSims=sims, cpuct=1, tempThreshold=15)
     np.random.seed(1)
-    mcts = MCTS(ev, args, graph=graph)
+    mcts = MCTS(ev, args, graph=graph, fast=fast)
     g = game.restarted()
     times = []
     for _ in range(moves):
@@ -43,21 +43,23 @@ def main():
     ap.add_argument("--game", default="othello6")
     ap.add_argument("--sims", type=int, default=25)
     ap.add_argument("--moves", type=int, default=12)
-    ap.add_argument("--forms", default="module,module-graph,inference-miopen,inference-auto")
+    ap.add_argument("--forms", default="module,module-graph,default,library,small")
     a = ap.parse_args()
     game = OthelloGame(6) if a.game == "othello6" else OthelloGame(8) if a.game == "othello8" else \
         InflexionGame(7, max_turns=343, max_power=6)
     torch.manual_seed(0)
     w = NNetWrapper(game, device="cuda")
     for form in a.forms.split(","):
-        if form.startswith("module"):
-            ev, graph = w, form.endswith("graph")
-        else:
-            kind = form.split("-")[1]
-            ev = (InferenceNet(w.nnet.eval(), small=True, gemm="f32") if kind == "small" else
-                  InferenceNet(w.nnet.eval(), conv=kind, gemm="f32"))
-            graph = True
-        t = run(ev, game, a.sims, graph, a.moves)
+        fast = True
+        if form.startswith("module"):  # the reference module itself (MCTS(fast=False))
+            ev, graph, fast = w, form.endswith("graph"), False
+        elif form == "default":  # MCTS's own default: the module's InferenceNet (small-batch kernels)
+            ev, graph = w, True
+        elif form == "library":  # BN folded, MIOpen / hipBLASLt at one leaf
+            ev, graph = InferenceNet(w.nnet.eval(), conv="miopen", gemm="f32", small=False), True
+        else:  # "small": azg_small.hip explicitly
+            ev, graph = InferenceNet(w.nnet.eval(), conv="miopen", gemm="f32", small=True), True
+        t = run(ev, game, a.sims, graph, a.moves, fast)
         print(json.dumps({"game": a.game, "form": form, "sims": a.sims, "ms_per_call": t * 1e3,
                           "sims_per_s": a.sims / t}), flush=True)
 

@@ -1,4 +1,4 @@
-"""Per-layer time of azg_small_layer at one leaf (C1's batch) on the 7x7 Inflexion network's
+"""Per-layer time of azg_small_conv3x3 / azg_small_fc at one leaf (C1's batch) on the 7x7 Inflexion network's
 shapes, against torch's conv2d / linear (MIOpen / hipBLASLt, + bias + ReLU) on the same
 inputs; medians of round-robin rounds.  Prints one JSON line per layer."""
 import ctypes
@@ -47,9 +47,15 @@ def main():
         y = torch.empty((B * Ho * Ho, cout), device="cuda")
 
         def azg():
-            _lib.check(L.azg_small_layer(ctypes.c_void_p(xin.data_ptr()), *strides, B, H, H, pad, taps,
-                                         ctypes.c_void_p(wk.data_ptr()), cin, cout, ctypes.c_void_p(b.data_ptr()), 1,
-                                         ctypes.c_void_p(y.data_ptr()), cout, st))
+            if taps == 9:
+                _lib.check(L.azg_small_conv3x3(ctypes.c_void_p(xin.data_ptr()), *strides, B, H, pad,
+                                               ctypes.c_void_p(wk.data_ptr()), cin, cout,
+                                               ctypes.c_void_p(b.data_ptr()), 1, ctypes.c_void_p(y.data_ptr()), cout,
+                                               st))
+            else:
+                _lib.check(L.azg_small_fc(ctypes.c_void_p(xin.data_ptr()), cin, B, ctypes.c_void_p(wk.data_ptr()),
+                                          cin, cout, ctypes.c_void_p(b.data_ptr()), 1,
+                                          ctypes.c_void_p(y.data_ptr()), cout, st))
 
         if taps == 9:
             xcl = x.contiguous(memory_format=torch.channels_last)
@@ -68,7 +74,7 @@ def main():
         for r in range(7):
             for k, f in (("azg", azg), ("lib", lib)) if r % 2 == 0 else (("lib", lib), ("azg", azg)):
                 ts[k].append(timeit(f))
-        print(json.dumps({"layer": name, "B": B, "azg_small_layer_us": sorted(ts["azg"])[3],
+        print(json.dumps({"layer": name, "B": B, "azg_us": sorted(ts["azg"])[3],
                           "torch_us": sorted(ts["lib"])[3]}), flush=True)
 
 

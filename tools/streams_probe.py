@@ -36,7 +36,49 @@ def build(net, G, K):
     return engs, streams
 
 
+class OneGraph:
+    """The K engines' moves captured as ONE graph whose K branches are forked onto K streams
+    inside the capture (event fork / join), so the graph itself carries the concurrency."""
+
+    def __init__(self, engs, streams):
+        self.engs, self.streams = engs, streams
+        torch.cuda.synchronize()
+        self.g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g):
+            main = torch.cuda.current_stream()
+            for e, s in zip(engs, streams):
+                s.wait_stream(main)
+                with torch.cuda.stream(s):
+                    for _ in range(e.sims):
+                        e.simulate()
+                    e.move_end()
+            for s in streams:
+                main.wait_stream(s)
+        torch.cuda.synchronize()
+
+
+def build_one_graph(net, G, K):
+    streams = [torch.cuda.Stream() for _ in range(K)]
+    engs = []
+    for k, s in enumerate(streams):
+        with torch.cuda.stream(s):
+            e = SelfPlayEngine(G // K, sims=25, evaluator=InferenceNet(net), max_turns=343, first_game=k * (G // K))
+            e.move()
+        engs.append(e)
+    torch.cuda.synchronize()
+    return OneGraph(engs, streams), None
+
+
 def timed(engs, streams, moves):
+    if isinstance(engs, OneGraph):
+        torch.cuda.synchronize()
+        e0 = sum(e.stats()["expansions"] for e in engs.engs)
+        t0 = time.perf_counter()
+        for _ in range(moves):
+            engs.g.replay()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        return (sum(e.stats()["expansions"] for e in engs.engs) - e0) / dt, dt / moves * 1e3
     torch.cuda.synchronize()
     e0 = sum(e.stats()["expansions"] for e in engs)
     t0 = time.perf_counter()
@@ -58,8 +100,9 @@ def main():
     a = ap.parse_args()
     torch.manual_seed(0)
     net = InflexionNNet().cuda().eval()
-    ks = [int(k) for k in a.ks.replace("/", ",").split(",")]
-    arr = {k: build(net, a.games, k) for k in ks}
+    ks = [int(k) if not k.startswith("g") else k for k in a.ks.replace("/", ",").split(",")]
+    arr = {k: (build(net, a.games, k) if isinstance(k, int) else build_one_graph(net, a.games, int(k[1:])))
+           for k in ks}
     res = {}
     for r in range(a.rounds):
         for k in ks:
@@ -69,6 +112,8 @@ def main():
     # records of the first moves equal whatever K (same games, same seeds)
     recs = {}
     for k, (engs, _) in arr.items():
+        if isinstance(engs, OneGraph):
+            engs = engs.engs
         torch.cuda.synchronize()
         for e in engs:
             e.check_evaluator()
