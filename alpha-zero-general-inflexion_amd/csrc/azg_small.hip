@@ -41,6 +41,8 @@ namespace {
 
 constexpr int SC_T = 512;  // small_conv threads
 constexpr size_t SC_LDS_MAX = 160 * 1024;  // the CU's whole LDS: one block per CU
+constexpr int SC_UNR = 16;   // input staging loads in flight per thread
+constexpr int SC_UNRW = 6;   // weight staging loads per thread (2 x 4608 floats: 4.5)
 constexpr int SF_T = 256;  // small_fc threads
 
 // LDS row pitch (floats) of a staged input pixel: channels rounded up to float4, + 4 so that
@@ -68,23 +70,55 @@ __global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restric
     const int KS = K / STEP;
     const int per = (KS + KSL - 1) / KSL;
     const int k0 = s * per, k1 = min(KS, k0 + per);
-    if constexpr (WLDS) {  // the block's weights: CO_PB contiguous rows, all loads in flight at once
-        const float4* __restrict__ w4 = (const float4*)(w + (long long)co0 * K);
-        const int n4 = CO_PB * K / 4;
-        for (int i = tid; i < n4; i += SC_T) ((float4*)ws)[i] = w4[i];
-    }
+    // staging: every thread's loads are issued together (SC_UNR float4 in flight per thread,
+    // one memory round trip per SC_UNR x 8 KB), then stored to LDS
+    const int nw4 = WLDS ? CO_PB * K / 4 : 0;  // the block's weights: CO_PB contiguous rows
+    const float4* __restrict__ w4 = (const float4*)(w + (long long)co0 * K);
     int oy = 0, ox = 0;
     if (p < hw) oy = p / Ho, ox = p - (p / Ho) * Ho;
     for (int b = 0; b < B; ++b) {
-        // stage leaf b's input plane into LDS (NHWC float4 rows, or any strides element-wise)
+        // stage leaf b's input plane into LDS (NHWC float4 rows, or any strides element-wise);
+        // with the weights on the first leaf
         const float* __restrict__ xb = x + b * sB;
         if constexpr (VEC) {
-            const int c4 = Cin / 4, n4 = H * H * c4;
-            for (int i = tid; i < n4; i += SC_T) {
-                const int pix = i / c4, c = (i - pix * c4) * 4, iy = pix / H, ix = pix - iy * H;
-                *(float4*)(xs + pix * P + c) = *(const float4*)(xb + (long long)iy * sY + (long long)ix * sX + c);
-            }
+            const int c4 = Cin / 4, nx4 = H * H * c4;
+            // one batch of input vectors from `base` (and with WW the block's weights: their loads
+            // issued first, their stores after the batch's loads are in flight)
+            auto batch = [&](int base, auto WW) {
+                constexpr bool WITHW = decltype(WW)::value;
+                float4 rw[WITHW ? SC_UNRW : 1];
+                if constexpr (WITHW) {
+#pragma unroll
+                    for (int u = 0; u < SC_UNRW; ++u) rw[u] = w4[min(tid + u * SC_T, nw4 - 1)];
+                }
+                float4 r[SC_UNR];
+#pragma unroll
+                for (int u = 0; u < SC_UNR; ++u) {  // past the end: a duplicate load, not stored
+                    const int i = min(base + u * SC_T, nx4 - 1);
+                    const int pix = i / c4, c = (i - pix * c4) * 4, iy = pix / H, ix = pix - iy * H;
+                    r[u] = *(const float4*)(xb + (long long)iy * sY + (long long)ix * sX + c);
+                }
+                if constexpr (WITHW) {
+#pragma unroll
+                    for (int u = 0; u < SC_UNRW; ++u)  // past the end: rewrites the last vector with its own value
+                        ((float4*)ws)[min(tid + u * SC_T, nw4 - 1)] = rw[u];
+                    for (int i = tid + SC_UNRW * SC_T; i < nw4; i += SC_T) ((float4*)ws)[i] = w4[i];
+                }
+#pragma unroll
+                for (int u = 0; u < SC_UNR; ++u) {
+                    const int i = base + u * SC_T;
+                    if (i < nx4) {
+                        const int pix = i / c4, c = (i - pix * c4) * 4;
+                        *(float4*)(xs + pix * P + c) = r[u];
+                    }
+                }
+            };
+            if (WLDS && b == 0) batch(tid, std::true_type{});
+            else batch(tid, std::false_type{});
+            for (int base = tid + SC_T * SC_UNR; base < nx4; base += SC_T * SC_UNR) batch(base, std::false_type{});
         } else {
+            if (b == 0)
+                for (int i = tid; i < nw4; i += SC_T) ((float4*)ws)[i] = w4[i];
             const int n = H * H * Cin;
             for (int i = tid; i < n; i += SC_T) {
                 const int pix = i / Cin, c = i - pix * Cin, iy = pix / H, ix = pix - iy * H;
@@ -161,7 +195,7 @@ __global__ __launch_bounds__(SF_T) void small_fc_kernel(const float* __restrict_
     for (int r = 0; r < NPB; ++r)
 #pragma unroll
         for (int b = 0; b < BMAX; ++b) acc[r][b] = 0.f;
-#pragma unroll 2
+#pragma unroll 8
     for (int k4 = tid; k4 < K4; k4 += SF_T) {
         float4 xv[BMAX];
 #pragma unroll

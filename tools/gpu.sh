@@ -17,6 +17,7 @@
 #   gemm_pmc[:<v>]      split-GEMM SQ/TCC counters on conv2's shape (variant v, default 4) -> v<v>_pmc.json
 #   configs             bench.py over C1 / C2 (full games, eager + graph) / C3 / C5 / C4 full games
 #   py:<script>[:<args>] python <script> <args> -> <script base>.out / .err
+#   profpy:<script>[:<args>] rocprofv3 --kernel-trace --stats over python <script> <args> -> prof_<base>.md
 set -e
 R=$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)
 NAME=${1:?usage: tools/gpu.sh <run-name> <task> ...}
@@ -104,6 +105,17 @@ for task in "$@"; do
         a=${a//,/ }
         b=$(basename "$script" .py)
         timeout -k 10 600 python -u "$script" $a > "$O/$b.out" 2> "$O/$b.err" ;;
+    profpy)
+        script=${arg%%:*}
+        a=""
+        [[ "$arg" == *:* ]] && a=${arg#*:}
+        a=${a//,/ }
+        b=$(basename "$script" .py)
+        d="$O/prof_$b"
+        (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o run \
+            -- python3 "$R/$script" $a > "$d.out" 2> "$d.err")
+        python3 tools/prof_summary.py "$d/run_kernel_stats.csv" > "$d.md"
+        rm -f "$d"/*trace*.csv ;;
     *)
         echo "unknown task $task" >&2
         exit 2 ;;
