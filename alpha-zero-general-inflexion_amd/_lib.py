@@ -83,8 +83,11 @@ SIGNATURES = [
                                               _VP]),
     ("azg_split_gemm_variant", ctypes.c_int, [_I32, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
     ("azg_small_conv3x3", ctypes.c_int, [_VP, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _I32, _I32, _VP, _I32,
-                                         _VP, _I32, _VP]),
+                                         _VP, _I32, _VP, _I64, _VP, _I32, _VP]),
     ("azg_small_fc", ctypes.c_int, [_VP, _I32, _I32, _VP, _I32, _I32, _VP, _I32, _VP, _I32, _VP]),
+    ("azg_small_conv12", ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _I32, _VP, _I32, _VP, _I64, _VP,
+                                        _I32, _VP]),
+    ("azg_small_heads", ctypes.c_int, [_VP, _I32, _I32, _VP, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     ("azg_split_gemm_pick", ctypes.c_int, [_I32, _VP, _VP, _I32]),
     ("azg_set_gemm_blocks", ctypes.c_int, [_I32]),
     ("azg_set_arena", ctypes.c_int, [_VP, _VP, _VP, _VP]),

@@ -181,12 +181,203 @@ __global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restric
     }
 }
 
-template <int NPB, int BMAX>
+// Split-K form for the 512-channel layers (conv2-4): block (co group of SK_CO = 8 channels, ci
+// quarter kg of SK_KG = 4), 512 threads = PXL pixels x (512 / PXL) slices of the quarter's
+// 9 x Cin / 4 products.  Eight output channels per lane reuse each staged input vector 8
+// times (LDS traffic per multiply-add a quarter of the 2-channel form's), and the quarter's
+// input (H * H x Cin / 4) and weights (8 x 9 x Cin / 4) are a quarter of the plane.  The four
+// quarters' partial sums meet in a workspace: each block publishes its [leaf][pixel][8] partials,
+// then (release fence, one atomic ticket per co group) the LAST of the four blocks to arrive sums
+// them in quarter order 0..3 (deterministic whatever the arrival order), adds the bias, applies
+// ReLU, writes the output and resets the ticket for the next launch.  No block waits on another.
+constexpr int SK_CO = 8, SK_KG = 4;
+constexpr size_t SK_LDS = 96 * 1024;  // staged quarter input + weights + slice partials (n <= 8: <= 87 KB)
+
+// F1 (conv1 fused, conv2 only): x is then the NCHW leaf planes [B][D][H][H] (sB per leaf) and
+// the staged quarter is conv1's output for that quarter's channels, relu(b1 + conv1(planes)) with
+// w1 [Cin][3][3][D] (channels_last, BN folded) -- conv1's 36 products per output are recomputed
+// by each of the co groups' blocks instead of a launch of their own.
+template <int PXL, bool F1>
+__global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __restrict__ x, long long sB, int sY,
+                                                             int sX, int B, int H, int pad,
+                                                             const float* __restrict__ w, int Cin,
+                                                             const float* __restrict__ bias, int relu,
+                                                             float* __restrict__ y, int ldy,
+                                                             float* __restrict__ part, unsigned* __restrict__ ticket,
+                                                             const float* __restrict__ w1, const float* __restrict__ b1,
+                                                             int D) {
+    constexpr int KSL = SC_T / PXL;
+    __shared__ __attribute__((aligned(16))) float lds[SK_LDS / 4];
+    __shared__ unsigned s_last;
+    const int tid = threadIdx.x;
+    const int p = tid % PXL, s = tid / PXL;
+    const int cg = blockIdx.x / SK_KG, kg = blockIdx.x % SK_KG;
+    const int co0 = cg * SK_CO;
+    const int Cq = Cin / SK_KG, ci_base = kg * Cq;
+    const int Ho = H + 2 * pad - 2, hw = Ho * Ho;
+    const int P = Cq + 4;                       // LDS pitch of a staged pixel
+    const int Kq = 9 * Cq;                      // this quarter's products per output
+    float* xs = lds;                            // [H * H][P]
+    float* ws = xs + H * H * P;                 // [Kq][SK_CO]: k-major, the 8 channels of a k adjacent
+    float* red = ws + Kq * SK_CO;               // [KSL][PXL][SK_CO]
+    // the quarter's weights: w[co0 + c][tap][ci_base + ci] -> ws[(tap * Cq + ci) * 8 + c]
+    {
+        const int n4 = SK_CO * 9 * (Cq / 4);
+        for (int i = tid; i < n4; i += SC_T) {
+            const int c = i / (9 * (Cq / 4)), r = i - c * 9 * (Cq / 4), tap = r / (Cq / 4), ci = (r - tap * (Cq / 4)) * 4;
+            const float4 v = *(const float4*)(w + ((long long)(co0 + c) * 9 + tap) * Cin + ci_base + ci);
+            float* d = ws + (tap * Cq + ci) * SK_CO + c;
+            d[0] = v.x;
+            d[SK_CO] = v.y;
+            d[2 * SK_CO] = v.z;
+            d[3 * SK_CO] = v.w;
+        }
+    }
+    int oy = 0, ox = 0;
+    if (p < hw) oy = p / Ho, ox = p - (p / Ho) * Ho;
+    const int KS = Kq / 4;  // float4 steps
+    const int per = (KS + KSL - 1) / KSL;
+    const int k0 = s * per, k1 = min(KS, k0 + per);
+    for (int b = 0; b < B; ++b) {
+        if constexpr (F1) {
+            // conv1 (pad 1) for the quarter's channels from the leaf planes: thread (c, g) keeps
+            // channel c's 9 D weights in registers and computes every 4th pixel from g; the
+            // planes (staged in the partials' area, free until the multiply-adds) are the same
+            // for the whole wave
+            float* pl = red;
+            for (int i = tid; i < D * H * H; i += SC_T) pl[i] = x[b * sB + i];
+            __syncthreads();
+            const int c = tid % Cq, g = tid / Cq, G1 = SC_T / Cq;
+            if (g < G1) {
+                float wr[36];
+                const float* __restrict__ wc = w1 + (long long)(ci_base + c) * 9 * D;
+#pragma unroll
+                for (int t = 0; t < 9; ++t)
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) wr[t * 4 + d] = d < D ? wc[t * D + d] : 0.f;
+                const float bc = b1[ci_base + c];
+                for (int pix = g; pix < H * H; pix += G1) {
+                    const int iy = pix / H, ix = pix - iy * H;
+                    float a = 0.f;
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) {
+                        const int yy = iy + t / 3 - 1, xx = ix + t % 3 - 1;
+                        if (yy < 0 || yy >= H || xx < 0 || xx >= H) continue;
+#pragma unroll
+                        for (int d = 0; d < 4; ++d)
+                            if (d < D) a = fmaf(wr[t * 4 + d], pl[(d * H + yy) * H + xx], a);
+                    }
+                    xs[pix * P + c] = fmaxf(a + bc, 0.f);
+                }
+            }
+        }
+        const float* __restrict__ xb = x + b * sB + ci_base;
+        const int c4 = Cq / 4, n4 = F1 ? 0 : H * H * c4;
+        for (int base = tid; base < n4; base += SC_T * SC_UNR) {
+            float4 r[SC_UNR];
+#pragma unroll
+            for (int u = 0; u < SC_UNR; ++u) {
+                const int i = min(base + u * SC_T, n4 - 1);
+                const int pix = i / c4, c = (i - pix * c4) * 4, iy = pix / H, ix = pix - iy * H;
+                r[u] = *(const float4*)(xb + (long long)iy * sY + (long long)ix * sX + c);
+            }
+#pragma unroll
+            for (int u = 0; u < SC_UNR; ++u) {
+                const int i = base + u * SC_T;
+                if (i < n4) {
+                    const int pix = i / c4, c = (i - pix * c4) * 4;
+                    *(float4*)(xs + pix * P + c) = r[u];
+                }
+            }
+        }
+        __syncthreads();
+        float acc[SK_CO];
+#pragma unroll
+        for (int c = 0; c < SK_CO; ++c) acc[c] = 0.f;
+        if (p < hw) {
+            int kk = k0;
+            while (kk < k1) {  // k = tap * Cq + ci: a slice is a few runs of one tap each
+                const int k = kk * 4;
+                const int tap = k / Cq, ci0 = k - tap * Cq;
+                const int run = min(k1 - kk, (Cq - ci0) / 4);
+                const int iy = oy + tap / 3 - pad, ix = ox + tap % 3 - pad;
+                if (iy >= 0 && iy < H && ix >= 0 && ix < H) {
+                    const float* xp = xs + (iy * H + ix) * P + ci0;
+                    const float* wp = ws + k * SK_CO;
+#pragma unroll 2
+                    for (int j = 0; j < run; ++j) {
+                        const float4 xv = *(const float4*)(xp + 4 * j);
+                        const float xs4[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float4 wa = *(const float4*)(wp + (4 * j + e) * SK_CO);
+                            const float4 wb = *(const float4*)(wp + (4 * j + e) * SK_CO + 4);
+                            acc[0] = fmaf(wa.x, xs4[e], acc[0]);
+                            acc[1] = fmaf(wa.y, xs4[e], acc[1]);
+                            acc[2] = fmaf(wa.z, xs4[e], acc[2]);
+                            acc[3] = fmaf(wa.w, xs4[e], acc[3]);
+                            acc[4] = fmaf(wb.x, xs4[e], acc[4]);
+                            acc[5] = fmaf(wb.y, xs4[e], acc[5]);
+                            acc[6] = fmaf(wb.z, xs4[e], acc[6]);
+                            acc[7] = fmaf(wb.w, xs4[e], acc[7]);
+                        }
+                    }
+                }
+                kk += run;
+            }
+        }
+        float4* r4 = (float4*)(red + (s * PXL + p) * SK_CO);
+        r4[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        r4[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+        __syncthreads();
+        // the block's partial for leaf b, slices summed in order -> part[kg][b][pixel][8]
+        for (int t = tid; t < hw * SK_CO; t += SC_T) {
+            const int pp = t / SK_CO, c = t - pp * SK_CO;
+            float sum = 0.f;
+            for (int q = 0; q < KSL; ++q) sum += red[(q * PXL + pp) * SK_CO + c];
+            part[(((long long)kg * (gridDim.x / SK_KG) + cg) * B + b) * hw * SK_CO + t] = sum;
+        }
+        __syncthreads();  // xs and red are rewritten for the next leaf
+    }
+    // publish (release: the partial stores written back before the ticket), then the last of the
+    // co group's SK_KG blocks combines the quarters in order
+    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(ticket + cg, 1u) == SK_KG - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    const int G = gridDim.x / SK_KG;
+    for (int t = tid; t < B * hw * SK_CO; t += SC_T) {
+        const int c = t % SK_CO, bp = t / SK_CO;  // bp = b * hw + pixel
+        float sum = 0.f;
+#pragma unroll
+        for (int q = 0; q < SK_KG; ++q) {  // coherent (agent-scope) loads: other CUs wrote them
+            const unsigned u = __hip_atomic_load((const unsigned*)(part + (((long long)q * G + cg) * B) * hw * SK_CO + t),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sum += __uint_as_float(u);
+        }
+        float o = sum + (bias ? bias[co0 + c] : 0.f);
+        if (relu) o = fmaxf(o, 0.f);
+        y[(long long)bp * ldy + co0 + c] = o;
+    }
+    if (tid == 0) ticket[cg] = 0u;  // every block of the group has arrived: ready for the next launch
+}
+
+// HEADS ([fc3 | fc4] + the heads, InflexionNNet.py:51-54 and NNet.py:94): y receives the
+// logits (no bias); each block then takes a ticket, and the last of the grid's blocks reads all
+// rows back (agent-scope loads) and writes P = softmax(hb[:A] + y[:A]) and v = tanh(hb[A] + y[A])
+// per leaf -- the arithmetic of azg_policy_value, one wave per leaf -- and resets the ticket.
+template <int NPB, int BMAX, bool HEADS>
 __global__ __launch_bounds__(SF_T) void small_fc_kernel(const float* __restrict__ x, int ldx, int B,
                                                         const float* __restrict__ w, int K, int N,
                                                         const float* __restrict__ bias, int relu,
-                                                        float* __restrict__ y, int ldy) {
+                                                        float* __restrict__ y, int ldy, const float* __restrict__ hb,
+                                                        float* __restrict__ P, float* __restrict__ V,
+                                                        unsigned* __restrict__ ticket) {
     __shared__ float red[SF_T / 64][NPB * BMAX];
+    __shared__ unsigned s_last;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n0 = blockIdx.x * NPB;
     const int K4 = K / 4;
@@ -238,6 +429,50 @@ __global__ __launch_bounds__(SF_T) void small_fc_kernel(const float* __restrict_
             y[(long long)b * ldy + n0 + r] = o;
         }
     }
+    if constexpr (HEADS) {
+        __threadfence();  // release: this block's rows before its ticket
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();
+        const int A = N - 1;
+        if (wv < B) {  // one wave per leaf
+            const float* yr = y + (long long)wv * ldy;
+            auto ld = [&](int a) {
+                return __uint_as_float(__hip_atomic_load((const unsigned*)(yr + a), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT));
+            };
+            constexpr int PL = 16;  // up to 1024 actions
+            float xa[PL];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < PL; ++j) {
+                const int a = lane + 64 * j;
+                xa[j] = a < A ? hb[a] + ld(a) : -INFINITY;
+                mx = fmaxf(mx, xa[j]);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            float sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < PL; ++j) {
+                xa[j] = lane + 64 * j < A ? expf(xa[j] - mx) : 0.f;
+                sm += xa[j];
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o);
+            const float inv = 1.f / sm;
+#pragma unroll
+            for (int j = 0; j < PL; ++j) {
+                const int a = lane + 64 * j;
+                if (a < A) P[(long long)wv * A + a] = xa[j] * inv;
+            }
+            if (lane == 0) V[wv] = tanhf(hb[A] + ld(A));
+        }
+        if (tid == 0) *ticket = 0u;
+    }
 }
 
 template <int PXL, bool VEC>
@@ -255,11 +490,20 @@ int launch_conv(dim3 grid, hipStream_t st, const float* x, long long sB, int sY,
     return 0;
 }
 
+template <int PXL, bool F1 = false>
+void launch_conv_sk(hipStream_t st, const float* x, long long sB, int sY, int sX, int B, int H, int pad,
+                    const float* w, int Cin, int Cout, const float* bias, int relu, float* y, int ldy, float* work,
+                    unsigned* tickets, const float* w1 = nullptr, const float* b1 = nullptr, int D = 0) {
+    hipLaunchKernelGGL((small_conv_sk_kernel<PXL, F1>), dim3((unsigned)(Cout / SK_CO * SK_KG)), dim3(SC_T), 0, st, x,
+                       sB, sY, sX, B, H, pad, w, Cin, bias, relu, y, ldy, work, tickets, w1, b1, D);
+}
+
 }  // namespace
 
 extern "C" int azg_small_conv3x3(const float* x, int64_t sB, int32_t sY, int32_t sX, int32_t sC, int32_t batch,
                                  int32_t H, int32_t pad, const float* w, int32_t Cin, int32_t Cout,
-                                 const float* bias, int32_t relu, float* y, int32_t ldy, void* stream) {
+                                 const float* bias, int32_t relu, float* y, int32_t ldy, float* work,
+                                 int64_t work_floats, uint32_t* tickets, int32_t n_tickets, void* stream) {
     const int Ho = H + 2 * pad - 2;
     if (!x || !w || !y || batch <= 0 || batch > 4 || H <= 0 || H > 16 || Ho <= 0 || pad < 0 || pad > 1 || Cin <= 0 ||
         Cout <= 0 || Cout % 2 || ldy < Cout || Ho * Ho > 256 || sB < 0 || sY < 0 || sX < 0 || sC < 0)
@@ -267,9 +511,24 @@ extern "C" int azg_small_conv3x3(const float* x, int64_t sB, int32_t sY, int32_t
     // NHWC input with float4 along the channels (aligned rows), else element-wise staging
     const bool vec = sC == 1 && Cin % 4 == 0 && sX % 4 == 0 && sY % 4 == 0 && sB % 4 == 0 &&
                      ((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0;
-    const dim3 grid((unsigned)(Cout / 2));
     hipStream_t st = (hipStream_t)stream;
     const int n = Ho * Ho;  // output pixels of one leaf: the leaves run one after another
+    // the split-K form (8 channels x a quarter of the input channels per block, quarters combined
+    // by the last block of each group) when the workspace holds the partials and the tickets
+    const long long need = (long long)SK_KG * Cout * batch * n;
+    const bool sk = vec && Cin % (4 * SK_KG) == 0 && Cout % SK_CO == 0 && work && tickets &&
+                    work_floats >= need && n_tickets >= Cout / SK_CO && ((uintptr_t)work & 15) == 0 &&
+                    (size_t)H * H * (Cin / SK_KG + 4) * 4 + (size_t)9 * Cin / SK_KG * SK_CO * 4 +
+                            (size_t)SC_T * SK_CO * 4 <= SK_LDS;
+    if (sk) {
+        if (n <= 16) launch_conv_sk<16>(st, x, sB, sY, sX, batch, H, pad, w, Cin, Cout, bias, relu, y, ldy, work, tickets);
+        else if (n <= 32) launch_conv_sk<32>(st, x, sB, sY, sX, batch, H, pad, w, Cin, Cout, bias, relu, y, ldy, work, tickets);
+        else if (n <= 64) launch_conv_sk<64>(st, x, sB, sY, sX, batch, H, pad, w, Cin, Cout, bias, relu, y, ldy, work, tickets);
+        else if (n <= 128) launch_conv_sk<128>(st, x, sB, sY, sX, batch, H, pad, w, Cin, Cout, bias, relu, y, ldy, work, tickets);
+        else launch_conv_sk<256>(st, x, sB, sY, sX, batch, H, pad, w, Cin, Cout, bias, relu, y, ldy, work, tickets);
+        return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+    }
+    const dim3 grid((unsigned)(Cout / 2));
     int rc = 0;
     auto go = [&](auto V_) {
         constexpr bool V = decltype(V_)::value;
@@ -285,17 +544,54 @@ extern "C" int azg_small_conv3x3(const float* x, int64_t sB, int32_t sY, int32_t
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
+extern "C" int azg_small_conv12(const float* planes, int32_t batch, int32_t depth, int32_t n, const float* w1,
+                                const float* b1, const float* w2, const float* b2, int32_t C, float* y, int32_t ldy,
+                                float* work, int64_t work_floats, uint32_t* tickets, int32_t n_tickets, void* stream) {
+    const int hw = n * n;
+    if (!planes || !w1 || !b1 || !w2 || !y || !work || !tickets || batch <= 0 || batch > 4 || depth < 1 || depth > 4 ||
+        n < 3 || n > 8 || C <= 0 || C % (4 * SK_KG) || C % SK_CO || ldy < C ||
+        work_floats < (long long)SK_KG * C * batch * hw || n_tickets < C / SK_CO || ((uintptr_t)w2 & 15) ||
+        ((uintptr_t)work & 15) ||
+        (size_t)hw * (C / SK_KG + 4) * 4 + (size_t)9 * C / SK_KG * SK_CO * 4 + (size_t)SC_T * SK_CO * 4 > SK_LDS)
+        return AZG_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const long long sB = (long long)depth * hw;
+    if (hw <= 64)
+        launch_conv_sk<64, true>(st, planes, sB, 0, 0, batch, n, 1, w2, C, C, b2, 1, y, ldy, work, tickets, w1, b1, depth);
+    else
+        return AZG_ERR_ARG;
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
 extern "C" int azg_small_fc(const float* x, int32_t ldx, int32_t batch, const float* w, int32_t K, int32_t N,
                             const float* bias, int32_t relu, float* y, int32_t ldy, void* stream) {
     if (!x || !w || !y || batch <= 0 || batch > 4 || K <= 0 || K % 4 || N <= 0 || ldx % 4 || ldx < K ||
         ldy < N || ((uintptr_t)x & 15) || ((uintptr_t)w & 15))
         return AZG_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)((N + 3) / 4));
     if (batch == 1)
-        hipLaunchKernelGGL((small_fc_kernel<4, 1>), dim3((unsigned)((N + 3) / 4)), dim3(SF_T), 0, st, x, ldx, batch, w,
-                           K, N, bias, relu, y, ldy);
+        hipLaunchKernelGGL((small_fc_kernel<4, 1, false>), grid, dim3(SF_T), 0, st, x, ldx, batch, w, K, N, bias, relu, y,
+                           ldy, nullptr, nullptr, nullptr, nullptr);
     else
-        hipLaunchKernelGGL((small_fc_kernel<4, 4>), dim3((unsigned)((N + 3) / 4)), dim3(SF_T), 0, st, x, ldx, batch, w,
-                           K, N, bias, relu, y, ldy);
+        hipLaunchKernelGGL((small_fc_kernel<4, 4, false>), grid, dim3(SF_T), 0, st, x, ldx, batch, w, K, N, bias, relu, y,
+                           ldy, nullptr, nullptr, nullptr, nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+extern "C" int azg_small_heads(const float* x, int32_t ldx, int32_t batch, const float* w34, int32_t K, int32_t A,
+                               const float* b34, float* logits, float* P, float* v, uint32_t* ticket, void* stream) {
+    if (!x || !w34 || !b34 || !logits || !P || !v || !ticket || batch <= 0 || batch > 4 || K <= 0 || K % 4 ||
+        A < 1 || A > 1023 || ldx % 4 || ldx < K || ((uintptr_t)x & 15) || ((uintptr_t)w34 & 15))
+        return AZG_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const int N = A + 1;
+    const dim3 grid((unsigned)((N + 3) / 4));
+    if (batch == 1)
+        hipLaunchKernelGGL((small_fc_kernel<4, 1, true>), grid, dim3(SF_T), 0, st, x, ldx, batch, w34, K, N, nullptr, 0,
+                           logits, N, b34, P, v, ticket);
+    else
+        hipLaunchKernelGGL((small_fc_kernel<4, 4, true>), grid, dim3(SF_T), 0, st, x, ldx, batch, w34, K, N, nullptr, 0,
+                           logits, N, b34, P, v, ticket);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }

@@ -704,13 +704,36 @@ class InferenceNet(nn.Module):
         dev = planes.device
         st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         x, strides, H, cin = planes, (self.depth * n * n, n, 1, n * n), n, self.depth
+        # the split-K convolutions' partial sums and per-channel-group tickets (zero between launches;
+        # the last word is the heads kernel's)
+        need = 4 * C * SMALL_MAX_B * n * n
+        if getattr(self, "_small_work", None) is None or self._small_work.numel() < need \
+                or self._small_work.device != dev:
+            self._small_work = torch.empty(need, device=dev, dtype=torch.float32)
+            self._small_tickets = torch.zeros(max(C // 8, 1) + 1, device=dev, dtype=torch.int32)
+        work, tickets = self._small_work, self._small_tickets
+        wp, tp = ctypes.c_void_p(work.data_ptr()), ctypes.c_void_p(tickets.data_ptr())
+        first = 1
+        if self.depth <= 4 and 3 <= n <= 8 and C % 16 == 0 and self.pads[:2] == [1, 1] \
+                and n * n * (C // 4 + 4) * 4 + 72 * C + 16384 <= 96 * 1024:  # azg_small_conv12's LDS
+            # conv1 + conv2 in one launch
+            y = torch.empty((B * n * n, C), device=dev, dtype=torch.float32)
+            _lib.check(L.azg_small_conv12(ctypes.c_void_p(planes.data_ptr()), B, self.depth, n,
+                                          ctypes.c_void_p(self.w1.data_ptr()), ctypes.c_void_p(self.b1.data_ptr()),
+                                          ctypes.c_void_p(self.w2.data_ptr()), ctypes.c_void_p(self.b2.data_ptr()),
+                                          C, ctypes.c_void_p(y.data_ptr()), C, wp, work.numel(), tp,
+                                          tickets.numel() - 1, st))
+            x, strides, H, cin, first = y, (n * n * C, n * C, C, 1), n, C, 3
         for i, pad in enumerate(self.pads, start=1):
+            if i < first:
+                continue
             Ho = H + 2 * pad - 2
             y = torch.empty((B * Ho * Ho, C), device=dev, dtype=torch.float32)
             _lib.check(L.azg_small_conv3x3(ctypes.c_void_p(x.data_ptr()), *strides, B, H, pad,
                                            ctypes.c_void_p(getattr(self, f"w{i}").data_ptr()), cin, C,
                                            ctypes.c_void_p(getattr(self, f"b{i}").data_ptr()), 1,
-                                           ctypes.c_void_p(y.data_ptr()), C, st))
+                                           ctypes.c_void_p(y.data_ptr()), C, wp, work.numel(), tp,
+                                           tickets.numel() - 1, st))
             x, H, cin = y, Ho, C
             strides = (H * H * C, H * C, C, 1)
         feat = H * H * C  # NHWC flatten (fw1's column order)
@@ -724,12 +747,15 @@ class InferenceNet(nn.Module):
             return out
         h1 = fc(x, feat, self.fw1, self.fb1, True)
         h2 = fc(h1, h1.shape[1], self.fw2, self.fb2, True)
-        pv = fc(h2, h2.shape[1], self.fw34, None, False)  # [B, A + 1]; the heads add fb34
         A = self.fw3.shape[0]
         p = torch.empty((B, A), device=dev, dtype=torch.float32)
         v = torch.empty((B, 1), device=dev, dtype=torch.float32)
-        _lib.check(L.azg_policy_value(ctypes.c_void_p(pv.data_ptr()), A + 1, ctypes.c_void_p(self.fb34.data_ptr()),
-                                      1.0, ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()), B, A, st))
+        logits = torch.empty((B, A + 1), device=dev, dtype=torch.float32)
+        _lib.check(L.azg_small_heads(ctypes.c_void_p(h2.data_ptr()), h2.shape[1], B, ctypes.c_void_p(self.fw34.data_ptr()),
+                                     self.fw34.shape[1], A, ctypes.c_void_p(self.fb34.data_ptr()),
+                                     ctypes.c_void_p(logits.data_ptr()), ctypes.c_void_p(p.data_ptr()),
+                                     ctypes.c_void_p(v.data_ptr()),
+                                     ctypes.c_void_p(tickets.data_ptr() + 4 * (tickets.numel() - 1)), st))
         return p, v
 
     def forward(self, s):

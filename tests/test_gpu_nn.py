@@ -504,7 +504,9 @@ def test_small_conv_matches_torch(B, H, pad, cin, cout):
     wk = w.contiguous(memory_format=torch.channels_last)
     Ho = H + 2 * pad - 2
     L = _lib.lib()
-    for layout in ("nchw", "nhwc"):
+    work = torch.full((4 * cout * B * Ho * Ho,), float("nan"), device="cuda")
+    tickets = torch.zeros(cout // 8 + 1, device="cuda", dtype=torch.int32)
+    for layout, split_k in (("nchw", False), ("nhwc", False), ("nhwc", True), ("nhwc", True)):
         if layout == "nchw":
             xin, strides = x.contiguous(), (cin * H * H, H, 1, H * H)
         else:
@@ -512,12 +514,16 @@ def test_small_conv_matches_torch(B, H, pad, cin, cout):
             strides = (H * H * cin, H * cin, cin, 1)
         y = torch.full((B * Ho * Ho, cout), float("nan"), device="cuda")
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        wp = ctypes.c_void_p(work.data_ptr()) if split_k else None
+        tp = ctypes.c_void_p(tickets.data_ptr()) if split_k else None
         _lib.check(L.azg_small_conv3x3(ctypes.c_void_p(xin.data_ptr()), *strides, B, H, pad,
                                        ctypes.c_void_p(wk.data_ptr()), cin, cout, ctypes.c_void_p(b.data_ptr()), 1,
-                                       ctypes.c_void_p(y.data_ptr()), cout, st))
+                                       ctypes.c_void_p(y.data_ptr()), cout, wp, work.numel() if split_k else 0,
+                                       tp, tickets.numel() if split_k else 0, st))
         torch.cuda.synchronize()
         err = ((y.double() - want).abs() / (want.abs() + 1.0)).max().item()
-        assert err < 1e-5, (layout, err)
+        assert err < 1e-5, (layout, split_k, err)
+        assert int(tickets.abs().sum()) == 0  # the split-K form leaves its tickets at zero
 
 
 @pytest.mark.parametrize("B,K,N,relu,bias", [(1, 4608, 1024, 1, True), (4, 4608, 1024, 1, True),
@@ -548,6 +554,69 @@ def test_small_fc_matches_torch(B, K, N, relu, bias):
     assert err < 1e-5, err
 
 
+@pytest.mark.parametrize("B,depth,n,C", [(1, 4, 7, 512), (4, 4, 7, 512), (2, 2, 6, 512), (3, 2, 8, 512),
+                                         (1, 1, 3, 16), (4, 3, 5, 64), (2, 4, 8, 32)])
+def test_small_conv12_matches_torch(B, depth, n, C):
+    """azg_small_conv12 (conv1 + conv2 in one launch, each split-K block recomputing conv1 for its
+    quarter of conv2's input channels): relu(conv2(relu(conv1(planes)))) against torch in f64,
+    padded 3x3 convs, 1-4 planes, boards 3..8, the tickets left at zero."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    torch.manual_seed(11)
+    x = (torch.rand(B, depth, n, n, device="cuda") < 0.3).float()
+    x[:, -1] = torch.randn(B, n, n, device="cuda")
+    w1 = torch.randn(C, depth, 3, 3, device="cuda") / (depth * 9) ** 0.5
+    w2 = torch.randn(C, C, 3, 3, device="cuda") / (C * 9) ** 0.5
+    b1, b2 = torch.randn(C, device="cuda"), torch.randn(C, device="cuda")
+    F = torch.nn.functional
+    want = torch.relu(F.conv2d(torch.relu(F.conv2d(x.double(), w1.double(), b1.double(), padding=1)),
+                               w2.double(), b2.double(), padding=1)).permute(0, 2, 3, 1).reshape(-1, C)
+    w1k = w1.contiguous(memory_format=torch.channels_last)
+    w2k = w2.contiguous(memory_format=torch.channels_last)
+    work = torch.full((4 * C * B * n * n,), float("nan"), device="cuda")
+    tickets = torch.zeros(C // 8, device="cuda", dtype=torch.int32)
+    V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    for _ in range(2):
+        y = torch.full((B * n * n, C), float("nan"), device="cuda")
+        _lib.check(_lib.lib().azg_small_conv12(V(x), B, depth, n, V(w1k), V(b1), V(w2k), V(b2), C, V(y), C, V(work),
+                                               work.numel(), V(tickets), tickets.numel(),
+                                               ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+        torch.cuda.synchronize()
+        err = ((y.double() - want).abs() / (want.abs() + 1.0)).max().item()
+        assert err < 1e-5, err
+        assert int(tickets.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("B,K,A", [(1, 512, 343), (4, 512, 343), (3, 512, 37), (2, 64, 1), (1, 36, 1023)])
+def test_small_heads_match_torch(B, K, A):
+    """azg_small_heads ([fc3 | fc4] + softmax / tanh in one launch, the heads by the last block
+    to finish): P, v against torch in f64 and the logits written out; ticket left at zero."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    torch.manual_seed(13)
+    x = torch.randn(B, K, device="cuda")
+    w = torch.randn(A + 1, K, device="cuda") / K ** 0.5
+    b = torch.randn(A + 1, device="cuda")
+    lg = x.double() @ w.double().t()
+    P_ref = torch.softmax(lg[:, :A] + b.double()[:A], 1)
+    v_ref = torch.tanh(lg[:, A] + b.double()[A])
+    logits = torch.full((B, A + 1), float("nan"), device="cuda")
+    P = torch.full((B, A), float("nan"), device="cuda")
+    v = torch.full((B, 1), float("nan"), device="cuda")
+    ticket = torch.zeros(1, device="cuda", dtype=torch.int32)
+    V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    for _ in range(2):
+        _lib.check(_lib.lib().azg_small_heads(V(x), K, B, V(w), K, A, V(b), V(logits), V(P), V(v), V(ticket),
+                                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+        torch.cuda.synchronize()
+        assert ((logits.double() - lg).abs() / (lg.abs() + 1)).max().item() < 1e-5
+        torch.testing.assert_close(P.double(), P_ref, rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(v.double().reshape(-1), v_ref, rtol=1e-5, atol=1e-6)
+        assert int(ticket.item()) == 0
+
+
 def test_small_kernels_reject_bad_arguments():
     """Shapes the small kernels do not serve return AZG_ERR_ARG instead of launching."""
     import ctypes
@@ -557,10 +626,17 @@ def test_small_kernels_reject_bad_arguments():
     x = torch.zeros(8 * 8 * 8 * 64, device="cuda")
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     P = ctypes.c_void_p(x.data_ptr())
-    assert L.azg_small_conv3x3(P, 64 * 64, 64 * 8, 64, 1, 5, 8, 1, P, 64, 64, None, 1, P, 64, st) == -1  # 320 px
-    assert L.azg_small_conv3x3(P, 64 * 49, 64 * 7, 64, 1, 1, 7, 1, P, 64, 63, None, 1, P, 64, st) == -1  # odd Cout
+    assert L.azg_small_conv3x3(P, 64 * 64, 64 * 8, 64, 1, 5, 8, 1, P, 64, 64, None, 1, P, 64, None, 0, None, 0,
+                               st) == -1  # 5 leaves
+    assert L.azg_small_conv3x3(P, 64 * 49, 64 * 7, 64, 1, 1, 7, 1, P, 64, 63, None, 1, P, 64, None, 0, None, 0,
+                               st) == -1  # odd Cout
     assert L.azg_small_fc(P, 64, 5, P, 64, 8, None, 1, P, 8, st) == -1  # batch 5
     assert L.azg_small_fc(P, 62, 1, P, 62, 8, None, 1, P, 8, st) == -1  # K % 4
+    assert L.azg_small_conv12(P, 1, 5, 7, P, P, P, P, 512, P, 512, P, 1 << 20, P, 64, st) == -1  # depth 5
+    assert L.azg_small_conv12(P, 1, 4, 9, P, P, P, P, 512, P, 512, P, 1 << 20, P, 64, st) == -1  # n 9
+    assert L.azg_small_conv12(P, 1, 4, 7, P, P, P, P, 520, P, 520, P, 1 << 20, P, 65, st) == -1  # C % 16
+    assert L.azg_small_heads(P, 64, 1, P, 64, 1024, P, P, P, P, P, st) == -1  # A > 1023
+    assert L.azg_small_heads(P, 64, 5, P, 64, 8, P, P, P, P, P, st) == -1  # batch 5
 
 
 @pytest.mark.parametrize("n,depth,A,B", [(7, 4, 343, 1), (7, 4, 343, 2), (7, 4, 343, 4), (6, 2, 37, 1),

@@ -1,4 +1,5 @@
-"""Per-layer time of azg_small_conv3x3 / azg_small_fc at one leaf (C1's batch) on the 7x7 Inflexion network's
+"""Per-layer time of azg_small_conv3x3 / azg_small_fc (and the fused conv12 / heads kernels, and
+the whole small-path forward) at one leaf (C1's batch) on the 7x7 Inflexion network's
 shapes, against torch's conv2d / linear (MIOpen / hipBLASLt, + bias + ReLU) on the same
 inputs; medians of round-robin rounds.  Prints one JSON line per layer."""
 import ctypes
@@ -45,13 +46,16 @@ def main():
             strides = (H * H * cin, H * cin, cin, 1)
         Ho = H + 2 * pad - 2 if taps == 9 else 1
         y = torch.empty((B * Ho * Ho, cout), device="cuda")
+        work = torch.empty(4 * cout * B * Ho * Ho, device="cuda")
+        tickets = torch.zeros(cout // 8, device="cuda", dtype=torch.int32)
 
         def azg():
             if taps == 9:
                 _lib.check(L.azg_small_conv3x3(ctypes.c_void_p(xin.data_ptr()), *strides, B, H, pad,
                                                ctypes.c_void_p(wk.data_ptr()), cin, cout,
                                                ctypes.c_void_p(b.data_ptr()), 1, ctypes.c_void_p(y.data_ptr()), cout,
-                                               st))
+                                               ctypes.c_void_p(work.data_ptr()), work.numel(),
+                                               ctypes.c_void_p(tickets.data_ptr()), tickets.numel(), st))
             else:
                 _lib.check(L.azg_small_fc(ctypes.c_void_p(xin.data_ptr()), cin, B, ctypes.c_void_p(wk.data_ptr()),
                                           cin, cout, ctypes.c_void_p(b.data_ptr()), 1,
@@ -76,6 +80,50 @@ def main():
                 ts[k].append(timeit(f))
         print(json.dumps({"layer": name, "B": B, "azg_us": sorted(ts["azg"])[3],
                           "torch_us": sorted(ts["lib"])[3]}), flush=True)
+    fused(L, st)
+
+
+def fused(L, st):
+    """conv1+conv2 (azg_small_conv12), [fc3|fc4]+heads (azg_small_heads), and the whole small-path
+    forward (InferenceNet at B leaves) against the library form (MIOpen / hipBLASLt)."""
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    C, n, depth = 512, 7, 4
+    planes = (torch.rand(B, depth, n, n, device="cuda") < 0.3).float()
+    w1 = torch.randn(C, depth, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
+    w2 = torch.randn(C, C, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
+    b1, b2 = torch.randn(C, device="cuda"), torch.randn(C, device="cuda")
+    y = torch.empty(B * n * n, C, device="cuda")
+    work = torch.empty(4 * C * B * n * n, device="cuda")
+    tickets = torch.zeros(C // 8 + 1, device="cuda", dtype=torch.int32)
+    x = torch.randn(B, 512, device="cuda")
+    w34, b34 = torch.randn(344, 512, device="cuda"), torch.randn(344, device="cuda")
+    lg, P, v = torch.empty(B, 344, device="cuda"), torch.empty(B, 343, device="cuda"), torch.empty(B, device="cuda")
+    tk = ctypes.c_void_p(tickets.data_ptr() + 4 * (C // 8))
+
+    def conv12():
+        _lib.check(L.azg_small_conv12(V(planes), B, depth, n, V(w1), V(b1), V(w2), V(b2), C, V(y), C, V(work),
+                                      work.numel(), V(tickets), C // 8, st))
+
+    def heads():
+        _lib.check(L.azg_small_heads(V(x), 512, B, V(w34), 512, 343, V(b34), V(lg), V(P), V(v), tk, st))
+    torch.manual_seed(0)
+    net = InflexionNNet().cuda().eval()
+    small, lib_form = InferenceNet(net), InferenceNet(net, conv="miopen", small=False)
+    s = (torch.rand(B, depth, n, n, device="cuda") < 0.3).float()
+
+    def fwd_small():
+        small(s)
+
+    def fwd_lib():
+        lib_form(s)
+    with torch.no_grad():
+        for name, f in (("conv12", conv12), ("heads", heads), ("forward_small", fwd_small),
+                        ("forward_library", fwd_lib)):
+            for _ in range(5):
+                f()
+            t = sorted(timeit(f) for _ in range(7))[3]
+            print(json.dumps({"layer": name, "B": B, "azg_us": t}), flush=True)
 
 
 if __name__ == "__main__":
