@@ -92,6 +92,7 @@ SIGNATURES = [
     ("azg_set_gemm_blocks", ctypes.c_int, [_I32]),
     ("azg_set_arena", ctypes.c_int, [_VP, _VP, _VP, _VP]),
     ("azg_opponent_move", ctypes.c_int, [_VP, _I32, _VP]),
+    ("azg_arena_follow", ctypes.c_int, [_VP, _VP, _VP]),
     ("azg_examples", ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _I32, _I32, _I64, _VP, _VP,
                                     _VP, ctypes.POINTER(_I64), _VP]),
 ]

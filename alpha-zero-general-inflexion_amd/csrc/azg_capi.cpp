@@ -231,6 +231,8 @@ static const char* err_name(int code) {
         case AZG_ERR_NODE_POOL: return "node pool or hash table full (raise node_capacity)";
         case AZG_ERR_PATH: return "search path deeper than max_depth";
         case AZG_ERR_NO_ACTION: return "no valid action at a searched node";
+        case AZG_ERR_STATE: return "arena: the leader engine failed in this slot";
+        case AZG_ERR_ACTION: return "arena: the leader's action is not valid in the follower's game";
         default: return "engine error";
     }
 }
@@ -370,6 +372,17 @@ int azg_opponent_move(azg_engine* e, int32_t kind, void* stream) {
     if (!e) return fail(AZG_ERR_ARG, "null engine");
     if (kind != AZG_OPPONENT_RANDOM && kind != AZG_OPPONENT_GREEDY) return fail(AZG_ERR_ARG, "unknown opponent");
     HIP_TRY(e->ops.opponent(e->d, kind, (hipStream_t)stream));
+    return 0;
+}
+
+int azg_arena_follow(azg_engine* e, const azg_engine* leader, void* stream) {
+    if (!e || !leader || e == leader) return fail(AZG_ERR_ARG, "need two distinct engines");
+    if (!(e->cfg.flags & AZG_FLAG_ARENA) || !(leader->cfg.flags & AZG_FLAG_ARENA))
+        return fail(AZG_ERR_STATE, "engines created without AZG_FLAG_ARENA");
+    if (e->cfg.game_kind != leader->cfg.game_kind || e->cfg.n != leader->cfg.n || e->d.G != leader->d.G ||
+        e->d.max_turns != leader->d.max_turns || e->device != leader->device)
+        return fail(AZG_ERR_ARG, "engines differ in game, size, slot count, max_turns or device");
+    HIP_TRY(e->ops.follow(e->d, leader->d, (hipStream_t)stream));
     return 0;
 }
 

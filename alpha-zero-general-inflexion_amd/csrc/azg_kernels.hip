@@ -1099,6 +1099,41 @@ __global__ __launch_bounds__(WAVE) void opponent_kernel(Dev E, int kind) {
     commit_move<R>(E, g, p, action, m);
 }
 
+// Arena between two searchers (Arena.playGame, Arena.py:54-69, with two MCTSPlayers): two
+// arena engines hold the same games, each searching for its own colour.  After the leader
+// S has moved in slot g, the follower E plays the same action in its copy of the game and
+// takes over S's numpy stream for the slot (the reference's two players draw from one
+// process-wide stream).  The action is checked against E's valid mask (Arena.py:64-67).
+template <class R>
+__global__ __launch_bounds__(WAVE) void follow_kernel(Dev E, Dev S) {
+    const int g = blockIdx.x, lane = lane_id();
+    if (!E.active[g] || E.err[g] || E.searcher[g] == 0 || searching(E, g)) return;
+    const int m = E.moves[g];
+    if (S.moves[g] != m + 1) return;  // the leader has not moved in this slot
+    if (S.err[g] || m >= S.max_moves) {
+        set_err(E, g, -6);  // AZG_ERR_STATE
+        return;
+    }
+    const int action = S.rec_action[(size_t)g * S.max_moves + m];
+    Pos p = load_root<R>(E, g);
+    uint64_t own, opp;
+    int cs, kt;
+    R::key(p, own, opp, kt, cs);
+    const typename R::VCtx vc = R::vctx(own, opp, cs);
+    const bool ok = __ballot(lane == 0 && action >= 0 && action < R::A && R::valid(action, vc)) != 0ull;
+    if (!ok) {
+        set_err(E, g, -7);  // AZG_ERR_ACTION
+        return;
+    }
+    for (int i = lane; i < MT_N; i += WAVE) E.mt[(size_t)g * MT_N + i] = S.mt[(size_t)g * MT_N + i];
+    if (lane == 0) E.mt_pos[g] = S.mt_pos[g];
+    if (m < E.max_moves && lane == 0) {
+        E.rec_action[(size_t)g * E.max_moves + m] = action;
+        E.rec_temp[(size_t)g * E.max_moves + m] = 0;
+    }
+    commit_move<R>(E, g, p, action, m);
+}
+
 // Root visit counts of one slot (drop-in MCTS.getActionProb, MCTS.py:48-49).
 template <class R>
 __global__ __launch_bounds__(WAVE) void root_counts_kernel(Dev E, int g, int32_t* out) {
@@ -1428,6 +1463,10 @@ struct Impl {
         hipLaunchKernelGGL(opponent_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, kind);
         return hipGetLastError();
     }
+    static hipError_t follow(const Dev& E, const Dev& S, hipStream_t st) {
+        hipLaunchKernelGGL(follow_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, S);
+        return hipGetLastError();
+    }
     static hipError_t root_counts(const Dev& E, int g, int32_t* out, hipStream_t st) {
         hipLaunchKernelGGL(root_counts_kernel<R>, dim3(1), dim3(WAVE), 0, st, E, g, out);
         return hipGetLastError();
@@ -1458,6 +1497,7 @@ static GameOps make_ops() {
     o.reset = &Impl<R>::reset;
     o.refill = &Impl<R>::refill;
     o.opponent = &Impl<R>::opponent;
+    o.follow = &Impl<R>::follow;
     o.replay = &Impl<R>::replay;
     o.emit = &Impl<R>::emit;
     return o;

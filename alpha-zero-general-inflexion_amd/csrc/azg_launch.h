@@ -63,6 +63,7 @@ struct GameOps {
     hipError_t (*reset)(const Dev&, uint32_t seed_base, long long first_game, hipStream_t);
     hipError_t (*refill)(const Dev&, const RefillArgs&, hipStream_t);
     hipError_t (*opponent)(const Dev&, int kind, hipStream_t);
+    hipError_t (*follow)(const Dev&, const Dev& leader, hipStream_t);
     hipError_t (*replay)(const ExampleArgs&, hipStream_t);
     hipError_t (*emit)(const ExampleArgs&, hipStream_t);
 };

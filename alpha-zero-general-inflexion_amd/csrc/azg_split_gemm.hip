@@ -78,7 +78,7 @@ struct SGArgs {
 __device__ __forceinline__ int b_col(int R) { return (R & ~63) | ((R & 15) << 2) | ((R >> 4) & 3); }
 
 // byte address of a __shared__ location in the workgroup's LDS (operand of ds_* asm)
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
+[[maybe_unused]] __device__ __forceinline__ unsigned lds_addr(const void* p) {
     return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
 }
 
@@ -291,7 +291,7 @@ __device__ __forceinline__ SGTile sg_tile(const SGArgs& g, int L) {
 // s_memtime stamps split each stage into [operand reads + DMA issue, reads landed],
 // [MFMA issue], [vmcnt(0)], [barrier] and the epilogue; per-wave sums go to g.stamps
 // (MI355X guide, in-kernel stamps: read the shares, not the length).
-__device__ __forceinline__ unsigned long long sg_stamp() {
+[[maybe_unused]] __device__ __forceinline__ unsigned long long sg_stamp() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");

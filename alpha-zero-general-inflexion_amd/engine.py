@@ -298,6 +298,11 @@ class SelfPlayEngine:
         code = {"random": _lib.OPPONENT_RANDOM, "greedy": _lib.OPPONENT_GREEDY}[kind]
         check(self.L.azg_opponent_move(self.h, code, self._stream()))
 
+    def follow(self, leader):
+        """Play the leader engine's last move in every slot where it just moved, taking over
+        the slot's numpy stream (an arena between two searchers, azg_arena_follow)."""
+        check(self.L.azg_arena_follow(self.h, leader.h, self._stream()))
+
     # ------------------------------------------------------------------ results
     def read_moves(self, counts=True):
         G, MM = self.G, self.max_moves

@@ -52,6 +52,7 @@ enum azg_err {
     AZG_ERR_PATH = -4,        /* search path deeper than max_depth              */
     AZG_ERR_NO_ACTION = -5,   /* no valid action (MCTS.py:131 best_act = -1)   */
     AZG_ERR_STATE = -6,       /* call out of order                               */
+    AZG_ERR_ACTION = -7,      /* arena: the leader's action is not valid here   */
 };
 
 typedef struct {
@@ -318,6 +319,15 @@ int  azg_device_ptrs(azg_engine* e, void** out /*[8]*/);
 int  azg_set_arena(azg_engine* e, const int32_t* searcher /*[G] host*/, const int32_t* first_player /*[G] host*/,
                    void* stream);
 int  azg_opponent_move(azg_engine* e, int32_t kind, void* stream);
+/* Arena between two searchers (Arena.py:23-88 with two MCTSPlayers; replaces the
+ * reference's per-game Arena.playGame loop for player1 = MCTSPlayer(net 1),
+ * player2 = MCTSPlayer(net 2)).  Two arena engines hold the same games, one searching
+ * for RED, the other for BLUE; after the leader's move (sim_begin / sim_end /
+ * move_end), azg_arena_follow plays the leader's action in e's copy of every slot
+ * where the leader just moved and gives e the leader's numpy stream for the slot (the
+ * reference's two players draw from one process-wide stream).  An action that is not
+ * valid in e's copy sets the slot's error (Arena.py:64-67). */
+int  azg_arena_follow(azg_engine* e, const azg_engine* leader, void* stream);
 
 /* Sizes of a supported game: out[0] cells, [1] actions (max_actions), [2] NN
  * input planes, [3] forms returned by game.symmetries(). */

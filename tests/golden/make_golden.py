@@ -338,7 +338,8 @@ def gen_mcts(np, quick, othello=False, realnet=False, toy=False):
 # -------------------------------------------------------------------------- Arena
 def gen_arena(np):
     """Reference Arena.playGame (Arena.py:38-88) between MCTSPlayer (stub
-    evaluator) and RandomPlayer / GreedyPlayer, one game per seed: game i of a
+    evaluator) and RandomPlayer / GreedyPlayer / a second MCTSPlayer (other sims and
+    cpuct), one game per seed: game i of a
     set is seeded np.random.seed(seed_base + i) and gets the colour order
     Arena.playGames gives index i (Arena.py:126-129).  Records every move
     played and the result counters."""
@@ -372,12 +373,22 @@ def gen_arena(np):
     sets = {
         "arena_random": dict(opponent="random", max_turns=100, sims=25, cpuct=1, num=8, seed_base=800),
         "arena_greedy": dict(opponent="greedy", max_turns=100, sims=25, cpuct=1, num=8, seed_base=900),
+        # two MCTSPlayers (Arena(player1, player2) with two searchers, one process stream)
+        "arena_mcts": dict(opponent="mcts", max_turns=100, sims=25, cpuct=1, num=6, seed_base=700,
+                           opp_sims=10, opp_cpuct=1.5),
     }
+    only = os.environ.get("AZG_GOLDEN_ARENA")
+    if only:
+        sets = {k: v for k, v in sets.items() if k in only.split(",")}
     red, blue = list(PlayerColour)
     for name, cfg in sets.items():
         game = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
         args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"]})
-        opp = RandomPlayer() if cfg["opponent"] == "random" else GreedyPlayer()
+        if cfg["opponent"] == "mcts":
+            args2 = dotdict({"numMCTSSims": cfg["opp_sims"], "cpuct": cfg["opp_cpuct"]})
+            opp = MCTSPlayer(mcts_mod.MCTS(StubNNet(game), args2))
+        else:
+            opp = RandomPlayer() if cfg["opponent"] == "random" else GreedyPlayer()
         arena = Arena(MCTSPlayer(mcts_mod.MCTS(StubNNet(game), args)), opp, game)
         games = []
         t0 = time.time()

