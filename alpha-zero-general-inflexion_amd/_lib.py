@@ -51,6 +51,7 @@ SIGNATURES = [
     ("azg_reset", ctypes.c_int, [_VP, _U32, _I64, _VP]),
     ("azg_sim_begin", ctypes.c_int, [_VP, _VP, _VP]),
     ("azg_sim_end", ctypes.c_int, [_VP, _VP, _I32, _VP, _VP]),
+    ("azg_sim_end_begin", ctypes.c_int, [_VP, _VP, _I32, _VP, _VP, _VP]),
     ("azg_stub_eval", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     ("azg_move_end", ctypes.c_int, [_VP, _VP]),
     ("azg_refill", ctypes.c_int, [_VP, _VP, _I64, _U32, _VP, _I64, _VP, _VP, _VP, _VP, _VP, _VP]),

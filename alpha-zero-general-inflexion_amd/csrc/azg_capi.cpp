@@ -127,6 +127,7 @@ int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
     ALLOC(d.node_turn, GM);
     ALLOC(d.node_P, GM * ROW);
     ALLOC(d.node_N, GM * ROW);
+    ALLOC(d.node_Qf, GM * ROW);
     ALLOC(d.node_Q, GM * ROW);
     ALLOC(d.free_stack, GM);
     ALLOC(d.free_top, G);
@@ -211,6 +212,13 @@ int azg_sim_begin(azg_engine* e, float* leaf_planes, void* stream) {
 int azg_sim_end(azg_engine* e, const float* P, int32_t p_stride, const float* v, void* stream) {
     if (!e || !P || !v || p_stride < e->ops.actions) return fail(AZG_ERR_ARG, "bad P/v");
     HIP_TRY(e->ops.expand_backup(e->d, P, p_stride, v, (hipStream_t)stream));
+    return 0;
+}
+
+int azg_sim_end_begin(azg_engine* e, const float* P, int32_t p_stride, const float* v, float* leaf_planes,
+                      void* stream) {
+    if (!e || !P || !v || !leaf_planes || p_stride < e->ops.actions) return fail(AZG_ERR_ARG, "bad P/v/planes");
+    HIP_TRY(e->ops.expand_select(e->d, P, p_stride, v, leaf_planes, (hipStream_t)stream));
     return 0;
 }
 

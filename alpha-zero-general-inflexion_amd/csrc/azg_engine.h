@@ -50,7 +50,8 @@ struct Dev {
     int32_t* node_turn;  // -1 = free (the node GC's scan reads this dense array)
     float* node_P;       // [G*M*AP]
     uint32_t* node_N;    // [G*M*AP]  bit31: Q is f32-typed
-    double* node_Q;      // [G*M*AP]
+    float* node_Qf;      // [G*M*AP]  Q of f32-typed edges (N bit31 set): read with P and N
+    double* node_Q;      // [G*M*AP]  Q of Python-float edges (bit31 clear): read only for those
     int32_t* free_stack; // [G*M]
     int32_t* free_top;   // [G]
     int32_t* live;       // [G] allocated nodes

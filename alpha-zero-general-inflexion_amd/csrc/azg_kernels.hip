@@ -599,14 +599,17 @@ __device__ int puct_select(const Dev& E, int g, int id, const typename R::VCtx& 
         if (ci[j] >= 0) {
             const float cp = E.cpuct_f * E.node_P[row + ci[j]];
             const uint32_t nr = E.node_N[row + ci[j]];
-            // Q loaded with P and N (not after N says the edge exists): one dependent
-            // round trip less per level; the value is used only where N > 0
-            const double qv = E.node_Q[row + ci[j]];
+            // the f32 Q loaded with P and N (not after N says the edge exists): one
+            // dependent round trip less per level; used only where N > 0.  An edge whose
+            // Q is still a Python float (only terminal values backed into it) reads its
+            // f64 Q after N: rare, near the end of a game
+            const float qf = E.node_Qf[row + ci[j]];
             const int n = (int)(nr & 0x7fffffffu);
             float u;
             if (n > 0) {
+                const float q = (nr >> 31) ? qf : (float)E.node_Q[row + ci[j]];
                 const float t = (cp * sq_edge) / (float)(1 + n);
-                u = (float)qv + t;
+                u = q + t;
             } else {
                 u = cp * sq_new;
             }
@@ -645,7 +648,7 @@ __device__ __forceinline__ void set_err(const Dev& E, int g, int code) {
 // sim_begin: MCTS.search down to a leaf (MCTS.py:83-132), writing the leaf's
 // randomly symmetrised planes (MCTS.py:91-92) as f32 into the NN batch.
 template <class R>
-__global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__ planes) {
+__device__ __forceinline__ void select_body(const Dev& E, float* __restrict__ planes) {
     __shared__ uint32_t s_mt[MT_N];
     const int g = blockIdx.x, lane = lane_id();
     float* out = planes + (size_t)g * R::PLANES * R::CELLS;
@@ -742,8 +745,8 @@ __global__ __launch_bounds__(WAVE) void stub_eval_kernel(const float* __restrict
 // (MCTS.py:136-145).  The path holds distinct nodes, so lanes update one edge
 // each with no atomics.
 template <class R>
-__global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float* __restrict__ Pin, int p_stride,
-                                                             const float* __restrict__ vin) {
+__device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __restrict__ Pin, int p_stride,
+                                                   const float* __restrict__ vin) {
     __shared__ float s_p[R::AP];
     __shared__ float s_acc[WAVE];
     __shared__ float s_leaf[16];
@@ -758,11 +761,11 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
     const int packed0 = lane < depth ? path[lane] : 0;
     const int top0 = kind == LEAF_EXPAND ? E.free_top[g] : 0;
     uint32_t nr0 = 0u;
-    double q0 = 0.0;
+    float qf0 = 0.0f;
     if (lane < depth) {
         const size_t erow = ((size_t)g * E.M + (packed0 >> 10)) * R::AP + (packed0 & 1023);
         nr0 = E.node_N[erow];
-        q0 = E.node_Q[erow];  // used only where N > 0
+        qf0 = E.node_Qf[erow];  // used only where N > 0 and Q is f32-typed
     }
     double ret;
     bool ret_f32;
@@ -849,7 +852,8 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
         const uint32_t nr = d < WAVE ? nr0 : E.node_N[row];
         const int n = (int)(nr & 0x7fffffffu);
         const bool qf = (nr >> 31) != 0;
-        double q = d < WAVE ? q0 : E.node_Q[row];
+        double q = 0.0;
+        if (n > 0) q = qf ? (double)(d < WAVE ? qf0 : E.node_Qf[row]) : E.node_Q[row];
         bool nf;
         if (n == 0) {  // an edge's first backup defines Q
             q = v;
@@ -863,10 +867,37 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
             q = ((double)n * q + v) / (double)(n + 1);
             nf = false;
         }
-        E.node_Q[row] = q;
+        if (nf)
+            E.node_Qf[row] = (float)q;  // exact: an f32-typed Q is an f32 value
+        else
+            E.node_Q[row] = q;
         E.node_N[row] = (uint32_t)(n + 1) | (nf ? 0x80000000u : 0u);
         E.node_key[ni].Ns += 1;
     }
+}
+
+template <class R>
+__global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__ planes) {
+    select_body<R>(E, planes);
+}
+
+template <class R>
+__global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float* __restrict__ Pin, int p_stride,
+                                                             const float* __restrict__ vin) {
+    expand_backup_body<R>(E, Pin, p_stride, vin);
+}
+
+// sim_end of one simulation and sim_begin of the next in one launch (same wave, same
+// order of operations as the two kernels: the tree writes of the backup are visible to
+// the next descent through the workgroup barrier): one kernel boundary less per
+// simulation where the search is launch-bound (one leaf per simulation, the drop-in).
+template <class R>
+__global__ __launch_bounds__(WAVE) void expand_select_kernel(Dev E, const float* __restrict__ Pin, int p_stride,
+                                                             const float* __restrict__ vin,
+                                                             float* __restrict__ planes) {
+    expand_backup_body<R>(E, Pin, p_stride, vin);
+    __syncthreads();
+    select_body<R>(E, planes);
 }
 
 // move_end: MCTS.getActionProb root policy (MCTS.py:48-60), Coach.executeEpisode
@@ -1455,6 +1486,11 @@ struct Impl {
         hipLaunchKernelGGL(expand_backup_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, P, p_stride, v);
         return hipGetLastError();
     }
+    static hipError_t expand_select(const Dev& E, const float* P, int p_stride, const float* v, float* planes,
+                                    hipStream_t st) {
+        hipLaunchKernelGGL(expand_select_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, P, p_stride, v, planes);
+        return hipGetLastError();
+    }
     static hipError_t move_end(const Dev& E, hipStream_t st) {
         hipLaunchKernelGGL(move_end_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E);
         return hipGetLastError();
@@ -1493,6 +1529,7 @@ static GameOps make_ops() {
     o.stub_eval = &Impl<R>::stub_eval;
     o.expand_backup = &Impl<R>::expand_backup;
     o.move_end = &Impl<R>::move_end;
+    o.expand_select = &Impl<R>::expand_select;
     o.root_counts = &Impl<R>::root_counts;
     o.reset = &Impl<R>::reset;
     o.refill = &Impl<R>::refill;

@@ -59,6 +59,8 @@ struct GameOps {
     hipError_t (*stub_eval)(const Dev&, const float* planes, float* P, float* v, hipStream_t);
     hipError_t (*expand_backup)(const Dev&, const float* P, int p_stride, const float* v, hipStream_t);
     hipError_t (*move_end)(const Dev&, hipStream_t);
+    hipError_t (*expand_select)(const Dev&, const float* P, int p_stride, const float* v, float* planes,
+                                hipStream_t);
     hipError_t (*root_counts)(const Dev&, int g, int32_t* out, hipStream_t);
     hipError_t (*reset)(const Dev&, uint32_t seed_base, long long first_game, hipStream_t);
     hipError_t (*refill)(const Dev&, const RefillArgs&, hipStream_t);

@@ -190,14 +190,14 @@ class MCTS:
         return self._engine
 
     def _capture(self, eng, sims):
-        """Record `sims` simulations (select, network, expand/backup) as one graph.
+        """Record `sims` simulations (select, then per simulation the network and the
+        backup fused with the next select) as one graph.
         Capturing launches nothing, so the tree is unchanged."""
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.device)
         try:
             with torch.cuda.device(self.device), torch.cuda.graph(g):
-                for _ in range(sims):
-                    eng.simulate()
+                eng.simulate_many(sims)
         except AzgError:
             raise  # an engine error is an error, not a capture limitation
         except RuntimeError as e:
@@ -210,8 +210,7 @@ class MCTS:
 
     def _simulate(self, eng, sims):
         if not self.graph or sims != int(self.args.numMCTSSims):
-            for _ in range(sims):
-                eng.simulate()
+            eng.simulate_many(sims)
             return
         g = self._sims_graph
         if g is not None and self._graph_sims != sims:  # args.numMCTSSims changed since the capture
@@ -221,8 +220,7 @@ class MCTS:
         if g is not None:
             g.replay()
             return
-        for _ in range(sims):  # first call: eager, initialises the evaluator's libraries
-            eng.simulate()
+        eng.simulate_many(sims)  # first call: eager, initialises the evaluator's libraries
         self._warm = True
 
     def _run(self, game, sims):

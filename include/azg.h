@@ -90,6 +90,11 @@ int  azg_reset(azg_engine* e, uint32_t seed_base, int64_t first_game, void* stre
  * ignore P/v. */
 int  azg_sim_begin(azg_engine* e, float* leaf_planes, void* stream);
 int  azg_sim_end(azg_engine* e, const float* P, int32_t p_stride, const float* v, void* stream);
+/* azg_sim_end of this simulation and azg_sim_begin of the next in one launch (same
+ * results: one wave per slot does the backup, then the next descent); saves a kernel
+ * boundary per simulation where the search is launch-bound (few slots, one leaf each). */
+int  azg_sim_end_begin(azg_engine* e, const float* P, int32_t p_stride, const float* v, float* leaf_planes,
+                       void* stream);
 
 /* Test evaluator (tests/golden/stubnet.py spec): planes -> P, v on device. */
 int  azg_stub_eval(azg_engine* e, const float* leaf_planes, float* P, float* v, void* stream);

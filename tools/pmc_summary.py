@@ -37,6 +37,8 @@ def group(name):
         return "select_kernel"
     if "azg::expand_backup_kernel" in name:
         return "expand_backup_kernel"
+    if "azg::expand_select_kernel" in name:
+        return "expand_select_kernel"
     if "azg::move_end_kernel" in name:
         return "move_end_kernel"
     if "bias_relu" in name:
