@@ -22,7 +22,7 @@ reference step's quantities:
   * every rank then takes the identical Adam step on the identical gradient, so the
     weights stay bitwise equal on all ranks and need no broadcast afterwards.
 
-The arithmetic is the reference step's up to summation order (tests/test_dist_gloo.py
+The arithmetic is the reference step's up to summation order (tests/test_ddp_gloo.py
 compares the trained weights with the single-process trainer's within the GPU trainer's
 tolerance, tests/test_gpu_train.py); at world size 1 NNetWrapper.train_examples is the
 single-process trainer itself, bit-identical to the reference on the CPU
