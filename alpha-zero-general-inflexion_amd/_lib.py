@@ -60,6 +60,8 @@ SIGNATURES = [
     ("azg_set_root", ctypes.c_int, [_VP, _I32, _VP, _I32, _I32, _VP]),
     ("azg_get_rng", ctypes.c_int, [_VP, _I32, _VP, ctypes.POINTER(_I32), _VP]),
     ("azg_set_rng", ctypes.c_int, [_VP, _I32, _VP, _I32, _VP]),
+    ("azg_slot_begin", ctypes.c_int, [_VP, _I32, _VP, _I32, _I32, _VP, _I32, _VP]),
+    ("azg_slot_end", ctypes.c_int, [_VP, _I32, _VP, _VP, _VP, _VP, _VP]),
     ("azg_root_counts", ctypes.c_int, [_VP, _I32, _VP, _VP]),
     ("azg_read_moves", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     ("azg_stats", ctypes.c_int, [_VP, _VP, _VP]),

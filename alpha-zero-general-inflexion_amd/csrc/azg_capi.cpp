@@ -49,7 +49,15 @@ struct azg_engine {
     long long* stats;   // device [8]
     int32_t* counts1;   // device [A]
     size_t bytes;
+    // drop-in slot I/O (azg_slot_begin / azg_slot_end), allocated at first use
+    int32_t* io_dev = nullptr;   // device [SLOT_IN_WORDS + A + SLOT_OUT_EXTRA]
+    int32_t* io_host = nullptr;  // pinned, same layout
+    hipEvent_t io_copied = nullptr;  // the last slot_begin's upload has been read
 };
+
+namespace {
+constexpr int SLOT_IN_WORDS = 19 + azg::MT_N, SLOT_OUT_EXTRA = azg::MT_N + 3;
+}
 
 // Zeroed on the caller's stream, ahead of azg_reset's kernels on that stream: a plain
 // hipMemset runs on the null stream, which a non-blocking stream (every torch side
@@ -170,6 +178,8 @@ int azg_create(const azg_config* cfg, void* stream, azg_engine** out) {
 
 void azg_destroy(azg_engine* e) {
     if (!e) return;
+    if (e->io_copied) (void)hipEventSynchronize(e->io_copied), (void)hipEventDestroy(e->io_copied);
+    if (e->io_host) (void)hipHostFree(e->io_host);
     for (void* p : e->allocs) (void)hipFree(p);
     delete e;
 }
@@ -292,6 +302,59 @@ int azg_set_root(azg_engine* e, int32_t slot, const int8_t* board, int32_t turn,
     HIP_TRY(hipMemcpyAsync(e->d.err + slot, &zero, 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(e->d.root_id + slot, 0xff, 4, st));  // -1: look the new root up
     HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+static int slot_io(azg_engine* e, void* stream) {
+    if (e->io_dev) return 0;
+    const size_t words = (size_t)SLOT_IN_WORDS + e->ops.actions + SLOT_OUT_EXTRA;
+    int r = dalloc(e, &e->io_dev, words, (hipStream_t)stream);
+    if (r) return r;
+    HIP_TRY(hipHostMalloc((void**)&e->io_host, words * 4, hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&e->io_copied, hipEventDisableTiming));
+    return 0;
+}
+
+int azg_slot_begin(azg_engine* e, int32_t slot, const int8_t* board, int32_t turn, int32_t player,
+                   const uint32_t* mt, int32_t pos, void* stream) {
+    if (!e || !board || !mt || slot < 0 || slot >= e->d.G || (player != 1 && player != -1) || pos < 0 ||
+        pos > azg::MT_N)
+        return fail(AZG_ERR_ARG, "bad slot_begin argument");
+    int r = slot_io(e, stream);
+    if (r) return r;
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipEventSynchronize(e->io_copied));  // the previous upload has left the staging buffer
+    int32_t* h = e->io_host;
+    memset(h, 0, 64);
+    memcpy(h, board, (size_t)e->ops.cells);
+    h[16] = turn;
+    h[17] = player;
+    h[18] = pos;
+    memcpy(h + 19, mt, azg::MT_N * 4);
+    HIP_TRY(hipMemcpyAsync(e->io_dev, h, (size_t)SLOT_IN_WORDS * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(e->io_copied, st));
+    HIP_TRY(e->ops.slot_begin(e->d, slot, e->io_dev, st));
+    return 0;
+}
+
+int azg_slot_end(azg_engine* e, int32_t slot, int32_t* counts, uint32_t* mt, int32_t* pos, int32_t* active,
+                 void* stream) {
+    if (!e || !counts || !mt || !pos || slot < 0 || slot >= e->d.G) return fail(AZG_ERR_ARG, "bad slot_end argument");
+    int r = slot_io(e, stream);
+    if (r) return r;
+    hipStream_t st = (hipStream_t)stream;
+    const int A = e->ops.actions;
+    int32_t* dout = e->io_dev + SLOT_IN_WORDS;
+    int32_t* hout = e->io_host + SLOT_IN_WORDS;
+    HIP_TRY(e->ops.slot_end(e->d, slot, dout, st));
+    HIP_TRY(hipMemcpyAsync(hout, dout, (size_t)(A + SLOT_OUT_EXTRA) * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    memcpy(counts, hout, (size_t)A * 4);
+    memcpy(mt, hout + A, azg::MT_N * 4);
+    *pos = hout[A + azg::MT_N];
+    if (active) *active = hout[A + azg::MT_N + 2];
+    const int err = hout[A + azg::MT_N + 1];
+    if (err) return fail(err, err_name(err));
     return 0;
 }
 

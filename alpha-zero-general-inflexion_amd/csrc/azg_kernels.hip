@@ -1165,6 +1165,51 @@ __global__ __launch_bounds__(WAVE) void follow_kernel(Dev E, Dev S) {
     commit_move<R>(E, g, p, action, m);
 }
 
+// The drop-in's per-call slot I/O in one launch each way (MCTS.getActionProb on one
+// game, numpy's global stream handed over and back).  in: board as 16 words of int8,
+// turn, player, mt_pos, mt[624] (SLOT_IN_WORDS); out: root visit counts [A], mt[624],
+// mt_pos, err, active (A + SLOT_OUT_EXTRA words).
+template <class R>
+__global__ __launch_bounds__(WAVE) void slot_begin_kernel(Dev E, int g, const int32_t* __restrict__ in) {
+    const int lane = lane_id();
+    if (lane < 16) ((int32_t*)(E.board + (size_t)g * 64))[lane] = in[lane];
+    for (int i = lane; i < MT_N; i += WAVE) E.mt[(size_t)g * MT_N + i] = (uint32_t)in[19 + i];
+    if (lane == 0) {
+        E.turn[g] = in[16];
+        E.player[g] = in[17];
+        E.mt_pos[g] = in[18];
+        E.outcome[g] = ONGOING;
+        E.active[g] = 1;
+        E.moves[g] = in[16];
+        E.err[g] = 0;
+        E.root_id[g] = -1;  // look the new root up
+    }
+}
+
+template <class R>
+__global__ __launch_bounds__(WAVE) void slot_end_kernel(Dev E, int g, int32_t* __restrict__ out) {
+    const int lane = lane_id();
+    Pos p = load_root<R>(E, g);
+    uint64_t own, opp;
+    int cs, kt, slot;
+    R::key(p, own, opp, kt, cs);
+    const int id = table_lookup(E, g, own, opp, kt, cs, &slot);
+    int ci[R::AJ];
+    edge_slots<R>(R::vctx(own, opp, cs), ci);
+#pragma unroll
+    for (int j = 0; j < R::AJ; ++j) {
+        const int a = lane + WAVE * j;
+        if (a < R::A)
+            out[a] = (id >= 0 && ci[j] >= 0) ? (int)(E.node_N[node_row<R>(E, g, id) + ci[j]] & 0x7fffffffu) : 0;
+    }
+    for (int i = lane; i < MT_N; i += WAVE) out[R::A + i] = (int32_t)E.mt[(size_t)g * MT_N + i];
+    if (lane == 0) {
+        out[R::A + MT_N] = E.mt_pos[g];
+        out[R::A + MT_N + 1] = E.err[g];
+        out[R::A + MT_N + 2] = E.active[g];
+    }
+}
+
 // Root visit counts of one slot (drop-in MCTS.getActionProb, MCTS.py:48-49).
 template <class R>
 __global__ __launch_bounds__(WAVE) void root_counts_kernel(Dev E, int g, int32_t* out) {
@@ -1503,6 +1548,14 @@ struct Impl {
         hipLaunchKernelGGL(follow_kernel<R>, dim3(E.G), dim3(WAVE), 0, st, E, S);
         return hipGetLastError();
     }
+    static hipError_t slot_begin(const Dev& E, int g, const int32_t* in, hipStream_t st) {
+        hipLaunchKernelGGL(slot_begin_kernel<R>, dim3(1), dim3(WAVE), 0, st, E, g, in);
+        return hipGetLastError();
+    }
+    static hipError_t slot_end(const Dev& E, int g, int32_t* out, hipStream_t st) {
+        hipLaunchKernelGGL(slot_end_kernel<R>, dim3(1), dim3(WAVE), 0, st, E, g, out);
+        return hipGetLastError();
+    }
     static hipError_t root_counts(const Dev& E, int g, int32_t* out, hipStream_t st) {
         hipLaunchKernelGGL(root_counts_kernel<R>, dim3(1), dim3(WAVE), 0, st, E, g, out);
         return hipGetLastError();
@@ -1531,6 +1584,8 @@ static GameOps make_ops() {
     o.move_end = &Impl<R>::move_end;
     o.expand_select = &Impl<R>::expand_select;
     o.root_counts = &Impl<R>::root_counts;
+    o.slot_begin = &Impl<R>::slot_begin;
+    o.slot_end = &Impl<R>::slot_end;
     o.reset = &Impl<R>::reset;
     o.refill = &Impl<R>::refill;
     o.opponent = &Impl<R>::opponent;

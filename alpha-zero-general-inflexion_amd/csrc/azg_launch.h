@@ -62,6 +62,8 @@ struct GameOps {
     hipError_t (*expand_select)(const Dev&, const float* P, int p_stride, const float* v, float* planes,
                                 hipStream_t);
     hipError_t (*root_counts)(const Dev&, int g, int32_t* out, hipStream_t);
+    hipError_t (*slot_begin)(const Dev&, int g, const int32_t* in, hipStream_t);
+    hipError_t (*slot_end)(const Dev&, int g, int32_t* out, hipStream_t);
     hipError_t (*reset)(const Dev&, uint32_t seed_base, long long first_game, hipStream_t);
     hipError_t (*refill)(const Dev&, const RefillArgs&, hipStream_t);
     hipError_t (*opponent)(const Dev&, int kind, hipStream_t);

@@ -356,6 +356,23 @@ class SelfPlayEngine:
         mt = np.ascontiguousarray(mt, np.uint32)
         check(self.L.azg_set_rng(self.h, int(slot), mt.ctypes.data, int(pos), self._stream()))
 
+    def slot_begin(self, slot, board, turn, player, mt, pos):
+        """set_root + set_rng in one upload (the drop-in's per-call input)."""
+        b = np.ascontiguousarray(np.asarray(board).reshape(-1), np.int8)
+        mt = np.ascontiguousarray(mt, np.uint32)
+        check(self.L.azg_slot_begin(self.h, int(slot), b.ctypes.data, int(turn), int(player), mt.ctypes.data,
+                                    int(pos), self._stream()))
+
+    def slot_end(self, slot):
+        """root_counts + get_rng + the slot's active flag in one download; raises the slot's
+        engine error.  Returns (counts [A] int32, mt [624] uint32, pos, active)."""
+        c = np.zeros(self.A, np.int32)
+        mt = np.zeros(624, np.uint32)
+        pos, act = ctypes.c_int32(), ctypes.c_int32()
+        check(self.L.azg_slot_end(self.h, int(slot), c.ctypes.data, mt.ctypes.data, ctypes.byref(pos),
+                                  ctypes.byref(act), self._stream()))
+        return c, mt, pos.value, act.value
+
     def root_counts(self, slot):
         c = np.zeros(self.A, np.int32)
         check(self.L.azg_root_counts(self.h, int(slot), c.ctypes.data, self._stream()))

@@ -235,16 +235,14 @@ class MCTS:
             return None
         eng = self._engine_for(game)
         state = np.random.get_state()
-        eng.set_rng(0, state[1], state[2])
-        eng.set_root(0, game._board, game._curr_turn, game.player.num)
+        eng.slot_begin(0, game._board, game._curr_turn, game.player.num, state[1], state[2])
         self._simulate(eng, sims)
-        # a full node pool (or any engine error) stops the slot's search: raise rather
-        # than return counts from a truncated search (azg_active_games reports it)
-        eng.active()
+        # a full node pool (or any engine error) stops the slot's search: slot_end raises
+        # rather than return counts from a truncated search
+        counts, mt, pos, _ = eng.slot_end(0)
         eng.check_evaluator()
-        mt, pos = eng.get_rng(0)
         np.random.set_state((state[0], mt, pos, state[3], state[4]))
-        return eng
+        return counts
 
     def search(self, game):
         """One simulation from `game` (MCTS.py:62-145); updates the tree."""
@@ -253,8 +251,8 @@ class MCTS:
     def getActionProb(self, game, temp=1):
         if not (isinstance(temp, (int, float)) and temp >= 0):
             raise AssertionError("temp must be a number >= 0")
-        eng = self._run(game, int(self.args.numMCTSSims))
-        counts = eng.root_counts(0).astype(np.int64) if eng is not None else self._host.root_counts(0, game)
+        counts = self._run(game, int(self.args.numMCTSSims))
+        counts = counts.astype(np.int64) if counts is not None else self._host.root_counts(0, game)
         if temp == 0:
             best = np.argwhere(counts == np.max(counts)).ravel()
             pick = np.random.choice(best)

@@ -125,6 +125,15 @@ int  azg_set_root(azg_engine* e, int32_t slot, const int8_t* board /*[n*n]*/, in
                   int32_t player, void* stream);
 int  azg_get_rng(azg_engine* e, int32_t slot, uint32_t* mt /*[624]*/, int32_t* pos, void* stream);
 int  azg_set_rng(azg_engine* e, int32_t slot, const uint32_t* mt /*[624]*/, int32_t pos, void* stream);
+/* The drop-in's per-call slot I/O (MCTS.getActionProb on one game) in one upload and one
+ * download: azg_slot_begin = azg_set_root + azg_set_rng (no host synchronisation; the
+ * engine's pinned staging buffer is reused once the previous upload has been read);
+ * azg_slot_end = azg_root_counts + azg_get_rng + the slot's active flag, and returns the
+ * slot's engine error (a full node pool, ...) as its code. */
+int  azg_slot_begin(azg_engine* e, int32_t slot, const int8_t* board, int32_t turn, int32_t player,
+                    const uint32_t* mt /*[624]*/, int32_t pos, void* stream);
+int  azg_slot_end(azg_engine* e, int32_t slot, int32_t* counts /*[A]*/, uint32_t* mt /*[624]*/, int32_t* pos,
+                  int32_t* active, void* stream);
 int  azg_root_counts(azg_engine* e, int32_t slot, int32_t* counts /*[A]*/, void* stream);
 
 /* Recorded moves: actions [G,max_moves], temps [G,max_moves], counts
