@@ -113,7 +113,8 @@ def load_pmc(G, game, impl, gemm="split"):
         return (d.get(k) or {}).get("hbm_bytes_per_forward") or 0.0
 
     out = {"transforms": sum(per_fwd(k) for k in ("winograd_first", "winograd_mid", "winograd_out")),
-           "tree": per_fwd("select_kernel") + per_fwd("expand_backup_kernel"),
+           # per simulation step: select + expand / backup, fused or not (azg_sim_end_begin)
+           "tree": per_fwd("select_kernel") + per_fwd("expand_backup_kernel") + per_fwd("expand_select_kernel"),
            "note": f"{os.path.relpath(path, ROOT)}: FETCH_SIZE x2 + WRITE_SIZE (split GEMM: per call; "
                    "transforms: per forward; tree: per simulation step); counts L2 misses incl. Infinity-Cache hits"}
     if per_fwd("split_gemm"):
@@ -414,14 +415,17 @@ def main():
 
     def timed_move(every=None):
         every = every or max(args.timer_every, 1)
+        run = 0  # uninstrumented simulations not yet launched
         for _ in range(eng.sims):
             on = inst["count"] % every == 0
             inst["count"] += 1
             if not on:
-                azg_amd._lib.check(eng.L.azg_sim_begin(eng.h, eng.planes.data_ptr(), eng._stream()))
-                P, v = eng.evaluate()
-                azg_amd._lib.check(eng.L.azg_sim_end(eng.h, P.data_ptr(), P.stride(0), v.data_ptr(), eng._stream()))
+                run += 1
                 continue
+            # the uninstrumented ones as the engine runs them: each expand / backup fused with
+            # the next select (azg_sim_end_begin); the instrumented one split, to time its parts
+            eng.simulate_many(run)
+            run = 0
             inst["on"] = True
             inst["sims"] += 1
             s = t_sel.start()
@@ -434,6 +438,7 @@ def main():
             azg_amd._lib.check(eng.L.azg_sim_end(eng.h, P.data_ptr(), P.stride(0), v.data_ptr(), eng._stream()))
             t_exp.stop(s)
             inst["on"] = False
+        eng.simulate_many(run)
         s = t_end.start()
         eng.move_end()
         t_end.stop(s)

@@ -74,8 +74,10 @@ def main():
             "fetch_kib_raw_median": median(f), "write_kib_median": median(w),
             "fetch_bytes_corrected": 2 * median(f) * 1024, "write_bytes": median(w) * 1024,
             "hbm_bytes": 2 * median(f) * 1024 + median(w) * 1024})
-    # per leaf forward = per simulation: totals over all dispatches / select_kernel dispatches
-    # (robust where several layers share one kernel name and grid, e.g. the three GEMM batches)
+    # per leaf forward = per simulation: totals over all dispatches / simulations (robust where
+    # several layers share one kernel name and grid, e.g. the three GEMM batches).  A simulation
+    # starts with select_kernel (a move's first) or expand_select_kernel (the previous one's
+    # expand / backup fused with this one's select: azg_sim_end_begin)
     tot = defaultdict(lambda: [0.0, 0.0, 0])
     for key in set(fetch) | set(write):
         g = group(key[0])
@@ -84,7 +86,7 @@ def main():
         tot[g][0] += 2 * sum(fetch.get(key, [])) * 1024
         tot[g][1] += sum(write.get(key, [])) * 1024
         tot[g][2] += max(len(fetch.get(key, [])), len(write.get(key, [])))
-    n_fwd = tot["select_kernel"][2] if "select_kernel" in tot else 0
+    n_fwd = sum(tot[g][2] for g in ("select_kernel", "expand_select_kernel") if g in tot)
     summary = {}
     for g, v in out.items():
         f, w, n = tot[g]
