@@ -3,12 +3,17 @@
 Self-play needs no communication (each game slot is independent and seeded by
 its global index, so results do not depend on the GPU count).  Once per
 iteration -- where the reference's Coach.learn (Coach.py:102-153) collects the
-iteration's examples and trains -- two collectives run over RCCL (backend
+iteration's examples and trains -- the records cross ranks over RCCL (backend
 "nccl" on ROCm) on xGMI:
 
-  * gather of every rank's compact move records to the trainer rank
-    (an all_reduce of the sizes, then gathers into the trainer only);
-  * broadcast of the trainer's weights (one flat f32 buffer, ~50 MB).
+  * with the data-parallel trainer (Coach.learn's default with several ranks,
+    ddp.py): an all-gather of every rank's compact move records, so every rank
+    builds the same examples; training then keeps the weights equal on every
+    rank (one gradient all-reduce per step), so no weight broadcast follows;
+  * with the single-rank trainer (args.distributedTrain "rank0"): a gather of
+    the records to the trainer rank (an all_reduce of the sizes, then gathers
+    into the trainer only) and, after training, a broadcast of the trainer's
+    weights (one flat f32 buffer, ~50 MB).
 
 A compact move record is (moves made, actions, root visit counts) per game:
 enough to rebuild every training example (Coach.py:74-90) by replaying the
@@ -223,8 +228,14 @@ def broadcast_weights(module, src=0, group=None):
     return nbytes
 
 
-def iteration_sync(engine, module, trainer=0, group=None):
-    """The per-iteration exchange of configs[3]: examples in, weights out."""
+def iteration_sync(engine, module, trainer=0, group=None, mode="ddp"):
+    """The per-iteration exchange of configs[3] as Coach.learn runs it: "ddp" (the default
+    with several ranks) all-gathers the records to every rank; "rank0" gathers them to the
+    trainer and broadcasts its weights.  Returns the bytes this rank sent."""
+    if mode == "ddp":
+        return gather_records(engine, dst=None, group=group)[1]
+    if mode != "rank0":
+        raise ValueError(f"unknown iteration_sync mode {mode!r}")
     _, sent = gather_records(engine, dst=trainer, group=group)
     wb = broadcast_weights(module, src=trainer, group=group)
     return sent + wb

@@ -475,7 +475,7 @@ def main():
         for _ in range(args.steps):
             step()
     sync_bytes = 0
-    if world > 1:  # per-iteration exchange: example gather to rank 0 + weight broadcast from rank 0
+    if world > 1:  # the per-iteration exchange of Coach.learn's data-parallel trainer: the records all-gathered
         sync_bytes = azg_dist.iteration_sync(eng, net)
     torch.cuda.synchronize()
     if world > 1:

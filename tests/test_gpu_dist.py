@@ -126,25 +126,29 @@ def _nccl_worker(port, q):
         m = int(mv.max())
         ok = (torch.equal(rec[0], mv) and torch.equal(rec[1], act[:, :m])
               and torch.equal(rec[2].to(torch.int32), cnt[:, :m]))
+        rec_all, _ = ad.gather_records(eng, dst=None)  # the all-gather of the data-parallel trainer
+        ok = ok and all(torch.equal(a, b) for a, b in zip(rec_all, rec))
         net = InflexionNNet(num_channels=16).cuda()
-        nb = ad.iteration_sync(eng, net)
+        nb = ad.iteration_sync(eng, net)  # "ddp": records only
+        nb_r0 = ad.iteration_sync(eng, net, mode="rank0")  # records + the weight broadcast
         eng.close()
-        q.put((ok, sent, nb))
+        q.put((ok, sent, (nb, nb_r0)))
     finally:
         dist.destroy_process_group()
 
 
 def test_rccl_single_rank_exchange():
     """The per-iteration exchange over the real RCCL backend (one rank: RCCL refuses two
-    ranks on one device): the gather of move records and the weight broadcast run through
-    ProcessGroupNCCL and return this rank's own records unchanged."""
+    ranks on one device): the gather and the all-gather of move records and the weight
+    broadcast run through ProcessGroupNCCL and return this rank's own records unchanged."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
     p.start()
     ok, sent, nb = q.get(timeout=300)
     p.join(timeout=60)
-    assert p.exitcode == 0 and ok and sent > 0 and nb > 0
+    assert p.exitcode == 0 and ok and sent > 0
+    assert nb[0] == sent and nb[1] > nb[0]
 
 
 def _overflow_worker(rank, world, port, q):
