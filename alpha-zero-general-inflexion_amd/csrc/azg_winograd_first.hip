@@ -9,13 +9,16 @@ extern "C" int azg_winograd_first_nchw(const float* planes, const float* w1, con
         c % 64 || bad_fmt(vfmt, overflow))
         return AZG_ERR_ARG;
     const dim3 grid((unsigned)(batch * (c / 64)));
+    // the boards' sides (6-8) have two tile rows for conv2 (pad 1): two waves per item
+    static_assert(WSeq(7).p == 2 && WSeq(8).p == 2 && WSeq(6).p == 2, "two tile rows");
+    const dim3 grid2((unsigned)(2 * batch * (c / 64)));
     const size_t lds_reg = 0, lds = (4 * 81 + (size_t)n * n * 64) * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
     const long long B = batch;
 #define AZG_FIRST(N, SP, L)                                                                                       \
     {                                                                                                             \
-        hipLaunchKernelGGL((winograd_first_kernel<N, SP>), grid, dim3(64), L, st, planes, w1, b1, V, depth, n, c, \
-                           B, overflow);                                                                          \
+        hipLaunchKernelGGL((winograd_first_kernel<N, SP, (N > 0 ? 2 : 1)>), N > 0 ? grid2 : grid, dim3(64), L, st, \
+                           planes, w1, b1, V, depth, n, c, B, overflow);                                          \
         return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                                 \
     }
 #define AZG_FIRST_FMT(N, L)                                          \

@@ -473,10 +473,12 @@ struct Plane {
 };
 
 // The next layer's input transform (pad PAD) of the lane's h x h plane: V out.  The
-// wave's lanes hold channels c0 + lane (c0 wave-uniform, a multiple of 64).
+// wave's lanes hold channels c0 + lane (c0 wave-uniform, a multiple of 64).  only_row >= 0:
+// only the tiles of that tile row (wave-uniform; the caller's waves split the rows).
 template <int HC, int FMT, int PAD, bool NT = false, class P>
 __device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, long long b, int c0, unsigned lane, int C,
-                                           long long B, void* __restrict__ Vout, int* overflow) {
+                                           long long B, void* __restrict__ Vout, int* overflow,
+                                           int only_row = -1) {
     const int h = HC > 0 ? HC : h_rt;
     const int c = c0 + (int)lane;
     const WSeq S(h + 2 * PAD - 2);
@@ -484,6 +486,7 @@ __device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, long long b, i
     bool bad = false;
     for_tiles<HO>(S, [&](auto A_, auto B_, int i, int j) {
         constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+        if (only_row >= 0 && i != only_row) return;
         const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
         const int y0 = S.off(i) - PAD, x0 = S.off(j) - PAD;
         float d[MA + 2][MB + 2];
@@ -632,12 +635,16 @@ __device__ __forceinline__ void conv1_sparse(const float* __restrict__ pb, const
 // The network's first two layers' front end in one pass: conv1 (depth -> C
 // channels, 3x3, pad 1) + bias + ReLU computed directly from the NCHW leaf
 // planes, then conv2's Winograd input transform (pad 1) -- conv1's activation
-// never leaves the chip.  One wave per (image, 64 output channels of conv1),
-// one channel per lane: with a compile-time side NC the planes are read as
-// wave-uniform scalars and conv1 runs as conv1_sparse, the lane's output plane in
-// registers; otherwise the image's planes are shared through LDS and each output
-// is gathered, the plane in the lane's own LDS column.
-template <int NC, int FMT>
+// never leaves the chip.  One wave per (image, 64 output channels of conv1,
+// tile row part of ROWS), one channel per lane: with a compile-time side NC the
+// planes are read as wave-uniform scalars and conv1 runs as conv1_sparse, the
+// lane's output plane in registers; otherwise the image's planes are shared
+// through LDS and each output is gathered, the plane in the lane's own LDS column.
+// ROWS = 2 (the boards' two tile rows): two waves per (image, channels), each
+// computing conv1 whole and storing one tile row's V: twice the (cheap, sparse)
+// conv1 work for half the stores per wave, measured 204 -> 175 us at 4096 leaves
+// and 18.8 -> 17.7 us at 256 (tools/first_probe.py).
+template <int NC, int FMT, int ROWS = 1>
 __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restrict__ planes,
                                                             const float* __restrict__ w1,
                                                             const float* __restrict__ b1, void* __restrict__ Vout,
@@ -648,9 +655,11 @@ __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restr
     const unsigned lane = threadIdx.x;
     const int cblocks = C / 64;
     // (blocks in dispatch order: the XCD-contiguous mapping of the mid kernels measured
-    // 7% slower here, where nothing is read back)
-    const long long b = blockIdx.x / cblocks;
-    const int k0 = (blockIdx.x % cblocks) * 64, k = k0 + (int)lane;
+    // 7% slower here, where nothing is read back; a (image, channels) item's ROWS waves adjacent)
+    const unsigned item = blockIdx.x / ROWS;
+    const int part = ROWS > 1 ? (int)(blockIdx.x % ROWS) : -1;
+    const long long b = item / cblocks;
+    const int k0 = (item % cblocks) * 64, k = k0 + (int)lane;
     const float bk = b1[k];
     Plane<NC> ys;
     if constexpr (NC > 0) {
@@ -691,7 +700,7 @@ __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restr
     // V2 goes out with non-temporal stores: nothing here reads it back, and the GEMM
     // reads it only after the whole grid (241 -> 209 us at 4096 leaves, DESIGN 6b,
     // profiles/r02_nt_store_probe)
-    plane_to_V<NC, FMT, 1, true>(ys, n, b, k0, lane, C, B, Vout, overflow);
+    plane_to_V<NC, FMT, 1, true>(ys, n, b, k0, lane, C, B, Vout, overflow, part);
 }
 
 // one thread per work item, rounded up to whole groups of 8 blocks (xcd_item)

@@ -49,7 +49,7 @@ def main():
         InflexionGame(7, max_turns=343, max_power=6)
     torch.manual_seed(0)
     w = NNetWrapper(game, device="cuda")
-    for form in a.forms.split(","):
+    for form in a.forms.replace("+", ",").split(","):  # ("+": tools/gpu.sh turns commas into spaces)
         fast = True
         if form.startswith("module"):  # the reference module itself (MCTS(fast=False))
             ev, graph, fast = w, form.endswith("graph"), False

@@ -36,7 +36,7 @@ __device__ __forceinline__ bool store_seg(unsigned short* rowp, unsigned lane, f
     }
 }
 
-template <int S, bool NT>
+template <int S, bool NT, int NPARTS = 2>
 __device__ __forceinline__ void plane_to_V_probe(const float (&ys)[49], long long b, int c0, unsigned lane, int C,
                                                  long long B, void* __restrict__ Vout, int* overflow, int only_row = -1) {
     constexpr int HO = 7;
@@ -44,7 +44,7 @@ __device__ __forceinline__ void plane_to_V_probe(const float (&ys)[49], long lon
     bool bad = false;
     for_tiles<HO>(Sq, [&](auto A_, auto B_, int i, int j) {
         constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
-        if (only_row >= 0 && i != only_row) return;  // (wave-uniform)
+        if (only_row >= 0 && (NPARTS == 2 ? i : i * 2 + j) != only_row) return;  // (wave-uniform)
         const long long row = Sq.row0(i, j, b, B), ps = Sq.pstride(i, j, B);
         const int y0 = Sq.off(i) - 1, x0 = Sq.off(j) - 1;
         float d[MA + 2][MB + 2];
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(64 * WPB) void first_probe_kernel(const float* __re
             float ys[49];
 #pragma unroll
             for (int q = 0; q < 49; ++q) ys[q] = fmaxf(acc[q] + bk, 0.f);
-            plane_to_V_probe<S, NT>(ys, b, k0, lane, C, B, Vout, overflow, half);
+            plane_to_V_probe<S, NT, HALVES>(ys, b, k0, lane, C, B, Vout, overflow, half);
         }
     };
     const long long it0 = (long long)blockIdx.x * WPB + w;
@@ -136,6 +136,10 @@ extern "C" int first_probe(int variant, const float* planes, const float* w1, co
         case 11: go(first_probe_kernel<0, 1, false, false>, 1, false); break;
         case 12: go(first_probe_kernel<0, 1, false, true, 2>, 1, false, 2); break;  // tile rows over 2 waves
         case 13: go(first_probe_kernel<1, 1, false, true, 2>, 1, false, 2); break;
+        case 14: go(first_probe_kernel<0, 4, false, true, 2>, 4, false, 2); break;
+        case 15: go(first_probe_kernel<0, 1, false, true, 4>, 1, false, 4); break;  // one tile per wave
+        case 16: go(first_probe_kernel<0, 4, false, true, 4>, 4, false, 4); break;
+        case 17: go(first_probe_kernel<0, 2, false, true, 2>, 2, false, 2); break;
         default: return AZG_ERR_ARG;
     }
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;

@@ -14,7 +14,9 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 NAMES = {0: "product", 1: "S0 wpb1", 2: "S1 wpb1", 3: "S0 wpb4", 4: "S1 wpb4", 5: "S0 wpb8", 6: "S1 wpb8",
          7: "S0 persist", 8: "S1 persist", 9: "S1 wpb4 persist", 10: "S1 wpb1 no-nt", 11: "S0 wpb1 no-nt",
-         12: "S0 tile rows over 2 waves", 13: "S1 tile rows over 2 waves"}
+         12: "S0 tile rows over 2 waves", 13: "S1 tile rows over 2 waves",
+         14: "S0 rows/2 waves, wpb4", 15: "S0 one tile per wave", 16: "S0 one tile per wave, wpb4",
+         17: "S0 rows/2 waves, wpb2"}
 
 
 def planes_like_leaves(B, n, gen):
@@ -45,7 +47,7 @@ def probe(B):
     V = torch.empty(B * 121 * 2 * C, dtype=torch.int16, device="cuda")
     ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
     st = vp(torch.cuda.current_stream().cuda_stream)
-    variants = [int(v) for v in os.environ.get("VARIANTS", ",".join(map(str, NAMES))).split(",")]
+    variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,3,5,12,14,15,16,17").split(",")]
     grid_waves = int(os.environ.get("GRID_WAVES", 0))
 
     def run(v):
