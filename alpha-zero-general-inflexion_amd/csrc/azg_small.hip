@@ -36,6 +36,7 @@
 #include <type_traits>
 
 #include "../../include/azg.h"
+#include "azg_conv1.h"
 
 namespace {
 
@@ -193,11 +194,16 @@ __global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restric
 constexpr int SK_CO = 8, SK_KG = 4;
 constexpr size_t SK_LDS = 96 * 1024;  // staged quarter input + weights + slice partials (n <= 8: <= 87 KB)
 
-// F1 (conv1 fused, conv2 only): x is then the NCHW leaf planes [B][D][H][H] (sB per leaf) and
-// the staged quarter is conv1's output for that quarter's channels, relu(b1 + conv1(planes)) with
-// w1 [Cin][3][3][D] (channels_last, BN folded) -- conv1's 36 products per output are recomputed
-// by each of the co groups' blocks instead of a launch of their own.
-template <int PXL, bool F1>
+// F1 > 0 (conv1 fused, conv2 only; F1 = the board side, 3..8): x is then the NCHW leaf planes
+// [B][D][F1][F1] (sB per leaf) and the staged quarter is conv1's output for that quarter's
+// channels, relu(b1 + conv1(planes)) with w1 [Cin][3][3][D] (channels_last, BN folded) --
+// computed by the block's first Cq / 64 waves, one channel per lane and the leaf's planes read as
+// wave-uniform scalars (conv1_sparse, azg_winograd_kern.h: constant planes one multiply-add per
+// output, 0/1 planes only their nonzero cells), instead of a launch of its own.
+// The block's weight quarter is loaded into registers first (SC_WPF float4 per thread) and
+// written to LDS once the leaf's input loads are in flight: one memory round trip for both.
+constexpr int SC_WPF = 5;  // 8 x 9 x 512 / 4 floats = 9216 = 4.5 x 2048 (Cin = 512)
+template <int PXL, int F1>
 __global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __restrict__ x, long long sB, int sY,
                                                              int sX, int B, int H, int pad,
                                                              const float* __restrict__ w, int Cin,
@@ -221,58 +227,73 @@ __global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __rest
     float* ws = xs + H * H * P;                 // [Kq][SK_CO]: k-major, the 8 channels of a k adjacent
     float* red = ws + Kq * SK_CO;               // [KSL][PXL][SK_CO]
     // the quarter's weights: w[co0 + c][tap][ci_base + ci] -> ws[(tap * Cq + ci) * 8 + c]
-    {
-        const int n4 = SK_CO * 9 * (Cq / 4);
-        for (int i = tid; i < n4; i += SC_T) {
-            const int c = i / (9 * (Cq / 4)), r = i - c * 9 * (Cq / 4), tap = r / (Cq / 4), ci = (r - tap * (Cq / 4)) * 4;
-            const float4 v = *(const float4*)(w + ((long long)(co0 + c) * 9 + tap) * Cin + ci_base + ci);
-            float* d = ws + (tap * Cq + ci) * SK_CO + c;
-            d[0] = v.x;
-            d[SK_CO] = v.y;
-            d[2 * SK_CO] = v.z;
-            d[3 * SK_CO] = v.w;
+    const int q4 = Cq / 4, nw4 = SK_CO * 9 * q4;
+    auto wload = [&](int i) {
+        const int c = i / (9 * q4), r = i - c * 9 * q4, tap = r / q4, ci = (r - tap * q4) * 4;
+        return *(const float4*)(w + ((long long)(co0 + c) * 9 + tap) * Cin + ci_base + ci);
+    };
+    auto wstore = [&](int i, float4 v) {
+        const int c = i / (9 * q4), r = i - c * 9 * q4, tap = r / q4, ci = (r - tap * q4) * 4;
+        float* d = ws + (tap * Cq + ci) * SK_CO + c;
+        d[0] = v.x;
+        d[SK_CO] = v.y;
+        d[2 * SK_CO] = v.z;
+        d[3 * SK_CO] = v.w;
+    };
+    float4 wpf[F1 > 0 ? 1 : SC_WPF];  // (conv12: the waves that compute no conv1 stage the weights)
+    if constexpr (F1 == 0) {
+#pragma unroll
+        for (int u = 0; u < SC_WPF; ++u) {
+            const int i = tid + u * SC_T;
+            if (i < nw4) wpf[u] = wload(i);
         }
     }
+    bool w_staged = F1 > 0;
+    auto stage_w = [&]() {  // (block-uniform)
+        if (w_staged) return;
+#pragma unroll
+        for (int u = 0; u < SC_WPF; ++u) {
+            const int i = tid + u * SC_T;
+            if (i < nw4) wstore(i, wpf[u]);
+        }
+        for (int i = tid + SC_WPF * SC_T; i < nw4; i += SC_T) wstore(i, wload(i));
+        w_staged = true;
+    };
     int oy = 0, ox = 0;
     if (p < hw) oy = p / Ho, ox = p - (p / Ho) * Ho;
     const int KS = Kq / 4;  // float4 steps
     const int per = (KS + KSL - 1) / KSL;
     const int k0 = s * per, k1 = min(KS, k0 + per);
     for (int b = 0; b < B; ++b) {
-        if constexpr (F1) {
-            // conv1 (pad 1) for the quarter's channels from the leaf planes: thread (c, g) keeps
-            // channel c's 9 D weights in registers and computes every 4th pixel from g; the
-            // planes (staged in the partials' area, free until the multiply-adds) are the same
-            // for the whole wave
-            float* pl = red;
-            for (int i = tid; i < D * H * H; i += SC_T) pl[i] = x[b * sB + i];
-            __syncthreads();
-            const int c = tid % Cq, g = tid / Cq, G1 = SC_T / Cq;
-            if (g < G1) {
-                float wr[36];
-                const float* __restrict__ wc = w1 + (long long)(ci_base + c) * 9 * D;
-#pragma unroll
-                for (int t = 0; t < 9; ++t)
-#pragma unroll
-                    for (int d = 0; d < 4; ++d) wr[t * 4 + d] = d < D ? wc[t * D + d] : 0.f;
+        if constexpr (F1 > 0) {
+            constexpr int NN = F1 * F1;
+            const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+            const unsigned lane = tid & 63;
+            const int nconv = (Cq + 63) / 64;  // conv1 waves; the others stage the weights (first leaf)
+            if (wv < nconv) {
+                const int c = min(wv * 64 + (int)lane, Cq - 1);  // (lanes past the quarter: a duplicate, not stored)
+                float acc1[NN];
+                conv1_sparse<F1>(x + b * sB, w1 + (long long)(ci_base + c) * 9 * D, D, lane, acc1, 1, D);
                 const float bc = b1[ci_base + c];
-                for (int pix = g; pix < H * H; pix += G1) {
-                    const int iy = pix / H, ix = pix - iy * H;
-                    float a = 0.f;
+                if (wv * 64 + (int)lane < Cq) {
 #pragma unroll
-                    for (int t = 0; t < 9; ++t) {
-                        const int yy = iy + t / 3 - 1, xx = ix + t % 3 - 1;
-                        if (yy < 0 || yy >= H || xx < 0 || xx >= H) continue;
+                    for (int q = 0; q < NN; ++q) xs[q * P + c] = fmaxf(acc1[q] + bc, 0.f);
+                }
+            } else if (b == 0) {
+                constexpr int U = 6;
+                const int t0 = tid - nconv * 64, nst = SC_T - nconv * 64;
+                for (int i0 = t0; i0 < nw4; i0 += nst * U) {
+                    float4 r[U];
 #pragma unroll
-                        for (int d = 0; d < 4; ++d)
-                            if (d < D) a = fmaf(wr[t * 4 + d], pl[(d * H + yy) * H + xx], a);
-                    }
-                    xs[pix * P + c] = fmaxf(a + bc, 0.f);
+                    for (int u = 0; u < U; ++u) r[u] = wload(min(i0 + u * nst, nw4 - 1));
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (i0 + u * nst < nw4) wstore(i0 + u * nst, r[u]);
                 }
             }
         }
         const float* __restrict__ xb = x + b * sB + ci_base;
-        const int c4 = Cq / 4, n4 = F1 ? 0 : H * H * c4;
+        const int c4 = Cq / 4, n4 = F1 > 0 ? 0 : H * H * c4;
         for (int base = tid; base < n4; base += SC_T * SC_UNR) {
             float4 r[SC_UNR];
 #pragma unroll
@@ -281,6 +302,7 @@ __global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __rest
                 const int pix = i / c4, c = (i - pix * c4) * 4, iy = pix / H, ix = pix - iy * H;
                 r[u] = *(const float4*)(xb + (long long)iy * sY + (long long)ix * sX + c);
             }
+            stage_w();  // the weights' stores once the first input loads are in flight
 #pragma unroll
             for (int u = 0; u < SC_UNR; ++u) {
                 const int i = base + u * SC_T;
@@ -290,6 +312,7 @@ __global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __rest
                 }
             }
         }
+        stage_w();
         __syncthreads();
         float acc[SK_CO];
 #pragma unroll
@@ -499,7 +522,7 @@ int launch_conv(dim3 grid, hipStream_t st, const float* x, long long sB, int sY,
     return 0;
 }
 
-template <int PXL, bool F1 = false>
+template <int PXL, int F1 = 0>
 void launch_conv_sk(hipStream_t st, const float* x, long long sB, int sY, int sX, int B, int H, int pad,
                     const float* w, int Cin, int Cout, const float* bias, int relu, float* y, int ldy, float* work,
                     unsigned* tickets, const float* w1 = nullptr, const float* b1 = nullptr, int D = 0) {
@@ -525,7 +548,9 @@ extern "C" int azg_small_conv3x3(const float* x, int64_t sB, int32_t sY, int32_t
     // the split-K form (8 channels x a quarter of the input channels per block, quarters combined
     // by the last block of each group) when the workspace holds the partials and the tickets
     const long long need = (long long)SK_KG * Cout * batch * n;
-    const bool sk = vec && Cin % (4 * SK_KG) == 0 && Cout % SK_CO == 0 && work && tickets &&
+    // (not for <= 16 output pixels, conv4: there the combine's round trips cost more than the
+    // 2-channel form's longer K loop, 13.0-13.3 vs 11.4-11.9 us at one leaf, tools/small_layer_bench.py)
+    const bool sk = n > 16 && vec && Cin % (4 * SK_KG) == 0 && Cout % SK_CO == 0 && work && tickets &&
                     work_floats >= need && n_tickets >= Cout / SK_CO && ((uintptr_t)work & 15) == 0 &&
                     (size_t)H * H * (Cin / SK_KG + 4) * 4 + (size_t)9 * Cin / SK_KG * SK_CO * 4 +
                             (size_t)SC_T * SK_CO * 4 <= SK_LDS;
@@ -558,17 +583,23 @@ extern "C" int azg_small_conv12(const float* planes, int32_t batch, int32_t dept
                                 float* work, int64_t work_floats, uint32_t* tickets, int32_t n_tickets, void* stream) {
     const int hw = n * n;
     if (!planes || !w1 || !b1 || !w2 || !y || !work || !tickets || batch <= 0 || batch > 4 || depth < 1 || depth > 4 ||
-        n < 3 || n > 8 || C <= 0 || C % (4 * SK_KG) || C % SK_CO || ldy < C ||
+        n < 6 || n > 8 || C <= 0 || C % (4 * SK_KG) || C % SK_CO || ldy < C ||
         work_floats < (long long)SK_KG * C * batch * hw || n_tickets < C / SK_CO || ((uintptr_t)w2 & 15) ||
         ((uintptr_t)work & 15) ||
         (size_t)hw * (C / SK_KG + 4) * 4 + (size_t)9 * C / SK_KG * SK_CO * 4 + (size_t)SC_T * SK_CO * 4 > SK_LDS)
         return AZG_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     const long long sB = (long long)depth * hw;
-    if (hw <= 64)
-        launch_conv_sk<64, true>(st, planes, sB, 0, 0, batch, n, 1, w2, C, C, b2, 1, y, ldy, work, tickets, w1, b1, depth);
-    else
-        return AZG_ERR_ARG;
+    auto go = [&](auto N_) {
+        launch_conv_sk<64, decltype(N_)::value>(st, planes, sB, 0, 0, batch, n, 1, w2, C, C, b2, 1, y, ldy, work,
+                                                tickets, w1, b1, depth);
+    };
+    switch (n) {  // the boards' sides: conv1's output plane in registers (conv1_sparse)
+        case 6: go(std::integral_constant<int, 6>{}); break;
+        case 7: go(std::integral_constant<int, 7>{}); break;
+        case 8: go(std::integral_constant<int, 8>{}); break;
+        default: return AZG_ERR_ARG;
+    }
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 

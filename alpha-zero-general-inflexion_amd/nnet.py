@@ -714,7 +714,7 @@ class InferenceNet(nn.Module):
         work, tickets = self._small_work, self._small_tickets
         wp, tp = ctypes.c_void_p(work.data_ptr()), ctypes.c_void_p(tickets.data_ptr())
         first = 1
-        if self.depth <= 4 and 3 <= n <= 8 and C % 16 == 0 and self.pads[:2] == [1, 1] \
+        if self.depth <= 4 and 6 <= n <= 8 and C % 16 == 0 and self.pads[:2] == [1, 1] \
                 and n * n * (C // 4 + 4) * 4 + 72 * C + 16384 <= 96 * 1024:  # azg_small_conv12's LDS
             # conv1 + conv2 in one launch
             y = torch.empty((B * n * n, C), device=dev, dtype=torch.float32)

@@ -265,7 +265,7 @@ int  azg_small_fc(const float* x, int32_t ldx, int32_t batch, const float* w, in
                   int32_t relu, float* y, int32_t ldy, void* stream);
 /* conv1 + conv2 at one to four leaves in one launch (the split-K form of azg_small_conv3x3, each
  * block computing relu(b1 + conv1(planes)) for its quarter of conv2's input channels itself):
- * planes [batch][depth][n][n] f32 (depth <= 4, 3 <= n <= 8), w1 [C][3][3][depth], w2 [C][3][3][C]
+ * planes [batch][depth][n][n] f32 (depth <= 4, the boards' sides 6 <= n <= 8), w1 [C][3][3][depth], w2 [C][3][3][C]
  * (channels_last, BN folded), y[px * ldy + co] = relu(b2 + conv2(...)) for the n x n outputs;
  * C % 16 == 0, work / tickets as azg_small_conv3x3's split-K form. */
 int  azg_small_conv12(const float* planes, int32_t batch, int32_t depth, int32_t n, const float* w1, const float* b1,

@@ -555,11 +555,11 @@ def test_small_fc_matches_torch(B, K, N, relu, bias):
 
 
 @pytest.mark.parametrize("B,depth,n,C", [(1, 4, 7, 512), (4, 4, 7, 512), (2, 2, 6, 512), (3, 2, 8, 512),
-                                         (1, 1, 3, 16), (4, 3, 5, 64), (2, 4, 8, 32)])
+                                         (1, 1, 6, 16), (4, 3, 7, 64), (2, 4, 8, 32), (1, 4, 6, 512)])
 def test_small_conv12_matches_torch(B, depth, n, C):
     """azg_small_conv12 (conv1 + conv2 in one launch, each split-K block recomputing conv1 for its
     quarter of conv2's input channels): relu(conv2(relu(conv1(planes)))) against torch in f64,
-    padded 3x3 convs, 1-4 planes, boards 3..8, the tickets left at zero."""
+    padded 3x3 convs, 1-4 planes (0/1 and dense), the boards' sides 6..8, the tickets left at zero."""
     import ctypes
     import azg_amd  # noqa: F401
     from azg_amd import _lib
@@ -634,6 +634,7 @@ def test_small_kernels_reject_bad_arguments():
     assert L.azg_small_fc(P, 62, 1, P, 62, 8, None, 1, P, 8, st) == -1  # K % 4
     assert L.azg_small_conv12(P, 1, 5, 7, P, P, P, P, 512, P, 512, P, 1 << 20, P, 64, st) == -1  # depth 5
     assert L.azg_small_conv12(P, 1, 4, 9, P, P, P, P, 512, P, 512, P, 1 << 20, P, 64, st) == -1  # n 9
+    assert L.azg_small_conv12(P, 1, 4, 5, P, P, P, P, 512, P, 512, P, 1 << 20, P, 64, st) == -1  # n 5
     assert L.azg_small_conv12(P, 1, 4, 7, P, P, P, P, 520, P, 520, P, 1 << 20, P, 65, st) == -1  # C % 16
     assert L.azg_small_heads(P, 64, 1, P, 64, 1024, P, P, P, P, P, st) == -1  # A > 1023
     assert L.azg_small_heads(P, 64, 5, P, 64, 8, P, P, P, P, P, st) == -1  # batch 5

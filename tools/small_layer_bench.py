@@ -49,13 +49,15 @@ def main():
         work = torch.empty(4 * cout * B * Ho * Ho, device="cuda")
         tickets = torch.zeros(cout // 8, device="cuda", dtype=torch.int32)
 
-        def azg():
+        def azg(sk=True):
             if taps == 9:
                 _lib.check(L.azg_small_conv3x3(ctypes.c_void_p(xin.data_ptr()), *strides, B, H, pad,
                                                ctypes.c_void_p(wk.data_ptr()), cin, cout,
                                                ctypes.c_void_p(b.data_ptr()), 1, ctypes.c_void_p(y.data_ptr()), cout,
-                                               ctypes.c_void_p(work.data_ptr()), work.numel(),
-                                               ctypes.c_void_p(tickets.data_ptr()), tickets.numel(), st))
+                                               ctypes.c_void_p(work.data_ptr()) if sk else None,
+                                               work.numel() if sk else 0,
+                                               ctypes.c_void_p(tickets.data_ptr()) if sk else None,
+                                               tickets.numel() if sk else 0, st))
             else:
                 _lib.check(L.azg_small_fc(ctypes.c_void_p(xin.data_ptr()), cin, B, ctypes.c_void_p(wk.data_ptr()),
                                           cin, cout, ctypes.c_void_p(b.data_ptr()), 1,
@@ -71,15 +73,20 @@ def main():
 
             def lib():
                 torch.relu_(torch.addmm(b, xr, w.t()))
-        for f in (azg, lib):
+        arms = [("azg", azg), ("lib", lib)]
+        if taps == 9:  # the one-block-per-2-channels form (no split-K combine)
+            arms.append(("azg_nosk", lambda: azg(False)))
+        for _, f in arms:
             for _ in range(5):
                 f()
-        ts = {"azg": [], "lib": []}
+        ts = {k: [] for k, _ in arms}
         for r in range(7):
-            for k, f in (("azg", azg), ("lib", lib)) if r % 2 == 0 else (("lib", lib), ("azg", azg)):
+            for k, f in (arms if r % 2 == 0 else arms[::-1]):
                 ts[k].append(timeit(f))
-        print(json.dumps({"layer": name, "B": B, "azg_us": sorted(ts["azg"])[3],
-                          "torch_us": sorted(ts["lib"])[3]}), flush=True)
+        out = {"layer": name, "B": B, "azg_us": sorted(ts["azg"])[3], "torch_us": sorted(ts["lib"])[3]}
+        if "azg_nosk" in ts:
+            out["azg_nosk_us"] = sorted(ts["azg_nosk"])[3]
+        print(json.dumps(out), flush=True)
     fused(L, st)
 
 
