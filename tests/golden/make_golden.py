@@ -24,6 +24,7 @@ Fixtures written (all small, gzip'd JSON or npz):
   arena_<set>.json.gz    Arena.playGame MCTSPlayer(stubnet) vs Random/Greedy players
   nnet_golden.npz        InflexionNNet(manual_seed 0) checksum + (planes -> P, v)
   train_golden.json.gz   NNetWrapper.train (32 channels, 2 epochs): losses + weight digests
+  train_full_golden.json.gz  the same at 512 channels, 1 epoch (2 steps), dropout 0, + digests after step 1
   realnet_sensitivity.json.gz  first divergent move of the reference's real-net traces when its network's
                          weights, or its outputs, move by 1e-7 / 1e-6 relative
   realnet_branches.json.gz     the perturbed reference's traces past those divergent moves
@@ -712,6 +713,76 @@ def gen_train(np):
     _dump("train_golden.json.gz", out)
 
 
+TRAIN_FULL_CFG = dict(TRAIN_CFG, num_channels=512, epochs=1)
+
+
+def gen_train_full(np):
+    """The reference trainer at the real network's size (512 channels, NNet.py:13-22), dropout 0,
+    one epoch over the same episode's examples (2 batches of 512: 2 Adam steps): every batch's
+    (l_pi, l_v) and digests of the weights after the first step (taken in the second batch's
+    loss, before its update) and after training.  torch's default threads (the GPU test compares
+    within a tolerance)."""
+    import torch
+    import MCTS as mcts_mod
+    from Coach import Coach
+    from inflexion.InflexionGame import InflexionGame
+    import inflexion.pytorch.NNet as nn_mod
+    from inflexion.pytorch.NNet import NNetWrapper
+    from utils import dotdict
+    from stubnet import stub_eval
+    c = TRAIN_FULL_CFG
+
+    class StubNNet(NNetWrapper):
+        def __init__(self, game):
+            self.n_actions = game.max_actions
+
+        def predict(self, board):
+            return stub_eval(board, self.n_actions)
+
+    class RecNNet(NNetWrapper):
+        losses = []
+        step1 = None
+
+        def loss_pi(self, targets, outputs):
+            lp = super().loss_pi(targets, outputs)
+            self.losses.append([float(lp.item()), None])
+            if len(self.losses) == 2:  # the weights after the first Adam step
+                RecNNet.step1 = state_digest(np, self.nnet.state_dict(), c["proj_seed"])
+            return lp
+
+        def loss_v(self, targets, outputs):
+            lv = super().loss_v(targets, outputs)
+            self.losses[-1][1] = float(lv.item())
+            return lv
+
+    game = InflexionGame(7, max_turns=c["max_turns"], max_power=6)
+    args = dotdict({"numMCTSSims": c["sims"], "cpuct": c["cpuct"], "tempThreshold": c["temp_threshold"]})
+    stub = StubNNet(game)
+    np.random.seed(c["seed"])
+    ex = Coach(game, stub, args).executeEpisode((game.restarted(), mcts_mod.MCTS(stub, args)))
+    saved = dict(nn_mod.args)
+    out = {"config": c, "n_examples": len(ex), "runs": {}}
+    try:
+        nn_mod.args.num_channels = c["num_channels"]
+        nn_mod.args.epochs = c["epochs"]
+        nn_mod.args.dropout = 0.0
+        torch.manual_seed(c["init_seed"])
+        w = RecNNet(game)
+        init = state_digest(np, w.nnet.state_dict(), c["proj_seed"])
+        RecNNet.losses = []
+        np.random.seed(c["batch_seed"])
+        torch.manual_seed(c["torch_seed"])
+        w.train(ex)
+        out["runs"]["nodropout"] = {"dropout": 0.0, "init": init, "losses": RecNNet.losses, "step1": RecNNet.step1,
+                                    "final": state_digest(np, w.nnet.state_dict(), c["proj_seed"]),
+                                    "rng_pos": int(np.random.get_state()[2])}
+        print(f"  train_full: {len(RecNNet.losses)} steps, losses {RecNNet.losses}", flush=True)
+    finally:
+        nn_mod.args.clear()
+        nn_mod.args.update(saved)
+    _dump("train_full_golden.json.gz", out)
+
+
 def main():
     _need_reference()
     import numpy as np
@@ -733,6 +804,7 @@ def main():
         "realnet_toy": lambda: gen_mcts(np, quick, toy=True, realnet=True),
         "arena": lambda: gen_arena(np),
         "train": lambda: gen_train(np),
+        "train_full": lambda: gen_train_full(np),
         "sensitivity": lambda: gen_realnet_sensitivity(np),
         "sensitivity_othello": lambda: gen_realnet_sensitivity(np, othello=True),
         "branches": lambda: gen_realnet_branches(np),

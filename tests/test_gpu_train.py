@@ -70,3 +70,56 @@ def test_trainer_gpu_within_tolerance(path):
         d_ref = np.array(r["final"][k]["proj"]) - np.array(r["init"][k]["proj"])
         d_gpu = final[k] - init[k]
         np.testing.assert_allclose(d_gpu, d_ref, rtol=5e-2, atol=5e-2 * float(np.abs(d_ref).max()), err_msg=k)
+
+
+@pytest.mark.parametrize("path", ["train", "train_examples"])
+def test_trainer_gpu_full_size(path):
+    """The real network's size (512 channels, InflexionNNet as NNet.py builds it) against the
+    reference trainer's full-size fixture (tests/golden/make_golden.py train_full: dropout 0, one
+    epoch = 2 Adam steps over the same episode's examples).  After ONE step Adam's noise has not
+    compounded yet, so the tolerances are tight: both batches' losses within 2e-5 relative, and the
+    first step's update of every weight matrix whose gradient no BatchNorm cancels (conv2-4,
+    fc1-3) within 2e-3 of its size, 2e-2 after the second step.  (Measured on MI355X: see the
+    assertion messages; the BatchNorm-cancelled biases take sign-random +-lr steps, as in the
+    32-channel test above.)"""
+    import azg_amd  # noqa: F401
+    from azg_amd.examples import ExampleSet
+    from azg_amd.nnet import NNetWrapper
+    from test_train_golden import reference_examples
+
+    g = ol.load_json("train_full_golden.json.gz")
+    c, r = g["config"], g["runs"]["nodropout"]
+    game, ex = reference_examples(c)
+    assert len(ex) == g["n_examples"]
+    torch.manual_seed(c["init_seed"])
+    w = NNetWrapper(game, dict(num_channels=c["num_channels"], epochs=c["epochs"], dropout=0.0), device="cuda")
+    init = _proj(w.nnet.state_dict(), c["proj_seed"])
+    for k in init:
+        np.testing.assert_allclose(init[k], r["init"][k]["proj"], rtol=1e-12, atol=1e-9, err_msg=f"initial {k}")
+    seen = {}
+
+    def hook(mod, inp):  # the weights after the first step, at the second batch's forward
+        seen["n"] = seen.get("n", 0) + 1
+        if seen["n"] == 2:
+            seen["step1"] = _proj(mod.state_dict(), c["proj_seed"])
+    h = w.nnet.register_forward_pre_hook(hook)
+    np.random.seed(c["batch_seed"])
+    torch.manual_seed(c["torch_seed"])
+    try:
+        if path == "train":
+            w.train(ex)
+            losses = None
+        else:
+            losses = w.train_examples(ExampleSet.from_list(ex, "cuda")).cpu().numpy().astype(np.float64)
+    finally:
+        h.remove()
+    assert int(np.random.get_state()[2]) == r["rng_pos"]
+    if losses is not None:
+        np.testing.assert_allclose(losses, np.array(r["losses"]), rtol=2e-5)
+    final = _proj(w.nnet.state_dict(), c["proj_seed"])
+    for k in ("conv2.weight", "conv3.weight", "conv4.weight", "fc1.weight", "fc2.weight", "fc3.weight"):
+        for name, got, tol in (("step1", seen["step1"], 2e-3), ("final", final, 2e-2)):
+            d_ref = np.array(r[name][k]["proj"]) - np.array(r["init"][k]["proj"])
+            d_gpu = got[k] - init[k]
+            err = float(np.abs(d_gpu - d_ref).max() / np.abs(d_ref).max())
+            assert err < tol, f"{k} after {name}: update off by {err:.2e} of its size"
