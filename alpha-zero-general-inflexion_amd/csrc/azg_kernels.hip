@@ -645,22 +645,43 @@ __device__ __forceinline__ void set_err(const Dev& E, int g, int code) {
 }
 
 // --------------------------------------------------------------- kernels
+// What a descent reads before its first tree access and no expansion / backup writes
+// (slot state, root position, the next random words): loaded together, and in the
+// fused expand_select kernel before the expansion, so none of it waits behind the
+// backup's round trips (the drop-in's one-game search is a chain of dependent loads).
+template <class R>
+struct SelPre {
+    int active, searcher;
+    Pos root;
+    BlockRng rg;
+};
+template <class R>
+__device__ __forceinline__ SelPre<R> select_prefetch(const Dev& E) {
+    __shared__ uint32_t s_mt[MT_N];
+    const int g = blockIdx.x;
+    SelPre<R> q;
+    q.active = E.active[g];
+    q.searcher = E.searcher[g];
+    q.root = load_root<R>(E, g);
+    q.rg = rng_open(E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt);  // the slot's next random words
+    return q;
+}
+
 // sim_begin: MCTS.search down to a leaf (MCTS.py:83-132), writing the leaf's
 // randomly symmetrised planes (MCTS.py:91-92) as f32 into the NN batch.
 template <class R>
-__device__ __forceinline__ void select_body(const Dev& E, float* __restrict__ planes) {
-    __shared__ uint32_t s_mt[MT_N];
+__device__ __forceinline__ void select_body(const Dev& E, float* __restrict__ planes, SelPre<R>& q) {
     const int g = blockIdx.x, lane = lane_id();
     float* out = planes + (size_t)g * R::PLANES * R::CELLS;
-    if (!E.active[g] || E.err[g] || !searching(E, g)) {
+    // (searching(): searcher 0 = self-play, else the searcher's colour to move)
+    if (!q.active || E.err[g] || !(q.searcher == 0 || q.searcher == q.root.player)) {
         for (int i = lane; i < R::PLANES * R::CELLS; i += WAVE) out[i] = 0.0f;
         if (lane == 0) E.leaf_kind[g] = LEAF_NONE;
         return;
     }
-    // the slot's next random words, fetched while the tree is walked
-    BlockRng rg = rng_open(E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt);
+    BlockRng& rg = q.rg;
     const int root_id = E.root_id[g];
-    Pos p = load_root<R>(E, g);
+    Pos p = q.root;
     int depth = 0, kind = LEAF_NONE, slot = -1, cs = 0, kt = 0;
     uint64_t own = 0, opp = 0;
     double tval = 0.0;
@@ -751,15 +772,30 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
     __shared__ float s_acc[WAVE];
     __shared__ float s_leaf[16];
     const int g = blockIdx.x, lane = lane_id();
+    // Every per-slot field the expansion and the backup read, the path entries and the
+    // leaf's P row and v are loaded before the first branch on any of them: one memory
+    // round trip instead of a chain (kind, then depth, then the path, ...).
     const int kind = E.leaf_kind[g];
+    const int depth = E.leaf_depth[g];
+    const int32_t* path = E.path + (size_t)g * E.DMAX;
+    const int pk = lane < E.DMAX ? path[lane] : 0;
+    const int top_ld = E.free_top[g];
+    const uint64_t l_own = E.leaf_own[g], l_opp = E.leaf_opp[g];
+    const int l_cs = E.leaf_cs[g], l_kt = E.leaf_turn[g], l_slot = E.leaf_slot[g];
+    const double l_value = E.leaf_value[g];
+    const float l_v = vin[g];
+    float praw[R::AJ];
+#pragma unroll
+    for (int j = 0; j < R::AJ; ++j) {
+        const int a = lane + WAVE * j;
+        praw[j] = a < R::A ? Pin[(size_t)g * p_stride + a] : 0.0f;
+    }
     if (kind == LEAF_NONE) return;
     // Everything the backup reads (path entry, edge N and Q; one level per lane) and
     // the free-stack top are fetched up front, so they travel with the leaf's P
     // row instead of after the expansion (the path's edges are never the new node).
-    const int depth = E.leaf_depth[g];
-    const int32_t* path = E.path + (size_t)g * E.DMAX;
-    const int packed0 = lane < depth ? path[lane] : 0;
-    const int top0 = kind == LEAF_EXPAND ? E.free_top[g] : 0;
+    const int packed0 = lane < depth ? pk : 0;
+    const int top0 = kind == LEAF_EXPAND ? top_ld : 0;
     uint32_t nr0 = 0u;
     float qf0 = 0.0f;
     if (lane < depth) {
@@ -770,8 +806,8 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
     double ret;
     bool ret_f32;
     if (kind == LEAF_EXPAND) {
-        const uint64_t own = E.leaf_own[g], opp = E.leaf_opp[g];
-        const int cs = E.leaf_cs[g], kt = E.leaf_turn[g];
+        const uint64_t own = l_own, opp = l_opp;
+        const int cs = l_cs, kt = l_kt;
         const typename R::VCtx vc = R::vctx(own, opp, cs);
         float pv[R::AJ];
         bool vv[R::AJ];
@@ -781,7 +817,7 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
         for (int j = 0; j < R::AJ; ++j) {
             const int a = lane + WAVE * j;
             vv[j] = ci[j] >= 0;
-            float x = a < R::A ? Pin[(size_t)g * p_stride + a] : 0.0f;
+            float x = praw[j];
             x = vv[j] ? x : x * 0.0f;  // policies *= valids
             pv[j] = x;
             s_p[a] = x;
@@ -834,13 +870,13 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
             E.node_key[ni] = NodeKey{own, opp, kt, cs, 0, 0};
             E.node_turn[ni] = kt;
             const uint64_t h = key_hash(own, opp, kt, cs);
-            E.table[(size_t)g * E.H + E.leaf_slot[g]] = ((h >> 32) << 32) | (uint64_t)(uint32_t)(id + 1);
+            E.table[(size_t)g * E.H + l_slot] = ((h >> 32) << 32) | (uint64_t)(uint32_t)(id + 1);
             E.st_exp[g] += 1;
         }
-        ret = -(double)vin[g];  // `return -v`, a float32 array (MCTS.py:112)
+        ret = -(double)l_v;  // `return -v`, a float32 array (MCTS.py:112)
         ret_f32 = true;
     } else {
-        ret = E.leaf_value[g];  // Python number (MCTS.py:87)
+        ret = l_value;  // Python number (MCTS.py:87)
         ret_f32 = false;
         if (lane == 0) E.st_term[g] += 1;
     }
@@ -878,7 +914,8 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
 
 template <class R>
 __global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__ planes) {
-    select_body<R>(E, planes);
+    SelPre<R> q = select_prefetch<R>(E);
+    select_body<R>(E, planes, q);
 }
 
 template <class R>
@@ -895,9 +932,10 @@ template <class R>
 __global__ __launch_bounds__(WAVE) void expand_select_kernel(Dev E, const float* __restrict__ Pin, int p_stride,
                                                              const float* __restrict__ vin,
                                                              float* __restrict__ planes) {
+    SelPre<R> q = select_prefetch<R>(E);  // (nothing the expansion writes)
     expand_backup_body<R>(E, Pin, p_stride, vin);
     __syncthreads();
-    select_body<R>(E, planes);
+    select_body<R>(E, planes, q);
 }
 
 // move_end: MCTS.getActionProb root policy (MCTS.py:48-60), Coach.executeEpisode
