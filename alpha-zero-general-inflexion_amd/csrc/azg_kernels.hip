@@ -544,6 +544,8 @@ __device__ __forceinline__ Pos load_root(const Dev& E, int g) {
 
 // Wave-cooperative open-addressing lookup: 64 consecutive slots per probe.
 // Returns node id or -1 (then *slot = first empty slot in probe order).
+__device__ int table_lookup(const Dev& E, int g, uint64_t own, uint64_t opp, int turn, int cs, int* slot);
+
 __device__ int table_lookup(const Dev& E, int g, uint64_t own, uint64_t opp, int turn, int cs, int* slot) {
     const int lane = lane_id();
     const uint64_t h = key_hash(own, opp, turn, cs);
@@ -579,31 +581,93 @@ __device__ int table_lookup(const Dev& E, int g, uint64_t own, uint64_t opp, int
     return -1;
 }
 
+// A node's edges as the PUCT scan reads them: the lane's compact slots, P, N and the
+// f32 Q per valid action, and the node's visit count.  Loaded together (one round trip),
+// and by the descent below the root together with the node's key check.
+template <class R>
+struct EdgeRow {
+    int ci[R::AJ];
+    float P[R::AJ], Qf[R::AJ];
+    uint32_t N[R::AJ];
+    int Ns;
+};
+template <class R>
+__device__ __forceinline__ void load_edges(const Dev& E, int g, int id, const typename R::VCtx& vc, EdgeRow<R>& er) {
+    const size_t row = node_row<R>(E, g, id);
+    er.Ns = E.node_key[(size_t)g * E.M + id].Ns;
+    edge_slots<R>(vc, er.ci);
+#pragma unroll
+    for (int j = 0; j < R::AJ; ++j) {
+        // the f32 Q loaded with P and N (not after N says the edge exists): one
+        // dependent round trip less per level; used only where N > 0
+        if (er.ci[j] >= 0) {
+            er.P[j] = E.node_P[row + er.ci[j]];
+            er.N[j] = E.node_N[row + er.ci[j]];
+            er.Qf[j] = E.node_Qf[row + er.ci[j]];
+        }
+    }
+}
+
+// The descent's lookup below the root: the first probe's slots, then -- for the first
+// slot whose tag matches, if no empty slot comes before it -- the node's key check and its
+// edges in ONE round trip (the edges speculatively: a tag match is almost always the node).
+// Same result as table_lookup (+ load_edges when found): a key that does not match, or no
+// decision in the first probe, falls back to table_lookup.
+template <class R>
+__device__ int lookup_with_edges(const Dev& E, int g, uint64_t own, uint64_t opp, int turn, int cs, int* slot,
+                                 const typename R::VCtx& vc, EdgeRow<R>& er) {
+    const int lane = lane_id();
+    const uint64_t h = key_hash(own, opp, turn, cs);
+    const uint32_t tag = (uint32_t)(h >> 32);
+    const uint64_t* T = E.table + (size_t)g * E.H;
+    const uint32_t hm = (uint32_t)E.H - 1;
+    const uint32_t base = (uint32_t)h & hm;
+    constexpr int W = 16;  // table_lookup's first probe
+    const bool in = lane < W && lane < E.H;
+    const uint64_t e = in ? T[(base + (uint32_t)lane) & hm] : ~0ull;
+    const uint64_t empty = __ballot(in && e == 0);
+    const uint64_t tagm = __ballot(in && e != 0 && (uint32_t)(e >> 32) == tag);
+    const int fe = empty ? __ffsll((unsigned long long)empty) - 1 : 64;
+    const int ft = tagm ? __ffsll((unsigned long long)tagm) - 1 : 64;
+    if (ft < fe) {  // a candidate before any empty slot
+        const int id = __shfl((int)(uint32_t)e - 1, ft);
+        const NodeKey k = E.node_key[(size_t)g * E.M + id];
+        load_edges<R>(E, g, id, vc, er);  // (speculative: with the key's round trip)
+        if (k.own == own && k.opp == opp && k.turn == turn && k.cs == cs) {
+            *slot = (int)((base + (uint32_t)ft) & hm);
+            return id;
+        }
+    } else if (fe < 64) {  // empty before any tag match: not in the table
+        *slot = (int)((base + (uint32_t)fe) & hm);
+        return -1;
+    }
+    const int id = table_lookup(E, g, own, opp, turn, cs, slot);
+    if (id >= 0) load_edges<R>(E, g, id, vc, er);
+    return id;
+}
+
 // PUCT argmax (MCTS.py:114-131): strict '>' scan in action order == max u,
 // ties to the lowest action; NaN never wins.  Returns the action; *edge gets its
 // compact edge slot (edge_slots).
 template <class R>
-__device__ int puct_select(const Dev& E, int g, int id, const typename R::VCtx& vc, int* edge) {
+__device__ int puct_select(const Dev& E, int g, int id, const EdgeRow<R>& er, int* edge) {
     const int lane = lane_id();
     const size_t row = node_row<R>(E, g, id);
-    const int Ns = E.node_key[(size_t)g * E.M + id].Ns;
+    const int Ns = er.Ns;
     const float sq_edge = (float)sqrt((double)Ns);
     const float sq_new = (float)sqrt((double)Ns + 1e-8);
-    int ci[R::AJ];
-    edge_slots<R>(vc, ci);
+    const int(&ci)[R::AJ] = er.ci;
     float best = -INFINITY;
     int besta = 0x7fffffff, besti = -1;
 #pragma unroll
     for (int j = 0; j < R::AJ; ++j) {
         const int a = lane + WAVE * j;
         if (ci[j] >= 0) {
-            const float cp = E.cpuct_f * E.node_P[row + ci[j]];
-            const uint32_t nr = E.node_N[row + ci[j]];
-            // the f32 Q loaded with P and N (not after N says the edge exists): one
-            // dependent round trip less per level; used only where N > 0.  An edge whose
-            // Q is still a Python float (only terminal values backed into it) reads its
-            // f64 Q after N: rare, near the end of a game
-            const float qf = E.node_Qf[row + ci[j]];
+            const float cp = E.cpuct_f * er.P[j];
+            const uint32_t nr = er.N[j];
+            // an edge whose Q is still a Python float (only terminal values backed into
+            // it) reads its f64 Q after N: rare, near the end of a game
+            const float qf = er.Qf[j];
             const int n = (int)(nr & 0x7fffffffu);
             float u;
             if (n > 0) {
@@ -693,11 +757,15 @@ __device__ __forceinline__ void select_body(const Dev& E, float* __restrict__ pl
             break;
         }
         R::key(p, own, opp, kt, cs);
+        const typename R::VCtx vc = R::vctx(own, opp, cs);
+        EdgeRow<R> er;
         // the root's node id is cached for the rest of the move (ids are stable;
         // commit_move / set_root invalidate it): one hash probe less per simulation
         int id = depth == 0 ? root_id : -1;
-        if (id < 0) {
-            id = table_lookup(E, g, own, opp, kt, cs, &slot);
+        if (id >= 0) {
+            load_edges<R>(E, g, id, vc, er);
+        } else {
+            id = lookup_with_edges<R>(E, g, own, opp, kt, cs, &slot, vc, er);
             if (depth == 0 && id >= 0 && lane == 0) E.root_id[g] = id;
         }
         if (id < 0) {
@@ -706,7 +774,7 @@ __device__ __forceinline__ void select_body(const Dev& E, float* __restrict__ pl
             break;
         }
         int ei;
-        const int a = puct_select<R>(E, g, id, R::vctx(own, opp, cs), &ei);
+        const int a = puct_select<R>(E, g, id, er, &ei);
         if (a < 0) {
             set_err(E, g, -5);
             kind = LEAF_NONE;
