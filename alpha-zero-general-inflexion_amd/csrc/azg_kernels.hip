@@ -840,9 +840,10 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
     __shared__ float s_acc[WAVE];
     __shared__ float s_leaf[16];
     const int g = blockIdx.x, lane = lane_id();
-    // Every per-slot field the expansion and the backup read, the path entries and the
-    // leaf's P row and v are loaded before the first branch on any of them: one memory
-    // round trip instead of a chain (kind, then depth, then the path, ...).
+    // Every per-slot field the expansion and the backup read and the path entries are
+    // loaded before the first branch on any of them: one memory round trip instead of a
+    // chain (kind, then depth, then the path, ...).  The leaf's P row follows the kind
+    // check (no slot without a leaf reads it), in the round trip of the path edges' N / Q.
     const int kind = E.leaf_kind[g];
     const int depth = E.leaf_depth[g];
     const int32_t* path = E.path + (size_t)g * E.DMAX;
@@ -852,13 +853,13 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
     const int l_cs = E.leaf_cs[g], l_kt = E.leaf_turn[g], l_slot = E.leaf_slot[g];
     const double l_value = E.leaf_value[g];
     const float l_v = vin[g];
+    if (kind == LEAF_NONE) return;
     float praw[R::AJ];
 #pragma unroll
     for (int j = 0; j < R::AJ; ++j) {
         const int a = lane + WAVE * j;
-        praw[j] = a < R::A ? Pin[(size_t)g * p_stride + a] : 0.0f;
+        praw[j] = a < R::A && kind == LEAF_EXPAND ? Pin[(size_t)g * p_stride + a] : 0.0f;
     }
-    if (kind == LEAF_NONE) return;
     // Everything the backup reads (path entry, edge N and Q; one level per lane) and
     // the free-stack top are fetched up front, so they travel with the leaf's P
     // row instead of after the expansion (the path's edges are never the new node).
