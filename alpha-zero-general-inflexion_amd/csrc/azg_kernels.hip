@@ -847,7 +847,8 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
     const int kind = E.leaf_kind[g];
     const int depth = E.leaf_depth[g];
     const int32_t* path = E.path + (size_t)g * E.DMAX;
-    const int pk = lane < E.DMAX ? path[lane] : 0;
+    constexpr int PATH0 = 16;  // path entries loaded with the record (one 64-B segment; deeper: below)
+    const int pk = lane < PATH0 && lane < E.DMAX ? path[lane] : 0;
     const int top_ld = E.free_top[g];
     const uint64_t l_own = E.leaf_own[g], l_opp = E.leaf_opp[g];
     const int l_cs = E.leaf_cs[g], l_kt = E.leaf_turn[g], l_slot = E.leaf_slot[g];
@@ -863,7 +864,7 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
     // Everything the backup reads (path entry, edge N and Q; one level per lane) and
     // the free-stack top are fetched up front, so they travel with the leaf's P
     // row instead of after the expansion (the path's edges are never the new node).
-    const int packed0 = lane < depth ? pk : 0;
+    const int packed0 = lane < depth ? (lane < PATH0 ? pk : path[lane]) : 0;
     const int top0 = kind == LEAF_EXPAND ? top_ld : 0;
     uint32_t nr0 = 0u;
     float qf0 = 0.0f;

@@ -628,7 +628,7 @@ def main():
                          "forward_tflops": nn_tflops,
                          "forward_per_launch": f"{leaves} leaves x {algo_fwd_leaf / 1e6:.1f} MFLOP / "
                                                f"{nn_avg * 1e3:.3f} ms (HIP events)"},
-            "roofline_tree": {"bound": "hbm", "kernel": "select_kernel + expand_backup_kernel",
+            "roofline_tree": {"bound": "hbm", "kernel": "select_kernel + expand_backup_kernel (timed split on the instrumented simulations; the others run as the fused expand_select_kernel, whose PMC bytes per simulation step are `traffic`)",
                               "achieved": tree_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": tree_gbs / HBM_PEAK_GBS, "traffic": None,
                               "bytes_per_expansion": b_exp,
