@@ -187,19 +187,22 @@ __global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restric
 // 9 x Cin / 4 products.  Eight output channels per lane reuse each staged input vector 8
 // times (LDS traffic per multiply-add a quarter of the 2-channel form's), and the quarter's
 // input (H * H x Cin / 4) and weights (8 x 9 x Cin / 4) are a quarter of the plane.  The four
-// quarters' partial sums meet in a workspace: each block publishes its [leaf][pixel][8] partials,
-// then (release fence, one atomic ticket per co group) the LAST of the four blocks to arrive sums
-// them in quarter order 0..3 (deterministic whatever the arrival order), adds the bias, applies
-// ReLU, writes the output and resets the ticket for the next launch.  No block waits on another.
+// quarters' partial sums meet in a workspace: each block publishes its [leaf][pixel][8] partials
+// (write-through stores, drained, then one relaxed atomic ticket per co group) and the LAST of the
+// four blocks to arrive sums them in quarter order 0..3 (deterministic whatever the arrival order),
+// adds the bias, applies ReLU, writes the output and resets the ticket for the next launch.  No
+// block waits on another.
 constexpr int SK_CO = 8, SK_KG = 4;
 constexpr size_t SK_LDS = 96 * 1024;  // staged quarter input + weights + slice partials (n <= 8: <= 87 KB)
 
-// F1 > 0 (conv1 fused, conv2 only; F1 = the board side, 3..8): x is then the NCHW leaf planes
+// F1 > 0 (conv1 fused, conv2 only; F1 = the board side, 6..8): x is then the NCHW leaf planes
 // [B][D][F1][F1] (sB per leaf) and the staged quarter is conv1's output for that quarter's
 // channels, relu(b1 + conv1(planes)) with w1 [Cin][3][3][D] (channels_last, BN folded) --
 // computed by the block's first Cq / 64 waves, one channel per lane and the leaf's planes read as
-// wave-uniform scalars (conv1_sparse, azg_winograd_kern.h: constant planes one multiply-add per
-// output, 0/1 planes only their nonzero cells), instead of a launch of its own.
+// wave-uniform scalars (conv1_sparse, azg_conv1.h: constant planes one multiply-add per output,
+// 0/1 planes only their nonzero cells), instead of a launch of its own, while the other waves
+// stage the block's weight quarter (azg_small_conv12's LDS bound keeps Cq <= 188: at least five
+// staging waves).
 // The block's weight quarter is loaded into registers first (SC_WPF float4 per thread) and
 // written to LDS once the leaf's input loads are in flight: one memory round trip for both.
 constexpr int SC_WPF = 5;  // 8 x 9 x 512 / 4 floats = 9216 = 4.5 x 2048 (Cin = 512)
