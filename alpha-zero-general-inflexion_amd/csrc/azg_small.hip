@@ -183,7 +183,7 @@ __global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restric
 }
 
 // Split-K form for the 512-channel layers (conv2-4): block (co group of SK_CO = 8 channels, ci
-// quarter kg of SK_KG = 4), 512 threads = PXL pixels x (512 / PXL) slices of the quarter's
+// part kg of KG: 8 for conv3 / conv4, 4 for conv12), 512 threads = PXL pixels x (512 / PXL) slices of the part's
 // 9 x Cin / 4 products.  Eight output channels per lane reuse each staged input vector 8
 // times (LDS traffic per multiply-add a quarter of the 2-channel form's), and the quarter's
 // input (H * H x Cin / 4) and weights (8 x 9 x Cin / 4) are a quarter of the plane.  The four
@@ -192,8 +192,14 @@ __global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restric
 // four blocks to arrive sums them in quarter order 0..3 (deterministic whatever the arrival order),
 // adds the bias, applies ReLU, writes the output and resets the ticket for the next launch.  No
 // block waits on another.
-constexpr int SK_CO = 8, SK_KG = 4;
-constexpr size_t SK_LDS = 96 * 1024;  // staged quarter input + weights + slice partials (n <= 8: <= 87 KB)
+// KG = SK_KG = 8 K-parts for conv3 / conv4 (staged input eighth + weights + slice partials, n <= 8,
+// Cin = 512: <= 52 KB, two blocks per CU) and SK_KG1 = 4 for conv12, whose conv1 registers
+// allow one 512-thread block per CU (<= 87 KB)
+// (4 / 8 / 16 K-parts for conv3 at one leaf: 16.2 / 14.3 / 19.0 us; 16 fit two blocks per CU for 1024
+// blocks, two rounds; tools/small_layer_bench.py)
+constexpr int SK_CO = 8, SK_KG = 8, SK_KG1 = 4;
+__host__ __device__ constexpr size_t sk_lds(int kg) { return kg == SK_KG1 ? 96 * 1024 : 56 * 1024; }
+__host__ __device__ constexpr int sk_wpf(int kg) { return kg == SK_KG1 ? 5 : 3; }  // 8 x 9 x 512 / kg / 4 / 512
 
 // F1 > 0 (conv1 fused, conv2 only; F1 = the board side, 6..8): x is then the NCHW leaf planes
 // [B][D][F1][F1] (sB per leaf) and the staged quarter is conv1's output for that quarter's
@@ -205,8 +211,7 @@ constexpr size_t SK_LDS = 96 * 1024;  // staged quarter input + weights + slice 
 // staging waves).
 // The block's weight quarter is loaded into registers first (SC_WPF float4 per thread) and
 // written to LDS once the leaf's input loads are in flight: one memory round trip for both.
-constexpr int SC_WPF = 5;  // 8 x 9 x 512 / 4 floats = 9216 = 4.5 x 2048 (Cin = 512)
-template <int PXL, int F1>
+template <int PXL, int F1, int KG>
 __global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __restrict__ x, long long sB, int sY,
                                                              int sX, int B, int H, int pad,
                                                              const float* __restrict__ w, int Cin,
@@ -216,13 +221,14 @@ __global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __rest
                                                              const float* __restrict__ w1, const float* __restrict__ b1,
                                                              int D) {
     constexpr int KSL = SC_T / PXL;
-    __shared__ __attribute__((aligned(16))) float lds[SK_LDS / 4];
+    constexpr int SC_WPF = sk_wpf(KG);
+    __shared__ __attribute__((aligned(16))) float lds[sk_lds(KG) / 4];
     __shared__ unsigned s_last;
     const int tid = threadIdx.x;
     const int p = tid % PXL, s = tid / PXL;
-    const int cg = blockIdx.x / SK_KG, kg = blockIdx.x % SK_KG;
+    const int cg = blockIdx.x / KG, kg = blockIdx.x % KG;
     const int co0 = cg * SK_CO;
-    const int Cq = Cin / SK_KG, ci_base = kg * Cq;
+    const int Cq = Cin / KG, ci_base = kg * Cq;
     const int Ho = H + 2 * pad - 2, hw = Ho * Ho;
     const int P = Cq + 4;                       // LDS pitch of a staged pixel
     const int Kq = 9 * Cq;                      // this quarter's products per output
@@ -362,29 +368,29 @@ __global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __rest
             float sum = 0.f;
             for (int q = 0; q < KSL; ++q) sum += red[(q * PXL + pp) * SK_CO + c];
             // write-through (sc1) stores: published by the drain below, no release fence
-            __hip_atomic_store((unsigned*)(part + (((long long)kg * (gridDim.x / SK_KG) + cg) * B + b) * hw * SK_CO + t),
+            __hip_atomic_store((unsigned*)(part + (((long long)kg * (gridDim.x / KG) + cg) * B + b) * hw * SK_CO + t),
                                __float_as_uint(sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();  // xs and red are rewritten for the next leaf
     }
     // publish (MI355X hand-off, cdna_hip_programming.md Guideline 16 R1): every wave drains its
     // write-through partial stores, then one relaxed ticket per block; the last of the co group's
-    // SK_KG blocks combines the quarters in order, reading them with sc1 loads only (no fences:
+    // KG blocks combines the quarters in order, reading them with sc1 loads only (no fences:
     // a __threadfence by every wave of every block -- an L2 write-back and invalidate each --
     // held these kernels at 64-91 us per leaf, the drop-in call at 6.7 ms instead of 2.7)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0)
-        s_last = __hip_atomic_fetch_add(ticket + cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == SK_KG - 1;
+        s_last = __hip_atomic_fetch_add(ticket + cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KG - 1;
     __syncthreads();
     if (!s_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler order only: every load below is sc1)
-    const int G = gridDim.x / SK_KG;
+    const int G = gridDim.x / KG;
     for (int t = tid; t < B * hw * SK_CO; t += SC_T) {
         const int c = t % SK_CO, bp = t / SK_CO;  // bp = b * hw + pixel
         float sum = 0.f;
 #pragma unroll
-        for (int q = 0; q < SK_KG; ++q) {  // coherent (agent-scope) loads: other CUs wrote them
+        for (int q = 0; q < KG; ++q) {  // coherent (agent-scope) loads: other CUs wrote them
             const unsigned u = __hip_atomic_load((const unsigned*)(part + (((long long)q * G + cg) * B) * hw * SK_CO + t),
                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             sum += __uint_as_float(u);
@@ -525,11 +531,11 @@ int launch_conv(dim3 grid, hipStream_t st, const float* x, long long sB, int sY,
     return 0;
 }
 
-template <int PXL, int F1 = 0>
+template <int PXL, int F1 = 0, int KG = SK_KG>
 void launch_conv_sk(hipStream_t st, const float* x, long long sB, int sY, int sX, int B, int H, int pad,
                     const float* w, int Cin, int Cout, const float* bias, int relu, float* y, int ldy, float* work,
                     unsigned* tickets, const float* w1 = nullptr, const float* b1 = nullptr, int D = 0) {
-    hipLaunchKernelGGL((small_conv_sk_kernel<PXL, F1>), dim3((unsigned)(Cout / SK_CO * SK_KG)), dim3(SC_T), 0, st, x,
+    hipLaunchKernelGGL((small_conv_sk_kernel<PXL, F1, KG>), dim3((unsigned)(Cout / SK_CO * KG)), dim3(SC_T), 0, st, x,
                        sB, sY, sX, B, H, pad, w, Cin, bias, relu, y, ldy, work, tickets, w1, b1, D);
 }
 
@@ -556,7 +562,7 @@ extern "C" int azg_small_conv3x3(const float* x, int64_t sB, int32_t sY, int32_t
     const bool sk = n > 16 && vec && Cin % (4 * SK_KG) == 0 && Cout % SK_CO == 0 && work && tickets &&
                     work_floats >= need && n_tickets >= Cout / SK_CO && ((uintptr_t)work & 15) == 0 &&
                     (size_t)H * H * (Cin / SK_KG + 4) * 4 + (size_t)9 * Cin / SK_KG * SK_CO * 4 +
-                            (size_t)SC_T * SK_CO * 4 <= SK_LDS;
+                            (size_t)SC_T * SK_CO * 4 <= sk_lds(SK_KG);
     if (sk) {
         if (n <= 16) launch_conv_sk<16>(st, x, sB, sY, sX, batch, H, pad, w, Cin, Cout, bias, relu, y, ldy, work, tickets);
         else if (n <= 32) launch_conv_sk<32>(st, x, sB, sY, sX, batch, H, pad, w, Cin, Cout, bias, relu, y, ldy, work, tickets);
@@ -586,16 +592,17 @@ extern "C" int azg_small_conv12(const float* planes, int32_t batch, int32_t dept
                                 float* work, int64_t work_floats, uint32_t* tickets, int32_t n_tickets, void* stream) {
     const int hw = n * n;
     if (!planes || !w1 || !b1 || !w2 || !y || !work || !tickets || batch <= 0 || batch > 4 || depth < 1 || depth > 4 ||
-        n < 6 || n > 8 || C <= 0 || C % (4 * SK_KG) || C % SK_CO || ldy < C ||
-        work_floats < (long long)SK_KG * C * batch * hw || n_tickets < C / SK_CO || ((uintptr_t)w2 & 15) ||
+        n < 6 || n > 8 || C <= 0 || C % (4 * SK_KG1) || C % SK_CO || ldy < C ||
+        work_floats < (long long)SK_KG1 * C * batch * hw || n_tickets < C / SK_CO || ((uintptr_t)w2 & 15) ||
         ((uintptr_t)work & 15) ||
-        (size_t)hw * (C / SK_KG + 4) * 4 + (size_t)9 * C / SK_KG * SK_CO * 4 + (size_t)SC_T * SK_CO * 4 > SK_LDS)
+        (size_t)hw * (C / SK_KG1 + 4) * 4 + (size_t)9 * C / SK_KG1 * SK_CO * 4 + (size_t)SC_T * SK_CO * 4 >
+            sk_lds(SK_KG1))
         return AZG_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     const long long sB = (long long)depth * hw;
     auto go = [&](auto N_) {
-        launch_conv_sk<64, decltype(N_)::value>(st, planes, sB, 0, 0, batch, n, 1, w2, C, C, b2, 1, y, ldy, work,
-                                                tickets, w1, b1, depth);
+        launch_conv_sk<64, decltype(N_)::value, SK_KG1>(st, planes, sB, 0, 0, batch, n, 1, w2, C, C, b2, 1, y, ldy,
+                                                        work, tickets, w1, b1, depth);
     };
     switch (n) {  // the boards' sides: conv1's output plane in registers (conv1_sparse)
         case 6: go(std::integral_constant<int, 6>{}); break;

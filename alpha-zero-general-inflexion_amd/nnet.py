@@ -706,7 +706,7 @@ class InferenceNet(nn.Module):
         x, strides, H, cin = planes, (self.depth * n * n, n, 1, n * n), n, self.depth
         # the split-K convolutions' partial sums and per-channel-group tickets (zero between launches;
         # the last word is the heads kernel's)
-        need = 4 * C * SMALL_MAX_B * n * n
+        need = 8 * C * SMALL_MAX_B * n * n  # (azg_small.hip SK_KG = 8 K-parts)
         if getattr(self, "_small_work", None) is None or self._small_work.numel() < need \
                 or self._small_work.device != dev:
             self._small_work = torch.empty(need, device=dev, dtype=torch.float32)
@@ -715,7 +715,7 @@ class InferenceNet(nn.Module):
         wp, tp = ctypes.c_void_p(work.data_ptr()), ctypes.c_void_p(tickets.data_ptr())
         first = 1
         if self.depth <= 4 and 6 <= n <= 8 and C % 16 == 0 and self.pads[:2] == [1, 1] \
-                and n * n * (C // 4 + 4) * 4 + 72 * C + 16384 <= 96 * 1024:  # azg_small_conv12's LDS
+                and n * n * (C // 4 + 4) * 4 + 72 * C + 16384 <= 96 * 1024:  # azg_small_conv12's LDS (4 K-parts)
             # conv1 + conv2 in one launch
             y = torch.empty((B * n * n, C), device=dev, dtype=torch.float32)
             _lib.check(L.azg_small_conv12(ctypes.c_void_p(planes.data_ptr()), B, self.depth, n,

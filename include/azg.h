@@ -250,11 +250,11 @@ int  azg_split_gemm_variant(int32_t variant, const void* a, const void* bt, floa
  *     px = (leaf, oy, ox) of the (H + 2 pad - 2)^2 output, x any layout given by its
  *     element strides (sB per leaf, sY, sX, sC: the NCHW leaf planes or the NHWC rows this
  *     writes); Cout even, at most 256 output pixels, pad 0 or 1; bias may be null.  With a
- *     device workspace (work: >= 4 Cout x batch x (output pixels) floats, 16-B aligned;
- *     tickets: >= Cout / 8 zero-initialised words, left zero after every launch) and NHWC
- *     float4 inputs with Cin % 16 == 0, Cout % 8 == 0, the split-K form runs (8 channels x a
- *     quarter of the input channels per block, the quarters summed in order by the last
- *     block of each channel group); else work / tickets may be null;
+ *     device workspace (work: >= 8 Cout x batch x (output pixels) floats, 16-B aligned;
+ *     tickets: >= Cout / 8 zero-initialised words, left zero after every launch), NHWC
+ *     float4 inputs with Cin % 32 == 0, Cout % 8 == 0 and more than 16 output pixels, the
+ *     split-K form runs (8 channels x an eighth of the input channels per block, the eighths
+ *     summed in order by the last block of each channel group); else work / tickets may be null;
  *   azg_small_fc: y[b * ldy + n] = relu?(bias[n] + sum_k w[n][k] x[b * ldx + k]), b < batch <= 4,
  *     w [N][K] row-major, K % 4 == 0, ldx % 4 == 0, x and w 16-B aligned; bias may be null. */
 int  azg_small_conv3x3(const float* x, int64_t sB, int32_t sY, int32_t sX, int32_t sC, int32_t batch, int32_t H,
@@ -267,7 +267,7 @@ int  azg_small_fc(const float* x, int32_t ldx, int32_t batch, const float* w, in
  * block computing relu(b1 + conv1(planes)) for its quarter of conv2's input channels itself):
  * planes [batch][depth][n][n] f32 (depth <= 4, the boards' sides 6 <= n <= 8), w1 [C][3][3][depth], w2 [C][3][3][C]
  * (channels_last, BN folded), y[px * ldy + co] = relu(b2 + conv2(...)) for the n x n outputs;
- * C % 16 == 0, work / tickets as azg_small_conv3x3's split-K form. */
+ * C % 16 == 0, work / tickets as azg_small_conv3x3's split-K form (4 K-parts here). */
 int  azg_small_conv12(const float* planes, int32_t batch, int32_t depth, int32_t n, const float* w1, const float* b1,
                       const float* w2, const float* b2, int32_t C, float* y, int32_t ldy, float* work,
                       int64_t work_floats, uint32_t* tickets, int32_t n_tickets, void* stream);

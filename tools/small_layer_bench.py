@@ -46,7 +46,7 @@ def main():
             strides = (H * H * cin, H * cin, cin, 1)
         Ho = H + 2 * pad - 2 if taps == 9 else 1
         y = torch.empty((B * Ho * Ho, cout), device="cuda")
-        work = torch.empty(4 * cout * B * Ho * Ho, device="cuda")
+        work = torch.empty(8 * cout * B * Ho * Ho, device="cuda")
         tickets = torch.zeros(cout // 8, device="cuda", dtype=torch.int32)
 
         def azg(sk=True):
@@ -101,7 +101,7 @@ def fused(L, st):
     w2 = torch.randn(C, C, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
     b1, b2 = torch.randn(C, device="cuda"), torch.randn(C, device="cuda")
     y = torch.empty(B * n * n, C, device="cuda")
-    work = torch.empty(4 * C * B * n * n, device="cuda")
+    work = torch.empty(8 * C * B * n * n, device="cuda")
     tickets = torch.zeros(C // 8 + 1, device="cuda", dtype=torch.int32)
     x = torch.randn(B, 512, device="cuda")
     w34, b34 = torch.randn(344, 512, device="cuda"), torch.randn(344, device="cuda")
