@@ -982,8 +982,10 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
     }
 }
 
+// (the descents' kernels held to 128 VGPRs, 4 waves per SIMD: 131 otherwise since the edge rows are
+// loaded with the key check; no spill, +0.7% at C4 alternating on one box, tools/ab_bench.sh)
 template <class R>
-__global__ __launch_bounds__(WAVE) void select_kernel(Dev E, float* __restrict__ planes) {
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) void select_kernel(Dev E, float* __restrict__ planes) {
     SelPre<R> q = select_prefetch<R>(E);
     select_body<R>(E, planes, q);
 }
@@ -999,7 +1001,7 @@ __global__ __launch_bounds__(WAVE) void expand_backup_kernel(Dev E, const float*
 // the next descent through the workgroup barrier): one kernel boundary less per
 // simulation where the search is launch-bound (one leaf per simulation, the drop-in).
 template <class R>
-__global__ __launch_bounds__(WAVE) void expand_select_kernel(Dev E, const float* __restrict__ Pin, int p_stride,
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) void expand_select_kernel(Dev E, const float* __restrict__ Pin, int p_stride,
                                                              const float* __restrict__ vin,
                                                              float* __restrict__ planes) {
     SelPre<R> q = select_prefetch<R>(E);  // (nothing the expansion writes)
