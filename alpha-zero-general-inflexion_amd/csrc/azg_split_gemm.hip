@@ -120,7 +120,11 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
     const _Float16* Be = g.Bt + (long long)(g.b_pt0[r] + e) * K * C2;
     float* Me = g.M + g.m_off[r] + (long long)e * T * K;
 
-    // DMA sources: wave w fills A tile rows (BM/8) w + 8i + lane/8 (i < AP) and B tile
+    // The A operand (V, read by the layer's GEMM and nothing after it) is loaded non-temporally (aux 2):
+// it then leaves the Infinity Cache to B (the layer's weights U, re-read every forward); at C2's
+// 256 leaves, where the GEMMs stream U, +0.9% exp/s, at C4 neutral (alternating A/B on one box,
+// profiles/r04_ab_gemm_nt_a, tools/ab_bench.sh).
+// DMA sources: wave w fills A tile rows (BM/8) w + 8i + lane/8 (i < AP) and B tile
     // rows 32w + 8i + lane/8 (i < 4); lane%8 is the physical 16-B chunk, holding logical
     // chunk lc = phys ^ ((row>>1)&7): hi channels 8lc.. (lc < 4) or lo channels 8(lc-4)..
     // of the stage
@@ -150,7 +154,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
         for (int i = 0; i < AP; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
                                                      (__attribute__((address_space(3))) void*)(abase + 8 * i * SG_ROWB),
-                                                     16, aoff[i & 1], ks * SG_STAGE_SOFF, 0, 0);
+                                                     16, aoff[i & 1], ks * SG_STAGE_SOFF, 0, 2);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
@@ -164,7 +168,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
         if (p < 4)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 2 ? ar0 : ar1,
                                                      (__attribute__((address_space(3))) void*)(base + 8 * q * SG_ROWB),
-                                                     16, aoff[q & 1], ks * SG_STAGE_SOFF, 0, 0);
+                                                     16, aoff[q & 1], ks * SG_STAGE_SOFF, 0, 2);
         else
             __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 2 ? br0 : br1,
                                                      (__attribute__((address_space(3))) void*)(base + ATILEB +
@@ -368,7 +372,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
                                                          (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
                                                          16, ((t.m0 + arow[i & 1]) * C2 + dcol[i & 1]) * 2,
-                                                         ks * SG_STAGE_SOFF, 0, 0);
+                                                         ks * SG_STAGE_SOFF, 0, 2);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
