@@ -121,9 +121,10 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
     float* Me = g.M + g.m_off[r] + (long long)e * T * K;
 
     // The A operand (V, read by the layer's GEMM and nothing after it) is loaded non-temporally (aux 2):
-// it then leaves the Infinity Cache to B (the layer's weights U, re-read every forward); at C2's
-// 256 leaves, where the GEMMs stream U, +0.9% exp/s, at C4 neutral (alternating A/B on one box,
-// profiles/r04_ab_gemm_nt_a, tools/ab_bench.sh).
+// it then leaves the Infinity Cache to B (the layer's weights U, re-read every forward).  Alternating
+// A/B on one box (profiles/r04_ab_gemm_nt_a, tools/ab_bench.sh): C2 +0.9%, C4 neutral -- within the
+// ~1.5% that C2's A/B pairs differ from box to box (non-temporal M stores measured +1.9% and -1% at
+// C2 on two boxes, -0.7% at C4: not kept).
 // DMA sources: wave w fills A tile rows (BM/8) w + 8i + lane/8 (i < AP) and B tile
     // rows 32w + 8i + lane/8 (i < 4); lane%8 is the physical 16-B chunk, holding logical
     // chunk lc = phys ^ ((row>>1)&7): hi channels 8lc.. (lc < 4) or lo channels 8(lc-4)..
