@@ -713,11 +713,17 @@ __device__ __forceinline__ void set_err(const Dev& E, int g, int code) {
 // (slot state, root position, the next random words): loaded together, and in the
 // fused expand_select kernel before the expansion, so none of it waits behind the
 // backup's round trips (the drop-in's one-game search is a chain of dependent loads).
+// The slot's error code and cached root id are loaded here too: in the fused kernel the expansion
+// hands over what it changes of them (ExpandOut) instead of the descent re-reading them.
 template <class R>
 struct SelPre {
-    int active, searcher;
+    int active, searcher, err, root_id;
     Pos root;
     BlockRng rg;
+};
+struct ExpandOut {
+    int err;      // error code the expansion set (0: none)
+    int root_id;  // node id the expansion made the root (-1: none)
 };
 template <class R>
 __device__ __forceinline__ SelPre<R> select_prefetch(const Dev& E) {
@@ -726,6 +732,8 @@ __device__ __forceinline__ SelPre<R> select_prefetch(const Dev& E) {
     SelPre<R> q;
     q.active = E.active[g];
     q.searcher = E.searcher[g];
+    q.err = E.err[g];
+    q.root_id = E.root_id[g];
     q.root = load_root<R>(E, g);
     q.rg = rng_open(E.mt + (size_t)g * MT_N, E.mt_pos + g, s_mt);  // the slot's next random words
     return q;
@@ -738,13 +746,13 @@ __device__ __forceinline__ void select_body(const Dev& E, float* __restrict__ pl
     const int g = blockIdx.x, lane = lane_id();
     float* out = planes + (size_t)g * R::PLANES * R::CELLS;
     // (searching(): searcher 0 = self-play, else the searcher's colour to move)
-    if (!q.active || E.err[g] || !(q.searcher == 0 || q.searcher == q.root.player)) {
+    if (!q.active || q.err || !(q.searcher == 0 || q.searcher == q.root.player)) {
         for (int i = lane; i < R::PLANES * R::CELLS; i += WAVE) out[i] = 0.0f;
         if (lane == 0) E.leaf_kind[g] = LEAF_NONE;
         return;
     }
     BlockRng& rg = q.rg;
-    const int root_id = E.root_id[g];
+    const int root_id = q.root_id;
     Pos p = q.root;
     int depth = 0, kind = LEAF_NONE, slot = -1, cs = 0, kt = 0;
     uint64_t own = 0, opp = 0;
@@ -834,8 +842,9 @@ __global__ __launch_bounds__(WAVE) void stub_eval_kernel(const float* __restrict
 // (MCTS.py:136-145).  The path holds distinct nodes, so lanes update one edge
 // each with no atomics.
 template <class R>
-__device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __restrict__ Pin, int p_stride,
-                                                   const float* __restrict__ vin) {
+__device__ __forceinline__ ExpandOut expand_backup_body(const Dev& E, const float* __restrict__ Pin, int p_stride,
+                                                        const float* __restrict__ vin) {
+    ExpandOut xo{0, -1};
     __shared__ float s_p[R::AP];
     __shared__ float s_acc[WAVE];
     __shared__ float s_leaf[16];
@@ -854,7 +863,7 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
     const int l_cs = E.leaf_cs[g], l_kt = E.leaf_turn[g], l_slot = E.leaf_slot[g];
     const double l_value = E.leaf_value[g];
     const float l_v = vin[g];
-    if (kind == LEAF_NONE) return;
+    if (kind == LEAF_NONE) return xo;
     float praw[R::AJ];
 #pragma unroll
     for (int j = 0; j < R::AJ; ++j) {
@@ -923,8 +932,10 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
         id = __shfl(id, 0);
         if (id < 0) {
             set_err(E, g, -3);
-            return;
+            xo.err = -3;
+            return xo;
         }
+        if (depth == 0) xo.root_id = id;
         const size_t ni = (size_t)g * E.M + id, row = ni * R::AP;
         // the valid actions' edges only, in their compact slots (edge_slots); Q is read
         // only where N > 0: no init
@@ -980,6 +991,7 @@ __device__ __forceinline__ void expand_backup_body(const Dev& E, const float* __
         E.node_N[row] = (uint32_t)(n + 1) | (nf ? 0x80000000u : 0u);
         E.node_key[ni].Ns += 1;
     }
+    return xo;
 }
 
 // (the descents' kernels held to 128 VGPRs, 4 waves per SIMD: 131 otherwise since the edge rows are
@@ -1004,8 +1016,10 @@ template <class R>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) void expand_select_kernel(Dev E, const float* __restrict__ Pin, int p_stride,
                                                              const float* __restrict__ vin,
                                                              float* __restrict__ planes) {
-    SelPre<R> q = select_prefetch<R>(E);  // (nothing the expansion writes)
-    expand_backup_body<R>(E, Pin, p_stride, vin);
+    SelPre<R> q = select_prefetch<R>(E);  // (the expansion's changes to err / root_id come back in xo)
+    const ExpandOut xo = expand_backup_body<R>(E, Pin, p_stride, vin);
+    if (xo.err && !q.err) q.err = xo.err;  // (set_err keeps the first code)
+    if (xo.root_id >= 0) q.root_id = xo.root_id;
     __syncthreads();
     select_body<R>(E, planes, q);
 }
