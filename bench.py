@@ -145,6 +145,8 @@ def parse():
                    help="fc2 and [fc3 | fc4] at >= 1024 leaves: libazg split-K split GEMMs (azg) or the round-2 "
                         "hipBLASLt fp16 GEMMs (blas)")
     p.add_argument("--fc-kparts", default=None, help="with --fc-tail azg: split-K parts of fc2,fc3|fc4 (e.g. 4,2)")
+    p.add_argument("--fc1-split-min", type=int, default=None,
+                   help="leaves from which the FC tail runs split-fp16 on libazg (nnet.FC1_SPLIT_MIN_BATCH, 1024)")
     p.add_argument("--net", default="inference", choices=["inference", "reference"],
                    help="inference: BN-folded NHWC InferenceNet; reference: InflexionNNet as written")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -365,6 +367,9 @@ def main():
     if args.fc_kparts:
         import azg_amd.nnet as nn_mod
         nn_mod.FC2_KPARTS, nn_mod.FC34_KPARTS = (int(x) for x in args.fc_kparts.split(","))
+    if args.fc1_split_min is not None:
+        import azg_amd.nnet as nn_mod
+        nn_mod.FC1_SPLIT_MIN_BATCH = args.fc1_split_min
     ev = ((InferenceNet(net, conv=args.conv, gemm=args.gemm) if args.net == "inference" else net)
           if args.evaluator == "net" else "stub")
     if args.fc_tail == "blas" and hasattr(ev, "fc_tail_azg"):
