@@ -120,11 +120,10 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
     const _Float16* Be = g.Bt + (long long)(g.b_pt0[r] + e) * K * C2;
     float* Me = g.M + g.m_off[r] + (long long)e * T * K;
 
-    // The A operand (V, read by the layer's GEMM and nothing after it) is loaded non-temporally (aux 2):
-// it then leaves the Infinity Cache to B (the layer's weights U, re-read every forward).  Alternating
-// A/B on one box (profiles/r04_ab_gemm_nt_a, tools/ab_bench.sh): C2 +0.9%, C4 neutral -- within the
-// ~1.5% that C2's A/B pairs differ from box to box (non-temporal M stores measured +1.9% and -1% at
-// C2 on two boxes, -0.7% at C4: not kept).
+    // (Non-temporal A-operand loads (aux 2) were A/B'd in round 4: C4 neutral, C2 +0.9% -- within the ~1.5%
+// box-to-box spread of C2's A/B pairs -- but +8% PMC bytes per launch at C4 (1.004 vs 0.925 GB): the two
+// column tiles of a row tile no longer share its A tile through the XCD's L2.  Not kept; nor non-temporal
+// M stores (C4 -0.7%, C2 +1.9% / -1% on two boxes).  profiles/r04_ab_gemm_nt_a, r04_ab_gemm_nt_m.)
 // DMA sources: wave w fills A tile rows (BM/8) w + 8i + lane/8 (i < AP) and B tile
     // rows 32w + 8i + lane/8 (i < 4); lane%8 is the physical 16-B chunk, holding logical
     // chunk lc = phys ^ ((row>>1)&7): hi channels 8lc.. (lc < 4) or lo channels 8(lc-4)..
@@ -155,7 +154,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
         for (int i = 0; i < AP; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
                                                      (__attribute__((address_space(3))) void*)(abase + 8 * i * SG_ROWB),
-                                                     16, aoff[i & 1], ks * SG_STAGE_SOFF, 0, 2);
+                                                     16, aoff[i & 1], ks * SG_STAGE_SOFF, 0, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
@@ -169,7 +168,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_kernel(SGArgs g) {
         if (p < 4)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 2 ? ar0 : ar1,
                                                      (__attribute__((address_space(3))) void*)(base + 8 * q * SG_ROWB),
-                                                     16, aoff[q & 1], ks * SG_STAGE_SOFF, 0, 2);
+                                                     16, aoff[q & 1], ks * SG_STAGE_SOFF, 0, 0);
         else
             __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 2 ? br0 : br1,
                                                      (__attribute__((address_space(3))) void*)(base + ATILEB +
@@ -373,7 +372,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? ar0 : ar1,
                                                          (__attribute__((address_space(3))) void*)(base + 8 * i * SG_ROWB),
                                                          16, ((t.m0 + arow[i & 1]) * C2 + dcol[i & 1]) * 2,
-                                                         ks * SG_STAGE_SOFF, 0, 2);
+                                                         ks * SG_STAGE_SOFF, 0, 0);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? br0 : br1,
