@@ -44,6 +44,9 @@ def run(label, channels_last=False, benchmark=False, batches=30, dtype="f32", fu
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["f32"]:  # the default trainer alone (e.g. under rocprofv3: kernel time vs wall)
+        run("nchw")
+        sys.exit(0)
     run("nchw")
     run("nchw+benchmark", benchmark=True)
     run("channels_last", channels_last=True)
