@@ -518,15 +518,18 @@ __device__ __forceinline__ void plane_to_V(const P& ys, int h_rt, long long b, i
 // (bias + ReLU applied) is kept in registers (compile-time side HC) or its own
 // LDS column -- only that lane reads it back, so no barrier -- and the next
 // layer's tiles are transformed from it: layer i's activation never goes to HBM.
-template <int HC, int FMT>
-__global__ __launch_bounds__(64) void winograd_mid_kernel(const float* __restrict__ Min, const float* __restrict__ bias,
-                                                          void* __restrict__ Vout, int h_rt, int C, long long B,
-                                                          float mscale, int* overflow) {
+template <int HC, int FMT, int WPB = 1>
+__global__ __launch_bounds__(64 * WPB) void winograd_mid_kernel(const float* __restrict__ Min,
+                                                                const float* __restrict__ bias,
+                                                                void* __restrict__ Vout, int h_rt, int C, long long B,
+                                                                float mscale, int* overflow) {
     extern __shared__ float ys_raw[];  // [h * h][64] when HC == 0
+    static_assert(WPB == 1 || HC > 0, "several items per block: register planes only");
     const int h = HC > 0 ? HC : h_rt;
-    const unsigned lane = threadIdx.x;
+    const unsigned lane = threadIdx.x & 63u;
     const int cblocks = C / 64;
-    const unsigned blk = xcd_block();
+    // WPB waves per block, one (image, 64 channels) item each, adjacent items
+    const unsigned blk = xcd_block() * WPB + (WPB > 1 ? (unsigned)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u);
     const long long b = blk / cblocks;
     const int c0 = (blk % cblocks) * 64, c = c0 + (int)lane;
     const float bc = bias[c];

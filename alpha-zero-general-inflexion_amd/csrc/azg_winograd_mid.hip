@@ -10,10 +10,17 @@ extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, void* V,
     const size_t lds = (size_t)h * h * 64 * sizeof(float);
     hipStream_t st = (hipStream_t)stream;
     const long long B = batch;
+// mid<5> (conv3 -> conv4) as four items per 256-thread block: +0.3% at C4 alternating on one box
+// (transforms 599-602 -> 594-598 us per forward; profiles/r04_ab_mid5_wpb4); mid<7> stays one wave
+// per block (four per block spilled it, 40% slower)
 #define AZG_MID(H, SP, L)                                                                                          \
     {                                                                                                              \
-        hipLaunchKernelGGL((winograd_mid_kernel<H, SP>), grid, dim3(64), L, st, M, bias, V, h, c, B, mscale,        \
-                           overflow);                                                                              \
+        if (H == 5 && grid.x % 32 == 0)                                                                            \
+            hipLaunchKernelGGL((winograd_mid_kernel<H, SP, (H == 5 ? 4 : 1)>), dim3(grid.x / 4), dim3(256), L, st, \
+                               M, bias, V, h, c, B, mscale, overflow);                                             \
+        else                                                                                                       \
+            hipLaunchKernelGGL((winograd_mid_kernel<H, SP>), grid, dim3(64), L, st, M, bias, V, h, c, B, mscale,    \
+                               overflow);                                                                          \
         return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;                                                  \
     }
     // the board sides of the supported games get register-resident planes
