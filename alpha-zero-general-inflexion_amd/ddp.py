@@ -161,11 +161,40 @@ def broadcast_example_sets(sets, src=0, group=None, device=None):
     return out
 
 
+def rank_dropout_seed(group=None, device=None):
+    """A seed for this rank's dropout masks: a base drawn from rank 0's torch CPU generator,
+    broadcast, plus the rank.  The reference draws an independent mask per sample of its
+    batch (NNet.py:64, F.dropout in InflexionNNet.py:50-51); the ranks' slices have equal
+    shapes and run the same ops, so with the generators every rank inherits (the same
+    torch.manual_seed) sample i of every slice would get the same mask."""
+    dev = device if device is not None else torch.device("cpu")
+    buf = torch.zeros(1, dtype=torch.int64, device=dev)
+    if dist.get_rank(group) == 0:
+        buf[0] = int(torch.randint(0, 2**31 - 1, (1,), dtype=torch.int64).item())
+    dist.broadcast(buf, src=group_src(group, 0), group=group)
+    return int(buf.item()) * 1000003 + dist.get_rank(group)
+
+
 def train_examples_dp(wrapper, ex, group=None):
     """NNetWrapper.train_examples over the ranks of `group`: the reference trainer's
     epochs, batches, losses and Adam steps, each batch split evenly over the ranks
     (module docstring).  Every rank calls this with the same ExampleSet; returns the
-    batches' global (l_pi, l_v) as a device tensor [batches, 2] on every rank."""
+    batches' global (l_pi, l_v) as a device tensor [batches, 2] on every rank.
+
+    Dropout masks come from a generator state of this rank's own (rank_dropout_seed),
+    forked for the duration of training: the caller's torch generators are restored."""
+    dev = wrapper.device
+    seed = rank_dropout_seed(group, dev if dist.get_backend(group) == "nccl" else None)
+    devices = [dev.index if dev.index is not None else torch.cuda.current_device()] if dev.type == "cuda" else []
+    with torch.random.fork_rng(devices=devices):
+        torch.default_generator.manual_seed(seed)
+        if dev.type == "cuda":
+            with torch.cuda.device(devices[0]):
+                torch.cuda.manual_seed(seed)
+        return _train_examples_dp(wrapper, ex, group)
+
+
+def _train_examples_dp(wrapper, ex, group):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     a = wrapper.args
@@ -218,4 +247,4 @@ def train_examples_dp(wrapper, ex, group=None):
 
 
 __all__ = ["GlobalBatchNorm", "broadcast_numpy_rng", "broadcast_perm", "broadcast_example_sets",
-           "train_examples_dp"]
+           "rank_dropout_seed", "train_examples_dp"]

@@ -101,3 +101,66 @@ def test_data_parallel_trainer_world2():
                                        atol=1e-3 * float(np.abs(r["final"][k]["proj"]).max()), err_msg=k)
         if k.endswith("num_batches_tracked"):
             assert int(res[0]["sd"][k]) == int(r["final"][k]["sum"]), k
+
+
+def _dropout_worker(rank, world, port, q):
+    """Train with the reference's dropout 0.3 and record every dropout mask this rank draws."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import torch.nn.functional as F
+        import azg_amd  # noqa: F401
+        import azg_amd.nnet as nnet_mod
+        from azg_amd.examples import ExampleSet
+        from azg_amd.nnet import NNetWrapper
+        from test_train_golden import golden, reference_examples
+        c = golden()["config"]
+        game, ex = reference_examples(c)
+        torch.manual_seed(c["init_seed"])  # every rank: the same torch generators, as under torchrun
+        w = NNetWrapper(game, dict(num_channels=c["num_channels"], epochs=1, dropout=0.3), device="cpu")
+        masks = []
+        orig = F.dropout
+
+        def recording_dropout(x, p=0.5, training=True, inplace=False):
+            m = orig(torch.ones_like(x), p, training)
+            masks.append((m != 0).numpy().copy())
+            return x * m
+        nnet_mod.F.dropout = recording_dropout
+        try:
+            np.random.seed(c["batch_seed"])
+            before = torch.get_rng_state()
+            w.train_examples(ExampleSet.from_list(ex, "cpu"), group=dist.group.WORLD)
+        finally:
+            nnet_mod.F.dropout = orig
+        sd = {k: v.detach().cpu().numpy().copy() for k, v in w.nnet.state_dict().items()}
+        q.put((rank, {"masks": masks, "sd": sd,
+                      "rng_restored": rank != 0 and torch.equal(torch.get_rng_state(), before)}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_dropout_masks_differ_across_ranks():
+    """with dropout > 0 each rank's slice gets its own masks (the reference draws an
+    independent mask per sample of the whole batch), while the weights stay bitwise equal."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dropout_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m0, m1 = res[0]["masks"], res[1]["masks"]
+    assert len(m0) == len(m1) > 0
+    for a, b in zip(m0, m1):
+        assert a.shape == b.shape
+        assert not np.array_equal(a, b)
+        assert 0.6 < a.mean() < 0.8 and 0.6 < b.mean() < 0.8  # keep probability 0.7
+    for k in res[0]["sd"]:
+        assert np.array_equal(res[0]["sd"][k], res[1]["sd"][k]), k
+    assert res[1]["rng_restored"]  # the caller's generator state is restored after training
