@@ -37,6 +37,16 @@ from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
 from .dist import group_src
 
 
+# collective accounting of a running train_examples_dp (its `stats` dict), else None
+_STATS = None
+
+
+def _count(key, nbytes):
+    if _STATS is not None:
+        _STATS[key + "_calls"] = _STATS.get(key + "_calls", 0) + 1
+        _STATS[key + "_bytes"] = _STATS.get(key + "_bytes", 0) + int(nbytes)
+
+
 class _AllReduceSum(torch.autograd.Function):
     """SUM all-reduce whose backward all-reduces the gradient (the loss is the sum of the
     ranks' losses, each of which reads the reduced value)."""
@@ -46,12 +56,14 @@ class _AllReduceSum(torch.autograd.Function):
         ctx.group = group
         y = x.clone()
         dist.all_reduce(y, op=dist.ReduceOp.SUM, group=group)
+        _count("bn_allreduce", y.numel() * y.element_size())
         return y
 
     @staticmethod
     def backward(ctx, g):
         g = g.clone()
         dist.all_reduce(g, op=dist.ReduceOp.SUM, group=ctx.group)
+        _count("bn_allreduce", g.numel() * g.element_size())
         return g, None
 
 
@@ -175,14 +187,19 @@ def rank_dropout_seed(group=None, device=None):
     return int(buf.item()) * 1000003 + dist.get_rank(group)
 
 
-def train_examples_dp(wrapper, ex, group=None):
+def train_examples_dp(wrapper, ex, group=None, stats=None):
     """NNetWrapper.train_examples over the ranks of `group`: the reference trainer's
     epochs, batches, losses and Adam steps, each batch split evenly over the ranks
     (module docstring).  Every rank calls this with the same ExampleSet; returns the
     batches' global (l_pi, l_v) as a device tensor [batches, 2] on every rank.
 
     Dropout masks come from a generator state of this rank's own (rank_dropout_seed),
-    forked for the duration of training: the caller's torch generators are restored."""
+    forked for the duration of training: the caller's torch generators are restored.
+
+    stats: a dict that receives the collectives' accounting (bench.py --learn-iteration):
+    calls and bytes of the gradient and BatchNorm all-reduces, and the gradient
+    all-reduce's time on the compute stream (HIP events on every `stats["every"]`-th step,
+    default 10, milliseconds summed in grad_allreduce_ms over grad_allreduce_timed steps)."""
     dev = wrapper.device
     seed = rank_dropout_seed(group, dev if dist.get_backend(group) == "nccl" else None)
     devices = [dev.index if dev.index is not None else torch.cuda.current_device()] if dev.type == "cuda" else []
@@ -191,10 +208,15 @@ def train_examples_dp(wrapper, ex, group=None):
         if dev.type == "cuda":
             with torch.cuda.device(devices[0]):
                 torch.cuda.manual_seed(seed)
-        return _train_examples_dp(wrapper, ex, group)
+        global _STATS
+        _STATS = stats
+        try:
+            return _train_examples_dp(wrapper, ex, group, stats)
+        finally:
+            _STATS = None
 
 
-def _train_examples_dp(wrapper, ex, group):
+def _train_examples_dp(wrapper, ex, group, stats=None):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     a = wrapper.args
@@ -230,7 +252,15 @@ def _train_examples_dp(wrapper, ex, group):
                 (l_pi + l_v).backward()
                 grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
                 flat = _flatten_dense_tensors(grads + [torch.stack([l_pi.detach(), l_v.detach()]).float()])
+                timed = stats is not None and dev.type == "cuda" and k % int(stats.get("every", 10)) == 0
+                if timed:
+                    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    ev0.record()
                 dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+                _count("grad_allreduce", flat.numel() * flat.element_size())
+                if timed:
+                    ev1.record()
+                    stats.setdefault("_events", []).append((ev0, ev1))
                 parts = _unflatten_dense_tensors(flat, grads + [losses[k]])
                 for p, g in zip(params, parts[:-1]):
                     if p.grad is None:
@@ -243,6 +273,13 @@ def _train_examples_dp(wrapper, ex, group):
     finally:
         for mod, name, child in swapped:
             setattr(mod, name, child)
+    if stats is not None:
+        evs = stats.pop("_events", [])
+        if evs:
+            torch.cuda.synchronize(dev)
+            stats["grad_allreduce_ms"] = sum(a.elapsed_time(b) for a, b in evs)
+            stats["grad_allreduce_timed"] = len(evs)
+        stats["steps"] = k
     return losses
 
 

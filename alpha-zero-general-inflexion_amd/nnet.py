@@ -223,6 +223,27 @@ def _fold_bn(weight, bias, bn):
     return w.float(), b.float()
 
 
+# Activation range the split-fp16 operands keep full precision in: an activation v is split
+# into hi = fp16(v), lo = fp16(v - hi); for |v| < 2^-3 lo falls into fp16's subnormals and v
+# keeps an absolute error of 2^-25 instead of a relative one of 2^-22, and |v| > 65504
+# overflows (the range flag, check_range).  Layers whose BatchNorm puts the activations
+# outside ACT_BAND are rescaled by a power of two so their estimate lands at ACT_TARGET.
+ACT_BAND = (0.5, 1024.0)
+ACT_TARGET = 8.0
+
+
+def act_exponent(bn):
+    """Power-of-two exponent e for the activations relu(BN(x)) of one layer: 0 if the
+    BatchNorm's own estimate of their size, max over channels of beta + 3 |gamma| (on data
+    like the running statistics' the pre-activation is N(beta, gamma^2) per channel), lies in
+    ACT_BAND, else round(log2(ACT_TARGET / estimate)).  Random-init BatchNorm (gamma 1, beta 0)
+    gives 3: unscaled.  A layer whose every channel is dead (estimate 0) stays unscaled."""
+    est = float((bn.bias.detach().double() + 3.0 * bn.weight.detach().double().abs()).clamp_min(0.0).max())
+    if est <= 0.0 or ACT_BAND[0] <= est <= ACT_BAND[1]:
+        return 0
+    return int(max(-30, min(30, round(np.log2(ACT_TARGET / est)))))
+
+
 class InferenceNet(nn.Module):
     """Inference form of InflexionNNet for the leaf batches (eval semantics only).
 
@@ -273,11 +294,19 @@ class InferenceNet(nn.Module):
         self.fuse_transforms = True  # conv2->3->4: output + next input transform in one pass
         self.n, self.depth, c = net.n, net.depth, net.num_channels
         self.pads = []
+        # power-of-two activation scales (act_exponent): layer i's folded weights and bias carry
+        # 2^(e_i - e_(i-1)) and 2^e_i, so its output is 2^e_i relu(BN(conv)) exactly (ReLU is
+        # positively homogeneous and the scalings are exact in f32); [fc3 | fc4] undo the last one
+        self.act_exp = {}
+        e_prev = 0
         h = net.n  # input side of conv i
         for i in range(1, 5):
             conv_i, bn = getattr(net, f"conv{i}"), getattr(net, f"bn{i}")
             h_out = h + 2 * conv_i.padding[0] - 2
             w, b = _fold_bn(conv_i.weight.detach(), conv_i.bias.detach(), bn)
+            e = act_exponent(bn)
+            w, b = w * 2.0 ** (e - e_prev), b * 2.0 ** e
+            self.act_exp[i], e_prev = e, e
             self.register_buffer(f"w{i}", w.contiguous(memory_format=torch.channels_last))
             self.register_buffer(f"b{i}", b)
             # [9*Cin, Cout] k-major copy for the libazg implicit GEMM (k = (dy*3+dx)*Cin + c)
@@ -295,6 +324,9 @@ class InferenceNet(nn.Module):
             h = h_out
         s = net.n - 4
         w1, b1 = _fold_bn(net.fc1.weight.detach(), net.fc1.bias.detach(), net.fc_bn1)
+        e = act_exponent(net.fc_bn1)
+        w1, b1 = w1 * 2.0 ** (e - e_prev), b1 * 2.0 ** e
+        self.act_exp["fc1"], e_prev = e, e
         w1 = w1.reshape(-1, c, s, s).permute(0, 2, 3, 1).reshape(w1.shape[0], -1)  # (c,h,w) -> (h,w,c)
         self.register_buffer("fw1", w1.contiguous())
         # fc1 as a split-fp16 GEMM (with a split GEMM form): conv4's output transform
@@ -317,11 +349,14 @@ class InferenceNet(nn.Module):
                 self.register_buffer("fw1_sk", split2_rows(hp, lp))  # [parts][N][2 chunk]
         self.register_buffer("fb1", b1)
         w2, b2 = _fold_bn(net.fc2.weight.detach(), net.fc2.bias.detach(), net.fc_bn2)
+        e = act_exponent(net.fc_bn2)
+        w2, b2 = w2 * 2.0 ** (e - e_prev), b2 * 2.0 ** e
+        self.act_exp["fc2"], e_prev = e, e
         self.register_buffer("fw2", w2.contiguous())
         self.register_buffer("fb2", b2)
-        self.register_buffer("fw3", net.fc3.weight.detach().clone())
+        self.register_buffer("fw3", net.fc3.weight.detach() * 2.0 ** -e_prev)
         self.register_buffer("fb3", net.fc3.bias.detach().clone())
-        self.register_buffer("fw4", net.fc4.weight.detach().clone())
+        self.register_buffer("fw4", net.fc4.weight.detach() * 2.0 ** -e_prev)
         self.register_buffer("fb4", net.fc4.bias.detach().clone())
         # fc3 and fc4 read the same activation: one GEMM over their stacked rows
         self.register_buffer("fw34", torch.cat([self.fw3, self.fw4], dim=0).contiguous())
@@ -910,7 +945,7 @@ class NNetWrapper:
                 (l_pi + l_v).backward()
                 opt.step()
 
-    def train_examples(self, ex, group=None):
+    def train_examples(self, ex, group=None, stats=None):
         """NNet.py:36-76 on an ExampleSet already resident on the device: the same
         Adam, epochs and batch draws (np.random.randint on numpy's global stream,
         so the sampled batches are the reference's), with the batch gathered on
@@ -920,12 +955,13 @@ class NNetWrapper:
         group: a torch.distributed group of more than one rank trains data-parallel
         (ddp.train_examples_dp: each batch split over the ranks, whole-batch
         BatchNorm statistics, one gradient all-reduce per step); every rank of the
-        group calls this with the same examples."""
+        group calls this with the same examples.  stats: a dict that receives the step
+        count (and, data-parallel, the collectives' accounting)."""
         if group is not None:
             import torch.distributed as dist
             if dist.get_world_size(group) > 1:
                 from .ddp import train_examples_dp
-                return train_examples_dp(self, ex, group)
+                return train_examples_dp(self, ex, group, stats=stats)
         opt = self._adam()
         bs = self.args["batch_size"]
         E = len(ex)
@@ -950,6 +986,8 @@ class NNetWrapper:
                 losses[k, 0] = l_pi.detach()
                 losses[k, 1] = l_v.detach()
                 k += 1
+        if stats is not None:
+            stats["steps"] = k
         return losses
 
     def save_checkpoint(self, folder="checkpoint", filename="checkpoint.pth.tar"):

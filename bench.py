@@ -157,6 +157,15 @@ def parse():
                    help="after the timed steps, restart every game and time one whole generation (all games to "
                         "their end): measured games/s in games_per_s.  auto: on for 7x7 Inflexion at <= 25 sims "
                         "(C2, C4: ~16 s), off for the 100-200-sim configs")
+    p.add_argument("--learn-iteration", choices=["auto", "on", "off"], default="auto",
+                   help="after the generation pass, the rest of one Coach.learn iteration (Coach.py:102-153) on "
+                        "its games: the records exchanged (all-gathered over the ranks), the example window built "
+                        "on the GPU, and NNetWrapper.train_examples on it, data-parallel over the ranks; reported in "
+                        "learn_iteration (self-play / exchange / train seconds, collective bytes and time per step). "
+                        "auto: whenever the generation pass runs")
+    p.add_argument("--train-epochs", type=int, default=10, help="--learn-iteration: epochs (NNet.py:19: 10)")
+    p.add_argument("--train-window", type=int, default=200000,
+                   help="--learn-iteration: examples kept from the iteration (main.py:19 maxlenOfQueue)")
     p.add_argument("--timer-every", type=int, default=25,
                    help="record the per-kernel HIP events (roofline, time split) on every N-th simulation of the "
                         "timed region only: each event record costs ~10 us of GPU idle time, which would otherwise "
@@ -303,6 +312,82 @@ def cpu_baseline(args, depth, A):
             "sample": f"max of the two arrangements ({best}); see one_process_sample / processes_sample",
             "tree_only_value": o2["expansions"] / dt2,
             "tree_only_sample": f"same search, hash evaluator, 1 thread: {o2['expansions']} expansions in {dt2:.2f}s"}
+
+
+def learn_iteration(args, eng, net, rank, world, gen):
+    """The rest of one Coach.learn iteration (Coach.py:102-153) after the generation pass,
+    whose games are the iteration's self-play (numEps = the games per rank): the compact
+    records all-gathered over the ranks (dist.gather_records, what Coach.learn's
+    data-parallel mode sends), the last `train_window` examples built on the GPU
+    (azg_examples, Coach.py:74-90 + the deque of :107), and NNetWrapper.train_examples on
+    them (NNet.py:36-76: 10 epochs of len/512 batches, Adam), split over the ranks with one
+    gradient all-reduce per step (ddp.py).  Every phase bracketed by a barrier and a
+    synchronize; times are the max over ranks."""
+    from azg_amd.dist import gather_records
+    from azg_amd.examples import engine_examples, examples_from_records
+    from azg_amd.nnet import NNetWrapper
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    def wall(t0):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
+
+    tt = eng.cfg.temp_threshold
+    t0 = time.perf_counter()
+    sent = 0
+    if world > 1:
+        rec, sent = gather_records(eng, dst=None, temp_threshold=tt)
+        ex = examples_from_records(eng.game, eng.n, eng.cfg.max_turns, tt, *rec, "reference", args.train_window)
+    else:
+        ex = engine_examples(eng, tt, "reference", args.train_window)
+    exchange_s = wall(t0)
+    if args.game == "othello":
+        from azg_amd.othello import OthelloGame
+        game = OthelloGame(args.n)
+    else:
+        from azg_amd.inflexion import InflexionGame
+        game = InflexionGame(args.n, max_turns=args.max_turns, max_power=6)
+    w = NNetWrapper(game, {"epochs": args.train_epochs}, device=dev)
+    w.nnet.load_state_dict(net.state_dict())
+    # Coach.py:149's shuffle, the same permutation on every rank
+    perm = torch.randperm(len(ex), generator=torch.Generator().manual_seed(0)).to(dev)
+    ex = ex.index(perm)
+    np.random.seed(0)
+    stats = {"every": 10}
+    t0 = time.perf_counter()
+    w.train_examples(ex, group=dist.group.WORLD if world > 1 else None, stats=stats)
+    train_s = wall(t0)
+    steps = stats.get("steps", 0)
+    bs = int(w.args["batch_size"])
+    _, depth, _ = __import__("azg_amd.engine", fromlist=["GAMES"]).GAMES[args.game]
+    flop_ex = 3 * net_flops(args.n, depth, eng.A)[0]  # forward + backward (2x) per example
+    out = {"what": "one Coach.learn iteration (Coach.py:102-153): the generation pass as its self-play, then the "
+                   "records exchanged, the example window built on the GPU, and NNetWrapper.train_examples",
+           "ranks": world, "games": gen["games"], "selfplay_s": gen["seconds"], "exchange_examples_s": exchange_s,
+           "examples": len(ex), "epochs": args.train_epochs, "batch_size": bs, "train_s": train_s,
+           "train_steps": steps, "train_examples_per_s": steps * bs / train_s if train_s > 0 else None,
+           "train_tflops": steps * bs * flop_ex / train_s / 1e12 if train_s > 0 else None,
+           "train_flops_note": "3 x 404.3 MFLOP per example (forward + backward of InflexionNNet, SURVEY 8(a) a9)",
+           "trainer": "data-parallel over the ranks (ddp.train_examples_dp)" if world > 1 else
+                      "single-GPU NNetWrapper.train_examples",
+           "iteration_s": gen["seconds"] + exchange_s + train_s,
+           "records_sent_bytes_per_rank": sent}
+    if steps and world > 1:
+        out["grad_allreduce_bytes_per_step"] = stats.get("grad_allreduce_bytes", 0) / steps
+        out["bn_allreduce_calls_per_step"] = stats.get("bn_allreduce_calls", 0) / steps
+        out["bn_allreduce_bytes_per_step"] = stats.get("bn_allreduce_bytes", 0) / steps
+        if stats.get("grad_allreduce_timed"):
+            out["grad_allreduce_ms_per_step"] = stats["grad_allreduce_ms"] / stats["grad_allreduce_timed"]
+            out["grad_allreduce_note"] = ("HIP events on the compute stream around the gradient all-reduce, every "
+                                          f"{stats['every']}th step, rank {rank}")
+    return out
 
 
 def rank_command(n, argv, port):
@@ -505,8 +590,9 @@ def main():
     # one whole generation after the timed steps: every game restarted and played to its end
     # (random-init games all run 344 moves), all ranks at once -- games/s measured, not estimated
     gen = None
-    if not args.full_games and (args.generation == "on" or (args.generation == "auto" and args.game == "inflexion"
-                                                             and args.sims <= 25 and args.evaluator == "net")):
+    if not args.full_games and (args.generation == "on" or args.learn_iteration == "on"
+                                or (args.generation == "auto" and args.game == "inflexion"
+                                    and args.sims <= 25 and args.evaluator == "net")):
         eng.drop_graph()
         eng.reset()
         if world > 1:
@@ -528,6 +614,9 @@ def main():
         gen = {"games": G * world, "seconds": gen_s, "moves": moves}
         if eng.stats()["error"]:
             raise RuntimeError(f"engine error {eng.stats()['error']} in the generation pass")
+    learn = None
+    if gen is not None and args.learn_iteration != "off" and args.evaluator == "net":
+        learn = learn_iteration(args, eng, net, rank, world, gen)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -646,6 +735,8 @@ def main():
                            "wall_ms": elapsed * 1e3, "graph": bool(args.graph)},
             "iteration_sync_bytes": sync_bytes,
         }
+        if learn is not None:
+            out["learn_iteration"] = learn
         # the dominant kernel: libazg's split GEMM (over half of the step's GPU time), its
         # launches timed with HIP events on their stream; executed MFMA FLOPs = the GEMM work
         # (Winograd: transformed points x 2 C K per leaf; fc1-fc4: the FC layers, split-K) x 3

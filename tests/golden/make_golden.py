@@ -159,7 +159,7 @@ def gen_pairwise(np):
 
 
 # -------------------------------------------------------------------------- MCTS
-def gen_mcts(np, quick, othello=False, realnet=False, toy=False):
+def gen_mcts(np, quick, othello=False, realnet=False, toy=False, trained=False):
     """Reference Coach.executeEpisode + MCTS traces.  With othello=True the
     reference search is driven with this repo's builder-authored OthelloGame
     plugin (the reference has no Othello): the rules are ours, the search,
@@ -211,6 +211,8 @@ def gen_mcts(np, quick, othello=False, realnet=False, toy=False):
             return super().predict(board)
 
     real_nets = {}
+    if trained:
+        realnet = True
 
     class Rec:
         in_search = False
@@ -268,6 +270,13 @@ def gen_mcts(np, quick, othello=False, realnet=False, toy=False):
         }
         if quick:
             sets = {"realnet_sims100": sets["realnet_sims100"]}
+    if trained:
+        # the same configurations with the network the reference trains on its own
+        # self-play (trained_net.npz, gen_trained_net): Coach.learn's second iteration
+        sets = {
+            "trained_main": dict(max_turns=343, sims=25, cpuct=1, temp_threshold=30, seeds=list(range(8))),
+            "trained_sims100": dict(max_turns=40, sims=100, cpuct=1, temp_threshold=30, seeds=[10, 11]),
+        }
     if othello:
         sets = {
             "othello6": dict(n=6, sims=25, cpuct=1, temp_threshold=15, seeds=list(range(500, 516))),
@@ -298,6 +307,8 @@ def gen_mcts(np, quick, othello=False, realnet=False, toy=False):
                     import torch
                     torch.manual_seed(0)  # Inflexion 7x7: the network of nnet_golden.npz (gen_nnet)
                     real_nets[key] = CountingNNet(game)
+                    if trained:
+                        load_trained(np, real_nets[key].nnet)
                 nnet = real_nets[key]
                 nnet.calls = 0
             else:
@@ -444,7 +455,7 @@ def gen_nnet(np, InflexionGame):
 
 
 # --------------------------------------------------------------- realnet sensitivity
-def gen_realnet_sensitivity(np, othello=False):
+def gen_realnet_sensitivity(np, othello=False, trained=False):
     """How far do the reference's own real-network traces survive a change of its
     network far below the north_star's 1e-5 tolerance?  The reference Coach/MCTS
     (main.py's configuration, the seeds of mcts_realnet_main) is rerun with
@@ -475,7 +486,7 @@ def gen_realnet_sensitivity(np, othello=False):
         bases = ["realnet_othello6", "realnet_othello8", "realnet_othello8_s200"]
         kinds = ("weights",)
     else:
-        bases = ["realnet_main"]
+        bases = ["trained_main" if trained else "realnet_main"]
         kinds = ("weights", "outputs")
 
     class NoisyNNet(NNetWrapper):
@@ -509,6 +520,8 @@ def gen_realnet_sensitivity(np, othello=False):
             for eps in (1e-7, 1e-6):
                 torch.manual_seed(0)
                 net = NoisyNNet(game0)
+                if trained:
+                    load_trained(np, net.nnet)
                 NoisyNNet.eps = eps if kind == "outputs" else 0.0
                 if kind == "weights":
                     g = torch.Generator().manual_seed(12345)
@@ -537,10 +550,11 @@ def gen_realnet_sensitivity(np, othello=False):
                           flush=True)
     if not othello:
         out["config"] = cfg
-    _dump("realnet_sensitivity_othello.json.gz" if othello else "realnet_sensitivity.json.gz", out)
+    _dump("realnet_sensitivity_othello.json.gz" if othello else
+          ("trained_sensitivity.json.gz" if trained else "realnet_sensitivity.json.gz"), out)
 
 
-def gen_realnet_branches(np):
+def gen_realnet_branches(np, trained=False):
     """The other side of each certified near-tie: for every (eps, seed) whose reference trace
     diverges under the 1e-7 / 1e-6 weight perturbation of gen_realnet_sensitivity, the
     perturbed reference's whole trace from its first divergent move on (counts, action, turn,
@@ -554,8 +568,10 @@ def gen_realnet_branches(np):
     from inflexion.pytorch.NNet import NNetWrapper
     from utils import dotdict
 
-    base = json.load(gzip.open(os.path.join(HERE, "mcts_realnet_main.json.gz"), "rt"))
-    sens = json.load(gzip.open(os.path.join(HERE, "realnet_sensitivity.json.gz"), "rt"))
+    bname = "trained_main" if trained else "realnet_main"
+    base = json.load(gzip.open(os.path.join(HERE, f"mcts_{bname}.json.gz"), "rt"))
+    sens = json.load(gzip.open(os.path.join(HERE, "trained_sensitivity.json.gz" if trained
+                                            else "realnet_sensitivity.json.gz"), "rt"))
     cfg = base["config"]
     game0 = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
     rec = {"actions": [], "last": None, "in_search": False}
@@ -586,12 +602,14 @@ def gen_realnet_branches(np):
     out = {"config": cfg, "branches": []}
     try:
         for eps in (1e-7, 1e-6):
-            todo = [r for r in sens["runs"] if r.get("set", "realnet_main") == "realnet_main"
+            todo = [r for r in sens["runs"] if r.get("set", "realnet_main") == bname
                     and r["kind"] == "weights" and r["eps"] == eps and r["first_divergent_move"] is not None]
             if not todo:
                 continue
             torch.manual_seed(0)
             net = NNetWrapper(game0)
+            if trained:
+                load_trained(np, net.nnet)
             g = torch.Generator().manual_seed(12345)  # the perturbation of gen_realnet_sensitivity
             with torch.no_grad():
                 for prm in net.nnet.parameters():
@@ -620,11 +638,87 @@ def gen_realnet_branches(np):
                       f"{time.time() - t0:.1f}s", flush=True)
     finally:
         InflexionGame.to_next_state = orig_tns
-    _dump("realnet_branches.json.gz", out)
+    _dump("trained_branches.json.gz" if trained else "realnet_branches.json.gz", out)
+
+
+# ------------------------------------------------------------------ trained network
+TRAINED_CFG = dict(example_seeds=[1000, 1001, 1002], max_turns=343, sims=25, cpuct=1, temp_threshold=30,
+                   init_seed=0, batch_seed=17, torch_seed=23, pairs=64, pair_seed=5)
+TRAINED_FILE = "trained_net.npz"
+
+
+def load_trained(np, module):
+    """Load trained_net.npz's state_dict into a reference (or this repo's) InflexionNNet."""
+    import torch
+    d = np.load(os.path.join(HERE, TRAINED_FILE))
+    sd = {k[3:].replace("__", "."): torch.from_numpy(d[k].copy()) for k in d.files if k.startswith("sd_")}
+    module.load_state_dict(sd)
+
+
+def gen_trained_net(np, InflexionGame):
+    """The network the reference's own loop trains (Coach.learn, Coach.py:102-153): the
+    512-channel InflexionNNet under torch.manual_seed(0) (the realnet network) plays
+    len(example_seeds) reference Coach.executeEpisode episodes at main.py's settings, and
+    the reference NNetWrapper.train (NNet.py:36-76, its own args: Adam lr 1e-3, dropout 0.3,
+    10 epochs of batch 512) trains it on their examples -- the network MCTS(self.nnet, ...)
+    searches with in the second iteration (Coach.py:110).  Written as data: every tensor of
+    its state_dict (running BatchNorm statistics included), plus (planes -> P, v) pairs
+    of its batch-1 predict on positions of random playouts, and the prior statistics that
+    show the training took (max prior, entropy at the initial position)."""
+    import torch
+    import MCTS as mcts_mod
+    from Coach import Coach
+    from inflexion.pytorch.NNet import NNetWrapper
+    from utils import dotdict
+    c = TRAINED_CFG
+    game = InflexionGame(7, max_turns=c["max_turns"], max_power=6)
+    torch.manual_seed(c["init_seed"])
+    w = NNetWrapper(game)
+    args = dotdict({"numMCTSSims": c["sims"], "cpuct": c["cpuct"], "tempThreshold": c["temp_threshold"]})
+    examples = []
+    t0 = time.time()
+    for seed in c["example_seeds"]:
+        np.random.seed(seed)
+        examples += Coach(game, w, args).executeEpisode((game.restarted(), mcts_mod.MCTS(w, args)))
+        print(f"  trained: episode {seed}: {len(examples)} examples, {time.time() - t0:.0f}s", flush=True)
+    p0, _ = w.predict(game.restarted().to_planes())
+    np.random.seed(c["batch_seed"])
+    torch.manual_seed(c["torch_seed"])
+    w.train(examples)
+    print(f"  trained: training done, {time.time() - t0:.0f}s", flush=True)
+    sd = w.nnet.state_dict()
+    rs = np.random.RandomState(c["pair_seed"])
+    planes, g = [], game.restarted()
+    while len(planes) < c["pairs"]:
+        p = g.to_planes()
+        planes.append(g.random_symmetry(p) if len(planes) % 2 else p)
+        v = np.nonzero(g.valid_actions_mask())[0]
+        g = g.to_next_state(int(v[rs.randint(len(v))]))
+        if g.outcome.value != 0:
+            g = game.restarted()
+    planes = np.array(planes, np.int64)
+    P, V = [], []
+    for p in planes:
+        pi, v = w.predict(p)
+        P.append(pi)
+        V.append(v[0])
+    p1, _ = w.predict(game.restarted().to_planes())
+
+    def entropy(p):
+        q = p[p > 0].astype(np.float64)
+        return float(-(q * np.log(q)).sum())
+    arrays = {"sd_" + k.replace(".", "__"): v.detach().cpu().numpy() for k, v in sd.items()}
+    path = os.path.join(HERE, TRAINED_FILE)
+    np.savez_compressed(path, planes=planes.astype(np.int16), P=np.array(P, np.float32), v=np.array(V, np.float32),
+                        n_examples=np.int64(len(examples)), init_max_prior=np.float32(p0.max()),
+                        init_entropy=np.float64(entropy(p0)), trained_max_prior=np.float32(p1.max()),
+                        trained_entropy=np.float64(entropy(p1)), **arrays)
+    print(f"wrote {path} {os.path.getsize(path)} bytes; initial position: max prior {p0.max():.4g} -> {p1.max():.4g}, "
+          f"entropy {entropy(p0):.4g} -> {entropy(p1):.4g}", flush=True)
 
 
 # ------------------------------------------------------------------------- train
-TRAIN_CFG = dict(max_turns=30, sims=8, cpuct=1.0, temp_threshold=10, seed=3, num_channels=32, epochs=2,
+TRAIN_CFG =dict(max_turns=30, sims=8, cpuct=1.0, temp_threshold=10, seed=3, num_channels=32, epochs=2,
                  batch_seed=11, torch_seed=5, init_seed=0, proj_seed=99)
 
 
@@ -808,6 +902,10 @@ def main():
         "sensitivity": lambda: gen_realnet_sensitivity(np),
         "sensitivity_othello": lambda: gen_realnet_sensitivity(np, othello=True),
         "branches": lambda: gen_realnet_branches(np),
+        "trained_net": lambda: gen_trained_net(np, InflexionGame),
+        "trained": lambda: gen_mcts(np, quick, trained=True),
+        "trained_sensitivity": lambda: gen_realnet_sensitivity(np, trained=True),
+        "trained_branches": lambda: gen_realnet_branches(np, trained=True),
     }
     for name, fn in jobs.items():
         if only and name not in only:

@@ -155,3 +155,13 @@ def golden_counts(move, A=343):
     for a, k in move["counts"]:
         c[a] = k
     return c
+
+
+def trained_net(module):
+    """Load tests/golden/trained_net.npz (the network the reference trains on its own self-play,
+    make_golden.py trained_net) into an InflexionNNet; returns the module."""
+    import torch
+    d = np.load(os.path.join(GOLDEN, "trained_net.npz"))
+    sd = {k[3:].replace("__", "."): torch.from_numpy(d[k].copy()) for k in d.files if k.startswith("sd_")}
+    module.load_state_dict(sd)
+    return module

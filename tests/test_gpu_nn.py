@@ -203,6 +203,111 @@ def test_split_gemm_error_not_above_f32():
     assert errs["split_blas"] <= 1.5 * errs["f32"], errs
 
 
+def _rescaled(net, layer, factor, nxt):
+    """`net` with BatchNorm `layer`'s gamma, beta times `factor` and the next layer's weights
+    divided by it: the same function, its activations between the two layers `factor` times smaller."""
+    import copy
+    out = copy.deepcopy(net)
+    with torch.no_grad():
+        bn = getattr(out, layer)
+        bn.weight.mul_(factor)
+        bn.bias.mul_(factor)
+        for name in (nxt if isinstance(nxt, tuple) else (nxt,)):
+            getattr(out, name).weight.div_(factor)
+    return out
+
+
+def _split_errors(net, x, band=None):
+    """Max relative P error and max absolute v error of the split / f32-GEMM forms against an f64
+    forward of `net` (band: nnet.ACT_BAND for the call, e.g. (0, inf) = no activation scaling)."""
+    import azg_amd.nnet as nn_mod
+    ref = type(net)().cuda().eval().double()
+    ref.load_state_dict(net.state_dict())
+    saved = nn_mod.ACT_BAND
+    if band is not None:
+        nn_mod.ACT_BAND = band
+    try:
+        with torch.no_grad():
+            logp, v64 = ref(x.double())
+            p64 = torch.exp(logp)
+            out = {}
+            for gemm in ("split", "f32"):
+                fast = nn_mod.InferenceNet(net, gemm=gemm).cuda()
+                p, v = fast(x)
+                fast.check_range()
+                out[gemm] = (((p.double() - p64).abs() / p64).max().item(),
+                             (v.double().reshape(-1) - v64.reshape(-1)).abs().max().item())
+    finally:
+        nn_mod.ACT_BAND = saved
+    return out
+
+
+@pytest.mark.parametrize("layer,nxt", [("bn1", "conv2"), ("bn2", "conv3"), ("bn3", "conv4"), ("bn4", "fc1"),
+                                       ("fc_bn1", "fc2"), ("fc_bn2", ("fc3", "fc4"))])
+def test_split_gemm_error_small_activations(layer, nxt):
+    """a split-GEMM operand below 2^-3 has its low half in fp16's subnormals.
+    A network whose BatchNorm shrinks one layer's activations by 1e-5 (the next layer's weights
+    grown to match: the same function) is evaluated with that layer rescaled by a power of two
+    (nnet.act_exponent), and its split forward stays within the f32-GEMM form's error and the
+    north_star's 1e-5 of an f64 forward -- 1024 leaves (split-K fc1 and the split FC tail).
+    Unscaled (ACT_BAND disabled) the same network's error is printed for comparison (CPU model,
+    tools/wino_error_sim.py: P 8.8e-6, v 4.3e-6 at conv3's input)."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InflexionNNet
+    torch.manual_seed(6)
+    net = _rescaled(InflexionNNet().cuda().eval(), layer, 1e-5, nxt).eval()
+    x = (torch.rand(1024, 4, 7, 7, device="cuda") < 0.3).float()
+    scaled = _split_errors(net, x)
+    unscaled = _split_errors(net, x, band=(0.0, float("inf")))
+    print(f"{layer} x 1e-5: scaled split P {scaled['split'][0]:.3g} v {scaled['split'][1]:.3g} (f32 GEMMs P "
+          f"{scaled['f32'][0]:.3g} v {scaled['f32'][1]:.3g}); unscaled split P {unscaled['split'][0]:.3g} "
+          f"v {unscaled['split'][1]:.3g}")
+    assert scaled["split"][0] < 1e-5 and scaled["split"][1] < 1e-5, scaled
+    assert scaled["split"][0] <= 1.5 * scaled["f32"][0] + 1e-7, scaled
+    assert scaled["split"][1] <= 1.5 * scaled["f32"][1] + 1e-7, scaled
+
+
+def test_split_gemm_error_trained_network():
+    """The split forward on the network the reference trains on its own self-play
+    (tests/golden/trained_net.npz, make_golden.py trained_net): within the f32-GEMM form's
+    error and 1e-5 of an f64 forward, on 1024 leaves of the positions of random playouts and
+    their random symmetries plus random planes."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InflexionNNet
+    net = ol.trained_net(InflexionNNet()).cuda().eval()
+    d = np.load(os.path.join(ol.GOLDEN, "trained_net.npz"))
+    pos = torch.from_numpy(d["planes"].astype(np.float32)).cuda()
+    rnd = (torch.rand(1024 - pos.shape[0], 4, 7, 7, device="cuda") < 0.3).float()
+    rnd[:, 2:] = rnd[:, 2:, :1, :1]  # the turn and can_spawn planes are constant
+    x = torch.cat([pos, rnd])
+    e = _split_errors(net, x)
+    print(f"trained network: split P {e['split'][0]:.3g} v {e['split'][1]:.3g}, f32 GEMMs P {e['f32'][0]:.3g} "
+          f"v {e['f32'][1]:.3g}")
+    assert e["split"][0] < 1e-5 and e["split"][1] < 1e-5, e
+    assert e["split"][0] <= 1.5 * e["f32"][0] + 1e-7, e
+    assert e["split"][1] <= 1.5 * e["f32"][1] + 1e-7, e
+
+
+@pytest.mark.parametrize("conv,gemm", [("winograd", "split"), ("winograd", "f32"), ("miopen", "f32")])
+@pytest.mark.parametrize("B", [1, 64, 1024])
+def test_inference_net_trained_network(conv, gemm, B):
+    """The inference forms on the trained network reproduce the reference NNetWrapper's batch-1
+    CPU predict on its 64 fixture positions (make_golden.py trained_net) within 1e-5; B leaves
+    (the positions tiled): the small-batch kernels at 1, the Winograd forms from 64."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    net = ol.trained_net(InflexionNNet()).cuda().eval()
+    d = np.load(os.path.join(ol.GOLDEN, "trained_net.npz"))
+    x = torch.from_numpy(d["planes"].astype(np.float32)).cuda()
+    idx = torch.arange(B, device="cuda") % x.shape[0]
+    fast = InferenceNet(net, conv=conv, gemm=gemm).cuda()
+    with torch.no_grad():
+        p, v = fast(x[idx])
+    fast.check_range()
+    np.testing.assert_allclose(p.cpu().numpy(), d["P"][idx.cpu().numpy()], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(v.cpu().numpy().ravel(), d["v"][idx.cpu().numpy()], rtol=1e-5, atol=1e-6)
+
+
 PROBE_VARIANTS = [1, 2, 3, 5, 7, 8, 11, 12, 19]  # tools/libazg_probes.so only (DESIGN 4.1)
 probes = pytest.mark.skipif(not os.environ.get("AZG_PROBES"),
                             reason="probe-only GEMM schedules: AZG_PROBES=1 (tools/Makefile builds them)")

@@ -64,16 +64,27 @@ class Args(dict):
 # per fixture set: game, board side, moves that must match before a certified near-tie may flip
 SETS = {"realnet_main": ("inflexion", 7, 40), "realnet_sims100": ("inflexion", 7, None),
         "realnet_othello6": ("othello", 6, 16), "realnet_othello8": ("othello", 8, 16),
-        "realnet_othello8_s200": ("othello", 8, 16)}
+        "realnet_othello8_s200": ("othello", 8, 16),
+        # the network the reference trains on its own self-play (make_golden.py trained_net):
+        # Coach.learn's second iteration searches with it (Coach.py:110, :152)
+        "trained_main": ("inflexion", 7, 40), "trained_sims100": ("inflexion", 7, None)}
 
 
-def _ref_net(game="inflexion", n=7):
-    """The reference's network for the game, as NNetWrapper(game) builds it under manual_seed(0)."""
+def _trained(name):
+    return name.startswith("trained")
+
+
+def _ref_net(game="inflexion", n=7, trained=False):
+    """The reference's network for the game, as NNetWrapper(game) builds it under manual_seed(0)
+    (trained: with the weights of tests/golden/trained_net.npz)."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InflexionNNet
     torch.manual_seed(0)
     if game == "inflexion":
-        return InflexionNNet().cuda().eval()
+        net = InflexionNNet()
+        if trained:
+            ol.trained_net(net)
+        return net.cuda().eval()
     return InflexionNNet(n=n, depth=2, action_size=n * n + 1).cuda().eval()
 
 
@@ -109,7 +120,8 @@ def _margin_report(net, evaluator, board, turn, player, template, batch=G_ENGINE
 
 
 def _sensitivity(name):
-    fname = "realnet_sensitivity_othello.json.gz" if "othello" in name else "realnet_sensitivity.json.gz"
+    fname = ("realnet_sensitivity_othello.json.gz" if "othello" in name else
+             "trained_sensitivity.json.gz" if _trained(name) else "realnet_sensitivity.json.gz")
     try:
         d = ol.load_json(fname)
     except FileNotFoundError:
@@ -121,10 +133,10 @@ def _sensitivity(name):
 def _branches(name):
     """The perturbed reference's traces past its divergent moves (make_golden.py `branches`):
     {(seed, move): [branch, ...]}."""
-    if name != "realnet_main":
+    if name not in ("realnet_main", "trained_main"):
         return {}
     try:
-        d = ol.load_json("realnet_branches.json.gz")
+        d = ol.load_json("trained_branches.json.gz" if _trained(name) else "realnet_branches.json.gz")
     except FileNotFoundError:
         return {}
     out = {}
@@ -206,7 +218,8 @@ def _check_episode(ep, counts, actions, n_moves, where, report, name, final=None
 
 
 DROPIN_CASES = ([("realnet_main", k) for k in range(8)] + [("realnet_sims100", 0)]
-                + [("realnet_othello6", i) for i in range(8)] + [("realnet_othello8", 0)])
+                + [("realnet_othello6", i) for i in range(8)] + [("realnet_othello8", 0)]
+                + [("trained_main", k) for k in range(8)] + [("trained_sims100", 0), ("trained_sims100", 1)])
 
 
 @pytest.mark.parametrize("form", ["module", "inference"])
@@ -230,6 +243,8 @@ def test_dropin_mcts_real_net(name, k, form):
     game = _game(name, cfg)
     torch.manual_seed(0)
     wrapper = NNetWrapper(game, device="cuda")
+    if _trained(name):
+        ol.trained_net(wrapper.nnet)
     ev = None
     if form == "inference":
         ev = InferenceNet(wrapper.nnet.eval(), conv="miopen", gemm="f32")
@@ -292,7 +307,7 @@ def test_engine_real_net(name, gemm, G):
     kind, n, _ = SETS[name]
     seeds = [ep["seed"] for ep in eps]
     assert seeds == list(range(seeds[0], seeds[0] + len(seeds)))
-    net = _ref_net(kind, n)
+    net = _ref_net(kind, n, _trained(name))
     ev = InferenceNet(net, gemm=gemm)
     game = _game(name, cfg)
     e = SelfPlayEngine(G, sims=cfg["sims"], cpuct=cfg["cpuct"], temp_threshold=cfg["temp_threshold"],

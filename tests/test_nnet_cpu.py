@@ -133,3 +133,58 @@ def test_split2_operand_blocks():
     bh, bl = split2_halves(b)
     assert scale == s2 and b.shape == (2, 256, 128)
     assert torch.equal(bh, uh.transpose(1, 2)) and torch.equal(bl, ul.transpose(1, 2))
+
+
+def _rescaled(net, layer, factor, nxt):
+    """net with BatchNorm `layer`'s gamma and beta times `factor` and the next layer's weights
+    divided by it: the same function (exactly, for a power of two), small activations between."""
+    import copy
+    out = copy.deepcopy(net)
+    with torch.no_grad():
+        bn = getattr(out, layer)
+        bn.weight.mul_(factor)
+        bn.bias.mul_(factor)
+        getattr(out, nxt).weight.div_(factor)
+    return out
+
+
+@pytest.mark.parametrize("layer,nxt", [("bn2", "conv3"), ("bn4", "fc1"), ("fc_bn1", "fc2")])
+def test_activation_scales_are_exact(layer, nxt):
+    """InferenceNet's power-of-two activation scales (nnet.act_exponent) change no f32 result:
+    a network whose BatchNorm shrinks one layer's activations by 2^-10 (the next layer's weights
+    grown by 2^10: the same function, exactly) is evaluated with that layer rescaled by 2^11 and
+    gives bit-identical P, v to the original network's inference form (f32 arithmetic is
+    invariant under exact power-of-two scalings); a random-init network is left unscaled."""
+    from azg_amd.nnet import InferenceNet
+    torch.manual_seed(0)
+    net = InflexionNNet().eval()
+    small = _rescaled(net, layer, 2.0 ** -10, nxt).eval()
+    a, b = InferenceNet(net), InferenceNet(small)
+    assert set(a.act_exp.values()) == {0}
+    key = {"bn2": 2, "bn4": 4, "fc_bn1": "fc1"}[layer]
+    assert b.act_exp[key] == 11 and all(v == 0 for k, v in b.act_exp.items() if k != key)
+    x = (torch.rand(16, 4, 7, 7, generator=torch.Generator().manual_seed(1)) < 0.3).float()
+    with torch.no_grad():
+        pa, va = a(x)
+        pb, vb = b(x)
+        lp, vr = small(x)
+    assert torch.equal(pa, pb) and torch.equal(va, vb)
+    torch.testing.assert_close(pb, torch.exp(lp), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(vb.reshape(-1), vr.reshape(-1), rtol=1e-5, atol=1e-6)
+
+
+def test_trained_network_fixture():
+    """tests/golden/trained_net.npz (make_golden.py trained_net: the reference NNetWrapper trained
+    by its own NNet.train on three of its own self-play episodes) loads into InflexionNNet, whose
+    batch-1 predict reproduces the reference's on the fixture's 64 positions; the training took:
+    the priors at the initial position are far from the random-init network's near-uniform ones."""
+    import oracle_lib as ol
+    d = np.load(os.path.join(ol.GOLDEN, "trained_net.npz"))
+    w = NNetWrapper(device="cpu")
+    ol.trained_net(w.nnet)
+    for planes, P, v in zip(d["planes"], d["P"], d["v"]):
+        p2, v2 = w.predict(planes.astype(np.int64))
+        np.testing.assert_allclose(p2, P, rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(v2[0], v, rtol=1e-5, atol=1e-6)
+    assert float(d["trained_max_prior"]) > 5 * float(d["init_max_prior"])
+    assert float(d["trained_entropy"]) < float(d["init_entropy"]) - 1.0
