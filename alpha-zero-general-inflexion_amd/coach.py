@@ -281,7 +281,22 @@ class Coach:
         else the trainer)."""
         import torch.distributed as dist
         from .examples import ExampleSet
-        ex = [e for exs, _ in self._host_selfplay(eps, 0, first) for e in exs]
+        # the ranks agree on how self-play went before the object exchange, as the native path
+        # does (ADVICE r4): a rank that raised would otherwise leave the others blocked in the
+        # gather until the process group's timeout
+        ex, err = None, None
+        try:
+            ex = [e for exs, _ in self._host_selfplay(eps, 0, first) for e in exs]
+        except Exception as e:  # noqa: BLE001 -- reported to every rank, re-raised below
+            err = e
+        dev = (torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl"
+               else torch.device("cpu"))
+        flag = torch.tensor([0 if err is None else 2], dtype=torch.int64, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if int(flag.item()):
+            if err is not None:
+                raise err
+            raise RuntimeError("host self-play failed on another rank; this rank stops with it")
         world = dist.get_world_size(group)
         if all_ranks:
             parts = [None] * world

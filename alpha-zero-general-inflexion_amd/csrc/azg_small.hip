@@ -38,6 +38,17 @@
 #include "../../include/azg.h"
 #include "azg_conv1.h"
 
+// The split-K hand-off below (partials stored with relaxed agent-scope atomic stores, every
+// wave draining them with `s_waitcnt vmcnt(0)`, one relaxed ticket per block, the last block
+// reading with relaxed agent-scope loads) relies on the gfx9 memory model as gfx950 implements
+// it: vmcnt counts stores as well as loads, and agent-scope atomic stores and loads bypass the
+// non-coherent caches (sc1), so a drained store is visible to every CU.  The HIP / C++ model
+// alone does not promise that (a target that counts stores separately, vscnt, would need the
+// release on the ticket); this file is built for gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "azg_small.hip's split-K hand-off assumes the gfx950 memory model (see the comment above)"
+#endif
+
 namespace {
 
 constexpr int SC_T = 512;  // small_conv threads

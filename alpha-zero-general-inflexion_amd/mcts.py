@@ -56,6 +56,8 @@ def fast_evaluator(module, device):
         with torch.cuda.device(device):
             ev = InferenceNet(module.to(device), conv="miopen", gemm="f32")
         _FAST[module] = [ver, ev]
+        # the pooled engines keep `ev` (~50 MB of folded weights) alive: drop them with the module
+        weakref.finalize(module, _drop_pooled, id(ev))
         return ev
     if hit[0] != ver:
         hit[1].refresh_from(module)
@@ -92,6 +94,8 @@ MAX_NODE_CAPACITY = (1 << 21) - 1  # azg_create's limit
 # and an entry is checked out by one live MCTS at a time.
 _POOL = {}
 _POOL_MAX = 2  # idle engines kept per key
+_POOL_TOTAL_MAX = 4  # idle engines kept over all keys: the least recently released go first
+_POOL_ORDER = []  # keys of the idle entries, in release order (one per entry)
 
 
 def clear_pool():
@@ -100,6 +104,44 @@ def clear_pool():
         for eng, *_ in idle:
             eng.close()
     _POOL.clear()
+    _POOL_ORDER.clear()
+
+
+def _drop_pooled(ev_id):
+    """Close the idle engines of an evaluator whose module is gone (weakref.finalize)."""
+    for key in [k for k in _POOL if k[0] == ev_id]:
+        for eng, *_ in _POOL.pop(key):
+            eng.close()
+    _POOL_ORDER[:] = [k for k in _POOL_ORDER if k[0] != ev_id]
+
+
+def _pool_put(key, entry):
+    """Keep an idle entry (at most _POOL_MAX per key, _POOL_TOTAL_MAX in all, LRU)."""
+    idle = _POOL.setdefault(key, [])
+    if len(idle) >= _POOL_MAX:
+        entry[0].close()
+        return
+    idle.append(entry)
+    _POOL_ORDER.append(key)
+    while len(_POOL_ORDER) > _POOL_TOTAL_MAX:
+        old = _POOL_ORDER.pop(0)
+        eng = _POOL[old].pop(0)[0]
+        if not _POOL[old]:
+            del _POOL[old]
+        eng.close()
+
+
+def _pool_get(key):
+    idle = _POOL.get(key)
+    if not idle:
+        return None
+    entry = idle.pop()
+    if not idle:
+        del _POOL[key]
+    # this key's most recent release (the entry just taken) leaves the LRU order
+    i = len(_POOL_ORDER) - 1 - _POOL_ORDER[::-1].index(key)
+    del _POOL_ORDER[i]
+    return entry
 
 
 def whole_game_capacity(sims, game):
@@ -154,12 +196,7 @@ class MCTS:
         """Hand this instance's engine (and graph) back to the pool."""
         if self._engine is None:
             return
-        entry = (self._engine, self._sims_graph, self._graph_sims, self._warm)
-        idle = _POOL.setdefault(self._key, [])
-        if len(idle) < _POOL_MAX:
-            idle.append(entry)
-        else:
-            self._engine.close()
+        _pool_put(self._key, (self._engine, self._sims_graph, self._graph_sims, self._warm))
         self._engine, self._sims_graph, self._warm = None, None, False
 
     def __del__(self):
@@ -176,9 +213,9 @@ class MCTS:
             cap = self.node_capacity or whole_game_capacity(self.args.numMCTSSims, game)
             ev = _evaluator_of(self.nnet, self.device, self.fast)
             self._key = self._pool_key(spec, ev, cap)
-            idle = _POOL.get(self._key)
-            if idle:
-                self._engine, self._sims_graph, self._graph_sims, self._warm = idle.pop()
+            entry = _pool_get(self._key)
+            if entry is not None:
+                self._engine, self._sims_graph, self._graph_sims, self._warm = entry
                 self._engine.reset()  # a fresh tree, as a new MCTS's empty dicts
             else:
                 self._engine = SelfPlayEngine(1, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct,

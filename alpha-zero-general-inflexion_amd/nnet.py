@@ -273,7 +273,8 @@ class InferenceNet(nn.Module):
         over [hi | lo | hi] rows) or "f32" (f32 MFMA GEMMs, hipBLASLt).
 
         small: up to SMALL_MAX_B leaves, run the whole forward on libazg's small-batch
-        kernels (azg_small.hip) instead of MIOpen / hipBLASLt (None: SMALL_PATH)."""
+        kernels (azg_small.hip) instead of MIOpen / hipBLASLt (None: SMALL_PATH) -- whatever
+        `conv` says (small=False keeps a form's library path at a few leaves too)."""
         super().__init__()
         if conv not in ("miopen", "azg", "auto", "winograd"):
             raise ValueError(f"unknown conv implementation {conv!r}")
@@ -793,10 +794,27 @@ class InferenceNet(nn.Module):
                                      ctypes.c_void_p(tickets.data_ptr() + 4 * (tickets.numel() - 1)), st))
         return p, v
 
+    def _small_ok(self, planes):
+        """Whether the small-batch kernels take this forward: at most SMALL_MAX_B leaves and
+        every precondition azg_small.hip's entry points check (the 3x3 layers: pad <= 1, a side
+        <= 16 with <= 256 output pixels, an even channel count; the FC layers and the heads:
+        K % 4 == 0 and row strides % 4 == 0, at most 1023 actions).  Any other shape takes the
+        library / Winograd path instead of an AZG_ERR_ARG."""
+        if not (self.small_path and planes.is_cuda and planes.shape[0] <= SMALL_MAX_B):
+            return False
+        C, A, n = self.w1.shape[0], self.fw3.shape[0], self.n
+        h = n
+        for pad in self.pads:
+            if pad > 1 or h > 16 or (h + 2 * pad - 2) ** 2 > 256 or h + 2 * pad - 2 <= 0:
+                return False
+            h = h + 2 * pad - 2
+        return (C % 2 == 0 and A <= 1023 and (h * h * C) % 4 == 0 and self.fw1.shape[1] == h * h * C
+                and self.fw2.shape[1] % 4 == 0 and self.fw34.shape[1] % 4 == 0)
+
     def forward(self, s):
         planes = s.view(-1, self.depth, self.n, self.n)
-        if (self.small_path and planes.is_cuda and planes.shape[0] <= SMALL_MAX_B and self.fw3.shape[0] <= 1024
-                and self.w1.shape[0] % 2 == 0 and planes.shape[-1] ** 2 * planes.shape[0] <= 256):
+        # the small-batch kernels whenever they apply -- for every conv form, conv="miopen" included
+        if self._small_ok(planes):
             return self._forward_small(planes)
         x = planes
         hook = self.conv_hook

@@ -205,3 +205,48 @@ def test_sparse_gather_rebuilds_examples_world2():
     assert res[0]["same"]
     for r in (0, 1):  # <= 15% of the dense int16 gather
         assert res[r]["sent"] <= 0.15 * res[r]["dense"], (res[r]["sent"], res[r]["dense"])
+
+
+def _host_fail_worker(rank, world, port, q):
+    """Rank 1's host self-play raises; every rank must raise instead of rank 0 waiting in the gather."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import azg_amd  # noqa: F401
+        from azg_amd.coach import Coach
+
+        class A(dict):
+            __getattr__ = dict.__getitem__
+        c = Coach(None, "stub", A(numEps=1, maxlenOfQueue=100, numMCTSSims=2, cpuct=1, tempThreshold=1))
+
+        def host(num_games, seed_base, first_game, evaluator=None):
+            if rank == 1:
+                raise ValueError("rank 1 failed")
+            return []
+        c._host_selfplay = host
+        try:
+            c._host_selfplay_iteration(0, 1, None, True)
+            q.put((rank, "returned"))
+        except ValueError as e:
+            q.put((rank, f"ValueError {e}"))
+        except RuntimeError as e:
+            q.put((rank, f"RuntimeError {e}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_selfplay_failure_reaches_every_rank():
+    """the multi-rank host path (plugins without native rules) agrees on failure
+    before its object gather, as the native path does: the failing rank re-raises its error,
+    the others raise too instead of blocking until the process group's timeout."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_fail_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[1] == "ValueError rank 1 failed"
+    assert res[0].startswith("RuntimeError host self-play failed on another rank")

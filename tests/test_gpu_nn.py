@@ -798,3 +798,22 @@ def test_split_form_under_expandable_segments():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("A,C", [(1024, 64), (343, 6), (343, 10)])
+def test_small_path_gate_falls_back(A, C):
+    """shapes the small-batch kernels reject (1024 actions: azg_small_heads takes at
+    most 1023; 6 or 10 channels: fc1's K = 9 C is not a multiple of 4) take the library path at
+    one leaf instead of raising AZG_ERR_ARG, and still match the module."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    torch.manual_seed(8)
+    net = InflexionNNet(action_size=A, num_channels=C).cuda().eval()
+    fast = InferenceNet(net, conv="miopen", gemm="f32").cuda()
+    x = (torch.rand(1, 4, 7, 7, device="cuda") < 0.3).float()
+    assert not fast._small_ok(x)
+    with torch.no_grad():
+        p, v = fast(x)
+        logp, v_ref = net(x)
+    torch.testing.assert_close(p, torch.exp(logp), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(v.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
