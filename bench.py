@@ -38,7 +38,7 @@ F32_MFMA_PEAK_TF = 157.3         # MI355X_MICROARCH.md: f32 matrix peak (dense)
 F16_MFMA_PEAK_TF = 2500.0        # MI355X_MICROARCH.md: BF16/FP16 MFMA peak (dense)
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E spec peak
 EXPANSIONS_PER_GAME_REF = 8555   # reference random-init Inflexion episodes
-GEMM_PMC_FILE = os.path.join(ROOT, "profiles", "r03_split_gemm_pmc_v4.json")  # the azg_split_gemm default
+GEMM_PMC_FILE = os.path.join(ROOT, "profiles", "r05_split_gemm_pmc_v4.json")  # the azg_split_gemm default (round 5 tree)
 # PMC passes of the current Winograd tiling (F(4,3)+F(3,3) / F(5,3) / F(3,3)); the r01 files
 # were measured on the earlier F(3,3)/F(2,3) tiling and are kept for the record only
 PMC_FILE_WINOGRAD = {"split": os.path.join(ROOT, "profiles", "r04_pmc_G4096_winograd_split.json")}
