@@ -74,6 +74,57 @@ __global__ __launch_bounds__(256) void fc_act_split_kernel(const float4* __restr
     if (bad) atomicOr(overflow, 1);
 }
 
+// fc_act with the GEMM's partial products TRANSPOSED, m [parts][n][rows] (the small-batch fc1,
+// computed as W x A^T so each weight tile is read once: nnet.InferenceNet._fc_split_azg): a block
+// takes 64 features x 64 rows, sums the parts in order with loads along the rows, turns the tile
+// through LDS and writes y = relu(bias + scale m) as the next layer's AZG_WINO_SPLIT2 K-parts
+// ([out_parts][rows][2 n / out_parts], 32-channel [hi | lo] blocks), as fc_act_split_kernel.
+__global__ __launch_bounds__(256) void fc_act_t_kernel(const float* __restrict__ m, int parts, long long pstride,
+                                                       const float* __restrict__ bias, float scale,
+                                                       unsigned short* __restrict__ out, int rows, int n, int relu,
+                                                       int out_parts, int* overflow) {
+    __shared__ float s[64][65];
+    const int t = threadIdx.x, f0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+    {
+        const int r = t & 63, fg = t >> 6;
+#pragma unroll 4
+        for (int j = 0; j < 16; ++j) {
+            const int f = fg + 4 * j;
+            const float* p = m + (long long)(f0 + f) * rows + r0 + r;
+            float x = p[0];
+            for (int q = 1; q < parts; ++q) x += p[q * pstride];  // split-K parts, in order
+            s[f][r] = x;
+        }
+    }
+    __syncthreads();
+    const int r = t >> 2, sub = t & 3;  // row, 16 features
+    const int np = n / out_parts, part = f0 / np, cc = f0 - part * np;  // 64 features never straddle a part
+    unsigned short* row = out + ((long long)part * rows + r0 + r) * 2 * np + 2 * cc;
+    bool bad = false;
+    unsigned short hi[16], lo[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int f = 16 * sub + j;
+        float y = bias[f0 + f] + scale * s[f][r];
+        if (relu) y = fmaxf(y, 0.f);
+        const _Float16 h = (_Float16)y;
+        const _Float16 l = (_Float16)(y - (float)h);
+        hi[j] = __builtin_bit_cast(unsigned short, h);
+        lo[j] = __builtin_bit_cast(unsigned short, l);
+        bad |= !(fabsf(y) <= 65504.f);
+    }
+    const int o = 64 * (sub >> 1) + 16 * (sub & 1);  // block sub / 2, hi half at its 16 features
+    using u16x8 = __attribute__((ext_vector_type(8))) unsigned short;
+    u16x8 a, b, c, d;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = hi[j], b[j] = hi[8 + j], c[j] = lo[j], d[j] = lo[8 + j];
+    *(u16x8*)(row + o) = a;
+    *(u16x8*)(row + o + 8) = b;
+    *(u16x8*)(row + o + 32) = c;
+    *(u16x8*)(row + o + 40) = d;
+    if (bad) atomicOr(overflow, 1);
+}
+
 constexpr int PV_MAX_PER_LANE = 16;  // up to 1024 actions per leaf (9x9 Inflexion: 567)
 
 template <int PV_PER_LANE>
@@ -143,6 +194,18 @@ extern "C" int azg_fc_act(const float* m, int32_t parts, int64_t part_stride, co
         hipLaunchKernelGGL(fc_act_split_kernel<AZG_WINO_SPLIT2>, grid, dim3(256), 0, (hipStream_t)stream,
                            (const float4*)m, parts, (long long)(part_stride / 4), (const float4*)bias, scale,
                            (ushort4*)out, (long long)rows, n / 4, relu, out_parts, overflow);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+extern "C" int azg_fc_act_t(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale,
+                            void* out, int32_t rows, int32_t n, int32_t relu, int32_t out_parts, int32_t* overflow,
+                            void* stream) {
+    if (!m || !bias || !out || !azg_device_writable(overflow) || rows <= 0 || rows % 64 || n <= 0 || n % 64 ||
+        parts < 1 || (parts > 1 && part_stride < (int64_t)rows * n) || out_parts < 1 || n % out_parts ||
+        (n / out_parts) % 64 || ((uintptr_t)out & 15))
+        return AZG_ERR_ARG;
+    hipLaunchKernelGGL(fc_act_t_kernel, dim3(n / 64, rows / 64), dim3(256), 0, (hipStream_t)stream, m, parts,
+                       (long long)part_stride, bias, scale, (unsigned short*)out, rows, n, relu, out_parts, overflow);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 

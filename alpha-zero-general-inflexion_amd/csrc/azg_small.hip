@@ -30,7 +30,7 @@
 // (tests/test_gpu_nn.py::test_small_forward_matches_reference).  The softmax / tanh heads are
 // azg_policy_value (azg_heads.hip).  Replaces round 3's split-K partial / reduce GEMMs and
 // one-launch layer (3.4-3.7 ms per 25-simulation drop-in call against the library form's
-// 3.0).
+// 3.0; HISTORY.md 6b).
 #include <hip/hip_runtime.h>
 
 #include <type_traits>

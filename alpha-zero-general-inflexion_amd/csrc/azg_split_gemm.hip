@@ -563,7 +563,7 @@ __global__ __launch_bounds__(512, 1) void split_gemm_persist_kernel(SGArgs g) {
 #ifdef AZG_SG_PROBES
 // ---------------------------------------------------------------------------
 // Probe-only schedules (variants 1, 2, 3, 5-8, 10-12, 15, 16, 19): measured, recorded in
-// DESIGN.md 4.1 / 6b, none faster than variant 4.  Built only into tools/libazg_probes.so
+// HISTORY.md 4.1 / 6b, none faster than variant 4.  Built only into tools/libazg_probes.so
 // (tools/Makefile, -DAZG_SG_PROBES), never into the product libazg.so.
 // Variant 12: ping-pong with the DMA split evenly and one stage stream across tiles.
 // Waves 0-3 (X, rows 0-127 of the tile, one per SIMD) and 4-7 (Y, rows 128-255) run

@@ -1,0 +1,415 @@
+// azg_wino_train.hip -- the trainer's 3x3 convolutions (NNetWrapper.train, NNet.py:36-76:
+// conv2-4 of InflexionNNet.py:39-45 forward and backward) on the Winograd transforms and
+// libazg's split-fp16 GEMM (azg_split_gemm.hip), f32-accurate like the inference form.
+//
+// Per layer, with V = B^T d B the input transform (azg_winograd_in_nhwc, AZG_WINO_SPLIT2),
+// U_e = G_a g G_b^T the weights' transform and M_e = V_e U_e per transformed point e:
+//
+//   forward   y  = A^T M A + b                       (wt_out: M -> NHWC y, no ReLU: BN follows)
+//   backward  dM = A dy A^T                          (wt_dout: the output transform's adjoint)
+//             dV_e = dM_e U_e^T                      (split GEMM, B operand U rows [c][k])
+//             dx = sum over tiles of B dV B^T        (wt_din: the input transform's adjoint,
+//                                                     overlapping windows gathered per pixel)
+//             dU_e = V_e^T dM_e                      (split GEMM over the tiles: both operands
+//                                                     transposed by wt_split2_transpose)
+//             dg = sum_e G_a^T dU_e G_b              (the caller, torch)
+//
+// Every split operand is scaled by a power of two chosen on the device from a max|.| the
+// kernels here reduce (no host synchronisation): U by 2^ku with max |U| 2^ku in (512, 1024]
+// (as nnet._split_u), dM by 2^kd with max |dy| 2^kd in (16, 32] (gradients are far below
+// fp16's normal range); the consumers undo them exactly (powers of two).
+#include <algorithm>
+
+#include "azg_winograd_kern.h"
+
+namespace {
+
+// nnet.WINOGRAD_G in f64 (F(m,3) weight transforms G [m+2][3])
+template <int M>
+struct WinoG;
+template <>
+struct WinoG<2> {
+    static constexpr double G[4][3] = {{1.0, 0.0, 0.0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0.0, 0.0, 1.0}};
+};
+template <>
+struct WinoG<3> {
+    static constexpr double G[5][3] = {
+        {0.5, 0.0, 0.0}, {-0.5, -0.5, -0.5}, {-1.0 / 6, 1.0 / 6, -1.0 / 6}, {1.0 / 6, 1.0 / 3, 2.0 / 3}, {0.0, 0.0, 1.0}};
+};
+template <>
+struct WinoG<4> {
+    static constexpr double G[6][3] = {{0.5, 0.0, 0.0},
+                                       {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                                       {1.0 / 6, -1.0 / 6, 1.0 / 6},
+                                       {1.0 / 30, 1.0 / 15, 2.0 / 15},
+                                       {-16.0 / 15, 8.0 / 15, -4.0 / 15},
+                                       {0.0, 0.0, 0.5}};
+};
+template <>
+struct WinoG<5> {
+    static constexpr double G[7][3] = {{1.0 / 6, 0.0, 0.0},           {-1.0 / 18, -1.0 / 18, -1.0 / 18},
+                                       {1.0 / 10, -1.0 / 10, 1.0 / 10}, {-4.0 / 9, 2.0 / 9, -1.0 / 9},
+                                       {-1.0 / 126, 1.0 / 63, -2.0 / 63}, {4.0 / 105, 2.0 / 35, 3.0 / 35},
+                                       {0.0, 0.0, 0.25}};
+};
+
+// 2^floor(log2(target / amax)) (1 for amax 0 or not finite): the power of two that puts the
+// largest magnitude in (target / 2, target]; every kernel of a step computes it from the same
+// amax, so producer and consumer agree bit for bit
+__device__ __forceinline__ float pow2_scale(unsigned amax_bits, float target) {
+    const float a = __uint_as_float(amax_bits);
+    if (!(a > 0.f) || !(a < 3.0e38f)) return 1.f;
+    int e;
+    (void)frexpf(target / a, &e);  // target / a = f 2^e, f in [0.5, 1)
+    return ldexpf(1.f, e - 1);
+}
+
+// U of one (c, k) pair for every point of the groups of an h_out-side layer, in the
+// order of nnet._winograd_u (groups (big,big) (big,small) (small,big) (small,small), point
+// e = a (mb + 2) + b within a group): f(point index, U value rounded to f32)
+template <class F>
+__device__ __forceinline__ void u_points(const float* __restrict__ w9, int h_out, F&& f) {
+    double g[3][3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) g[i / 3][i % 3] = (double)w9[i];
+    const WSeq S(h_out);
+    int e0 = 0;
+    for (int q = 0; q < 4; ++q) {
+        const int ma = q < 2 ? S.big : S.small(), mb = (q & 1) ? S.small() : S.big;
+        if (S.cnt(ma) * S.cnt(mb) == 0) continue;  // absent tile type
+        with_types(ma, mb, [&](auto A_, auto B_) {
+            constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+            double s[MA + 2][3];
+#pragma unroll
+            for (int a = 0; a < MA + 2; ++a)
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    s[a][c] = WinoG<MA>::G[a][0] * g[0][c] + WinoG<MA>::G[a][1] * g[1][c] + WinoG<MA>::G[a][2] * g[2][c];
+#pragma unroll
+            for (int a = 0; a < MA + 2; ++a)
+#pragma unroll
+                for (int b = 0; b < MB + 2; ++b)
+                    f(e0 + a * (MB + 2) + b,
+                      (float)(s[a][0] * WinoG<MB>::G[b][0] + s[a][1] * WinoG<MB>::G[b][1] + s[a][2] * WinoG<MB>::G[b][2]));
+        });
+        e0 += (ma + 2) * (mb + 2);
+    }
+}
+
+// max |x| of n floats (x % 4 == 0 handled by the caller) -> atomicMax on the bit pattern
+// (non-negative floats order as their bits); *out must be 0 before the launch
+__global__ __launch_bounds__(256) void wt_absmax_kernel(const float4* __restrict__ x, long long n4,
+                                                        unsigned* __restrict__ out) {
+    float m = 0.f;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+        const float4 v = x[i];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// max |U| over every point and (c, k): one thread per (k, c)
+__global__ __launch_bounds__(256) void wt_u_absmax_kernel(const float* __restrict__ w, int C, int K, int h_out,
+                                                          unsigned* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    float m = 0.f;
+    if (i < (long long)C * K) u_points(w + i * 9, h_out, [&](int, float u) { m = fmaxf(m, fabsf(u)); });
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// U 2^ku split into AZG_WINO_SPLIT2 rows: ROWS_K (the forward GEMM's B operand, U^T):
+// [P][K][2C], one thread per (k, c) with c fastest; else (the dV GEMM's B operand, U):
+// [P][C][2K], one thread per (c, k) with k fastest.  ku from max |U| (wt_u_absmax_kernel).
+template <bool ROWS_K>
+__global__ __launch_bounds__(256) void wt_u_split_kernel(const float* __restrict__ w, int C, int K, int h_out,
+                                                         const unsigned* __restrict__ uamax,
+                                                         unsigned short* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)C * K) return;
+    const int k = ROWS_K ? (int)(i / C) : (int)(i % K), c = ROWS_K ? (int)(i % C) : (int)(i / K);
+    const float sc = pow2_scale(*uamax, 1024.f);
+    const int R = ROWS_K ? K : C, W = ROWS_K ? C : K, r = ROWS_K ? k : c, x = ROWS_K ? c : k;
+    u_points(w + ((long long)k * C + c) * 9, h_out, [&](int e, float u) {
+        const float us = u * sc;  // exact (a power of two)
+        const _Float16 hi = (_Float16)us;
+        const _Float16 lo = (_Float16)(us - (float)hi);
+        unsigned short* row = out + ((long long)e * R + r) * 2 * W;
+        const int o = 64 * (x >> 5) + (x & 31);
+        row[o] = __builtin_bit_cast(unsigned short, hi);
+        row[o + 32] = __builtin_bit_cast(unsigned short, lo);
+    });
+}
+
+// Forward output transform without ReLU (BatchNorm follows): y = bias + 2^-ku A^T M A,
+// NHWC f32, one thread per (tile, 4 channels) (winograd_out_kernel with the scale read on
+// the device)
+template <int HC>
+__global__ __launch_bounds__(256) void wt_out_kernel(const float4* __restrict__ Min, const float4* __restrict__ bias,
+                                                     float4* __restrict__ y, int Ho, int K4, long long B,
+                                                     const unsigned* __restrict__ uamax) {
+    const WSeq S(HC > 0 ? HC : Ho);
+    if (HC > 0) Ho = HC;
+    const long long item = xcd_item();
+    if (item >= B * S.p * S.p * K4) return;
+    const int k4 = (int)(item % K4);
+    const long long t = item / K4;
+    const int j = (int)(t % S.p);
+    const long long r = t / S.p;
+    const int i = (int)(r % S.p);
+    const long long b = r / S.p;
+    const float mscale = 1.f / pow2_scale(*uamax, 1024.f);
+    const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
+    const float4 bb = bias[k4];
+    with_types_of<HC>(S.m(i), S.m(j), [&](auto A_, auto B_) {
+        constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+        float4 m[MA + 2][MB + 2];
+#pragma unroll
+        for (int e = 0; e < (MA + 2) * (MB + 2); ++e)
+            m[e / (MB + 2)][e % (MB + 2)] = vmul(mscale, Min[(row + e * ps) * K4 + k4]);
+        float4 yt[MA][MB];
+        out_tile<MA, MB>(m, yt);
+#pragma unroll
+        for (int a = 0; a < MA; ++a)
+#pragma unroll
+            for (int q = 0; q < MB; ++q) {
+                const int oy = S.off(i) + a, ox = S.off(j) + q;
+                if (oy >= Ho || ox >= Ho) continue;
+                y[((b * Ho + oy) * Ho + ox) * K4 + k4] = vadd(yt[a][q], bb);
+            }
+    });
+}
+
+// dM = 2^kd A dy A^T (the adjoint of Y = A^T M A), AZG_WINO_SPLIT2 rows [P][T][2K] in the
+// layout of M; one thread per (tile, 4 channels).  |dM| > 65504 sets *overflow.
+template <int HC>
+__global__ __launch_bounds__(256) void wt_dout_kernel(const float4* __restrict__ dy, void* __restrict__ dM, int Ho,
+                                                      int K4, long long B, const unsigned* __restrict__ dyamax,
+                                                      int* overflow) {
+    const WSeq S(HC > 0 ? HC : Ho);
+    if (HC > 0) Ho = HC;
+    const long long item = xcd_item();
+    if (item >= B * S.p * S.p * K4) return;
+    const int k4 = (int)(item % K4);
+    const long long t = item / K4;
+    const int j = (int)(t % S.p);
+    const long long r = t / S.p;
+    const int i = (int)(r % S.p);
+    const long long b = r / S.p;
+    const float sd = pow2_scale(*dyamax, 32.f);
+    const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
+    with_types_of<HC>(S.m(i), S.m(j), [&](auto A_, auto B_) {
+        constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+        float4 g[MA][MB];
+#pragma unroll
+        for (int a = 0; a < MA; ++a)
+#pragma unroll
+            for (int q = 0; q < MB; ++q) {
+                const int oy = S.off(i) + a, ox = S.off(j) + q;
+                g[a][q] = (oy < Ho && ox < Ho) ? vmul(sd, dy[((b * Ho + oy) * Ho + ox) * K4 + k4])
+                                               : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        // s[a][v] = sum_q AT_b[q][v] g[a][q]; dM[u][v] = sum_a AT_a[a][u] s[a][v]
+        float4 s[MA][MB + 2];
+#pragma unroll
+        for (int a = 0; a < MA; ++a)
+#pragma unroll
+            for (int v = 0; v < MB + 2; ++v) {
+                float cf[MB];
+#pragma unroll
+                for (int q = 0; q < MB; ++q) cf[q] = WinoT<MB>::AT[q][v];
+                s[a][v] = combine<MB, float4>(cf, [&](int q) { return g[a][q]; });
+            }
+#pragma unroll
+        for (int u = 0; u < MA + 2; ++u)
+#pragma unroll
+            for (int v = 0; v < MB + 2; ++v) {
+                float cf[MA];
+#pragma unroll
+                for (int a = 0; a < MA; ++a) cf[a] = WinoT<MA>::AT[a][u];
+                const float4 d = combine<MA, float4>(cf, [&](int a) { return s[a][v]; });
+                store_v<AZG_WINO_SPLIT2>(dM, row + (u * (MB + 2) + v) * ps, K4, k4, d, overflow);
+            }
+    });
+}
+
+// dx = 2^-(kd + ku) sum over the tiles whose input window holds the pixel of B dV B^T
+// (the adjoint of V = B^T d B with zero padding PAD); dV f32 [P][T][C] in the layout of
+// V.  One wave per (image, 64 channels), one channel per lane, the lane's H x H gradient
+// plane in registers, tiles accumulated in a fixed order (deterministic).
+template <int H, int PAD>
+__global__ __launch_bounds__(64) void wt_din_kernel(const float* __restrict__ dV, float* __restrict__ dx, int C,
+                                                    long long B, const unsigned* __restrict__ uamax,
+                                                    const unsigned* __restrict__ dyamax) {
+    constexpr int HO = H + 2 * PAD - 2;
+    const unsigned lane = threadIdx.x;
+    const int cblocks = C / 64;
+    const long long b = blockIdx.x / cblocks;
+    const int c0 = (blockIdx.x % cblocks) * 64;
+    const float inv = 1.f / (pow2_scale(*uamax, 1024.f) * pow2_scale(*dyamax, 32.f));
+    const WSeq S(HO);
+    float pl[H * H];
+#pragma unroll
+    for (int q = 0; q < H * H; ++q) pl[q] = 0.f;
+    for_tiles<HO>(S, [&](auto A_, auto B_, int i, int j) {
+        constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+        const long long row = S.row0(i, j, b, B), ps = S.pstride(i, j, B);
+        const int y0 = S.off(i) - PAD, x0 = S.off(j) - PAD;
+        float v[MA + 2][MB + 2];
+#pragma unroll
+        for (int e = 0; e < (MA + 2) * (MB + 2); ++e) v[e / (MB + 2)][e % (MB + 2)] = dV[(row + e * ps) * C + c0 + lane];
+        // s[a][x] = sum_b BT_b[b][x] v[a][b]; d[u][x] = sum_a BT_a[a][u] s[a][x]
+        float s[MA + 2][MB + 2];
+#pragma unroll
+        for (int a = 0; a < MA + 2; ++a)
+#pragma unroll
+            for (int xx = 0; xx < MB + 2; ++xx) {
+                float cf[MB + 2];
+#pragma unroll
+                for (int bb = 0; bb < MB + 2; ++bb) cf[bb] = WinoT<MB>::BT[bb][xx];
+                s[a][xx] = combine<MB + 2, float>(cf, [&](int bb) { return v[a][bb]; });
+            }
+#pragma unroll
+        for (int u = 0; u < MA + 2; ++u)
+#pragma unroll
+            for (int xx = 0; xx < MB + 2; ++xx) {
+                const int iy = y0 + u, ix = x0 + xx;
+                if (iy < 0 || iy >= H || ix < 0 || ix >= H) continue;  // compile-time with HO > 0
+                float cf[MA + 2];
+#pragma unroll
+                for (int a = 0; a < MA + 2; ++a) cf[a] = WinoT<MA>::BT[a][u];
+                pl[iy * H + ix] += combine<MA + 2, float>(cf, [&](int a) { return s[a][xx]; });
+            }
+    });
+#pragma unroll
+    for (int q = 0; q < H * H; ++q) dx[(b * H * H + q) * C + c0 + lane] = pl[q] * inv;
+}
+
+// AZG_WINO_SPLIT2 [P][T][2C] -> [P][C][2T]: 64 x 64 (t, c) tiles through LDS, 256 threads
+__global__ __launch_bounds__(256) void wt_split2_transpose_kernel(const unsigned short* __restrict__ src,
+                                                                  unsigned short* __restrict__ dst, int T, int C) {
+    __shared__ unsigned short hi[64][65], lo[64][65];
+    const int tt = blockIdx.x, ct = blockIdx.y, e = blockIdx.z;
+    const int t0 = tt * 64, c0 = ct * 64;
+    const unsigned short* s = src + (long long)e * T * 2 * C;
+    unsigned short* d = dst + (long long)e * C * 2 * T;
+    // read: 64 rows t, each 128 halves (two 32-channel blocks [hi | lo])
+    for (int q = threadIdx.x; q < 64 * 128; q += 256) {
+        const int r = q >> 7, x = q & 127;  // x: 64 (block) + 32 (lo) + lane
+        const unsigned short v = s[(long long)(t0 + r) * 2 * C + 2 * c0 + x];
+        const int c = ((x >> 6) << 5) + (x & 31);
+        if (x & 32) lo[r][c] = v;
+        else hi[r][c] = v;
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < 64 * 128; q += 256) {
+        const int r = q >> 7, x = q & 127;  // r: channel, x: t in the same block layout
+        const int t = ((x >> 6) << 5) + (x & 31);
+        d[(long long)(c0 + r) * 2 * T + 2 * t0 + x] = (x & 32) ? lo[t][r] : hi[t][r];
+    }
+}
+
+template <class F>
+int by_side(int h, F&& f) {
+    switch (h) {
+        case 3: f(IC<3>{}); break;
+        case 5: f(IC<5>{}); break;
+        case 7: f(IC<7>{}); break;
+        default: return AZG_ERR_ARG;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int azg_absmax(const float* x, int64_t n, uint32_t* out, void* stream) {
+    if (!x || !out || n <= 0 || n % 4 || ((uintptr_t)x & 15)) return AZG_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(out, 0, 4, st) != hipSuccess) return AZG_ERR_HIP;
+    const long long n4 = n / 4;
+    const unsigned grid = (unsigned)std::min<long long>((n4 + 255) / 256, 2048);
+    hipLaunchKernelGGL(wt_absmax_kernel, dim3(grid), dim3(256), 0, st, (const float4*)x, n4, out);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+extern "C" int azg_wt_u_build(const float* w, int32_t c, int32_t k, int32_t h_out, uint32_t* uamax, void* ut,
+                              void* un, void* stream) {
+    if (!w || !uamax || (!ut && !un) || c <= 0 || k <= 0 || c % 32 || k % 32 || h_out < 2 || h_out > 9)
+        return AZG_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(uamax, 0, 4, st) != hipSuccess) return AZG_ERR_HIP;
+    const dim3 grid((unsigned)(((long long)c * k + 255) / 256));
+    hipLaunchKernelGGL(wt_u_absmax_kernel, grid, dim3(256), 0, st, w, c, k, h_out, uamax);
+    if (ut) hipLaunchKernelGGL(wt_u_split_kernel<true>, grid, dim3(256), 0, st, w, c, k, h_out, uamax, (unsigned short*)ut);
+    if (un) hipLaunchKernelGGL(wt_u_split_kernel<false>, grid, dim3(256), 0, st, w, c, k, h_out, uamax, (unsigned short*)un);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+extern "C" int azg_wt_out(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,
+                          const uint32_t* uamax, void* stream) {
+    if (!M || !bias || !y || !uamax || batch <= 0 || k <= 0 || k % 4 || ((uintptr_t)M & 15) || ((uintptr_t)bias & 15) ||
+        ((uintptr_t)y & 15))
+        return AZG_ERR_ARG;
+    const WSeq S(h_out);
+    const dim3 grid(grid_for((long long)batch * S.p * S.p * (k / 4)));
+    const int rc = by_side(h_out, [&](auto H_) {
+        hipLaunchKernelGGL((wt_out_kernel<decltype(H_)::value>), grid, dim3(256), 0, (hipStream_t)stream,
+                           (const float4*)M, (const float4*)bias, (float4*)y, h_out, k / 4, (long long)batch, uamax);
+    });
+    return rc ? rc : (hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP);
+}
+
+extern "C" int azg_wt_dout(const float* dy, void* dM, int32_t batch, int32_t h_out, int32_t k, const uint32_t* dyamax,
+                           int32_t* overflow, void* stream) {
+    if (!dy || !dM || !dyamax || batch <= 0 || k <= 0 || k % 32 || ((uintptr_t)dy & 15) || ((uintptr_t)dM & 15) ||
+        !azg_device_writable(overflow))
+        return AZG_ERR_ARG;
+    const WSeq S(h_out);
+    const dim3 grid(grid_for((long long)batch * S.p * S.p * (k / 4)));
+    const int rc = by_side(h_out, [&](auto H_) {
+        hipLaunchKernelGGL((wt_dout_kernel<decltype(H_)::value>), grid, dim3(256), 0, (hipStream_t)stream,
+                           (const float4*)dy, dM, h_out, k / 4, (long long)batch, dyamax, overflow);
+    });
+    return rc ? rc : (hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP);
+}
+
+extern "C" int azg_wt_din(const float* dV, float* dx, int32_t batch, int32_t h_in, int32_t pad, int32_t c,
+                          const uint32_t* uamax, const uint32_t* dyamax, void* stream) {
+    if (!dV || !dx || !uamax || !dyamax || batch <= 0 || c <= 0 || c % 64) return AZG_ERR_ARG;
+    const dim3 grid((unsigned)(batch * (c / 64)));
+    hipStream_t st = (hipStream_t)stream;
+    if (h_in == 7 && pad == 1)
+        hipLaunchKernelGGL((wt_din_kernel<7, 1>), grid, dim3(64), 0, st, dV, dx, c, (long long)batch, uamax, dyamax);
+    else if (h_in == 7 && pad == 0)
+        hipLaunchKernelGGL((wt_din_kernel<7, 0>), grid, dim3(64), 0, st, dV, dx, c, (long long)batch, uamax, dyamax);
+    else if (h_in == 5 && pad == 0)
+        hipLaunchKernelGGL((wt_din_kernel<5, 0>), grid, dim3(64), 0, st, dV, dx, c, (long long)batch, uamax, dyamax);
+    else
+        return AZG_ERR_ARG;
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+extern "C" int azg_wt_split2_transpose(const void* src, void* dst, int32_t points, int32_t t, int32_t c,
+                                       void* stream) {
+    if (!src || !dst || points <= 0 || t <= 0 || c <= 0 || t % 64 || c % 64) return AZG_ERR_ARG;
+    hipLaunchKernelGGL(wt_split2_transpose_kernel, dim3(t / 64, c / 64, points), dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned short*)src, (unsigned short*)dst, t, c);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+namespace {
+__global__ void wt_pow2_scale_kernel(const unsigned* amax, float target, float* out) {
+    if (threadIdx.x == 0) out[0] = pow2_scale(*amax, target);
+}
+}  // namespace
+
+// *out = the power of two the kernels above scale by for this amax and target (1024 for U,
+// 32 for the output gradients): the host side (torch) undoes it from the same device value
+extern "C" int azg_wt_pow2_scale(const uint32_t* amax, float target, float* out, void* stream) {
+    if (!amax || !out || !(target > 0.f)) return AZG_ERR_ARG;
+    hipLaunchKernelGGL(wt_pow2_scale_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, amax, target, out);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}

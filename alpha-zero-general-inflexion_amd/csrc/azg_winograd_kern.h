@@ -567,7 +567,7 @@ __global__ __launch_bounds__(64 * WPB) void winograd_mid_kernel(const float* __r
 // ROWS = 2 (the boards' two tile rows): two waves per (image, channels), each
 // computing conv1 whole and storing one tile row's V: twice the (cheap, sparse)
 // conv1 work for half the stores per wave, measured 204 -> 175 us at 4096 leaves
-// and 18.8 -> 17.7 us at 256 (tools/first_probe.py).
+// and 18.8 -> 17.7 us at 256 (tools/first_probe.py, HISTORY.md 6b).
 template <int NC, int FMT, int ROWS = 1>
 __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restrict__ planes,
                                                             const float* __restrict__ w1,
@@ -622,7 +622,7 @@ __global__ __launch_bounds__(64) void winograd_first_kernel(const float* __restr
             }
     }
     // V2 goes out with non-temporal stores: nothing here reads it back, and the GEMM
-    // reads it only after the whole grid (241 -> 209 us at 4096 leaves, DESIGN 6b,
+    // reads it only after the whole grid (241 -> 209 us at 4096 leaves, HISTORY.md 6b,
     // profiles/r02_nt_store_probe)
     plane_to_V<NC, FMT, 1, true>(ys, n, b, k0, lane, C, B, Vout, overflow, part);
 }

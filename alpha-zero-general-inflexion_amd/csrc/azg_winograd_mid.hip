@@ -12,7 +12,7 @@ extern "C" int azg_winograd_mid_nhwc(const float* M, const float* bias, void* V,
     const long long B = batch;
 // mid<5> (conv3 -> conv4) as four items per 256-thread block: +0.3% at C4 alternating on one box
 // (transforms 599-602 -> 594-598 us per forward; profiles/r04_ab_mid5_wpb4); mid<7> stays one wave
-// per block (four per block spilled it, 40% slower)
+// per block (four per block spilled it, 40% slower, HISTORY.md 4.1)
 #define AZG_MID(H, SP, L)                                                                                          \
     {                                                                                                              \
         if (H == 5 && grid.x % 32 == 0)                                                                            \

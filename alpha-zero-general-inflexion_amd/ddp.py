@@ -245,7 +245,7 @@ def _train_examples_dp(wrapper, ex, group, stats=None):
                 mine = torch.from_numpy(ids[rank * sl:(rank + 1) * sl]).to(dev)
                 tp, tv = pis[mine], vs[mine]
                 with wrapper._autocast():
-                    out_pi, out_v = net(planes[mine])
+                    out_pi, out_v = wrapper._train_forward(planes[mine])
                     l_pi = -torch.sum(tp * out_pi) / bs
                     l_v = torch.sum((tv - out_v.view(-1)) ** 2) / bs
                 opt.zero_grad()

@@ -26,7 +26,11 @@ DEFAULT_ARGS = dict(lr=0.001, dropout=0.3, epochs=10, batch_size=512, num_channe
                     # |grad| ~ eps), train_dtype "bf16" = autocast forward/backward (2.5x
                     # examples/s); both opt-in, not the reference's arithmetic
                     # (profiles/r01_train_probe.json)
-                    fused_adam=False, train_dtype="f32")
+                    fused_adam=False, train_dtype="f32",
+                    # conv2-4 of the GPU training step: "winograd" (libazg's Winograd transforms and
+                    # split-fp16 GEMMs, forward and backward, wino_train.py) or "library" (torch /
+                    # MIOpen as the reference).  The CPU trainer is always the reference's.
+                    train_conv="winograd")
 WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C1: 1 game)
 # up to SMALL_MAX_B leaves: the whole forward on libazg's small-batch kernels (azg_small.hip: one
 # launch per layer, no library) instead of MIOpen / hipBLASLt
@@ -39,6 +43,14 @@ FC1_KPARTS = 4  # split-K parts of fc1 on libazg's split GEMM (4608 = 4 x 1152 f
 # fastest of 4/8/16 x 2/4 at 4096 leaves (tools/fc_tail_bench.py, profiles/r03_fc_tail_bench.json)
 FC2_KPARTS = 4
 FC34_KPARTS = 2
+# the FC tail below FC1_SPLIT_MIN_BATCH leaves (C2's 256; leaves % 256 == 0), also all on libazg's
+# split GEMM: fc1 TRANSPOSED (W1 x A^T: the weights as the GEMM's rows, the leaves one column
+# tile, so every weight tile is read once instead of once per 64-leaf row tile) in FC1T_KPARTS
+# K-parts, azg_fc_act_t summing its transposed partials; fc2 and [fc3 | fc4] as before in
+# FCS_KPARTS2 / FCS_KPARTS3 parts (short launches: more parts, fewer K stages each)
+FC1T_KPARTS = 18
+FCS_KPARTS2 = 16
+FCS_KPARTS3 = 8
 
 
 class InflexionNNet(nn.Module):
@@ -383,6 +395,16 @@ class InferenceNet(nn.Module):
             w34 = torch.zeros((n34p, self.fw34.shape[1]), dtype=self.fw34.dtype, device=self.fw34.device)
             w34[:n34] = self.fw34
             self.register_buffer("fw34_sk", self._split_k_weights(w34, FC34_KPARTS, self.fc34_scale))
+            # the small-batch tail (FC1T_KPARTS, FCS_KPARTS2 / 3; _fc_split_small)
+            w1w = w1.shape[1]
+            self.fc_tail_small = (w1w % (64 * FC1T_KPARTS) == 0 and w1.shape[0] % 64 == 0
+                                  and w2.shape[1] % (64 * FCS_KPARTS2) == 0 and n2 % (64 * FCS_KPARTS3) == 0)
+            if self.fc_tail_small:
+                self.register_buffer("fw1_skT", self._split_k_weights(w1, FC1T_KPARTS, self.fc1_scale))
+                self.register_buffer("fw2_skS", self._split_k_weights(w2, FCS_KPARTS2, self.fc2_scale))
+                self.register_buffer("fw34_skS", self._split_k_weights(w34, FCS_KPARTS3, self.fc34_scale))
+        else:
+            self.fc_tail_small = False
         # sticky device flag: a split-GEMM operand fp16 could not hold (checked by check_range).
         # It lives where the kernels run: the transforms set it with a device atomic, so a
         # host-memory flag would fault the GPU the first time an operand overflowed.
@@ -588,7 +610,7 @@ class InferenceNet(nn.Module):
         if split_out:
             # the flattened NHWC activation as fc1's A operand: [parts][B][chunk] split2 blocks
             # for libazg's split-K GEMM, else one [hi | lo | hi] fp16 row per image (hipBLASLt)
-            kp = self.fc1_kparts
+            kp = self.fc1_kparts if B >= FC1_SPLIT_MIN_BATCH else FC1T_KPARTS  # (the small tail: _fc_split_small)
             y = torch.empty((B, (2 if kp else 3) * Ho * Ho * K), device=dev, dtype=torch.float16)
             self._khook("transform", i, "start")
             _lib.check(L.azg_winograd_out_split(M, bias, ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, mscale,
@@ -639,6 +661,8 @@ class InferenceNet(nn.Module):
         B, dev = a.shape[0], a.device
         st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         ovf = ctypes.c_void_p(self._overflow_ptr())
+        if self.fc_tail_small and B < FC1_SPLIT_MIN_BATCH:
+            return self._fc_split_small(a, B, dev, st, ovf)
         if self.fc_tail_azg and self.fc1_kparts:
             return self._fc_split_azg(a, B, dev, st, ovf)
         for layer, (w, b, scale) in enumerate(((self.fw1_s, self.fb1, self.fc1_scale),
@@ -705,6 +729,52 @@ class InferenceNet(nn.Module):
         m2 = gemm(6, a2, self.fw2_sk, kp2, self.fw2_sk.shape[1])
         a3 = act(m2, kp2, self.fb2, self.fc2_scale, kp3)
         m3 = gemm(7, a3, self.fw34_sk, kp3, self.fw34_sk.shape[1])
+        A = self.fw34.shape[0] - 1
+        p = torch.empty((B, A), device=dev, dtype=torch.float32)
+        v = torch.empty((B, 1), device=dev, dtype=torch.float32)
+        n3 = m3.shape[2]
+        _lib.check(L.azg_policy_value_parts(ctypes.c_void_p(m3.data_ptr()), kp3, B * n3, n3,
+                                            ctypes.c_void_p(self.fb34.data_ptr()), self.fc34_scale,
+                                            ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()), B, A, st))
+        return p, v
+
+    def _fc_split_small(self, a, B, dev, st, ovf):
+        """The FC tail below FC1_SPLIT_MIN_BATCH leaves (leaves % 256 == 0, C2's 256): fc1 as the
+        transposed split-K GEMM M1^T [parts][1024][B] = W1 A^T (the weights the rows, the leaves one
+        256-column tile: each weight tile read once), azg_fc_act_t summing its parts in order into
+        fc2's split2 K-parts; fc2 and [fc3 | fc4] as _fc_split_azg's, in FCS_KPARTS2 / 3 parts."""
+        import ctypes
+        from . import _lib
+        L = _lib.lib()
+        kp1, kp2, kp3 = FC1T_KPARTS, FCS_KPARTS2, FCS_KPARTS3
+        n1, c1 = self.fw1_skT.shape[1], self.fw1_skT.shape[2] // 2
+        m1 = torch.empty((kp1, n1, B), device=dev, dtype=torch.float32)
+        pts, rows = (ctypes.c_int32 * 1)(kp1), (ctypes.c_int32 * 1)(n1)
+        self._khook("gemm", 5, "start")
+        _lib.check(L.azg_split_gemm(ctypes.c_void_p(self.fw1_skT.data_ptr()), ctypes.c_void_p(a.data_ptr()),
+                                    ctypes.c_void_p(m1.data_ptr()), 1, pts, rows, c1, B, st))
+        self._khook("gemm", 5, "stop", 3.0 * 2 * kp1 * c1 * n1 * B,
+                    self._gemm_pick([kp1], [n1], B) if self.kernel_hook else None)
+        n2 = self.fw2_skS.shape[1]
+        a2 = torch.empty((kp2, B, 2 * n1 // kp2), device=dev, dtype=torch.float16)
+        _lib.check(L.azg_fc_act_t(ctypes.c_void_p(m1.data_ptr()), kp1, n1 * B, ctypes.c_void_p(self.fb1.data_ptr()),
+                                  self.fc1_scale, ctypes.c_void_p(a2.data_ptr()), B, n1, 1, kp2, ovf, st))
+
+        def gemm(layer, A_, W, kp, n):
+            c = A_.shape[-1] // 2
+            m = torch.empty((kp, B, n), device=dev, dtype=torch.float32)
+            pts, rows = (ctypes.c_int32 * 1)(kp), (ctypes.c_int32 * 1)(B)
+            self._khook("gemm", layer, "start")
+            _lib.check(L.azg_split_gemm(ctypes.c_void_p(A_.data_ptr()), ctypes.c_void_p(W.data_ptr()),
+                                        ctypes.c_void_p(m.data_ptr()), 1, pts, rows, c, n, st))
+            self._khook("gemm", layer, "stop", 3.0 * 2 * kp * c * n * B,
+                        self._gemm_pick([kp], [B], n) if self.kernel_hook else None)
+            return m
+        m2 = gemm(6, a2, self.fw2_skS, kp2, n2)
+        a3 = torch.empty((kp3, B, 2 * n2 // kp3), device=dev, dtype=torch.float16)
+        _lib.check(L.azg_fc_act(ctypes.c_void_p(m2.data_ptr()), kp2, B * n2, ctypes.c_void_p(self.fb2.data_ptr()),
+                                self.fc2_scale, ctypes.c_void_p(a3.data_ptr()), B, n2, 1, 2, kp3, ovf, st))
+        m3 = gemm(7, a3, self.fw34_skS, kp3, self.fw34_skS.shape[1])
         A = self.fw34.shape[0] - 1
         p = torch.empty((B, A), device=dev, dtype=torch.float32)
         v = torch.empty((B, 1), device=dev, dtype=torch.float32)
@@ -849,7 +919,8 @@ class InferenceNet(nn.Module):
             elif impl == "azg":
                 x = self._conv_azg(x, i, pad)
             elif impl == "winograd":
-                split_out = i == 4 and self.fc1_split and self.gemm != "f32" and B >= FC1_SPLIT_MIN_BATCH
+                split_out = i == 4 and self.fc1_split and self.gemm != "f32" and (
+                    B >= FC1_SPLIT_MIN_BATCH or (self.fc_tail_small and B % 256 == 0))
                 x = self._conv_winograd(x, i, pad, in_bias=pending, carried=carried, B=B, H=H, fuse_next=fuse_next,
                                         split_out=split_out)
                 if split_out:
@@ -931,6 +1002,15 @@ class NNetWrapper:
             pi, v = self.nnet(planes)
         return torch.exp(pi), v.view(-1)
 
+    def _train_forward(self, x):
+        """The training forward: InflexionNNet.forward, with conv2-4 on libazg's training
+        kernels (wino_train.train_forward) on the GPU in f32 when args["train_conv"] is
+        "winograd" -- the module itself otherwise (CPU: the reference's arithmetic)."""
+        if x.is_cuda and self.args.get("train_conv", "winograd") == "winograd" and self.args["train_dtype"] == "f32":
+            from .wino_train import train_forward
+            return train_forward(self.nnet, x)
+        return self.nnet(x)
+
     def _adam(self):
         if self.args["fused_adam"]:
             return torch.optim.Adam(self.nnet.parameters(), fused=True)
@@ -956,7 +1036,7 @@ class NNetWrapper:
                 tp = torch.FloatTensor(np.array(pis)).to(self.device)
                 tv = torch.FloatTensor(np.array(vs).astype(np.float64)).to(self.device)
                 with self._autocast():
-                    out_pi, out_v = self.nnet(boards)
+                    out_pi, out_v = self._train_forward(boards)
                     l_pi = -torch.sum(tp * out_pi) / tp.size()[0]
                     l_v = torch.sum((tv - out_v.view(-1)) ** 2) / tv.size()[0]
                 opt.zero_grad()
@@ -995,7 +1075,7 @@ class NNetWrapper:
                 ids = torch.from_numpy(np.random.randint(E, size=bs)).to(self.device)
                 tp, tv = pis[ids], vs[ids]
                 with self._autocast():
-                    out_pi, out_v = self.nnet(planes[ids])
+                    out_pi, out_v = self._train_forward(planes[ids])
                     l_pi = -torch.sum(tp * out_pi) / tp.size()[0]
                     l_v = torch.sum((tv - out_v.view(-1)) ** 2) / tv.size()[0]
                 opt.zero_grad()

@@ -1,0 +1,207 @@
+"""The trainer's 3x3 convolutions on libazg's Winograd transforms and split-fp16 GEMM.
+
+NNetWrapper.train (inflexion/pytorch/NNet.py:36-76) spends ~80% of a 512-example step in
+conv2-4 of InflexionNNet.forward (InflexionNNet.py:39-45) and their autograd, on MIOpen's
+f32 implicit GEMMs (profiles/r05_prof_train_probe.md: ~6.6 of 8.2 ms).  `WinogradConv3x3`
+computes the same convolution (raw conv weights and bias; the BatchNorm after it stays
+torch's, training mode) and its three gradients in the Winograd domain of the inference
+form (nnet.InferenceNet) -- F(4,3)+F(3,3) / F(5,3) / F(3,3) tiles, each
+transformed point one split-fp16 GEMM (f32-accurate products on the fp16 MFMA):
+
+    forward   V = B^T x B (azg_winograd_in_nhwc), M = V U (azg_split_gemm), y = A^T M A + b
+    backward  dM = A dy A^T, dV = dM U^T, dx = sum of B dV B^T over the overlapping tiles,
+              dU = V^T dM (both operands transposed), dw = sum_e G_a^T dU_e G_b (torch),
+              db = sum dy
+
+(csrc/azg_wino_train.hip).  Operands are scaled by powers of two chosen on the device (U:
+max in (512, 1024]; dy: in (16, 32]) and unscaled exactly, so no step waits on the host.
+`train_forward` is InflexionNNet.forward with conv2-4 replaced when `applies` holds (a GPU
+batch, 512-style channel counts, the 7x7 board's layer sides); everything else -- conv1,
+BatchNorm (GlobalBatchNorm under the data-parallel trainer), ReLU, dropout, the FC layers,
+the losses and Adam -- is the reference's torch code.
+"""
+import ctypes
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from .nnet import WINOGRAD_G, winograd_groups, winograd_points
+
+SPLIT2 = 2  # azg.h AZG_WINO_SPLIT2
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _runs(h_out, B):
+    """[(points, rows)] of the layer's GEMMs: tile groups with equal tiles per image merged."""
+    runs = []
+    for _, _, P, n in winograd_groups(h_out):
+        if runs and runs[-1][2] == n:
+            runs[-1][0] += P
+        else:
+            runs.append([P, B * n, n])
+    return [(P, rows) for P, rows, _ in runs]
+
+
+def _gemm(A, Bt, M, runs, c, k, dev):
+    pts = (ctypes.c_int32 * len(runs))(*[P for P, _ in runs])
+    rows = (ctypes.c_int32 * len(runs))(*[r for _, r in runs])
+    _lib.check(_lib.lib().azg_split_gemm(_p(A), _p(Bt), _p(M), len(runs), pts, rows, c, k, _stream(dev)))
+
+
+def applies(x, conv):
+    """Whether conv (nn.Conv2d 3x3) on x runs here: a CUDA batch divisible by 64 (the transposed
+    operands of dU), channel counts the split GEMM tiles (in % 64, out % 256 and in % 256 for the
+    input-gradient GEMM), and a layer the kernels are built for (7x7 -> 7x7, 7 -> 5, 5 -> 3)."""
+    if not (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32 and conv.kernel_size == (3, 3)
+            and conv.stride == (1, 1) and conv.bias is not None):
+        return False
+    B, C, H, W = x.shape
+    pad = conv.padding[0]
+    return (H == W and (H, pad) in ((7, 1), (7, 0), (5, 0)) and B % 64 == 0 and C % 256 == 0
+            and conv.out_channels % 256 == 0 and conv.in_channels == C)
+
+
+class WinogradConv3x3(torch.autograd.Function):
+    """y = conv3x3(x, w) + b (no ReLU) and its gradients on libazg's training kernels.
+    x: [B, C, H, H] f32 CUDA (any memory format; channels_last avoids a copy), w: [K, C, 3, 3],
+    b: [K].  Returns y [B, K, Ho, Ho] in channels_last memory format."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, pad):
+        L = _lib.lib()
+        dev = x.device
+        st = _stream(dev)
+        B, C, H, _ = x.shape
+        K = w.shape[0]
+        Ho = H + 2 * pad - 2
+        P = winograd_points(Ho)
+        runs = _runs(Ho, B)
+        rows = sum(p * r for p, r in runs)
+        xc = x.contiguous(memory_format=torch.channels_last)
+        wc = w.detach().contiguous()
+        ovf = _flag(dev)
+        V = torch.empty(rows * 2 * C, dtype=torch.float16, device=dev)
+        _lib.check(L.azg_winograd_in_nhwc(_p(xc), None, _p(V), B, H, pad, C, SPLIT2, _p(ovf), st))
+        uamax = torch.empty(1, dtype=torch.int32, device=dev)
+        ut = torch.empty(P * K * 2 * C, dtype=torch.float16, device=dev)
+        un = torch.empty(P * C * 2 * K, dtype=torch.float16, device=dev)
+        _lib.check(L.azg_wt_u_build(_p(wc), C, K, Ho, _p(uamax), _p(ut), _p(un), st))
+        M = torch.empty(rows * K, dtype=torch.float32, device=dev)
+        _gemm(V, ut, M, runs, C, K, dev)
+        y = torch.empty((B, K, Ho, Ho), dtype=torch.float32, device=dev, memory_format=torch.channels_last)
+        _lib.check(L.azg_wt_out(_p(M), _p(b.detach().contiguous()), _p(y), B, Ho, K, _p(uamax), st))
+        ctx.save_for_backward(V, un, uamax)
+        ctx.shape = (B, C, H, K, Ho, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        V, un, uamax = ctx.saved_tensors
+        ovf = _flag(dy.device)
+        B, C, H, K, Ho, pad = ctx.shape
+        dev = dy.device
+        st = _stream(dev)
+        runs = _runs(Ho, B)
+        rows = sum(p * r for p, r in runs)
+        P = winograd_points(Ho)
+        dyc = dy.contiguous(memory_format=torch.channels_last)
+        dyamax = torch.empty(1, dtype=torch.int32, device=dev)
+        _lib.check(L.azg_absmax(_p(dyc), dyc.numel(), _p(dyamax), st))
+        dM = torch.empty(rows * 2 * K, dtype=torch.float16, device=dev)
+        _lib.check(L.azg_wt_dout(_p(dyc), _p(dM), B, Ho, K, _p(dyamax), _p(ovf), st))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dV = torch.empty(rows * C, dtype=torch.float32, device=dev)
+            _gemm(dM, un, dV, runs, K, C, dev)
+            dx = torch.empty((B, C, H, H), dtype=torch.float32, device=dev, memory_format=torch.channels_last)
+            _lib.check(L.azg_wt_din(_p(dV), _p(dx), B, H, pad, C, _p(uamax), _p(dyamax), st))
+        dw = None
+        if ctx.needs_input_grad[1]:
+            # dU_e [C][K] = V_e^T dM_e, contracted over the tiles: operands transposed per run
+            dU = torch.empty((P, C, K), dtype=torch.float32, device=dev)
+            row = pt = 0
+            for Pr, T in runs:
+                Vt = torch.empty(Pr * C * 2 * T, dtype=torch.float16, device=dev)
+                dMt = torch.empty(Pr * K * 2 * T, dtype=torch.float16, device=dev)
+                _lib.check(L.azg_wt_split2_transpose(_p(V[row * 2 * C:]), _p(Vt), Pr, T, C, st))
+                _lib.check(L.azg_wt_split2_transpose(_p(dM[row * 2 * K:]), _p(dMt), Pr, T, K, st))
+                _gemm(Vt, dMt, dU[pt:pt + Pr], [(Pr, C)], T, K, dev)
+                row += Pr * T
+                pt += Pr
+            # dw[k][c][r][s] = sum over the groups of G_a^T dU G_b, then the dy scale undone
+            dw = torch.zeros((K, C, 3, 3), dtype=torch.float32, device=dev)
+            e = 0
+            for ma, mb, Pg, _ in winograd_groups(Ho):
+                Ga, Gb = _g(ma, dev), _g(mb, dev)
+                dw += torch.einsum("ar,abck,bs->kcrs", Ga, dU[e:e + Pg].view(ma + 2, mb + 2, C, K), Gb)
+                e += Pg
+            sd = torch.empty(1, dtype=torch.float32, device=dev)
+            _lib.check(L.azg_wt_pow2_scale(_p(dyamax), 32.0, _p(sd), st))
+            dw /= sd
+        db = dy.sum(dim=(0, 2, 3)) if ctx.needs_input_grad[2] else None
+        return dx, dw, db, None
+
+
+def conv3x3(x, conv):
+    """conv(x) on the training kernels when `applies`, else the module itself."""
+    if applies(x, conv):
+        return WinogradConv3x3.apply(x, conv.weight, conv.bias, conv.padding[0])
+    return conv(x)
+
+
+def train_forward(net, s):
+    """InflexionNNet.forward (InflexionNNet.py:39-54) in training, conv2-4 on the Winograd
+    kernels (conv3x3).  Returns (log_softmax(fc3), tanh(fc4)) as the module does."""
+    x = s.view(-1, net.depth, net.n, net.n)
+    if x.is_cuda:
+        x = x.contiguous(memory_format=torch.channels_last)
+    x = F.relu(net.bn1(net.conv1(x)))
+    for i in range(2, 5):
+        x = F.relu(getattr(net, f"bn{i}")(conv3x3(x, getattr(net, f"conv{i}"))))
+    x = x.reshape(x.shape[0], -1)
+    x = F.dropout(F.relu(net.fc_bn1(net.fc1(x))), p=net.dropout, training=net.training)
+    x = F.dropout(F.relu(net.fc_bn2(net.fc2(x))), p=net.dropout, training=net.training)
+    return F.log_softmax(net.fc3(x), dim=1), torch.tanh(net.fc4(x))
+
+
+def check_range(device=None):
+    """Raise FloatingPointError if a split operand of the training convolutions left fp16's
+    range since the last call (an activation above 65504, or a non-finite one; the scaled
+    gradients cannot: |dM| <= 32 (sum |A|)^2 <= 30752 for these tiles), and clear the flag."""
+    for dev, f in list(_FLAGS.items()):
+        if device is not None and dev != torch.device(device):
+            continue
+        if int(f.item()):
+            f.zero_()
+            raise FloatingPointError("training convolution operand out of fp16 range")
+
+
+_FLAGS = {}
+_G = {}
+
+
+def _g(m, dev):
+    """nnet.WINOGRAD_G[m] as an f32 device tensor (cached: no host copy per backward)."""
+    t = _G.get((m, dev))
+    if t is None:
+        t = _G[(m, dev)] = torch.tensor(WINOGRAD_G[m], dtype=torch.float32, device=dev)
+    return t
+
+
+def _flag(dev):
+    f = _FLAGS.get(dev)
+    if f is None:
+        f = _FLAGS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return f
+
+
+__all__ = ["WinogradConv3x3", "applies", "check_range", "conv3x3", "train_forward"]

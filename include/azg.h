@@ -236,7 +236,7 @@ int  azg_split_gemm(const void* a, const void* bt, float* m, int32_t nruns, cons
 /* The same with an explicit kernel schedule, for tests: 0 (reads, then MFMAs per stage,
  * one tile per workgroup), 4 (variant 0 persistent, the azg_split_gemm default), 17 / 18
  * (variant 0 on 128 / 64-row tiles, azg_split_gemm's pick for short launches).  The
- * probe-only schedules measured in DESIGN.md (1-3, 5-8, 10-12, 15, 16, 19) are not in the
+ * probe-only schedules measured in HISTORY.md (1-3, 5-8, 10-12, 15, 16, 19) are not in the
  * product library: tools/Makefile builds them into tools/libazg_probes.so, which exports this
  * entry point for all of them and azg_split_gemm_stamps (per-wave phase stamps of variant 4);
  * other values return AZG_ERR_ARG here. */
@@ -315,6 +315,11 @@ int  azg_fc_act(const float* m, int32_t parts, int64_t part_stride, const float*
                 void* stream);
 int  azg_policy_value_parts(const float* m, int32_t parts, int64_t part_stride, int32_t ldm, const float* bias,
                             float scale, float* P, float* v, int32_t rows, int32_t actions, void* stream);
+/* azg_fc_act (AZG_WINO_SPLIT2 output) for TRANSPOSED partial products m [parts][n][rows] (the
+ * small-batch fc1 computed as W x A^T, every weight tile read once); rows % 64 == 0, n % 64 == 0,
+ * (n / out_parts) % 64 == 0.  Same arithmetic: y = bias + scale * (parts summed in order). */
+int  azg_fc_act_t(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale, void* out,
+                  int32_t rows, int32_t n, int32_t relu, int32_t out_parts, int32_t* overflow, void* stream);
 
 /* Device pointers of the engine state (for zero-copy consumers, e.g. the
  * example gather): [0] boards i8 [1] turns [2] players [3] outcomes [4] active
@@ -366,6 +371,35 @@ int  azg_examples(int32_t game_kind, int32_t n, int32_t max_turns, int32_t temp_
                   int32_t max_moves, const int32_t* moves, const int32_t* actions, const void* counts,
                   int32_t counts_bytes, int32_t label_mode, int64_t maxlen, float* planes, float* pis,
                   float* vs, int64_t* count, void* stream);
+
+/* ---- trainer convolutions (azg_wino_train.hip; NNetWrapper.train, NNet.py:36-76) ------------
+ * conv2-4 of the training forward and backward on the Winograd transforms and the split GEMM
+ * (azg_amd/wino_train.py drives them; replaces the MIOpen convolutions torch runs for
+ * InflexionNNet.py:39-45 and their autograd).  Device pointers, caller's stream, no sync.
+ *   azg_absmax          : *out = bits of max |x| over n floats (n % 4 == 0; *out zeroed first).
+ *   azg_wt_u_build      : U_e = G_a w G_b^T of conv weights w [k][c][3][3] for an h_out-side
+ *                         output (nnet._winograd_u's point order), scaled by 2^ku (max |U| 2^ku
+ *                         in (512, 1024], *uamax = bits of max |U|), split into AZG_WINO_SPLIT2
+ *                         rows: ut [P][k][2c] (the forward GEMM's B operand) and/or un
+ *                         [P][c][2k] (the input-gradient GEMM's).
+ *   azg_wt_out          : y NHWC = bias + 2^-ku A^T M A (no ReLU), h_out in {3, 5, 7}.
+ *   azg_wt_dout         : dM [P][T][2k] AZG_WINO_SPLIT2 = 2^kd A dy A^T (dy NHWC; 2^kd puts
+ *                         max |dy| in (16, 32]); |dM| > 65504 sets *overflow.
+ *   azg_wt_din          : dx NHWC [batch, h_in, h_in, c] = 2^-(kd+ku) sum over tiles of
+ *                         B dV B^T (dV f32 [P][T][c]); (h_in, pad) in {(7,1), (7,0), (5,0)}.
+ *   azg_wt_split2_transpose: AZG_WINO_SPLIT2 [points][t][2c] -> [points][c][2t] (t, c % 64).
+ *   azg_wt_pow2_scale   : *out = the power of two the kernels scale by for amax, target. */
+int  azg_absmax(const float* x, int64_t n, uint32_t* out, void* stream);
+int  azg_wt_u_build(const float* w, int32_t c, int32_t k, int32_t h_out, uint32_t* uamax, void* ut, void* un,
+                    void* stream);
+int  azg_wt_out(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,
+                const uint32_t* uamax, void* stream);
+int  azg_wt_dout(const float* dy, void* dM, int32_t batch, int32_t h_out, int32_t k, const uint32_t* dyamax,
+                 int32_t* overflow, void* stream);
+int  azg_wt_din(const float* dV, float* dx, int32_t batch, int32_t h_in, int32_t pad, int32_t c,
+                const uint32_t* uamax, const uint32_t* dyamax, void* stream);
+int  azg_wt_split2_transpose(const void* src, void* dst, int32_t points, int32_t t, int32_t c, void* stream);
+int  azg_wt_pow2_scale(const uint32_t* amax, float target, float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -308,7 +308,7 @@ def test_inference_net_trained_network(conv, gemm, B):
     np.testing.assert_allclose(v.cpu().numpy().ravel(), d["v"][idx.cpu().numpy()], rtol=1e-5, atol=1e-6)
 
 
-PROBE_VARIANTS = [1, 2, 3, 5, 7, 8, 11, 12, 19]  # tools/libazg_probes.so only
+PROBE_VARIANTS = [1, 2, 3, 5, 7, 8, 11, 12, 19]  # tools/libazg_probes.so only (HISTORY.md 4.1)
 probes = pytest.mark.skipif(not os.environ.get("AZG_PROBES"),
                             reason="probe-only GEMM schedules: AZG_PROBES=1 (tools/Makefile builds them)")
 
@@ -803,8 +803,10 @@ def test_split_form_under_expandable_segments():
 @pytest.mark.parametrize("A,C", [(1024, 64), (343, 6), (343, 10)])
 def test_small_path_gate_falls_back(A, C):
     """shapes the small-batch kernels reject (1024 actions: azg_small_heads takes at
-    most 1023; 6 or 10 channels: fc1's K = 9 C is not a multiple of 4) take the library path at
-    one leaf instead of raising AZG_ERR_ARG, and still match the module."""
+    most 1023; 6 or 10 channels: fc1's K = 9 C is not a multiple of 4) are refused by the gate
+    instead of raising AZG_ERR_ARG inside it; the 1024-action net then runs the library path at
+    one leaf and matches the module.  (C = 2 mod 4 cannot run the library path either: its
+    bias / ReLU pass takes float4 rows.)"""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
     torch.manual_seed(8)
@@ -812,8 +814,59 @@ def test_small_path_gate_falls_back(A, C):
     fast = InferenceNet(net, conv="miopen", gemm="f32").cuda()
     x = (torch.rand(1, 4, 7, 7, device="cuda") < 0.3).float()
     assert not fast._small_ok(x)
+    if C % 4:
+        return
     with torch.no_grad():
         p, v = fast(x)
         logp, v_ref = net(x)
     torch.testing.assert_close(p, torch.exp(logp), rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(v.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B", [256, 512, 768])
+def test_small_fc_tail_matches_reference(B):
+    """The FC tail below FC1_SPLIT_MIN_BATCH leaves on libazg only (InferenceNet._fc_split_small:
+    fc1 as the transposed split-K GEMM W1 A^T, azg_fc_act_t, then fc2 / [fc3 | fc4] split-K; C2's
+    256 leaves) against the reference module (1e-5) and the f32 hipBLASLt tail it replaces."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    torch.manual_seed(13)
+    net = InflexionNNet().cuda().eval()
+    fast = InferenceNet(net).cuda()
+    assert fast.fc_tail_small
+    x = (torch.rand(B, 4, 7, 7, device="cuda") < 0.3).float()
+    x[:, 2:] = x[:, 2:, :1, :1]
+    with torch.no_grad():
+        p, v = fast(x)
+        fast.check_range()
+        logp, v_ref = net(x)
+        fast.fc_tail_small = False
+        p32, v32 = fast(x)
+    torch.testing.assert_close(p, torch.exp(logp), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(v.reshape(-1), v_ref.reshape(-1), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p, p32, rtol=1e-5, atol=1e-7)
+
+
+def test_fc_act_t_kernel():
+    """azg_fc_act_t: transposed partial products [parts][n][rows] summed in order, bias, ReLU,
+    written as split2 K-parts -- equal to azg_fc_act on the same partials transposed back."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    torch.manual_seed(14)
+    parts, n, rows, out_parts = 5, 1024, 256, 16
+    m = torch.randn(parts, n, rows, device="cuda")
+    bias = torch.randn(n, device="cuda")
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    a = torch.empty((out_parts, rows, 2 * n // out_parts), dtype=torch.float16, device="cuda")
+    b = torch.empty_like(a)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    L = _lib.lib()
+    _lib.check(L.azg_fc_act_t(ctypes.c_void_p(m.data_ptr()), parts, n * rows, ctypes.c_void_p(bias.data_ptr()), 0.25,
+                              ctypes.c_void_p(a.data_ptr()), rows, n, 1, out_parts, ctypes.c_void_p(ovf.data_ptr()), st))
+    mt = m.transpose(1, 2).contiguous()
+    _lib.check(L.azg_fc_act(ctypes.c_void_p(mt.data_ptr()), parts, n * rows, ctypes.c_void_p(bias.data_ptr()), 0.25,
+                            ctypes.c_void_p(b.data_ptr()), rows, n, 1, 2, out_parts, ctypes.c_void_p(ovf.data_ptr()), st))
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    assert int(ovf.item()) == 0

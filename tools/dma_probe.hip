@@ -1,7 +1,7 @@
 // dma_probe.hip -- how fast can LDS-DMA (buffer_load_dwordx4 ... lds) fill LDS on gfx950,
 // as a function of where the bytes come from (L2-resident, Infinity-Cache-resident, HBM)?
 // The split GEMM (azg_split_gemm.hip) moves 64 KB per 256x256x32 stage per CU this way;
-// its stage time follows those bytes.  This probe keeps the GEMM's stage
+// its stage time follows those bytes (HISTORY.md 4.1).  This probe keeps the GEMM's stage
 // structure -- 512-thread workgroups, one per CU, double-buffered 64 KB stages, every
 // wave issuing its pieces then vmcnt(0) + barrier -- with no MFMAs and no LDS reads.
 //

@@ -1,5 +1,5 @@
 // first_probe.hip -- probe build (not the product): winograd_first_kernel's write path
-// in other shapes, to find what holds it at ~5.1 TB/s.
+// in other shapes, to find what holds it at ~5.1 TB/s (HISTORY.md 6b).
 // Every variant computes exactly the product kernel's values and layout (conv1_sparse,
 // in_tile, the AZG_WINO_SPLIT2 rows); only the store shape and the block / grid shape
 // differ:

@@ -1,5 +1,5 @@
 """winograd_mid<7> (conv2 -> conv3) timed alone and right after a conv2-shaped split GEMM,
-to tell a layout cost from the clock a preceding GEMM leaves behind.
+to tell a layout cost from the clock a preceding GEMM leaves behind (HISTORY.md 6b).
 
     python tools/mid_probe.py > gpurun_out/mid_probe.json
 """

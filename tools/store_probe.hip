@@ -1,4 +1,4 @@
-// Store-shape probe for the Winograd input transforms ("Transform stores"):
+// Store-shape probe for the Winograd input transforms (HISTORY.md 6b, "Transform stores"):
 // the V2 write of winograd_first (4096 images x 169 points x 512 channels, hi + lo fp16,
 // 1.42 GB) as one wave per (image, 64 channels), each lane one channel, written
 //   mode 0: as today, [hi(512) | lo(512)] rows: two 2-byte stores per point (128 B per

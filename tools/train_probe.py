@@ -18,10 +18,10 @@ from azg_amd.inflexion import InflexionGame  # noqa: E402
 from azg_amd.nnet import NNetWrapper  # noqa: E402
 
 
-def run(label, channels_last=False, benchmark=False, batches=30, dtype="f32", fused=False):
+def run(label, channels_last=False, benchmark=False, batches=30, dtype="f32", fused=False, conv="winograd"):
     torch.backends.cudnn.benchmark = benchmark
     torch.manual_seed(0)
-    w = NNetWrapper(InflexionGame(7), dict(epochs=1, batch_size=512, fused_adam=fused, train_dtype=dtype), device="cuda")
+    w = NNetWrapper(InflexionGame(7), dict(epochs=1, batch_size=512, fused_adam=fused, train_dtype=dtype, train_conv=conv), device="cuda")
     if channels_last:
         w.nnet.to(memory_format=torch.channels_last)
     E = 512 * batches
@@ -46,6 +46,11 @@ def run(label, channels_last=False, benchmark=False, batches=30, dtype="f32", fu
 if __name__ == "__main__":
     if sys.argv[1:] == ["f32"]:  # the default trainer alone (e.g. under rocprofv3: kernel time vs wall)
         run("nchw")
+        sys.exit(0)
+    if sys.argv[1:] == ["conv"]:  # the Winograd training convolutions against the library ones, alternating
+        for _ in range(3):
+            run("winograd")
+            run("library", conv="library")
         sys.exit(0)
     run("nchw")
     run("nchw+benchmark", benchmark=True)
