@@ -38,33 +38,38 @@ def test_winograd_conv_forward_backward(H, pad, B):
 
 
 def test_train_forward_matches_module():
-    """wino_train.train_forward (conv2-4 on the training kernels) gives the module's training-mode
-    outputs and parameter gradients within the f32 tolerance (BatchNorm in training mode, dropout 0)."""
+    """wino_train.train_forward (conv2-4 on the training kernels) against the module's training-mode
+    forward / backward, both judged against an f64 run of the module (BatchNorm in training mode,
+    dropout 0): outputs within 1e-4, and every parameter gradient no farther from the f64 one than
+    twice the f32 library path's distance (+1e-5 of its size).  The conv / fc biases ahead of a
+    BatchNorm have a zero gradient up to rounding and are skipped; so is conv1 (MIOpen in both)."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InflexionNNet
     from azg_amd.wino_train import train_forward
     torch.manual_seed(12)
-    net = InflexionNNet(dropout=0.0).cuda().train()
-    ref = InflexionNNet(dropout=0.0).cuda().train()
-    ref.load_state_dict(net.state_dict())
+    nets = [InflexionNNet(dropout=0.0).cuda().train() for _ in range(3)]
+    for m in nets[1:]:
+        m.load_state_dict(nets[0].state_dict())
+    nets[2].double()
     x = (torch.rand(128, 4, 7, 7, device="cuda") < 0.3).float()
     tp = torch.softmax(torch.randn(128, 343, device="cuda"), 1)
     tv = torch.rand(128, device="cuda") * 2 - 1
     outs = []
-    for m, fwd in ((net, lambda s: train_forward(net, s)), (ref, ref)):
-        pi, v = fwd(x)
-        loss = -torch.sum(tp * pi) / 128 + torch.sum((tv - v.view(-1)) ** 2) / 128
+    for m, fwd, dt in ((nets[0], lambda s: train_forward(nets[0], s), torch.float32),
+                       (nets[1], nets[1], torch.float32), (nets[2], nets[2], torch.float64)):
+        pi, v = fwd(x.to(dt))
+        loss = -torch.sum(tp.to(dt) * pi) / 128 + torch.sum((tv.to(dt) - v.view(-1)) ** 2) / 128
         loss.backward()
-        outs.append((pi.detach(), v.detach(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
-    (p1, v1, g1), (p2, v2, g2) = outs
-    torch.testing.assert_close(p1, p2, rtol=1e-4, atol=1e-5)
-    torch.testing.assert_close(v1, v2, rtol=1e-4, atol=1e-5)
-    for k in g1:
-        err = (g1[k] - g2[k]).abs().max().item() / max(g2[k].abs().max().item(), 1e-30)
-        # the conv / fc biases ahead of a BatchNorm have a zero gradient up to rounding
+        outs.append((pi.detach().double(), v.detach().double(),
+                     {k: p.grad.detach().double() for k, p in m.named_parameters()}))
+    (pw, vw, gw), (pl, vl, gl), (p64, v64, g64) = outs
+    torch.testing.assert_close(pw, p64, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(vw, v64, rtol=1e-4, atol=1e-5)
+    for k in g64:
         if k.endswith("bias") and k.split(".")[0] in ("conv1", "conv2", "conv3", "conv4", "fc1", "fc2"):
             continue
-        assert err < 1e-3, (k, err)
-    for name in ("bn2", "bn3", "bn4"):  # running statistics of the training-mode BatchNorm
-        np.testing.assert_allclose(getattr(net, name).running_var.cpu().numpy(),
-                                   getattr(ref, name).running_var.cpu().numpy(), rtol=1e-4)
+        scale = max(g64[k].abs().max().item(), 1e-30)
+        ew = (gw[k] - g64[k]).abs().max().item() / scale
+        el = (gl[k] - g64[k]).abs().max().item() / scale
+        print(f"{k}: winograd {ew:.3g}, library {el:.3g} of max |grad|")
+        assert ew <= 2 * el + 1e-5, (k, ew, el)
