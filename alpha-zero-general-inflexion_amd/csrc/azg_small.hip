@@ -62,17 +62,46 @@ constexpr int SF_T = 256;  // small_fc threads
 // 4-bank groups (pitch % 64 == 4 for Cin % 64 == 0)
 __host__ __device__ constexpr int sc_pitch(int cin) { return ((cin + 3) & ~3) + 4; }
 
-template <int PXL, int CO_PB, bool VEC, bool WLDS>
-__global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restrict__ x, long long sB, int sY, int sX,
-                                                          int sC, int B, int H, int pad,
-                                                          const float* __restrict__ w, int Cin, int Cout,
-                                                          const float* __restrict__ bias, int relu,
-                                                          float* __restrict__ y, int ldy) {
+// COH (the fused forward, small_net_kernel): activations another block of the same launch wrote
+// are read with agent-scope loads and written with agent-scope (write-through) stores -- the
+// split-K hand-off's rule (see above) applied to every layer boundary inside the launch
+template <bool COH>
+__device__ __forceinline__ float4 ld4(const float* p) {
+    if constexpr (COH) {
+        const unsigned* u = (const unsigned*)p;
+        return make_float4(__uint_as_float(__hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                           __uint_as_float(__hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                           __uint_as_float(__hip_atomic_load(u + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                           __uint_as_float(__hip_atomic_load(u + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+    } else {
+        return *(const float4*)p;
+    }
+}
+template <bool COH>
+__device__ __forceinline__ float ld1(const float* p) {
+    if constexpr (COH)
+        return __uint_as_float(__hip_atomic_load((const unsigned*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    else
+        return *p;
+}
+template <bool COH>
+__device__ __forceinline__ void st1(float* p, float v) {
+    if constexpr (COH)
+        __hip_atomic_store((unsigned*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
+template <int PXL, int CO_PB, bool VEC, bool WLDS, bool COH = false>
+__device__ __forceinline__ void small_conv_body(int bid, float* __restrict__ lds, const float* __restrict__ x,
+                                                long long sB, int sY, int sX, int sC, int B, int H, int pad,
+                                                const float* __restrict__ w, int Cin, int Cout,
+                                                const float* __restrict__ bias, int relu, float* __restrict__ y,
+                                                int ldy) {
     constexpr int KSL = SC_T / PXL;  // K slices
-    __shared__ __attribute__((aligned(16))) float lds[SC_LDS_MAX / 4];
     const int tid = threadIdx.x;
     const int p = tid % PXL, s = tid / PXL;
-    const int co0 = blockIdx.x * CO_PB;
+    const int co0 = bid * CO_PB;
     const int Ho = H + 2 * pad - 2, hw = Ho * Ho;
     const int K = 9 * Cin, P = sc_pitch(Cin);
     float* xs = lds;                          // [H * H][P] one leaf's input
@@ -108,7 +137,7 @@ __global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restric
                 for (int u = 0; u < SC_UNR; ++u) {  // past the end: a duplicate load, not stored
                     const int i = min(base + u * SC_T, nx4 - 1);
                     const int pix = i / c4, c = (i - pix * c4) * 4, iy = pix / H, ix = pix - iy * H;
-                    r[u] = *(const float4*)(xb + (long long)iy * sY + (long long)ix * sX + c);
+                    r[u] = ld4<COH>(xb + (long long)iy * sY + (long long)ix * sX + c);
                 }
                 if constexpr (WITHW) {
 #pragma unroll
@@ -134,7 +163,7 @@ __global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restric
             const int n = H * H * Cin;
             for (int i = tid; i < n; i += SC_T) {
                 const int pix = i / Cin, c = i - pix * Cin, iy = pix / H, ix = pix - iy * H;
-                xs[pix * P + c] = xb[(long long)iy * sY + (long long)ix * sX + (long long)c * sC];
+                xs[pix * P + c] = ld1<COH>(xb + (long long)iy * sY + (long long)ix * sX + (long long)c * sC);
             }
         }
         __syncthreads();
@@ -187,10 +216,21 @@ __global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restric
             for (int q = 0; q < KSL; ++q) sum += red[(q * PXL + pp) * CO_PB + c];  // slice order
             float o = sum + (bias ? bias[co0 + c] : 0.f);
             if (relu) o = fmaxf(o, 0.f);
-            y[(long long)(b * hw + pp) * ldy + co0 + c] = o;
+            st1<COH>(y + (long long)(b * hw + pp) * ldy + co0 + c, o);
         }
         __syncthreads();  // xs and red are rewritten for the next leaf
     }
+}
+
+template <int PXL, int CO_PB, bool VEC, bool WLDS>
+__global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restrict__ x, long long sB, int sY, int sX,
+                                                          int sC, int B, int H, int pad,
+                                                          const float* __restrict__ w, int Cin, int Cout,
+                                                          const float* __restrict__ bias, int relu,
+                                                          float* __restrict__ y, int ldy) {
+    __shared__ __attribute__((aligned(16))) float lds[SC_LDS_MAX / 4];
+    small_conv_body<PXL, CO_PB, VEC, WLDS>(blockIdx.x, lds, x, sB, sY, sX, sC, B, H, pad, w, Cin, Cout, bias, relu, y,
+                                           ldy);
 }
 
 // Split-K form for the 512-channel layers (conv2-4): block (co group of SK_CO = 8 channels, ci
@@ -222,22 +262,18 @@ __host__ __device__ constexpr int sk_wpf(int kg) { return kg == SK_KG1 ? 5 : 3; 
 // staging waves).
 // The block's weight quarter is loaded into registers first (SC_WPF float4 per thread) and
 // written to LDS once the leaf's input loads are in flight: one memory round trip for both.
-template <int PXL, int F1, int KG>
-__global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __restrict__ x, long long sB, int sY,
-                                                             int sX, int B, int H, int pad,
-                                                             const float* __restrict__ w, int Cin,
-                                                             const float* __restrict__ bias, int relu,
-                                                             float* __restrict__ y, int ldy,
-                                                             float* __restrict__ part, unsigned* __restrict__ ticket,
-                                                             const float* __restrict__ w1, const float* __restrict__ b1,
-                                                             int D) {
+template <int PXL, int F1, int KG, bool COH = false>
+__device__ __forceinline__ void small_conv_sk_body(int bid, int nblk, float* __restrict__ lds, unsigned& s_last,
+                                                   const float* __restrict__ x, long long sB, int sY, int sX, int B,
+                                                   int H, int pad, const float* __restrict__ w, int Cin,
+                                                   const float* __restrict__ bias, int relu, float* __restrict__ y,
+                                                   int ldy, float* __restrict__ part, unsigned* __restrict__ ticket,
+                                                   const float* __restrict__ w1, const float* __restrict__ b1, int D) {
     constexpr int KSL = SC_T / PXL;
     constexpr int SC_WPF = sk_wpf(KG);
-    __shared__ __attribute__((aligned(16))) float lds[sk_lds(KG) / 4];
-    __shared__ unsigned s_last;
     const int tid = threadIdx.x;
     const int p = tid % PXL, s = tid / PXL;
-    const int cg = blockIdx.x / KG, kg = blockIdx.x % KG;
+    const int cg = bid / KG, kg = bid % KG;
     const int co0 = cg * SK_CO;
     const int Cq = Cin / KG, ci_base = kg * Cq;
     const int Ho = H + 2 * pad - 2, hw = Ho * Ho;
@@ -320,7 +356,7 @@ __global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __rest
             for (int u = 0; u < SC_UNR; ++u) {
                 const int i = min(base + u * SC_T, n4 - 1);
                 const int pix = i / c4, c = (i - pix * c4) * 4, iy = pix / H, ix = pix - iy * H;
-                r[u] = *(const float4*)(xb + (long long)iy * sY + (long long)ix * sX + c);
+                r[u] = ld4<COH>(xb + (long long)iy * sY + (long long)ix * sX + c);
             }
             stage_w();  // the weights' stores once the first input loads are in flight
 #pragma unroll
@@ -379,7 +415,7 @@ __global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __rest
             float sum = 0.f;
             for (int q = 0; q < KSL; ++q) sum += red[(q * PXL + pp) * SK_CO + c];
             // write-through (sc1) stores: published by the drain below, no release fence
-            __hip_atomic_store((unsigned*)(part + (((long long)kg * (gridDim.x / KG) + cg) * B + b) * hw * SK_CO + t),
+            __hip_atomic_store((unsigned*)(part + (((long long)kg * (nblk / KG) + cg) * B + b) * hw * SK_CO + t),
                                __float_as_uint(sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();  // xs and red are rewritten for the next leaf
@@ -396,7 +432,7 @@ __global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __rest
     __syncthreads();
     if (!s_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler order only: every load below is sc1)
-    const int G = gridDim.x / KG;
+    const int G = nblk / KG;
     for (int t = tid; t < B * hw * SK_CO; t += SC_T) {
         const int c = t % SK_CO, bp = t / SK_CO;  // bp = b * hw + pixel
         float sum = 0.f;
@@ -408,26 +444,44 @@ __global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __rest
         }
         float o = sum + (bias ? bias[co0 + c] : 0.f);
         if (relu) o = fmaxf(o, 0.f);
-        y[(long long)bp * ldy + co0 + c] = o;
+        st1<COH>(y + (long long)bp * ldy + co0 + c, o);
     }
-    if (tid == 0) ticket[cg] = 0u;  // every block of the group has arrived: ready for the next launch
+    // every block of the group has arrived: ready for the next launch (or the fused forward's next layer)
+    if (tid == 0) __hip_atomic_store(ticket + cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int PXL, int F1, int KG>
+__global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __restrict__ x, long long sB, int sY,
+                                                             int sX, int B, int H, int pad,
+                                                             const float* __restrict__ w, int Cin,
+                                                             const float* __restrict__ bias, int relu,
+                                                             float* __restrict__ y, int ldy,
+                                                             float* __restrict__ part, unsigned* __restrict__ ticket,
+                                                             const float* __restrict__ w1, const float* __restrict__ b1,
+                                                             int D) {
+    __shared__ __attribute__((aligned(16))) float lds[sk_lds(KG) / 4];
+    __shared__ unsigned s_last;
+    small_conv_sk_body<PXL, F1, KG>(blockIdx.x, gridDim.x, lds, s_last, x, sB, sY, sX, B, H, pad, w, Cin, bias, relu,
+                                    y, ldy, part, ticket, w1, b1, D);
 }
 
 // HEADS ([fc3 | fc4] + the heads, InflexionNNet.py:51-54 and NNet.py:94): y receives the
 // logits (no bias); each block then takes a ticket, and the last of the grid's blocks reads all
 // rows back (agent-scope loads) and writes P = softmax(hb[:A] + y[:A]) and v = tanh(hb[A] + y[A])
 // per leaf -- the arithmetic of azg_policy_value, one wave per leaf -- and resets the ticket.
-template <int NPB, int BMAX, bool HEADS>
-__global__ __launch_bounds__(SF_T) void small_fc_kernel(const float* __restrict__ x, int ldx, int B,
-                                                        const float* __restrict__ w, int K, int N,
-                                                        const float* __restrict__ bias, int relu,
-                                                        float* __restrict__ y, int ldy, const float* __restrict__ hb,
-                                                        float* __restrict__ P, float* __restrict__ V,
-                                                        unsigned* __restrict__ ticket) {
-    __shared__ float red[SF_T / 64][NPB * BMAX];
-    __shared__ unsigned s_last;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int n0 = blockIdx.x * NPB;
+// tid: the thread's index in the (virtual) block of SF_T threads; valid = false: a block half with no
+// row group in this round (the fused kernel runs two groups per 512-thread block) -- it computes and
+// stores nothing, takes no ticket, but meets every barrier of the block
+template <int NPB, int BMAX, bool HEADS, bool COH = false>
+__device__ __forceinline__ void small_fc_body(int bid, int nblk, int tid, bool valid, float (*red)[NPB * BMAX],
+                                              unsigned& s_last, const float* __restrict__ x, int ldx, int B,
+                                              const float* __restrict__ w, int K, int N,
+                                              const float* __restrict__ bias, int relu, float* __restrict__ y,
+                                              int ldy, const float* __restrict__ hb, float* __restrict__ P,
+                                              float* __restrict__ V, unsigned* __restrict__ ticket) {
+    constexpr int T = SF_T;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int n0 = bid * NPB;
     const int K4 = K / 4;
     float acc[NPB][BMAX];
 #pragma unroll
@@ -435,11 +489,11 @@ __global__ __launch_bounds__(SF_T) void small_fc_kernel(const float* __restrict_
 #pragma unroll
         for (int b = 0; b < BMAX; ++b) acc[r][b] = 0.f;
 #pragma unroll 8
-    for (int k4 = tid; k4 < K4; k4 += SF_T) {
+    for (int k4 = tid; k4 < (valid ? K4 : 0); k4 += T) {
         float4 xv[BMAX];
 #pragma unroll
         for (int b = 0; b < BMAX; ++b)
-            xv[b] = b < B ? *(const float4*)(x + (long long)b * ldx + 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            xv[b] = b < B ? ld4<COH>(x + (long long)b * ldx + 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int r = 0; r < NPB; ++r) {
             if (n0 + r >= N) break;
@@ -466,26 +520,29 @@ __global__ __launch_bounds__(SF_T) void small_fc_kernel(const float* __restrict_
             if (lane == 0) red[wv][r * BMAX + b] = v;
         }
     __syncthreads();
-    if (tid < NPB * BMAX) {
+    if (tid < NPB * BMAX && valid) {
         const int r = tid / BMAX, b = tid - r * BMAX;
         if (n0 + r < N && b < B) {
             float sum = 0.f;
 #pragma unroll
-            for (int q = 0; q < SF_T / 64; ++q) sum += red[q][tid];
+            for (int q = 0; q < T / 64; ++q) sum += red[q][tid];
             float o = sum + (bias ? bias[n0 + r] : 0.f);
             if (relu) o = fmaxf(o, 0.f);
             if constexpr (HEADS)  // write-through (sc1): read back by the grid's last block
                 __hip_atomic_store((unsigned*)(y + (long long)b * ldy + n0 + r), __float_as_uint(o), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             else
-                y[(long long)b * ldy + n0 + r] = o;
+                st1<COH>(y + (long long)b * ldy + n0 + r, o);
         }
     }
+    if constexpr (COH && !HEADS) __syncthreads();  // red is rewritten by the block's next row group
     if constexpr (HEADS) {
         // publish as small_conv_sk_kernel does: drain, one relaxed ticket, sc1 loads in the last block
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+        if (tid == 0)
+            s_last = valid && __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                                  (unsigned)nblk - 1;
         __syncthreads();
         if (!s_last) return;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler order only: the loads are sc1)
@@ -523,8 +580,125 @@ __global__ __launch_bounds__(SF_T) void small_fc_kernel(const float* __restrict_
             }
             if (lane == 0) V[wv] = tanhf(hb[A] + ld(A));
         }
-        if (tid == 0) *ticket = 0u;
+        if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+template <int NPB, int BMAX, bool HEADS>
+__global__ __launch_bounds__(SF_T) void small_fc_kernel(const float* __restrict__ x, int ldx, int B,
+                                                        const float* __restrict__ w, int K, int N,
+                                                        const float* __restrict__ bias, int relu,
+                                                        float* __restrict__ y, int ldy, const float* __restrict__ hb,
+                                                        float* __restrict__ P, float* __restrict__ V,
+                                                        unsigned* __restrict__ ticket) {
+    __shared__ float red[SF_T / 64][NPB * BMAX];
+    __shared__ unsigned s_last;
+    small_fc_body<NPB, BMAX, HEADS>(blockIdx.x, gridDim.x, threadIdx.x, true, red, s_last, x, ldx, B, w, K, N, bias,
+                                    relu, y, ldy, hb, P, V, ticket);
+}
+
+// ---- the whole forward in one launch (small_net_kernel) ---------------------------------------
+// conv1 + conv2 (split-K, 4 K-parts), conv3 (split-K, 4 K-parts), conv4 (2-channel blocks), fc1, fc2,
+// [fc3 | fc4] + heads: the same block bodies as the per-layer kernels above (same arithmetic, same
+// summation orders: bit-identical results), one persistent grid of at most one 512-thread block per
+// CU, the layers separated by grid barriers instead of kernel boundaries.  Activations cross the
+// layers inside the launch as write-through stores drained before the barrier and agent-scope loads
+// after it (the split-K hand-off's rule); the barrier is a monotonic 64-bit arrival counter (each
+// launch adds 5 x grid; a block's targets follow from the value its first arrival returns), spun on
+// with s_sleep, and gives up after ~2^24 polls (setting *err) rather than hang.
+struct SmallNetArgs {
+    const float* planes;
+    const float *w1, *b1, *w2, *b2, *w3, *b3, *w4, *b4, *fw1, *fb1, *fw2, *fb2, *fw34, *fb34;
+    float *y2, *y3, *y4, *h1, *h2, *logits, *P, *v;
+    float* part;
+    unsigned* tickets;
+    unsigned* heads_ticket;
+    unsigned long long* bar;
+    int* err;
+    int B, D, C, A, N1, N2;
+};
+
+constexpr int SN_POOL = 96 * 1024;  // LDS of the fused kernel: the largest layer's (conv1 + conv2's split-K block)
+
+__device__ __forceinline__ void grid_sync(const SmallNetArgs& a, unsigned long long& base, int j) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's write-through stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long old = __hip_atomic_fetch_add(a.bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (j == 1) base = old - old % gridDim.x;
+        const unsigned long long target = base + (unsigned long long)j * gridDim.x;
+        for (unsigned spins = 0; __hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) {  // a block never arrived: report instead of hanging the GPU
+                atomicOr(a.err, 1);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+template <int NB, int BMAX, bool WLDS3, bool WLDS4>
+__global__ __launch_bounds__(SC_T) void small_net_kernel(SmallNetArgs a) {
+    __shared__ __attribute__((aligned(16))) float pool[SN_POOL / 4];
+    __shared__ unsigned s_last;
+    constexpr int H3 = NB - 2, H4 = NB - 4;  // conv3's and conv4's output sides (pads 1, 1, 0, 0)
+    constexpr int P12 = NB * NB <= 64 ? 64 : 128, P3 = H3 * H3 <= 16 ? 16 : H3 * H3 <= 32 ? 32 : 64,
+                  P4 = H4 * H4 <= 16 ? 16 : 32;
+    const int G = gridDim.x, C = a.C, B = a.B;
+    unsigned long long base = 0;
+    const int nsk = C / SK_CO * SK_KG1;
+    for (int it = blockIdx.x; it < nsk; it += G)
+        small_conv_sk_body<P12, NB, SK_KG1, true>(it, nsk, pool, s_last, a.planes, (long long)a.D * NB * NB, 0, 0, B,
+                                                  NB, 1, a.w2, C, a.b2, 1, a.y2, C, a.part, a.tickets, a.w1, a.b1,
+                                                  a.D);
+    grid_sync(a, base, 1);
+    if constexpr (H3 * H3 > 16) {  // conv3 as the per-layer path runs it: split-K in 8 K-parts ...
+        const int nsk3 = C / SK_CO * SK_KG;
+        for (int it = blockIdx.x; it < nsk3; it += G)
+            small_conv_sk_body<P3, 0, SK_KG, true>(it, nsk3, pool, s_last, a.y2, (long long)NB * NB * C, NB * C, C, B,
+                                                   NB, 0, a.w3, C, a.b3, 1, a.y3, C, a.part, a.tickets, nullptr,
+                                                   nullptr, 0);
+    } else {  // ... or, for <= 16 output pixels (6x6 boards), in 2-channel blocks
+        for (int it = blockIdx.x; it < C / 2; it += G)
+            small_conv_body<P3, 2, true, WLDS3, true>(it, pool, a.y2, (long long)NB * NB * C, NB * C, C, 1, B, NB, 0,
+                                                      a.w3, C, C, a.b3, 1, a.y3, C);
+    }
+    grid_sync(a, base, 2);
+    for (int it = blockIdx.x; it < C / 2; it += G)
+        small_conv_body<P4, 2, true, WLDS4, true>(it, pool, a.y3, (long long)H3 * H3 * C, H3 * C, C, 1, B, H3, 0, a.w4,
+                                                  C, C, a.b4, 1, a.y4, C);
+    grid_sync(a, base, 3);
+    // the FC layers: two row groups per block round, one per 256-thread half, each exactly the
+    // per-layer small_fc_kernel's block (its NPB for the layer's width, its reduction order)
+    const int K1 = H4 * H4 * C, half = threadIdx.x / SF_T, ht = threadIdx.x % SF_T;
+    __shared__ unsigned s_half[2];
+    auto fc = [&](auto NPB_, auto HEADS_, int nrow, const float* x, int ldx, const float* w, int K, const float* bias,
+                  int relu, float* y, int ldy, const float* hb, float* P, float* V, unsigned* ticket) {
+        constexpr int NPB = decltype(NPB_)::value;
+        constexpr bool HD = decltype(HEADS_)::value;
+        const int ng = (nrow + NPB - 1) / NPB;
+        float(*red)[NPB * BMAX] = (float(*)[NPB * BMAX])(pool + half * (SF_T / 64) * NPB * BMAX);
+        for (int g0 = 2 * blockIdx.x; g0 < ng; g0 += 2 * G)
+            small_fc_body<NPB, BMAX, HD, true>(g0 + half, ng, ht, g0 + half < ng, red, s_half[half], x, ldx, B, w, K,
+                                               nrow, bias, relu, y, ldy, hb, P, V, ticket);
+    };
+    if (a.N1 >= 2048) fc(std::integral_constant<int, 4>{}, std::false_type{}, a.N1, a.y4, K1, a.fw1, K1, a.fb1, 1, a.h1,
+                         a.N1, nullptr, nullptr, nullptr, nullptr);
+    else if (a.N1 >= 1024) fc(std::integral_constant<int, 2>{}, std::false_type{}, a.N1, a.y4, K1, a.fw1, K1, a.fb1, 1,
+                              a.h1, a.N1, nullptr, nullptr, nullptr, nullptr);
+    else fc(std::integral_constant<int, 1>{}, std::false_type{}, a.N1, a.y4, K1, a.fw1, K1, a.fb1, 1, a.h1, a.N1,
+            nullptr, nullptr, nullptr, nullptr);
+    grid_sync(a, base, 4);
+    if (a.N2 >= 2048) fc(std::integral_constant<int, 4>{}, std::false_type{}, a.N2, a.h1, a.N1, a.fw2, a.N1, a.fb2, 1,
+                         a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
+    else if (a.N2 >= 1024) fc(std::integral_constant<int, 2>{}, std::false_type{}, a.N2, a.h1, a.N1, a.fw2, a.N1, a.fb2,
+                              1, a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
+    else fc(std::integral_constant<int, 1>{}, std::false_type{}, a.N2, a.h1, a.N1, a.fw2, a.N1, a.fb2, 1, a.h2, a.N2,
+            nullptr, nullptr, nullptr, nullptr);
+    grid_sync(a, base, 5);
+    fc(std::integral_constant<int, 4>{}, std::true_type{}, a.A + 1, a.h2, a.N2, a.fw34, a.N2, nullptr, 0, a.logits,
+       a.A + 1, a.fb34, a.P, a.v, a.heads_ticket);
 }
 
 template <int PXL, bool VEC>
@@ -664,5 +838,74 @@ extern "C" int azg_small_heads(const float* x, int32_t ldx, int32_t batch, const
     else
         hipLaunchKernelGGL((small_fc_kernel<4, 4, true>), grid, dim3(SF_T), 0, st, x, ldx, batch, w34, K, N, nullptr, 0,
                            logits, N, b34, P, v, ticket);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+// The whole small-batch forward in one launch (small_net_kernel above).  w: 14 device pointers
+// w1 b1 w2 b2 w3 b3 w4 b4 fw1 fb1 fw2 fb2 fw34 fb34 (BN folded, conv weights [co][3][3][ci] as the
+// per-layer kernels take them, w1 [co][3][3][depth]); acts: the activations (y2 | y3 | y4 | h1 | h2 |
+// logits, sized by the caller); bar: the grid barrier's u64 counter (zero once, before first use);
+// err: set when a barrier gave up (the caller resets bar then).
+extern "C" int azg_small_net(const float* planes, int32_t batch, int32_t depth, int32_t n, int32_t C, int32_t A,
+                             int32_t n1, int32_t n2, const float* const* w, float* acts, int64_t acts_floats, float* P,
+                             float* v, float* work, int64_t work_floats, uint32_t* tickets, int32_t n_tickets,
+                             uint64_t* bar, int32_t* err, void* stream) {
+    if (!planes || !w || !acts || !P || !v || !work || !tickets || !bar || !err || batch <= 0 || batch > 4 ||
+        depth < 1 || depth > 4 || n < 6 || n > 8 || C <= 0 || C % (4 * SK_KG1) || C % SK_CO || A < 1 || A > 1023 ||
+        n1 <= 0 || n1 % 4 || n2 <= 0 || n2 % 4 || n_tickets < C / SK_CO + 1 || ((uintptr_t)work & 15) ||
+        ((uintptr_t)acts & 15))
+        return AZG_ERR_ARG;
+    for (int i = 0; i < 14; ++i)
+        if (!w[i] || ((uintptr_t)w[i] & 15)) return AZG_ERR_ARG;
+    const int hw = n * n, h3 = n - 2, h4 = n - 4;
+    const long long need_acts = (long long)batch * (hw * C + h3 * h3 * C + h4 * h4 * C + n1 + n2 + (A + 1));
+    if (acts_floats < need_acts || work_floats < (long long)SK_KG1 * C * batch * hw) return AZG_ERR_ARG;
+    // LDS: conv1 + conv2 and conv3 as split-K blocks, conv4 as 2-channel blocks (weights in LDS if they fit)
+    const size_t sk12 = (size_t)hw * (C / SK_KG1 + 4) * 4 + (size_t)9 * C / SK_KG1 * SK_CO * 4 + (size_t)SC_T * SK_CO * 4;
+    const size_t c3 = (size_t)hw * sc_pitch(C) * 4 + (size_t)SC_T * 2 * 4;  // conv3 in 2-channel blocks (6x6)
+    const size_t c4 = (size_t)h3 * h3 * sc_pitch(C) * 4 + (size_t)SC_T * 2 * 4, w4b = (size_t)2 * 9 * C * 4;
+    if (sk12 > SN_POOL || c4 > SN_POOL || (h3 * h3 <= 16 && c3 > SN_POOL)) return AZG_ERR_ARG;
+    const bool wlds3 = c3 + w4b <= SN_POOL, wlds4 = c4 + w4b <= SN_POOL;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            return AZG_ERR_HIP;
+    }
+    SmallNetArgs a{};
+    a.planes = planes;
+    a.w1 = w[0], a.b1 = w[1], a.w2 = w[2], a.b2 = w[3], a.w3 = w[4], a.b3 = w[5], a.w4 = w[6], a.b4 = w[7];
+    a.fw1 = w[8], a.fb1 = w[9], a.fw2 = w[10], a.fb2 = w[11], a.fw34 = w[12], a.fb34 = w[13];
+    a.y2 = acts;
+    a.y3 = a.y2 + (long long)batch * hw * C;
+    a.y4 = a.y3 + (long long)batch * h3 * h3 * C;
+    a.h1 = a.y4 + (long long)batch * h4 * h4 * C;
+    a.h2 = a.h1 + (long long)batch * n1;
+    a.logits = a.h2 + (long long)batch * n2;
+    a.P = P, a.v = v, a.part = work, a.tickets = tickets, a.heads_ticket = tickets + C / SK_CO;
+    a.bar = (unsigned long long*)bar, a.err = err;
+    a.B = batch, a.D = depth, a.C = C, a.A = A, a.N1 = n1, a.N2 = n2;
+    const dim3 grid((unsigned)cus);
+    hipStream_t st = (hipStream_t)stream;
+    auto go = [&](auto N_, auto B_, auto W3_, auto W4_) {
+        hipLaunchKernelGGL((small_net_kernel<decltype(N_)::value, decltype(B_)::value, decltype(W3_)::value,
+                                             decltype(W4_)::value>),
+                           grid, dim3(SC_T), 0, st, a);
+    };
+    auto by_w = [&](auto N_, auto B_) {  // (WLDS3 matters for 6x6 boards only)
+        if (wlds3 && wlds4) go(N_, B_, std::true_type{}, std::true_type{});
+        else if (wlds4) go(N_, B_, std::false_type{}, std::true_type{});
+        else go(N_, B_, std::false_type{}, std::false_type{});
+    };
+    auto by_b = [&](auto N_) {
+        if (batch == 1) by_w(N_, std::integral_constant<int, 1>{});
+        else by_w(N_, std::integral_constant<int, 4>{});
+    };
+    switch (n) {
+        case 6: by_b(std::integral_constant<int, 6>{}); break;
+        case 7: by_b(std::integral_constant<int, 7>{}); break;
+        default: by_b(std::integral_constant<int, 8>{}); break;
+    }
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }

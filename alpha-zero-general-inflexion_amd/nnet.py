@@ -36,6 +36,9 @@ WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C
 # launch per layer, no library) instead of MIOpen / hipBLASLt
 SMALL_PATH = True
 SMALL_MAX_B = 4
+# the small-batch forward as ONE launch (azg_small_net: the per-layer kernels' block bodies in a
+# persistent grid, grid barriers between the layers; bit-identical results), else one launch per layer
+SMALL_FUSED = True
 FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
 FC1_KPARTS = 4  # split-K parts of fc1 on libazg's split GEMM (4608 = 4 x 1152 for the 7x7 board)
 # split-K parts of fc2 (1024 -> 512) and [fc3 | fc4] (512 -> 344, padded to 512 columns) when the whole
@@ -819,6 +822,8 @@ class InferenceNet(nn.Module):
             self._small_tickets = torch.zeros(max(C // 8, 1) + 1, device=dev, dtype=torch.int32)
         work, tickets = self._small_work, self._small_tickets
         wp, tp = ctypes.c_void_p(work.data_ptr()), ctypes.c_void_p(tickets.data_ptr())
+        if self._fused_ok(B):
+            return self._forward_small_fused(planes, B, dev, st, wp, tp)
         first = 1
         if self.depth <= 4 and 6 <= n <= 8 and C % 16 == 0 and self.pads[:2] == [1, 1] \
                 and n * n * (C // 4 + 4) * 4 + 72 * C + 16384 <= 96 * 1024:  # azg_small_conv12's LDS (4 K-parts)
@@ -863,6 +868,46 @@ class InferenceNet(nn.Module):
                                      ctypes.c_void_p(v.data_ptr()),
                                      ctypes.c_void_p(tickets.data_ptr() + 4 * (tickets.numel() - 1)), st))
         return p, v
+
+    def _fused_ok(self, B):
+        """azg_small_net's preconditions (the conv1 + conv2 split-K form, pads 1, 1, 0, 0, its LDS pool)."""
+        n, C = self.n, self.w1.shape[0]
+        return (getattr(self, "small_fused", SMALL_FUSED) and self.depth <= 4 and 6 <= n <= 8 and C % 16 == 0
+                and self.pads == [1, 1, 0, 0] and n * n * (C // 4 + 4) * 4 + 72 * C + 16384 <= 96 * 1024
+                and (n - 2) ** 2 * (C + 4) * 4 + 4096 <= 96 * 1024 and B <= SMALL_MAX_B)
+
+    def _forward_small_fused(self, planes, B, dev, st, wp, tp):
+        """The small-batch forward in one launch (azg_small_net): conv1 + conv2, conv3, conv4, fc1,
+        fc2, [fc3 | fc4] + softmax / tanh, grid barriers between the layers."""
+        import ctypes
+        from . import _lib
+        n, C, A = self.n, self.w1.shape[0], self.fw3.shape[0]
+        n1, n2 = self.fw1.shape[0], self.fw2.shape[0]
+        need = SMALL_MAX_B * (n * n * C + (n - 2) ** 2 * C + (n - 4) ** 2 * C + n1 + n2 + A + 1)
+        if getattr(self, "_fused_acts", None) is None or self._fused_acts.device != dev:
+            self._fused_acts = torch.empty(need, device=dev, dtype=torch.float32)
+            self._fused_bar = torch.zeros(2, device=dev, dtype=torch.int64)  # [0] barrier counter, [1] error flag
+            ptrs = [self.w1, self.b1, self.w2, self.b2, self.w3, self.b3, self.w4, self.b4, self.fw1, self.fb1,
+                    self.fw2, self.fb2, self.fw34, self.fb34]
+            self._fused_ptrs = (ctypes.c_void_p * 14)(*[t.data_ptr() for t in ptrs])
+        # (the 14 weight pointers stay valid: refresh_from copies new weights into the same storage)
+        p = torch.empty((B, A), device=dev, dtype=torch.float32)
+        v = torch.empty((B, 1), device=dev, dtype=torch.float32)
+        bar = self._fused_bar
+        _lib.check(_lib.lib().azg_small_net(
+            ctypes.c_void_p(planes.data_ptr()), B, self.depth, n, C, A, n1, n2, self._fused_ptrs,
+            ctypes.c_void_p(self._fused_acts.data_ptr()), self._fused_acts.numel(), ctypes.c_void_p(p.data_ptr()),
+            ctypes.c_void_p(v.data_ptr()), wp, self._small_work.numel(), tp, self._small_tickets.numel(),
+            ctypes.c_void_p(bar.data_ptr()), ctypes.c_void_p(bar.data_ptr() + 8), st))
+        return p, v
+
+    def check_fused(self):
+        """Raise if a grid barrier of the fused small-batch forward gave up waiting (a block never
+        arrived: the results of that launch are void), and reset the barrier."""
+        bar = getattr(self, "_fused_bar", None)
+        if bar is not None and int(bar[1].item()) != 0:
+            bar.zero_()
+            raise RuntimeError("azg_small_net: a grid barrier timed out")
 
     def _small_ok(self, planes):
         """Whether the small-batch kernels take this forward: at most SMALL_MAX_B leaves and

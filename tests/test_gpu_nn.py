@@ -870,3 +870,33 @@ def test_fc_act_t_kernel():
     torch.cuda.synchronize()
     assert torch.equal(a.view(torch.int16), b.view(torch.int16))
     assert int(ovf.item()) == 0
+
+
+@pytest.mark.parametrize("n,depth,A", [(7, 4, 343), (6, 2, 37), (8, 2, 65)])
+@pytest.mark.parametrize("B", [1, 2, 4])
+def test_small_fused_forward_bit_identical(n, depth, A, B):
+    """azg_small_net (the whole small-batch forward in one launch, grid barriers between the
+    layers) gives P, v bit-identical to the per-layer small kernels and within 1e-5 of the module,
+    over 40 launches with changing planes (a stale activation read across the barriers would
+    show as a mismatch); no barrier timed out."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    torch.manual_seed(20 + n)
+    net = InflexionNNet(n=n, depth=depth, action_size=A).cuda().eval()
+    fused = InferenceNet(net, conv="miopen", gemm="f32").cuda()
+    layers = InferenceNet(net, conv="miopen", gemm="f32").cuda()
+    layers.small_fused = False
+    assert fused._fused_ok(B)
+    for i in range(40):
+        x = (torch.rand(B, depth, n, n, device="cuda") < 0.3).float()
+        if depth == 4:
+            x[:, 2:] = x[:, 2:, :1, :1]
+        with torch.no_grad():
+            pf, vf = fused(x)
+            pl, vl = layers(x)
+            if i % 10 == 0:
+                logp, vr = net(x)
+                torch.testing.assert_close(pf, torch.exp(logp), rtol=1e-5, atol=1e-7)
+                torch.testing.assert_close(vf.reshape(-1), vr.reshape(-1), rtol=1e-5, atol=1e-6)
+        assert torch.equal(pf, pl) and torch.equal(vf, vl), i
+    fused.check_fused()

@@ -14,6 +14,8 @@
 #   bench[:<args>]      python bench.py <args> (commas become spaces) -> bench[_<tag>].json / .err
 #   prof[:<args>]       rocprofv3 --kernel-trace --stats over bench.py <args> (summary prof[_<tag>].md)
 #   pmc                 FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 2 -> pmc_summary.json
+#   trace[:<args>]      rocprofv3 --kernel-trace over bench.py <args>, kept; per-launch summaries of
+#                       winograd_first and the persistent split GEMM (tools/trace_summary.py)
 #   gemm_pmc[:<v>]      split-GEMM SQ/TCC counters on conv2's shape (variant v, default 4) -> v<v>_pmc.json
 #   configs             bench.py over C1 / C2 (full games, eager + graph) / C3 / C5 / C4 full games
 #   py:<script>[:<args>] python <script> <args> -> <script base>.out / .err
@@ -68,6 +70,15 @@ for task in "$@"; do
             -- python3 "$R/bench.py" $a > "$d.json" 2> "$d.err")
         python3 tools/prof_summary.py "$d/run_kernel_stats.csv" > "$d.md"
         rm -f "$d"/*trace*.csv ;;
+    trace)
+        # kernel trace kept (per-launch durations and neighbours): tools/trace_summary.py <csv> <kernel>
+        a=${arg//,/ }
+        t=$(tag_of "$a")
+        d="$O/trace${t:+_$t}"
+        (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$d" -o run \
+            -- python3 "$R/bench.py" $a > "$d.json" 2> "$d.err")
+        python3 tools/trace_summary.py "$d/run_kernel_trace.csv" winograd_first > "$d.first.json"
+        python3 tools/trace_summary.py "$d/run_kernel_trace.csv" split_gemm_persist > "$d.gemm.json" ;;
     pmc)
         (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run \
             -- python3 "$R/bench.py" --steps 2 --no-cpu-baseline > "$O/pmc_fetch.log" 2>&1)
