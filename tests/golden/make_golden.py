@@ -28,6 +28,10 @@ Fixtures written (all small, gzip'd JSON or npz):
   realnet_sensitivity.json.gz  first divergent move of the reference's real-net traces when its network's
                          weights, or its outputs, move by 1e-7 / 1e-6 relative
   realnet_branches.json.gz     the perturbed reference's traces past those divergent moves
+  trained_net.npz        the reference NNetWrapper trained by its own NNet.train on 3 of its own
+                         self-play episodes (Coach.learn's second-iteration network): state_dict + pairs
+  mcts_trained_*.json.gz, trained_sensitivity.json.gz, trained_branches.json.gz
+                         the realnet traces / certificates with that network
 """
 import gzip
 import hashlib
