@@ -240,9 +240,12 @@ def _train_examples_dp(wrapper, ex, group, stats=None):
     try:
         for _ in range(a["epochs"]):
             net.train()
-            for _ in range(nb):
-                ids = np.random.randint(E, size=bs)
-                mine = torch.from_numpy(ids[rank * sl:(rank + 1) * sl]).to(dev)
+            # the epoch's batch draws in one call (the same numpy stream as nb calls) and one upload
+            ids_all = np.random.randint(E, size=(nb, bs))
+            mine_all = torch.from_numpy(np.ascontiguousarray(ids_all[:, rank * sl:(rank + 1) * sl])).to(dev) \
+                if nb else None
+            for j in range(nb):
+                mine = mine_all[j]
                 tp, tv = pis[mine], vs[mine]
                 with wrapper._autocast():
                     out_pi, out_v = wrapper._train_forward(planes[mine])

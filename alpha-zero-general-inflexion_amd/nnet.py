@@ -1116,8 +1116,12 @@ class NNetWrapper:
         k = 0
         for _ in range(self.args["epochs"]):
             self.nnet.train()
-            for _ in range(nb):
-                ids = torch.from_numpy(np.random.randint(E, size=bs)).to(self.device)
+            # the epoch's nb batch draws of NNet.py:52 in one call (numpy's legacy randint draws
+            # element by element, so this is the same stream as nb calls of size bs) and one upload:
+            # no host-device synchronisation inside the epoch
+            ids_all = torch.from_numpy(np.random.randint(E, size=(nb, bs))).to(self.device) if nb else None
+            for j in range(nb):
+                ids = ids_all[j]
                 tp, tv = pis[ids], vs[ids]
                 with self._autocast():
                     out_pi, out_v = self._train_forward(planes[ids])
