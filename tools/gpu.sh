@@ -70,6 +70,10 @@ for task in "$@"; do
             -- python3 "$R/bench.py" $a > "$d.json" 2> "$d.err")
         python3 tools/prof_summary.py "$d/run_kernel_stats.csv" > "$d.md"
         rm -f "$d"/*trace*.csv ;;
+    fetch_calib)
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch_calib" -o run \
+            -- python3 "$R/tools/fetch_calib.py" > "$O/fetch_calib.log" 2>&1)
+        python3 tools/fetch_calib.py --summary "$O/fetch_calib/run_counter_collection.csv" > "$O/fetch_calib.json" ;;
     trace)
         # kernel trace kept (per-launch durations and neighbours): tools/trace_summary.py <csv> <kernel>
         a=${arg//,/ }
@@ -80,12 +84,18 @@ for task in "$@"; do
         python3 tools/trace_summary.py "$d/run_kernel_trace.csv" winograd_first > "$d.first.json"
         python3 tools/trace_summary.py "$d/run_kernel_trace.csv" split_gemm_persist > "$d.gemm.json" ;;
     pmc)
-        (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run \
-            -- python3 "$R/bench.py" --steps 2 --no-cpu-baseline > "$O/pmc_fetch.log" 2>&1)
-        (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o run \
-            -- python3 "$R/bench.py" --steps 2 --no-cpu-baseline > "$O/pmc_write.log" 2>&1)
-        python3 tools/pmc_summary.py "$O/pmc_fetch/run_counter_collection.csv" \
-            "$O/pmc_write/run_counter_collection.csv" > "$O/pmc_summary.json" ;;
+        # pmc[:<bench args>] (default: the C4 line, 2 steps); no generation / learn-iteration pass
+        a=${arg//,/ }
+        t=$(tag_of "$a")
+        [ -z "$a" ] && a="--steps 2"
+        (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc${t:+_$t}_fetch" -o run \
+            -- python3 "$R/bench.py" $a --no-cpu-baseline --generation off --learn-iteration off \
+            > "$O/pmc${t:+_$t}_fetch.log" 2>&1)
+        (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc${t:+_$t}_write" -o run \
+            -- python3 "$R/bench.py" $a --no-cpu-baseline --generation off --learn-iteration off \
+            > "$O/pmc${t:+_$t}_write.log" 2>&1)
+        python3 tools/pmc_summary.py "$O/pmc${t:+_$t}_fetch/run_counter_collection.csv" \
+            "$O/pmc${t:+_$t}_write/run_counter_collection.csv" > "$O/pmc${t:+_$t}_summary.json" ;;
     gemm_pmc)
         v=${arg:-4}
         (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
