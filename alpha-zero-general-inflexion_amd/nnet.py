@@ -1052,8 +1052,9 @@ class NNetWrapper:
         kernels (wino_train.train_forward) on the GPU in f32 when args["train_conv"] is
         "winograd" -- the module itself otherwise (CPU: the reference's arithmetic)."""
         if x.is_cuda and self.args.get("train_conv", "winograd") == "winograd" and self.args["train_dtype"] == "f32":
-            from .wino_train import train_forward
-            return train_forward(self.nnet, x)
+            from .wino_train import applies_net, train_forward
+            if applies_net(self.nnet, x):
+                return train_forward(self.nnet, x)
         return self.nnet(x)
 
     def _adam(self):

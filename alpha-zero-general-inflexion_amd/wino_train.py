@@ -151,6 +151,15 @@ class WinogradConv3x3(torch.autograd.Function):
         return dx, dw, db, None
 
 
+def applies_net(net, s):
+    """Whether train_forward puts conv2-4 of `net` on the training kernels for planes s: a CUDA
+    batch of 64k leaves, the 7x7 board's layer sides (pads 1, 1, 0, 0), channel counts % 256.
+    Otherwise NNetWrapper trains the module itself, as the reference does (NCHW, MIOpen)."""
+    return (s.is_cuda and s.dtype == torch.float32 and s.numel() // (net.depth * net.n * net.n) % 64 == 0
+            and net.n == 7 and net.num_channels % 256 == 0
+            and [getattr(net, f"conv{i}").padding[0] for i in range(1, 5)] == [1, 1, 0, 0])
+
+
 def conv3x3(x, conv):
     """conv(x) on the training kernels when `applies`, else the module itself."""
     if applies(x, conv):
@@ -204,4 +213,4 @@ def _flag(dev):
     return f
 
 
-__all__ = ["WinogradConv3x3", "applies", "check_range", "conv3x3", "train_forward"]
+__all__ = ["WinogradConv3x3", "applies", "applies_net", "check_range", "conv3x3", "train_forward"]
