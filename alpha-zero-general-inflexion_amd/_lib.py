@@ -108,6 +108,7 @@ SIGNATURES = [
     ("azg_wt_din", ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),
     ("azg_wt_split2_transpose", ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _VP]),
     ("azg_wt_pow2_scale", ctypes.c_int, [_VP, ctypes.c_float, _VP, _VP]),
+    ("azg_wt_dw", ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _VP, _VP]),
 ]
 
 _lib = None

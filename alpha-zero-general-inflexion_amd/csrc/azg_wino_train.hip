@@ -401,6 +401,58 @@ extern "C" int azg_wt_split2_transpose(const void* src, void* dst, int32_t point
 }
 
 namespace {
+// dw[k][c][r][s] = 2^-kd sum over the groups of sum_{a,b} G_a[a][r] G_b[b][s] dU_e[c][k] (e = the
+// group's point (a, b)): the adjoint of U = G g G^T, one thread per (c, k) with k fastest (the dU
+// reads coalesced), f32
+__global__ __launch_bounds__(256) void wt_dw_kernel(const float* __restrict__ dU, int C, int K, int h_out,
+                                                    const unsigned* __restrict__ dyamax, float* __restrict__ dw) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)C * K) return;
+    const int k = (int)(i % K), c = (int)(i / K);
+    const long long CK = (long long)C * K;
+    const float* u = dU + (long long)c * K + k;
+    float acc[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    const WSeq S(h_out);
+    int e0 = 0;
+    for (int q = 0; q < 4; ++q) {
+        const int ma = q < 2 ? S.big : S.small(), mb = (q & 1) ? S.small() : S.big;
+        if (S.cnt(ma) * S.cnt(mb) == 0) continue;
+        with_types(ma, mb, [&](auto A_, auto B_) {
+            constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+            float t[MA + 2][3];  // t[a][s] = sum_b G_b[b][s] dU[(a, b)]
+#pragma unroll
+            for (int a = 0; a < MA + 2; ++a) {
+                float v[MB + 2];
+#pragma unroll
+                for (int b = 0; b < MB + 2; ++b) v[b] = u[(long long)(e0 + a * (MB + 2) + b) * CK];
+#pragma unroll
+                for (int s2 = 0; s2 < 3; ++s2) {
+                    float x = 0.f;
+#pragma unroll
+                    for (int b = 0; b < MB + 2; ++b) x = fmaf((float)WinoG<MB>::G[b][s2], v[b], x);
+                    t[a][s2] = x;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int s2 = 0; s2 < 3; ++s2) {
+                    float x = acc[r][s2];
+#pragma unroll
+                    for (int a = 0; a < MA + 2; ++a) x = fmaf((float)WinoG<MA>::G[a][r], t[a][s2], x);
+                    acc[r][s2] = x;
+                }
+        });
+        e0 += (ma + 2) * (mb + 2);
+    }
+    const float inv = 1.f / pow2_scale(*dyamax, 32.f);
+    float* o = dw + ((long long)k * C + c) * 9;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s2 = 0; s2 < 3; ++s2) o[r * 3 + s2] = acc[r][s2] * inv;
+}
+
 __global__ void wt_pow2_scale_kernel(const unsigned* amax, float target, float* out) {
     if (threadIdx.x == 0) out[0] = pow2_scale(*amax, target);
 }
@@ -411,5 +463,14 @@ __global__ void wt_pow2_scale_kernel(const unsigned* amax, float target, float* 
 extern "C" int azg_wt_pow2_scale(const uint32_t* amax, float target, float* out, void* stream) {
     if (!amax || !out || !(target > 0.f)) return AZG_ERR_ARG;
     hipLaunchKernelGGL(wt_pow2_scale_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, amax, target, out);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+// dw [k][c][3][3] from dU [P][c][k] (the weight gradient's adjoint transform, scale undone)
+extern "C" int azg_wt_dw(const float* dU, int32_t c, int32_t k, int32_t h_out, const uint32_t* dyamax, float* dw,
+                         void* stream) {
+    if (!dU || !dyamax || !dw || c <= 0 || k <= 0 || h_out < 2 || h_out > 9) return AZG_ERR_ARG;
+    hipLaunchKernelGGL(wt_dw_kernel, dim3((unsigned)(((long long)c * k + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, dU, c, k, h_out, dyamax, dw);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }

@@ -10,7 +10,7 @@ transformed point one split-fp16 GEMM (f32-accurate products on the fp16 MFMA):
 
     forward   V = B^T x B (azg_winograd_in_nhwc), M = V U (azg_split_gemm), y = A^T M A + b
     backward  dM = A dy A^T, dV = dM U^T, dx = sum of B dV B^T over the overlapping tiles,
-              dU = V^T dM (both operands transposed), dw = sum_e G_a^T dU_e G_b (torch),
+              dU = V^T dM (both operands transposed), dw = sum_e G_a^T dU_e G_b (azg_wt_dw),
               db = sum dy
 
 (csrc/azg_wino_train.hip).  Operands are scaled by powers of two chosen on the device (U:
@@ -137,16 +137,9 @@ class WinogradConv3x3(torch.autograd.Function):
                 _gemm(Vt, dMt, dU[pt:pt + Pr], [(Pr, C)], T, K, dev)
                 row += Pr * T
                 pt += Pr
-            # dw[k][c][r][s] = sum over the groups of G_a^T dU G_b, then the dy scale undone
-            dw = torch.zeros((K, C, 3, 3), dtype=torch.float32, device=dev)
-            e = 0
-            for ma, mb, Pg, _ in winograd_groups(Ho):
-                Ga, Gb = _g(ma, dev), _g(mb, dev)
-                dw += torch.einsum("ar,abck,bs->kcrs", Ga, dU[e:e + Pg].view(ma + 2, mb + 2, C, K), Gb)
-                e += Pg
-            sd = torch.empty(1, dtype=torch.float32, device=dev)
-            _lib.check(L.azg_wt_pow2_scale(_p(dyamax), 32.0, _p(sd), st))
-            dw /= sd
+            # dw[k][c][r][s] = sum over the groups of G_a^T dU G_b, the dy scale undone (azg_wt_dw)
+            dw = torch.empty((K, C, 3, 3), dtype=torch.float32, device=dev)
+            _lib.check(L.azg_wt_dw(_p(dU), C, K, Ho, _p(dyamax), _p(dw), st))
         db = dy.sum(dim=(0, 2, 3)) if ctx.needs_input_grad[2] else None
         return dx, dw, db, None
 

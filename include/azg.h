@@ -412,6 +412,8 @@ int  azg_wt_din(const float* dV, float* dx, int32_t batch, int32_t h_in, int32_t
                 const uint32_t* uamax, const uint32_t* dyamax, void* stream);
 int  azg_wt_split2_transpose(const void* src, void* dst, int32_t points, int32_t t, int32_t c, void* stream);
 int  azg_wt_pow2_scale(const uint32_t* amax, float target, float* out, void* stream);
+/* dw [k][c][3][3] = 2^-kd sum_e G_a^T dU_e G_b from dU [P][c][k] (the weights' adjoint transform). */
+int  azg_wt_dw(const float* dU, int32_t c, int32_t k, int32_t h_out, const uint32_t* dyamax, float* dw, void* stream);
 
 #ifdef __cplusplus
 }
