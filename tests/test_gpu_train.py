@@ -89,6 +89,7 @@ def test_trainer_gpu_full_size(path):
     from azg_amd.examples import ExampleSet
     from azg_amd.nnet import NNetWrapper
     from test_train_golden import reference_examples
+    from torch.optim.optimizer import register_optimizer_step_post_hook
 
     g = ol.load_json("train_full_golden.json.gz")
     c, r = g["config"], g["runs"]["nodropout"]
@@ -101,11 +102,11 @@ def test_trainer_gpu_full_size(path):
         np.testing.assert_allclose(init[k], r["init"][k]["proj"], rtol=1e-12, atol=1e-9, err_msg=f"initial {k}")
     seen = {}
 
-    def hook(mod, inp):  # the weights after the first step, at the second batch's forward
+    def hook(opt, args, kwargs):  # the weights after the first optimizer step (whichever forward ran)
         seen["n"] = seen.get("n", 0) + 1
-        if seen["n"] == 2:
-            seen["step1"] = _proj(mod.state_dict(), c["proj_seed"])
-    h = w.nnet.register_forward_pre_hook(hook)
+        if seen["n"] == 1:
+            seen["step1"] = _proj(w.nnet.state_dict(), c["proj_seed"])
+    h = register_optimizer_step_post_hook(hook)
     np.random.seed(c["batch_seed"])
     torch.manual_seed(c["torch_seed"])
     try:

@@ -21,6 +21,7 @@
 #   py:<script>[:<args>] python <script> <args> -> <script base>.out / .err
 #   profpy:<script>[:<args>] rocprofv3 --kernel-trace --stats over python <script> <args> -> prof_<base>.md
 set -e
+FAILED=0
 R=$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)
 NAME=${1:?usage: tools/gpu.sh <run-name> <task> ...}
 shift
@@ -51,12 +52,19 @@ for task in "$@"; do
         log="$O/test_$(basename "$path" .py)"
         if [ -n "$k" ]; then log="${log}_$(tag_of "$k")"; fi
         log="$log.log"
-        if [ -n "$k" ]; then
-            timeout -k 10 1100 python -u -m pytest "$path" -m gpu -x -v -s --timeout 300 --timeout-method thread \
-                --durations 10 -k "$k" > "$log" 2>&1
-        else
-            timeout -k 10 1100 python -u -m pytest "$path" -m gpu -x -v -s --timeout 300 --timeout-method thread \
-                --durations 10 > "$log" 2>&1
+        kk=()
+        [ -n "$k" ] && kk=(-k "$k")
+        rc=0
+        timeout -k 10 1100 python -u -m pytest "$path" -m gpu -x -v -s --timeout 300 --timeout-method thread \
+            --durations 10 "${kk[@]}" > "$log" 2>&1 || rc=$?
+        # exit 1 = assertion failures only: the run goes on to its other tasks unless the log shows
+        # a device error; any other status (abort, fault, time limit) ends the run here
+        if [ $rc -ne 0 ]; then
+            echo "   $path: pytest exit $rc"
+            if [ $rc -ne 1 ] || grep -qi "hipError\|memory access fault\|illegal address\|HSA_STATUS" "$log"; then
+                exit $rc
+            fi
+            FAILED=1
         fi ;;
     bench)
         a=${arg//,/ }
@@ -143,3 +151,4 @@ for task in "$@"; do
     esac
 done
 echo "== done ($(date +%T))"
+exit ${FAILED:-0}
