@@ -40,6 +40,8 @@ SMALL_MAX_B = 4
 # persistent grid, grid barriers between the layers; bit-identical results), else one launch per layer
 SMALL_FUSED = True
 FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
+# NNetWrapper.train_examples on the GPU: steps run eagerly before the step is captured as a HIP graph
+_GRAPH_EAGER_STEPS = 3
 FC1_KPARTS = 4  # split-K parts of fc1 on libazg's split GEMM (4608 = 4 x 1152 for the 7x7 board)
 # split-K parts of fc2 (1024 -> 512) and [fc3 | fc4] (512 -> 344, padded to 512 columns) when the whole
 # FC tail runs on libazg's split GEMM (InferenceNet.fc_tail_azg): 4 x 256 and 2 x 256 channels, the
@@ -1064,11 +1066,11 @@ class NNetWrapper:
             return torch.optim.Adam(self.nnet.parameters(), fused=True)
         return torch.optim.Adam(self.nnet.parameters())
 
-    def _autocast(self):
+    def _autocast(self, cache=True):
         dt = self.args["train_dtype"]
         if dt not in ("f32", "bf16"):
             raise ValueError(f"train_dtype must be 'f32' or 'bf16', got {dt!r}")
-        return torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=dt == "bf16")
+        return torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=dt == "bf16", cache_enabled=cache)
 
     def train(self, examples):
         """Reference training loop (NNet.py:36-76): Adam, 10 epochs of batches
@@ -1096,19 +1098,64 @@ class NNetWrapper:
         Adam, epochs and batch draws (np.random.randint on numpy's global stream,
         so the sampled batches are the reference's), with the batch gathered on
         the GPU instead of converted from Python lists.  Returns per-batch
-        (l_pi, l_v) as a device tensor [batches, 2] (one host sync at the end).
+        (l_pi, l_v) as a device tensor [batches, 2].
+
+        On the GPU the steps after the first _GRAPH_EAGER_STEPS replay one captured HIP
+        graph of the whole step (args["train_graph"], default on: _train_graph).  When the
+        Winograd training convolutions (wino_train) met an operand fp16 cannot hold, the
+        call is undone -- weights, BatchNorm buffers, numpy's and torch's RNG states -- and
+        run again with the library convolutions (the self-play replay_form rule applied to
+        training), so the result never carries a saturated operand.
 
         group: a torch.distributed group of more than one rank trains data-parallel
         (ddp.train_examples_dp: each batch split over the ranks, whole-batch
         BatchNorm statistics, one gradient all-reduce per step); every rank of the
         group calls this with the same examples.  stats: a dict that receives the step
         count (and, data-parallel, the collectives' accounting)."""
+        dp = None
         if group is not None:
             import torch.distributed as dist
             if dist.get_world_size(group) > 1:
                 from .ddp import train_examples_dp
+                dp = dist
+
+        def run():
+            if dp is not None:
                 return train_examples_dp(self, ex, group, stats=stats)
-        opt = self._adam()
+            return self._train_single(ex, stats)
+
+        wino = (self.device.type == "cuda" and self.args.get("train_conv", "winograd") == "winograd"
+                and self.args["train_dtype"] == "f32")
+        if not wino:
+            return run()
+        from . import wino_train
+        wino_train.take_flag(self.device)  # a stale flag from an earlier call is not this call's
+        saved = ({k: v.detach().clone() for k, v in self.nnet.state_dict().items()}, np.random.get_state(),
+                 torch.get_rng_state(), torch.cuda.get_rng_state(self.device))
+        losses = run()
+        flag = wino_train.take_flag(self.device)
+        if dp is not None:  # every rank replays when any rank saw an out-of-range operand
+            backend_dev = self.device if dp.get_backend(group) == "nccl" else torch.device("cpu")
+            t = torch.tensor([flag], dtype=torch.int32, device=backend_dev)
+            dp.all_reduce(t, op=dp.ReduceOp.MAX, group=group)
+            flag = int(t.item())
+        if flag:
+            sd, nps, cpu_rng, dev_rng = saved
+            self.nnet.load_state_dict(sd)
+            np.random.set_state(nps)
+            torch.set_rng_state(cpu_rng)
+            torch.cuda.set_rng_state(dev_rng, self.device)
+            conv = self.args["train_conv"]
+            self.args["train_conv"] = "library"
+            try:
+                losses = run()
+            finally:
+                self.args["train_conv"] = conv
+            if stats is not None:
+                stats["replayed_library"] = True
+        return losses
+
+    def _train_single(self, ex, stats):
         bs = self.args["batch_size"]
         E = len(ex)
         nb = int(E / bs)
@@ -1116,6 +1163,15 @@ class NNetWrapper:
         planes = ex.planes.to(self.device)
         pis = ex.pis.to(self.device)
         vs = ex.vs.to(self.device)
+        if stats is not None:
+            stats["steps"] = self.args["epochs"] * nb
+        if (self.args.get("train_graph", True) and self.device.type == "cuda"
+                and self.args["epochs"] * nb > _GRAPH_EAGER_STEPS):
+            if stats is not None:
+                stats["graph"] = True
+            self._train_graph(planes, pis, vs, nb, losses)
+            return losses
+        opt = self._adam()
         k = 0
         for _ in range(self.args["epochs"]):
             self.nnet.train()
@@ -1136,9 +1192,75 @@ class NNetWrapper:
                 losses[k, 0] = l_pi.detach()
                 losses[k, 1] = l_v.detach()
                 k += 1
-        if stats is not None:
-            stats["steps"] = k
         return losses
+
+    def _train_graph(self, planes, pis, vs, nb, losses):
+        """_train_single's loop with the step replayed as one captured HIP graph: forward
+        (conv2-4 on the Winograd training kernels), the losses, backward and the Adam update
+        are ~400 launches per 512-example step, whose host-side issue cost the GPU more
+        time than their work.  The same batches are drawn at the same points of numpy's
+        stream; the first _GRAPH_EAGER_STEPS steps run eagerly on a side stream (real
+        steps, which also warm up every kernel's one-time queries and the allocator), then
+        one step is captured and replayed, each replay reading the batch's indices from a
+        static buffer.  Adam is torch's capturable form (its step count and bias
+        corrections on the device: the same update up to rounding); dropout draws from
+        torch's graph-safe philox offsets."""
+        bs = self.args["batch_size"]
+        dev = self.device
+        E = planes.shape[0]
+        kw = dict(capturable=True)
+        if self.args["fused_adam"]:
+            kw["fused"] = True
+        opt = torch.optim.Adam(self.nnet.parameters(), **kw)
+        ids_buf = torch.zeros(bs, dtype=torch.int64, device=dev)
+        loss_buf = torch.zeros(2, dtype=torch.float32, device=dev)
+
+        def step():
+            tp, tv = pis[ids_buf], vs[ids_buf]
+            with self._autocast(cache=False):
+                out_pi, out_v = self._train_forward(planes[ids_buf])
+                l_pi = -torch.sum(tp * out_pi) / tp.size()[0]
+                l_v = torch.sum((tv - out_v.view(-1)) ** 2) / tv.size()[0]
+            (l_pi + l_v).backward()
+            opt.step()
+            loss_buf[0].copy_(l_pi.detach())
+            loss_buf[1].copy_(l_v.detach())
+
+        cur = torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(dev)
+        graph = None
+        k = 0
+        self.nnet.train()
+        try:
+            for _ in range(self.args["epochs"]):
+                ids_all = torch.from_numpy(np.random.randint(E, size=(nb, bs))).to(dev) if nb else None
+                for j in range(nb):
+                    if graph is None and k < _GRAPH_EAGER_STEPS:
+                        side.wait_stream(cur)
+                        with torch.cuda.stream(side):
+                            ids_buf.copy_(ids_all[j])
+                            opt.zero_grad(set_to_none=True)
+                            step()
+                            losses[k].copy_(loss_buf)
+                        cur.wait_stream(side)
+                    else:
+                        if graph is None:
+                            graph = torch.cuda.CUDAGraph()
+                            opt.zero_grad(set_to_none=True)
+                            with torch.cuda.graph(graph):
+                                step()
+                        ids_buf.copy_(ids_all[j])
+                        graph.replay()
+                        losses[k].copy_(loss_buf)
+                    k += 1
+        finally:
+            if graph is not None:
+                torch.cuda.current_stream(dev).synchronize()
+                # the parameters' .grad live in the graph's pool: hand back plain tensors
+                for p in self.nnet.parameters():
+                    if p.grad is not None:
+                        p.grad = p.grad.clone()
+                del graph
 
     def save_checkpoint(self, folder="checkpoint", filename="checkpoint.pth.tar"):
         os.makedirs(folder, exist_ok=True)

@@ -180,11 +180,23 @@ def check_range(device=None):
     range since the last call (an activation above 65504, or a non-finite one; the scaled
     gradients cannot: |dM| <= 32 (sum |A|)^2 <= 30752 for these tiles), and clear the flag."""
     for dev, f in list(_FLAGS.items()):
-        if device is not None and dev != torch.device(device):
+        if device is not None and dev != _key(device):
             continue
         if int(f.item()):
             f.zero_()
             raise FloatingPointError("training convolution operand out of fp16 range")
+
+
+def take_flag(device):
+    """The out-of-range flag of `device`'s training convolutions since the last call (0 / 1),
+    cleared (one host synchronisation)."""
+    f = _FLAGS.get(_key(device))
+    if f is None:
+        return 0
+    v = int(f.item())
+    if v:
+        f.zero_()
+    return v
 
 
 _FLAGS = {}
@@ -199,11 +211,19 @@ def _g(m, dev):
     return t
 
 
+def _key(dev):
+    dev = torch.device(dev)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
 def _flag(dev):
+    dev = _key(dev)
     f = _FLAGS.get(dev)
     if f is None:
         f = _FLAGS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
     return f
 
 
-__all__ = ["WinogradConv3x3", "applies", "applies_net", "check_range", "conv3x3", "train_forward"]
+__all__ = ["WinogradConv3x3", "applies", "applies_net", "check_range", "conv3x3", "take_flag", "train_forward"]

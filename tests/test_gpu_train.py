@@ -130,3 +130,72 @@ def test_trainer_gpu_full_size(path):
             errs[f"{k} {name}"] = float(np.abs(d_gpu - d_ref).max() / np.abs(d_ref).max())
     print("update errors:", {k: f"{v:.1e}" for k, v in errs.items()})
     assert max(errs.values()) < 5e-2, errs
+
+
+def test_graph_trainer_matches_eager():
+    """train_examples' captured-graph form (NNetWrapper._train_graph: the step after the first
+    _GRAPH_EAGER_STEPS replayed as one HIP graph, Adam in torch's capturable form) against the
+    eager loop on the same examples and batch draws, dropout 0, 512 channels (conv2-4 on the
+    Winograd training kernels in both): the eager steps are the same launches, so their losses
+    are equal; the replayed steps differ only by the capturable Adam's device-side bias
+    corrections (rounding), within 1e-4 relative over 8 steps, as are the weight matrices (in
+    norm); numpy's stream ends at the same position."""
+    import azg_amd  # noqa: F401
+    from azg_amd.examples import ExampleSet
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.nnet import _GRAPH_EAGER_STEPS, NNetWrapper
+
+    gen = torch.Generator().manual_seed(3)
+    E = 512 * 8
+    planes = (torch.rand((E, 4, 7, 7), generator=gen) < 0.3).float()
+    pis = torch.softmax(torch.randn((E, 343), generator=gen), 1)
+    vs = torch.randint(0, 2, (E,), generator=gen).float() * 2 - 1
+    out = {}
+    for graph in (False, True):
+        torch.manual_seed(0)
+        w = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0, train_graph=graph), device="cuda")
+        np.random.seed(5)
+        st = {}
+        losses = w.train_examples(ExampleSet(planes.cuda(), pis.cuda(), vs.cuda()), stats=st)
+        out[graph] = (losses.cpu().numpy(), np.random.get_state()[2],
+                      {k: v.detach().cpu() for k, v in w.nnet.state_dict().items()}, st)
+    assert out[True][3].get("graph") and not out[False][3].get("graph")
+    assert out[True][1] == out[False][1]
+    le, lg = out[False][0], out[True][0]
+    np.testing.assert_array_equal(lg[:_GRAPH_EAGER_STEPS], le[:_GRAPH_EAGER_STEPS])
+    np.testing.assert_allclose(lg, le, rtol=1e-4)
+    for k in ("conv2.weight", "conv4.weight", "fc1.weight", "fc3.weight"):
+        a, b = out[False][2][k], out[True][2][k]
+        d0 = ((a - b).norm() / a.norm()).item()
+        assert d0 <= 1e-4, (k, d0)
+
+
+def test_out_of_range_training_replays_on_library():
+    """A network whose conv1 activations leave fp16's range (bn1's gamma 1e6): the Winograd
+    training convolutions flag it, and train_examples undoes the call (weights, BatchNorm
+    buffers, numpy's and torch's streams) and runs it again on the library convolutions, so
+    the result is the library trainer's from the same start."""
+    import azg_amd  # noqa: F401
+    from azg_amd.examples import ExampleSet
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.nnet import NNetWrapper
+
+    gen = torch.Generator().manual_seed(4)
+    E = 512 * 5
+    ex = ExampleSet((torch.rand((E, 4, 7, 7), generator=gen) < 0.3).float().cuda(),
+                    torch.softmax(torch.randn((E, 343), generator=gen), 1).cuda(),
+                    (torch.randint(0, 2, (E,), generator=gen).float() * 2 - 1).cuda())
+    out = {}
+    for conv in ("winograd", "library"):
+        torch.manual_seed(0)
+        w = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0, train_conv=conv), device="cuda")
+        with torch.no_grad():
+            w.nnet.bn1.weight.fill_(1e6)
+        np.random.seed(9)
+        st = {}
+        losses = w.train_examples(ex, stats=st).cpu().numpy()
+        out[conv] = (losses, np.random.get_state()[2], w.nnet.state_dict()["fc3.weight"].cpu(), st)
+    assert out["winograd"][3].get("replayed_library") and not out["library"][3].get("replayed_library")
+    assert out["winograd"][1] == out["library"][1]
+    np.testing.assert_allclose(out["winograd"][0], out["library"][0], rtol=1e-6)
+    torch.testing.assert_close(out["winograd"][2], out["library"][2], rtol=1e-6, atol=1e-7)
