@@ -100,6 +100,7 @@ SIGNATURES = [
                                     _VP, ctypes.POINTER(_I64), _VP]),
     ("azg_small_net", ctypes.c_int, [_VP, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _VP,
                                      _I64, _VP, _I32, _VP, _VP, _VP]),
+    ("azg_small_net_blocks", ctypes.c_int, [_I32]),
     ("azg_fc_act_t", ctypes.c_int, [_VP, _I32, _I64, _VP, ctypes.c_float, _VP, _I32, _I32, _I32, _I32, _VP, _VP]),
     ("azg_absmax", ctypes.c_int, [_VP, _I64, _VP, _VP]),
     ("azg_wt_u_build", ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),

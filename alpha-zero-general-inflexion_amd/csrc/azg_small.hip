@@ -598,14 +598,22 @@ __global__ __launch_bounds__(SF_T) void small_fc_kernel(const float* __restrict_
 }
 
 // ---- the whole forward in one launch (small_net_kernel) ---------------------------------------
-// conv1 + conv2 (split-K, 4 K-parts), conv3 (split-K, 4 K-parts), conv4 (2-channel blocks), fc1, fc2,
+// conv1 + conv2 (split-K, 4 K-parts), conv3 (split-K, 8 K-parts), conv4 (2-channel blocks), fc1, fc2,
 // [fc3 | fc4] + heads: the same block bodies as the per-layer kernels above (same arithmetic, same
-// summation orders: bit-identical results), one persistent grid of at most one 512-thread block per
-// CU, the layers separated by grid barriers instead of kernel boundaries.  Activations cross the
-// layers inside the launch as write-through stores drained before the barrier and agent-scope loads
-// after it (the split-K hand-off's rule); the barrier is a monotonic 64-bit arrival counter (each
-// launch adds 5 x grid; a block's targets follow from the value its first arrival returns), spun on
-// with s_sleep, and gives up after ~2^24 polls (setting *err) rather than hang.
+// summation orders: bit-identical results), in one grid of at most one 512-thread block per CU.
+//
+// The layers' block bodies are ITEMS of one in-order work queue (layer 0's items first, then layer
+// 1's, ...): a block takes the next item with one atomic, and before an item of layer L it waits
+// until every item of layer L-1 is done (a per-layer done counter).  An item is handed out only
+// after every item of the layers before it, to a block that is already running, and the items a
+// block waits for were all handed out earlier -- so the launch completes whatever number of its
+// blocks is resident at once (a GPU shared with another process, or other kernels in flight): no
+// grid barrier, which a persistent grid can only pass when all of its blocks are co-resident (two
+// processes' launches each holding part of the CUs timed out before, tests/test_gpu_dist.py).
+// Activations cross the layers as write-through stores drained before the done count and agent-scope
+// loads after the wait (the split-K hand-off's rule).  Each block prefetches its next item while it
+// works on the current one; the last block to leave resets the counters for the next launch.  A wait
+// gives up after ~2^24 polls (setting *err) rather than hang.
 struct SmallNetArgs {
     const float* planes;
     const float *w1, *b1, *w2, *b2, *w3, *b3, *w4, *b4, *fw1, *fb1, *fw2, *fb2, *fw34, *fb34;
@@ -613,92 +621,129 @@ struct SmallNetArgs {
     float* part;
     unsigned* tickets;
     unsigned* heads_ticket;
-    unsigned long long* bar;
+    unsigned* sched;  // [0] next item, [1] blocks finished, [2 + L] items of layer L done (L < 5)
     int* err;
     int B, D, C, A, N1, N2;
 };
 
 constexpr int SN_POOL = 96 * 1024;  // LDS of the fused kernel: the largest layer's (conv1 + conv2's split-K block)
-
-__device__ __forceinline__ void grid_sync(const SmallNetArgs& a, unsigned long long& base, int j) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's write-through stores have landed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned long long old = __hip_atomic_fetch_add(a.bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (j == 1) base = old - old % gridDim.x;
-        const unsigned long long target = base + (unsigned long long)j * gridDim.x;
-        for (unsigned spins = 0; __hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) {  // a block never arrived: report instead of hanging the GPU
-                atomicOr(a.err, 1);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-}
+constexpr int SN_SCHED_WORDS = 8;
 
 template <int NB, int BMAX, bool WLDS3, bool WLDS4>
 __global__ __launch_bounds__(SC_T) void small_net_kernel(SmallNetArgs a) {
     __shared__ __attribute__((aligned(16))) float pool[SN_POOL / 4];
     __shared__ unsigned s_last;
+    __shared__ unsigned s_half[2];
+    __shared__ int s_next;
     constexpr int H3 = NB - 2, H4 = NB - 4;  // conv3's and conv4's output sides (pads 1, 1, 0, 0)
     constexpr int P12 = NB * NB <= 64 ? 64 : 128, P3 = H3 * H3 <= 16 ? 16 : H3 * H3 <= 32 ? 32 : 64,
                   P4 = H4 * H4 <= 16 ? 16 : 32;
-    const int G = gridDim.x, C = a.C, B = a.B;
-    unsigned long long base = 0;
+    const int C = a.C, B = a.B, tid = threadIdx.x;
+    const int K1 = H4 * H4 * C, half = tid / SF_T, ht = tid % SF_T;
+    // items per layer: conv12 split-K blocks; conv3 split-K blocks (or 2-channel blocks for <= 16
+    // output pixels, 6x6 boards); conv4 2-channel blocks; fc1 / fc2 / heads row-group pairs (one group
+    // per 256-thread half, each exactly the per-layer small_fc_kernel's block)
     const int nsk = C / SK_CO * SK_KG1;
-    for (int it = blockIdx.x; it < nsk; it += G)
-        small_conv_sk_body<P12, NB, SK_KG1, true>(it, nsk, pool, s_last, a.planes, (long long)a.D * NB * NB, 0, 0, B,
-                                                  NB, 1, a.w2, C, a.b2, 1, a.y2, C, a.part, a.tickets, a.w1, a.b1,
-                                                  a.D);
-    grid_sync(a, base, 1);
-    if constexpr (H3 * H3 > 16) {  // conv3 as the per-layer path runs it: split-K in 8 K-parts ...
-        const int nsk3 = C / SK_CO * SK_KG;
-        for (int it = blockIdx.x; it < nsk3; it += G)
-            small_conv_sk_body<P3, 0, SK_KG, true>(it, nsk3, pool, s_last, a.y2, (long long)NB * NB * C, NB * C, C, B,
-                                                   NB, 0, a.w3, C, a.b3, 1, a.y3, C, a.part, a.tickets, nullptr,
-                                                   nullptr, 0);
-    } else {  // ... or, for <= 16 output pixels (6x6 boards), in 2-channel blocks
-        for (int it = blockIdx.x; it < C / 2; it += G)
-            small_conv_body<P3, 2, true, WLDS3, true>(it, pool, a.y2, (long long)NB * NB * C, NB * C, C, 1, B, NB, 0,
-                                                      a.w3, C, C, a.b3, 1, a.y3, C);
-    }
-    grid_sync(a, base, 2);
-    for (int it = blockIdx.x; it < C / 2; it += G)
-        small_conv_body<P4, 2, true, WLDS4, true>(it, pool, a.y3, (long long)H3 * H3 * C, H3 * C, C, 1, B, H3, 0, a.w4,
-                                                  C, C, a.b4, 1, a.y4, C);
-    grid_sync(a, base, 3);
-    // the FC layers: two row groups per block round, one per 256-thread half, each exactly the
-    // per-layer small_fc_kernel's block (its NPB for the layer's width, its reduction order)
-    const int K1 = H4 * H4 * C, half = threadIdx.x / SF_T, ht = threadIdx.x % SF_T;
-    __shared__ unsigned s_half[2];
-    auto fc = [&](auto NPB_, auto HEADS_, int nrow, const float* x, int ldx, const float* w, int K, const float* bias,
-                  int relu, float* y, int ldy, const float* hb, float* P, float* V, unsigned* ticket) {
+    const int n3 = H3 * H3 > 16 ? C / SK_CO * SK_KG : C / 2;
+    const int npb1 = a.N1 >= 2048 ? 4 : a.N1 >= 1024 ? 2 : 1, npb2 = a.N2 >= 2048 ? 4 : a.N2 >= 1024 ? 2 : 1;
+    const int ng1 = (a.N1 + npb1 - 1) / npb1, ng2 = (a.N2 + npb2 - 1) / npb2, ng3 = (a.A + 1 + 3) / 4;
+    const int cnt[6] = {nsk, n3, C / 2, (ng1 + 1) / 2, (ng2 + 1) / 2, (ng3 + 1) / 2};
+    int end[6];
+    end[0] = cnt[0];
+    for (int L = 1; L < 6; ++L) end[L] = end[L - 1] + cnt[L];
+    unsigned* q = a.sched;
+
+    auto fc = [&](auto NPB_, auto HEADS_, int g0, int nrow, const float* x, int ldx, const float* w, int K,
+                  const float* bias, int relu, float* y, int ldy, const float* hb, float* P, float* V,
+                  unsigned* ticket) {
         constexpr int NPB = decltype(NPB_)::value;
         constexpr bool HD = decltype(HEADS_)::value;
         const int ng = (nrow + NPB - 1) / NPB;
         float(*red)[NPB * BMAX] = (float(*)[NPB * BMAX])(pool + half * (SF_T / 64) * NPB * BMAX);
-        for (int g0 = 2 * blockIdx.x; g0 < ng; g0 += 2 * G)
-            small_fc_body<NPB, BMAX, HD, true>(g0 + half, ng, ht, g0 + half < ng, red, s_half[half], x, ldx, B, w, K,
-                                               nrow, bias, relu, y, ldy, hb, P, V, ticket);
+        small_fc_body<NPB, BMAX, HD, true>(g0 + half, ng, ht, g0 + half < ng, red, s_half[half], x, ldx, B, w, K,
+                                           nrow, bias, relu, y, ldy, hb, P, V, ticket);
     };
-    if (a.N1 >= 2048) fc(std::integral_constant<int, 4>{}, std::false_type{}, a.N1, a.y4, K1, a.fw1, K1, a.fb1, 1, a.h1,
-                         a.N1, nullptr, nullptr, nullptr, nullptr);
-    else if (a.N1 >= 1024) fc(std::integral_constant<int, 2>{}, std::false_type{}, a.N1, a.y4, K1, a.fw1, K1, a.fb1, 1,
-                              a.h1, a.N1, nullptr, nullptr, nullptr, nullptr);
-    else fc(std::integral_constant<int, 1>{}, std::false_type{}, a.N1, a.y4, K1, a.fw1, K1, a.fb1, 1, a.h1, a.N1,
-            nullptr, nullptr, nullptr, nullptr);
-    grid_sync(a, base, 4);
-    if (a.N2 >= 2048) fc(std::integral_constant<int, 4>{}, std::false_type{}, a.N2, a.h1, a.N1, a.fw2, a.N1, a.fb2, 1,
-                         a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
-    else if (a.N2 >= 1024) fc(std::integral_constant<int, 2>{}, std::false_type{}, a.N2, a.h1, a.N1, a.fw2, a.N1, a.fb2,
-                              1, a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
-    else fc(std::integral_constant<int, 1>{}, std::false_type{}, a.N2, a.h1, a.N1, a.fw2, a.N1, a.fb2, 1, a.h2, a.N2,
-            nullptr, nullptr, nullptr, nullptr);
-    grid_sync(a, base, 5);
-    fc(std::integral_constant<int, 4>{}, std::true_type{}, a.A + 1, a.h2, a.N2, a.fw34, a.N2, nullptr, 0, a.logits,
-       a.A + 1, a.fb34, a.P, a.v, a.heads_ticket);
+
+    if (tid == 0) s_next = (int)__hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    int known = 0;  // layers [0, known) are complete as far as this block has seen
+    for (;;) {
+        const int item = s_next;
+        __syncthreads();  // every thread has read s_next before it is overwritten below
+        if (item >= end[5]) break;
+        unsigned nxt = 0;  // the next item, fetched while this one runs (thread 0)
+        if (tid == 0) nxt = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int L = 0;
+        while (item >= end[L]) ++L;
+        const int i = item - (L ? end[L - 1] : 0);
+        if (known < L) {  // layer L-1 done (and so every layer before it: its items waited in turn)
+            if (tid == 0) {
+                const unsigned target = (unsigned)cnt[L - 1];
+                for (unsigned spins = 0;
+                     __hip_atomic_load(q + 2 + (L - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 24)) {  // an item never finished: report instead of hanging the GPU
+                        atomicOr(a.err, 1);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            known = L;
+        }
+        switch (L) {
+            case 0:
+                small_conv_sk_body<P12, NB, SK_KG1, true>(i, nsk, pool, s_last, a.planes, (long long)a.D * NB * NB, 0,
+                                                          0, B, NB, 1, a.w2, C, a.b2, 1, a.y2, C, a.part, a.tickets,
+                                                          a.w1, a.b1, a.D);
+                break;
+            case 1:
+                if constexpr (H3 * H3 > 16)  // conv3 as the per-layer path runs it: split-K in 8 K-parts ...
+                    small_conv_sk_body<P3, 0, SK_KG, true>(i, n3, pool, s_last, a.y2, (long long)NB * NB * C, NB * C,
+                                                           C, B, NB, 0, a.w3, C, a.b3, 1, a.y3, C, a.part, a.tickets,
+                                                           nullptr, nullptr, 0);
+                else  // ... or, for <= 16 output pixels (6x6 boards), in 2-channel blocks
+                    small_conv_body<P3, 2, true, WLDS3, true>(i, pool, a.y2, (long long)NB * NB * C, NB * C, C, 1, B,
+                                                              NB, 0, a.w3, C, C, a.b3, 1, a.y3, C);
+                break;
+            case 2:
+                small_conv_body<P4, 2, true, WLDS4, true>(i, pool, a.y3, (long long)H3 * H3 * C, H3 * C, C, 1, B, H3,
+                                                          0, a.w4, C, C, a.b4, 1, a.y4, C);
+                break;
+            case 3:
+                if (npb1 == 4) fc(std::integral_constant<int, 4>{}, std::false_type{}, 2 * i, a.N1, a.y4, K1, a.fw1, K1,
+                                  a.fb1, 1, a.h1, a.N1, nullptr, nullptr, nullptr, nullptr);
+                else if (npb1 == 2) fc(std::integral_constant<int, 2>{}, std::false_type{}, 2 * i, a.N1, a.y4, K1,
+                                       a.fw1, K1, a.fb1, 1, a.h1, a.N1, nullptr, nullptr, nullptr, nullptr);
+                else fc(std::integral_constant<int, 1>{}, std::false_type{}, 2 * i, a.N1, a.y4, K1, a.fw1, K1, a.fb1, 1,
+                        a.h1, a.N1, nullptr, nullptr, nullptr, nullptr);
+                break;
+            case 4:
+                if (npb2 == 4) fc(std::integral_constant<int, 4>{}, std::false_type{}, 2 * i, a.N2, a.h1, a.N1, a.fw2,
+                                  a.N1, a.fb2, 1, a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
+                else if (npb2 == 2) fc(std::integral_constant<int, 2>{}, std::false_type{}, 2 * i, a.N2, a.h1, a.N1,
+                                       a.fw2, a.N1, a.fb2, 1, a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
+                else fc(std::integral_constant<int, 1>{}, std::false_type{}, 2 * i, a.N2, a.h1, a.N1, a.fw2, a.N1,
+                        a.fb2, 1, a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
+                break;
+            default:
+                fc(std::integral_constant<int, 4>{}, std::true_type{}, 2 * i, a.A + 1, a.h2, a.N2, a.fw34, a.N2, nullptr,
+                   0, a.logits, a.A + 1, a.fb34, a.P, a.v, a.heads_ticket);
+                break;
+        }
+        // this item's write-through stores have landed (every wave), then it counts as done
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            if (L < 5) __hip_atomic_fetch_add(q + 2 + L, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_next = (int)nxt;
+        }
+        __syncthreads();
+    }
+    // the last block to leave resets the queue for the next launch (every block has taken its last item)
+    if (tid == 0 &&
+        __hip_atomic_fetch_add(q + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u)
+        for (int w = 0; w < SN_SCHED_WORDS; ++w) __hip_atomic_store(q + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int PXL, bool VEC>
@@ -841,16 +886,25 @@ extern "C" int azg_small_heads(const float* x, int32_t ldx, int32_t batch, const
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
+// grid of azg_small_net (azg_small_net_blocks; 0: one block per CU)
+static int g_small_net_blocks = 0;
+
+extern "C" int azg_small_net_blocks(int32_t blocks) {
+    if (blocks < 0) return AZG_ERR_ARG;
+    g_small_net_blocks = blocks;
+    return 0;
+}
+
 // The whole small-batch forward in one launch (small_net_kernel above).  w: 14 device pointers
 // w1 b1 w2 b2 w3 b3 w4 b4 fw1 fb1 fw2 fb2 fw34 fb34 (BN folded, conv weights [co][3][3][ci] as the
 // per-layer kernels take them, w1 [co][3][3][depth]); acts: the activations (y2 | y3 | y4 | h1 | h2 |
-// logits, sized by the caller); bar: the grid barrier's u64 counter (zero once, before first use);
-// err: set when a barrier gave up (the caller resets bar then).
+// logits, sized by the caller); sched: the work queue's SN_SCHED_WORDS u32 counters (zero before the
+// first launch; every launch leaves them zero); err: set when a wait gave up (the caller zeroes sched then).
 extern "C" int azg_small_net(const float* planes, int32_t batch, int32_t depth, int32_t n, int32_t C, int32_t A,
                              int32_t n1, int32_t n2, const float* const* w, float* acts, int64_t acts_floats, float* P,
                              float* v, float* work, int64_t work_floats, uint32_t* tickets, int32_t n_tickets,
-                             uint64_t* bar, int32_t* err, void* stream) {
-    if (!planes || !w || !acts || !P || !v || !work || !tickets || !bar || !err || batch <= 0 || batch > 4 ||
+                             uint32_t* sched, int32_t* err, void* stream) {
+    if (!planes || !w || !acts || !P || !v || !work || !tickets || !sched || !err || batch <= 0 || batch > 4 ||
         depth < 1 || depth > 4 || n < 6 || n > 8 || C <= 0 || C % (4 * SK_KG1) || C % SK_CO || A < 1 || A > 1023 ||
         n1 <= 0 || n1 % 4 || n2 <= 0 || n2 % 4 || n_tickets < C / SK_CO + 1 || ((uintptr_t)work & 15) ||
         ((uintptr_t)acts & 15))
@@ -884,9 +938,10 @@ extern "C" int azg_small_net(const float* planes, int32_t batch, int32_t depth, 
     a.h2 = a.h1 + (long long)batch * n1;
     a.logits = a.h2 + (long long)batch * n2;
     a.P = P, a.v = v, a.part = work, a.tickets = tickets, a.heads_ticket = tickets + C / SK_CO;
-    a.bar = (unsigned long long*)bar, a.err = err;
+    a.sched = sched, a.err = err;
     a.B = batch, a.D = depth, a.C = C, a.A = A, a.N1 = n1, a.N2 = n2;
-    const dim3 grid((unsigned)cus);
+    const int blocks = g_small_net_blocks > 0 && g_small_net_blocks < cus ? g_small_net_blocks : cus;
+    const dim3 grid((unsigned)blocks);
     hipStream_t st = (hipStream_t)stream;
     auto go = [&](auto N_, auto B_, auto W3_, auto W4_) {
         hipLaunchKernelGGL((small_net_kernel<decltype(N_)::value, decltype(B_)::value, decltype(W3_)::value,

@@ -36,8 +36,9 @@ WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C
 # launch per layer, no library) instead of MIOpen / hipBLASLt
 SMALL_PATH = True
 SMALL_MAX_B = 4
-# the small-batch forward as ONE launch (azg_small_net: the per-layer kernels' block bodies in a
-# persistent grid, grid barriers between the layers; bit-identical results), else one launch per layer
+# the small-batch forward as ONE launch (azg_small_net: the per-layer kernels' block bodies as items of
+# an in-order work queue, an item waiting for the previous layer's done count; bit-identical results),
+# else one launch per layer
 SMALL_FUSED = True
 FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
 # NNetWrapper.train_examples on the GPU: steps run eagerly before the step is captured as a HIP graph
@@ -882,7 +883,7 @@ class InferenceNet(nn.Module):
 
     def _forward_small_fused(self, planes, B, dev, st, wp, tp):
         """The small-batch forward in one launch (azg_small_net): conv1 + conv2, conv3, conv4, fc1,
-        fc2, [fc3 | fc4] + softmax / tanh, grid barriers between the layers."""
+        fc2, [fc3 | fc4] + softmax / tanh, the layers' blocks as items of one in-order work queue."""
         import ctypes
         from . import _lib
         n, C, A = self.n, self.w1.shape[0], self.fw3.shape[0]
@@ -890,7 +891,8 @@ class InferenceNet(nn.Module):
         need = SMALL_MAX_B * (n * n * C + (n - 2) ** 2 * C + (n - 4) ** 2 * C + n1 + n2 + A + 1)
         if getattr(self, "_fused_acts", None) is None or self._fused_acts.device != dev:
             self._fused_acts = torch.empty(need, device=dev, dtype=torch.float32)
-            self._fused_bar = torch.zeros(2, device=dev, dtype=torch.int64)  # [0] barrier counter, [1] error flag
+            # [0:8] the work queue's counters (azg_small_net: zero, and left zero by every launch), [8] error flag
+            self._fused_bar = torch.zeros(16, device=dev, dtype=torch.int32)
             ptrs = [self.w1, self.b1, self.w2, self.b2, self.w3, self.b3, self.w4, self.b4, self.fw1, self.fb1,
                     self.fw2, self.fb2, self.fw34, self.fb34]
             self._fused_ptrs = (ctypes.c_void_p * 14)(*[t.data_ptr() for t in ptrs])
@@ -902,16 +904,16 @@ class InferenceNet(nn.Module):
             ctypes.c_void_p(planes.data_ptr()), B, self.depth, n, C, A, n1, n2, self._fused_ptrs,
             ctypes.c_void_p(self._fused_acts.data_ptr()), self._fused_acts.numel(), ctypes.c_void_p(p.data_ptr()),
             ctypes.c_void_p(v.data_ptr()), wp, self._small_work.numel(), tp, self._small_tickets.numel(),
-            ctypes.c_void_p(bar.data_ptr()), ctypes.c_void_p(bar.data_ptr() + 8), st))
+            ctypes.c_void_p(bar.data_ptr()), ctypes.c_void_p(bar.data_ptr() + 32), st))
         return p, v
 
     def check_fused(self):
-        """Raise if a grid barrier of the fused small-batch forward gave up waiting (a block never
-        arrived: the results of that launch are void), and reset the barrier."""
+        """Raise if a wait of the fused small-batch forward gave up (a layer's items never all
+        finished: the results of that launch are void), and reset its work queue."""
         bar = getattr(self, "_fused_bar", None)
-        if bar is not None and int(bar[1].item()) != 0:
+        if bar is not None and int(bar[8].item()) != 0:
             bar.zero_()
-            raise RuntimeError("azg_small_net: a grid barrier timed out")
+            raise RuntimeError("azg_small_net: a layer wait timed out")
 
     def _small_ok(self, planes):
         """Whether the small-batch kernels take this forward: at most SMALL_MAX_B leaves and

@@ -276,16 +276,20 @@ int  azg_small_conv12(const float* planes, int32_t batch, int32_t depth, int32_t
  * (azg_policy_value's arithmetic) by the last block to finish; *ticket zero before and after. */
 /* The whole small-batch forward (conv1 + conv2, conv3, conv4, fc1, fc2, [fc3 | fc4] + softmax / tanh)
  * in ONE launch: the blocks of the per-layer entry points above (same arithmetic and summation
- * orders: bit-identical P, v) in a persistent grid of one 512-thread block per CU, grid barriers
- * between the layers (a monotonic u64 arrival counter *bar, zeroed once before first use; a barrier
- * that waits ~2^24 polls gives up and sets *err).  w: 14 device pointers w1 b1 w2 b2 w3 b3 w4 b4
+ * orders: bit-identical P, v) as the items of one in-order work queue over a grid of one 512-thread
+ * block per CU, an item of layer L waiting for layer L-1's done count -- correct whatever number of
+ * the blocks is resident at once (no grid barrier).  sched: 8 u32 counters, zero before the first
+ * launch, left zero by every launch; a wait of ~2^24 polls gives up and sets *err (zero sched then).  w: 14 device pointers w1 b1 w2 b2 w3 b3 w4 b4
  * fw1 fb1 fw2 fb2 fw34 fb34 (BN folded; the layouts azg_small_conv12 / conv3x3 / fc / heads take);
  * acts >= batch (n^2 C + (n-2)^2 C + (n-4)^2 C + n1 + n2 + actions + 1) floats; batch <= 4, 6 <= n <= 8,
  * pads 1, 1, 0, 0 (the boards' nets); work / tickets as azg_small_conv12's (n_tickets >= C / 8 + 1). */
 int  azg_small_net(const float* planes, int32_t batch, int32_t depth, int32_t n, int32_t C, int32_t actions,
                    int32_t n1, int32_t n2, const float* const* w, float* acts, int64_t acts_floats, float* P, float* v,
-                   float* work, int64_t work_floats, uint32_t* tickets, int32_t n_tickets, uint64_t* bar, int32_t* err,
+                   float* work, int64_t work_floats, uint32_t* tickets, int32_t n_tickets, uint32_t* sched, int32_t* err,
                    void* stream);
+/* azg_small_net's grid, process-wide: `blocks` workgroups (0 = one per CU, the default; larger
+ * values are capped at the CU count).  Results do not depend on it (the tests run 1 to 256). */
+int  azg_small_net_blocks(int32_t blocks);
 int  azg_small_heads(const float* x, int32_t ldx, int32_t batch, const float* w34, int32_t K, int32_t A,
                      const float* b34, float* logits, float* P, float* v, uint32_t* ticket, void* stream);
 /* The schedule azg_split_gemm picks for a launch of this shape (4, 17 or 18). */

@@ -215,3 +215,33 @@ def test_overflow_on_one_rank_replays_all_ranks():
     planes, pis, vs = res[0]["ex"]
     assert (planes == ref.planes.cpu().numpy()).all() and (pis == ref.pis.cpu().numpy()).all()
     assert (vs == ref.vs.cpu().numpy()).all()
+
+
+def test_bench_two_ranks_learn_iteration():
+    """`bench.py --gpus 2 --learn-iteration on`, rehearsed as two ranks on
+    one GPU over gloo: the launcher starts the ranks itself, rank 0 prints one JSON line whose
+    learn_iteration carries the self-play / exchange / train split of the data-parallel
+    iteration and the gradient and BatchNorm all-reduces' bytes and time per step."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--games", "64", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--learn-iteration", "on",
+           "--max-turns", "40", "--train-epochs", "1", "--train-window", "4096"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    # the ranks' stderr goes straight to the test log (progress on a long run)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=150, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_games"] == 128
+    li = out["learn_iteration"]
+    assert li["ranks"] == 2 and li["games"] == 128 and li["examples"] == 4096
+    assert li["train_steps"] == 8 and li["selfplay_s"] > 0 and li["train_s"] > 0
+    assert li["records_sent_bytes_per_rank"] > 0
+    # one flat gradient buffer per step (every parameter + the two losses), f32
+    assert li["grad_allreduce_bytes_per_step"] > 4 * 10e6
+    assert li["bn_allreduce_calls_per_step"] == 12  # 6 BatchNorm layers, forward + backward
+    assert li["grad_allreduce_ms_per_step"] > 0

@@ -43,7 +43,7 @@ for task in "$@"; do
     suite)
         # no -x: one run lists every failing test; exit 1 (assertion failures only) lets the run go on
         rc=0
-        timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread \
+        timeout -k 10 1100 python -u -m pytest tests -m gpu -v -rf --timeout 170 --timeout-method thread \
             --durations 15 > "$O/pytest_gpu.log" 2>&1 || rc=$?
         if [ $rc -ne 0 ]; then
             echo "   suite: pytest exit $rc"
