@@ -76,35 +76,47 @@ __global__ __launch_bounds__(256) void fc_act_split_kernel(const float4* __restr
 
 // fc_act with the GEMM's partial products TRANSPOSED, m [parts][n][rows] (the small-batch fc1,
 // computed as W x A^T so each weight tile is read once: nnet.InferenceNet._fc_split_azg): a block
-// takes 64 features x 64 rows, sums the parts in order with loads along the rows, turns the tile
-// through LDS and writes y = relu(bias + scale m) as the next layer's AZG_WINO_SPLIT2 K-parts
-// ([out_parts][rows][2 n / out_parts], 32-channel [hi | lo] blocks), as fc_act_split_kernel.
+// takes 16 features x 64 rows (C2's 1024 x 256: 256 blocks, one per CU), each thread one row of 4
+// features with every part's load issued before the in-order sum (up to FT_PMAX parts in flight),
+// turns the tile through LDS and writes y = relu(bias + scale m) as the next layer's
+// AZG_WINO_SPLIT2 K-parts ([out_parts][rows][2 n / out_parts], 32-channel [hi | lo] blocks), as
+// fc_act_split_kernel.  (The first form, 64 x 64 tiles with one load in flight per part: 64 blocks,
+// 68.9 us at C2 -- 22.6% of its kernel time, profiles/r05_prof_C2_fc_act_t.md.)
+constexpr int FT_PMAX = 32;
+
 __global__ __launch_bounds__(256) void fc_act_t_kernel(const float* __restrict__ m, int parts, long long pstride,
                                                        const float* __restrict__ bias, float scale,
                                                        unsigned short* __restrict__ out, int rows, int n, int relu,
                                                        int out_parts, int* overflow) {
-    __shared__ float s[64][65];
-    const int t = threadIdx.x, f0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+    __shared__ float s[16][65];
+    const int t = threadIdx.x, f0 = blockIdx.x * 16, r0 = blockIdx.y * 64;
     {
         const int r = t & 63, fg = t >> 6;
-#pragma unroll 4
-        for (int j = 0; j < 16; ++j) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
             const int f = fg + 4 * j;
             const float* p = m + (long long)(f0 + f) * rows + r0 + r;
-            float x = p[0];
-            for (int q = 1; q < parts; ++q) x += p[q * pstride];  // split-K parts, in order
+            float v[FT_PMAX];
+#pragma unroll
+            for (int q = 0; q < FT_PMAX; ++q) v[q] = q < parts ? __builtin_nontemporal_load(p + q * pstride) : 0.f;
+            float x = v[0];
+#pragma unroll
+            for (int q = 1; q < FT_PMAX; ++q)
+                if (q < parts) x += v[q];  // split-K parts, in order
             s[f][r] = x;
         }
     }
     __syncthreads();
-    const int r = t >> 2, sub = t & 3;  // row, 16 features
-    const int np = n / out_parts, part = f0 / np, cc = f0 - part * np;  // 64 features never straddle a part
-    unsigned short* row = out + ((long long)part * rows + r0 + r) * 2 * np + 2 * cc;
+    const int r = t >> 2, sub = t & 3;  // row, 4 features
+    const int np = n / out_parts, part = f0 / np, cc = f0 - part * np;  // 16 features never straddle a part
+    const int c = cc + 4 * sub;  // the thread's first column within its part: 4 columns of one 32-block
+    unsigned short* row = out + ((long long)part * rows + r0 + r) * 2 * np + 64 * (c >> 5) + (c & 31);
     bool bad = false;
-    unsigned short hi[16], lo[16];
+    using u16x4 = __attribute__((ext_vector_type(4))) unsigned short;
+    u16x4 hi, lo;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int f = 16 * sub + j;
+    for (int j = 0; j < 4; ++j) {
+        const int f = 4 * sub + j;
         float y = bias[f0 + f] + scale * s[f][r];
         if (relu) y = fmaxf(y, 0.f);
         const _Float16 h = (_Float16)y;
@@ -113,15 +125,8 @@ __global__ __launch_bounds__(256) void fc_act_t_kernel(const float* __restrict__
         lo[j] = __builtin_bit_cast(unsigned short, l);
         bad |= !(fabsf(y) <= 65504.f);
     }
-    const int o = 64 * (sub >> 1) + 16 * (sub & 1);  // block sub / 2, hi half at its 16 features
-    using u16x8 = __attribute__((ext_vector_type(8))) unsigned short;
-    u16x8 a, b, c, d;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] = hi[j], b[j] = hi[8 + j], c[j] = lo[j], d[j] = lo[8 + j];
-    *(u16x8*)(row + o) = a;
-    *(u16x8*)(row + o + 8) = b;
-    *(u16x8*)(row + o + 32) = c;
-    *(u16x8*)(row + o + 40) = d;
+    *(u16x4*)row = hi;
+    *(u16x4*)(row + 32) = lo;
     if (bad) atomicOr(overflow, 1);
 }
 
@@ -201,10 +206,10 @@ extern "C" int azg_fc_act_t(const float* m, int32_t parts, int64_t part_stride, 
                             void* out, int32_t rows, int32_t n, int32_t relu, int32_t out_parts, int32_t* overflow,
                             void* stream) {
     if (!m || !bias || !out || !azg_device_writable(overflow) || rows <= 0 || rows % 64 || n <= 0 || n % 64 ||
-        parts < 1 || (parts > 1 && part_stride < (int64_t)rows * n) || out_parts < 1 || n % out_parts ||
-        (n / out_parts) % 64 || ((uintptr_t)out & 15))
+        parts < 1 || parts > FT_PMAX || (parts > 1 && part_stride < (int64_t)rows * n) || out_parts < 1 ||
+        n % out_parts || (n / out_parts) % 64 || ((uintptr_t)out & 15))
         return AZG_ERR_ARG;
-    hipLaunchKernelGGL(fc_act_t_kernel, dim3(n / 64, rows / 64), dim3(256), 0, (hipStream_t)stream, m, parts,
+    hipLaunchKernelGGL(fc_act_t_kernel, dim3(n / 16, rows / 64), dim3(256), 0, (hipStream_t)stream, m, parts,
                        (long long)part_stride, bias, scale, (unsigned short*)out, rows, n, relu, out_parts, overflow);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }

@@ -63,26 +63,31 @@ constexpr int SF_T = 256;  // small_fc threads
 __host__ __device__ constexpr int sc_pitch(int cin) { return ((cin + 3) & ~3) + 4; }
 
 // COH (the fused forward, small_net_kernel): activations another block of the same launch wrote
-// are read with agent-scope loads and written with agent-scope (write-through) stores -- the
-// split-K hand-off's rule (see above) applied to every layer boundary inside the launch
+// are read with device-scope (sc1) loads and written with agent-scope (write-through) stores -- the
+// split-K hand-off's rule (see above) applied to every layer boundary inside the launch.  The loads
+// are 128-bit buffer loads with the sc1 cache policy from a wave-uniform base (one instruction per
+// float4; relaxed agent-scope atomic loads are 32-bit, four instructions per float4)
+constexpr int BUF_SC1 = 16;  // cache-policy bit of sc1 in the buffer intrinsics' aux operand (gfx940+)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t coh_rsrc(const float* base) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+}
+
 template <bool COH>
-__device__ __forceinline__ float4 ld4(const float* p) {
-    if constexpr (COH) {
-        const unsigned* u = (const unsigned*)p;
-        return make_float4(__uint_as_float(__hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                           __uint_as_float(__hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                           __uint_as_float(__hip_atomic_load(u + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                           __uint_as_float(__hip_atomic_load(u + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-    } else {
-        return *(const float4*)p;
-    }
+__device__ __forceinline__ float4 ld4(const float* base, long long off) {  // base: wave-uniform
+    if constexpr (COH)
+        return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(coh_rsrc(base), (int)(off * 4), 0,
+                                                                                BUF_SC1));
+    else
+        return *(const float4*)(base + off);
 }
 template <bool COH>
-__device__ __forceinline__ float ld1(const float* p) {
+__device__ __forceinline__ float ld1(const float* base, long long off) {  // base: wave-uniform
     if constexpr (COH)
-        return __uint_as_float(__hip_atomic_load((const unsigned*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(coh_rsrc(base), (int)(off * 4), 0,
+                                                                              BUF_SC1));
     else
-        return *p;
+        return base[off];
 }
 template <bool COH>
 __device__ __forceinline__ void st1(float* p, float v) {
@@ -137,7 +142,7 @@ __device__ __forceinline__ void small_conv_body(int bid, float* __restrict__ lds
                 for (int u = 0; u < SC_UNR; ++u) {  // past the end: a duplicate load, not stored
                     const int i = min(base + u * SC_T, nx4 - 1);
                     const int pix = i / c4, c = (i - pix * c4) * 4, iy = pix / H, ix = pix - iy * H;
-                    r[u] = ld4<COH>(xb + (long long)iy * sY + (long long)ix * sX + c);
+                    r[u] = ld4<COH>(xb, (long long)iy * sY + (long long)ix * sX + c);
                 }
                 if constexpr (WITHW) {
 #pragma unroll
@@ -163,7 +168,7 @@ __device__ __forceinline__ void small_conv_body(int bid, float* __restrict__ lds
             const int n = H * H * Cin;
             for (int i = tid; i < n; i += SC_T) {
                 const int pix = i / Cin, c = i - pix * Cin, iy = pix / H, ix = pix - iy * H;
-                xs[pix * P + c] = ld1<COH>(xb + (long long)iy * sY + (long long)ix * sX + (long long)c * sC);
+                xs[pix * P + c] = ld1<COH>(xb, (long long)iy * sY + (long long)ix * sX + (long long)c * sC);
             }
         }
         __syncthreads();
@@ -356,7 +361,7 @@ __device__ __forceinline__ void small_conv_sk_body(int bid, int nblk, float* __r
             for (int u = 0; u < SC_UNR; ++u) {
                 const int i = min(base + u * SC_T, n4 - 1);
                 const int pix = i / c4, c = (i - pix * c4) * 4, iy = pix / H, ix = pix - iy * H;
-                r[u] = ld4<COH>(xb + (long long)iy * sY + (long long)ix * sX + c);
+                r[u] = ld4<COH>(xb, (long long)iy * sY + (long long)ix * sX + c);
             }
             stage_w();  // the weights' stores once the first input loads are in flight
 #pragma unroll
@@ -493,7 +498,7 @@ __device__ __forceinline__ void small_fc_body(int bid, int nblk, int tid, bool v
         float4 xv[BMAX];
 #pragma unroll
         for (int b = 0; b < BMAX; ++b)
-            xv[b] = b < B ? ld4<COH>(x + (long long)b * ldx + 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            xv[b] = b < B ? ld4<COH>(x + (long long)b * ldx, 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int r = 0; r < NPB; ++r) {
             if (n0 + r >= N) break;
@@ -919,6 +924,10 @@ extern "C" int azg_small_net(const float* planes, int32_t batch, int32_t depth, 
     const size_t c3 = (size_t)hw * sc_pitch(C) * 4 + (size_t)SC_T * 2 * 4;  // conv3 in 2-channel blocks (6x6)
     const size_t c4 = (size_t)h3 * h3 * sc_pitch(C) * 4 + (size_t)SC_T * 2 * 4, w4b = (size_t)2 * 9 * C * 4;
     if (sk12 > SN_POOL || c4 > SN_POOL || (h3 * h3 <= 16 && c3 > SN_POOL)) return AZG_ERR_ARG;
+    // conv3's split-K form (> 16 output pixels) as azg_small_conv3x3 takes it: C % (4 SK_KG), its LDS
+    if (h3 * h3 > 16 && (C % (4 * SK_KG) || (size_t)hw * (C / SK_KG + 4) * 4 + (size_t)9 * C / SK_KG * SK_CO * 4 +
+                                                     (size_t)SC_T * SK_CO * 4 > (size_t)SN_POOL))
+        return AZG_ERR_ARG;
     const bool wlds3 = c3 + w4b <= SN_POOL, wlds4 = c4 + w4b <= SN_POOL;
     static int cus = 0;
     if (!cus) {

@@ -879,7 +879,9 @@ class InferenceNet(nn.Module):
         n, C = self.n, self.w1.shape[0]
         return (getattr(self, "small_fused", SMALL_FUSED) and self.depth <= 4 and 6 <= n <= 8 and C % 16 == 0
                 and self.pads == [1, 1, 0, 0] and n * n * (C // 4 + 4) * 4 + 72 * C + 16384 <= 96 * 1024
-                and (n - 2) ** 2 * (C + 4) * 4 + 4096 <= 96 * 1024 and B <= SMALL_MAX_B)
+                and (n - 2) ** 2 * (C + 4) * 4 + 4096 <= 96 * 1024 and B <= SMALL_MAX_B
+                # conv3 split-K in 8 K-parts where it has > 16 output pixels (7x7, 8x8 boards)
+                and ((n - 2) ** 2 <= 16 or (C % 32 == 0 and n * n * (C // 8 + 4) * 4 + 36 * C + 16384 <= 96 * 1024)))
 
     def _forward_small_fused(self, planes, B, dev, st, wp, tp):
         """The small-batch forward in one launch (azg_small_net): conv1 + conv2, conv3, conv4, fc1,

@@ -333,7 +333,7 @@ int  azg_policy_value_parts(const float* m, int32_t parts, int64_t part_stride, 
                             float scale, float* P, float* v, int32_t rows, int32_t actions, void* stream);
 /* azg_fc_act (AZG_WINO_SPLIT2 output) for TRANSPOSED partial products m [parts][n][rows] (the
  * small-batch fc1 computed as W x A^T, every weight tile read once); rows % 64 == 0, n % 64 == 0,
- * (n / out_parts) % 64 == 0.  Same arithmetic: y = bias + scale * (parts summed in order). */
+ * (n / out_parts) % 64 == 0, 1 <= parts <= 32.  Same arithmetic: y = bias + scale * (parts summed in order). */
 int  azg_fc_act_t(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale, void* out,
                   int32_t rows, int32_t n, int32_t relu, int32_t out_parts, int32_t* overflow, void* stream);
 
