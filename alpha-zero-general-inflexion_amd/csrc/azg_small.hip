@@ -652,10 +652,9 @@ __global__ __launch_bounds__(SC_T) void small_net_kernel(SmallNetArgs a) {
     const int n3 = H3 * H3 > 16 ? C / SK_CO * SK_KG : C / 2;
     const int npb1 = a.N1 >= 2048 ? 4 : a.N1 >= 1024 ? 2 : 1, npb2 = a.N2 >= 2048 ? 4 : a.N2 >= 1024 ? 2 : 1;
     const int ng1 = (a.N1 + npb1 - 1) / npb1, ng2 = (a.N2 + npb2 - 1) / npb2, ng3 = (a.A + 1 + 3) / 4;
-    const int cnt[6] = {nsk, n3, C / 2, (ng1 + 1) / 2, (ng2 + 1) / 2, (ng3 + 1) / 2};
-    int end[6];
-    end[0] = cnt[0];
-    for (int L = 1; L < 6; ++L) end[L] = end[L - 1] + cnt[L];
+    // (scalars, not arrays: a dynamically indexed local array lives in scratch memory)
+    const int e0 = nsk, e1 = e0 + n3, e2 = e1 + C / 2, e3 = e2 + (ng1 + 1) / 2, e4 = e3 + (ng2 + 1) / 2,
+              e5 = e4 + (ng3 + 1) / 2;
     unsigned* q = a.sched;
 
     auto fc = [&](auto NPB_, auto HEADS_, int g0, int nrow, const float* x, int ldx, const float* w, int K,
@@ -675,19 +674,24 @@ __global__ __launch_bounds__(SC_T) void small_net_kernel(SmallNetArgs a) {
     for (;;) {
         const int item = s_next;
         __syncthreads();  // every thread has read s_next before it is overwritten below
-        if (item >= end[5]) break;
+        if (item >= e5) break;
         unsigned nxt = 0;  // the next item, fetched while this one runs (thread 0)
         if (tid == 0) nxt = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int L = 0;
-        while (item >= end[L]) ++L;
-        const int i = item - (L ? end[L - 1] : 0);
+        const int L = item < e0 ? 0 : item < e1 ? 1 : item < e2 ? 2 : item < e3 ? 3 : item < e4 ? 4 : 5;
+        const int lo = L == 0 ? 0 : L == 1 ? e0 : L == 2 ? e1 : L == 3 ? e2 : L == 4 ? e3 : e4;
+        const int i = item - lo;
         if (known < L) {  // layer L-1 done (and so every layer before it: its items waited in turn)
             if (tid == 0) {
-                const unsigned target = (unsigned)cnt[L - 1];
+                // layer L-1's item count
+                const unsigned target = (unsigned)(lo - (L == 1 ? 0 : L == 2 ? e0 : L == 3 ? e1 : L == 4 ? e2 : e3));
+                // polls back off (64 .. 512 clocks apart): up to 256 blocks poll one counter, and the
+                // blocks still working on layer L-1 increment it through the same memory channel
                 for (unsigned spins = 0;
                      __hip_atomic_load(q + 2 + (L - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 24)) {  // an item never finished: report instead of hanging the GPU
+                    if (spins < 4) __builtin_amdgcn_s_sleep(1);
+                    else if (spins < 16) __builtin_amdgcn_s_sleep(4);
+                    else __builtin_amdgcn_s_sleep(8);
+                    if (++spins > (1u << 22)) {  // an item never finished: report instead of hanging the GPU
                         atomicOr(a.err, 1);
                         break;
                     }

@@ -896,6 +896,7 @@ def _fused_vs_layers(n, depth, A, B):
     torch.manual_seed(20 + n)
     net = InflexionNNet(n=n, depth=depth, action_size=A).cuda().eval()
     fused = InferenceNet(net, conv="miopen", gemm="f32").cuda()
+    fused.small_fused = True
     layers = InferenceNet(net, conv="miopen", gemm="f32").cuda()
     layers.small_fused = False
     assert fused._fused_ok(B)
@@ -922,6 +923,7 @@ def _contend_worker(rank, q):
         torch.manual_seed(31)
         net = InflexionNNet(n=7, depth=4, action_size=343).cuda().eval()
         fused = InferenceNet(net, conv="miopen", gemm="f32").cuda()
+        fused.small_fused = True
         layers = InferenceNet(net, conv="miopen", gemm="f32").cuda()
         layers.small_fused = False
         g = torch.Generator(device="cuda").manual_seed(rank)

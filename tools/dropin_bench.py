@@ -57,11 +57,12 @@ def main():
             ev, graph = w, True
         elif form == "library":  # BN folded, MIOpen / hipBLASLt at one leaf
             ev, graph = InferenceNet(w.nnet.eval(), conv="miopen", gemm="f32", small=False), True
-        elif form == "layers":  # azg_small.hip one launch per layer (the round-4 default)
+        elif form == "layers":  # azg_small.hip one launch per layer (the default)
             ev, graph = InferenceNet(w.nnet.eval(), conv="miopen", gemm="f32", small=True), True
             ev.small_fused = False
         else:  # "small": azg_small.hip explicitly (the fused one-launch forward, azg_small_net)
             ev, graph = InferenceNet(w.nnet.eval(), conv="miopen", gemm="f32", small=True), True
+            ev.small_fused = True
         t = run(ev, game, a.sims, graph, a.moves, fast)
         print(json.dumps({"game": a.game, "form": form, "sims": a.sims, "ms_per_call": t * 1e3,
                           "sims_per_s": a.sims / t}), flush=True)
