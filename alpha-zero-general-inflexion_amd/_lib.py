@@ -103,6 +103,9 @@ SIGNATURES = [
     ("azg_small_net_blocks", ctypes.c_int, [_I32]),
     ("azg_fc_act_t", ctypes.c_int, [_VP, _I32, _I64, _VP, ctypes.c_float, _VP, _I32, _I32, _I32, _I32, _VP, _VP]),
     ("azg_absmax", ctypes.c_int, [_VP, _I64, _VP, _VP]),
+    ("azg_bn_relu_fwd", ctypes.c_int, [_VP, _I64, _I32, _VP, _VP, ctypes.c_float, ctypes.c_float, _VP, _VP, _VP,
+                                       _VP, _VP, _VP]),
+    ("azg_bn_relu_bwd", ctypes.c_int, [_VP, _VP, _I64, _I32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     ("azg_wt_u_build", ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
     ("azg_wt_out", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _VP, _VP]),
     ("azg_wt_dout", ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _VP, _VP, _VP]),

@@ -1,0 +1,229 @@
+// azg_train_bn.hip -- the trainer's BatchNorm2d + ReLU (InflexionNNet.py:39-45:
+// relu(bn_i(conv_i(x))), training mode) on channels-last activations, forward and backward.
+//
+// torch hands channels-last BatchNorm to MIOpen's NHWC kernels, which ran at ~1.3 TB/s on the
+// trainer's 512 x 512 x 7 x 7 activations (BwdSpatialDX + BwdSpatialDScaleDBias 116 + 115 us,
+// FwdTrainSpatialNorm 84 us per layer and step; profiles/r05_prof_train_probe_wino.md).  Here x is
+// [rows][C] (rows = batch x H x W, the channels contiguous) and every pass streams it with float4
+// loads:
+//
+//   forward   stats  : per channel sum x, sum x^2 over the rows (f64, block partials reduced in a
+//                      fixed order), mean, biased var, invstd = 1/sqrt(var + eps); scale = gamma
+//                      invstd, shift = beta - mean scale; running stats (momentum, unbiased var)
+//             apply  : y = max(x scale + shift, 0)
+//   backward  reduce : g = dy where x scale + shift > 0 (the forward's own f32 expression, so the
+//                      same mask), per channel sum g and sum g xhat, xhat = (x - mean) invstd (f64)
+//             apply  : dx = scale (g - sum g / n - xhat sum(g xhat) / n); dgamma = sum g xhat,
+//                      dbeta = sum g
+//
+// Deterministic (fixed partial order).  Tolerance-equal to torch's f32 BatchNorm (the sums are
+// f64 here); the trainer's tests bound the whole step against the reference trainer.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/azg.h"
+
+namespace {
+
+constexpr int BN_T = 256;       // threads per block
+constexpr int BN_PARTS = 512;   // row ranges (blocks) of the reductions
+
+// per block: channel quad q = t % C4 of rows r = row0 + t / C4 + k (T / C4) for k >= 0
+template <class F>
+__device__ __forceinline__ void rows_of_block(long long rows, int C4, F&& f) {
+    const int lanes = BN_T / C4;  // row lanes per block (C4 <= BN_T)
+    const int q = threadIdx.x % C4, l = threadIdx.x / C4;
+    if (l >= lanes) return;
+    const long long per = (rows + gridDim.x - 1) / gridDim.x;
+    const long long r0 = (long long)blockIdx.x * per, r1 = r0 + per < rows ? r0 + per : rows;
+#pragma unroll 4
+    for (long long r = r0 + l; r < r1; r += lanes) f(r, q);
+}
+
+// the block's row lanes' f64 quads summed in lane order -> part[blockIdx][which][4 q .. 4 q + 3]
+__device__ __forceinline__ void block_sum_store(double (&a)[8], int C4, double* __restrict__ part) {
+    __shared__ double red[BN_T][9];  // (padded: 9 doubles per thread)
+    const int lanes = BN_T / C4, q = threadIdx.x % C4, l = threadIdx.x / C4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[threadIdx.x][i] = a[i];
+    __syncthreads();
+    if (l == 0) {
+        for (int k = 1; k < lanes; ++k)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a[i] += red[k * C4 + q][i];
+        double* p = part + (long long)blockIdx.x * 8 * C4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            p[4 * q + i] = a[i];           // [0, C): first sums
+            p[4 * C4 + 4 * q + i] = a[4 + i];  // [C, 2C): second sums
+        }
+    }
+}
+
+__global__ __launch_bounds__(BN_T) void bn_stats_kernel(const float4* __restrict__ x, long long rows, int C4,
+                                                        double* __restrict__ part) {
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    rows_of_block(rows, C4, [&](long long r, int q) {
+        const float4 v = x[r * C4 + q];
+        const double d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            a[i] += d[i];
+            a[4 + i] += d[i] * d[i];
+        }
+    });
+    block_sum_store(a, C4, part);
+}
+
+// per channel: the parts in order -> mean, var, scale / shift (f32), running stats; one thread per channel
+__global__ __launch_bounds__(BN_T) void bn_stats_final_kernel(const double* __restrict__ part, int nparts, int C,
+                                                              long long n, const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, float eps,
+                                                              float momentum, float* __restrict__ run_mean,
+                                                              float* __restrict__ run_var, float* __restrict__ sv) {
+    const int c = blockIdx.x * BN_T + threadIdx.x;
+    if (c >= C) return;
+    double s = 0, s2 = 0;
+#pragma unroll 8
+    for (int p = 0; p < nparts; ++p) {
+        s += part[(long long)p * 2 * C + c];
+        s2 += part[(long long)p * 2 * C + C + c];
+    }
+    const double mean = s / (double)n;
+    double var = s2 / (double)n - mean * mean;
+    if (var < 0) var = 0;
+    const double invstd = 1.0 / sqrt(var + (double)eps);
+    const float scale = (float)((double)gamma[c] * invstd);
+    sv[c] = scale;                                                  // scale
+    sv[C + c] = (float)((double)beta[c] - mean * (double)scale);    // shift
+    sv[2 * C + c] = (float)mean;                                    // mean
+    sv[3 * C + c] = (float)invstd;                                  // invstd
+    if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+    if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)(var * (double)n / (double)(n - 1));
+}
+
+__global__ __launch_bounds__(BN_T) void bn_apply_relu_kernel(const float4* __restrict__ x,
+                                                             const float4* __restrict__ sv, long long n4, int C4,
+                                                             float4* __restrict__ y) {
+    for (long long i = (long long)blockIdx.x * BN_T + threadIdx.x; i < n4; i += (long long)gridDim.x * BN_T) {
+        const int q = (int)(i % C4);
+        const float4 v = x[i], sc = sv[q], sh = sv[C4 + q];
+        y[i] = make_float4(fmaxf(v.x * sc.x + sh.x, 0.f), fmaxf(v.y * sc.y + sh.y, 0.f),
+                           fmaxf(v.z * sc.z + sh.z, 0.f), fmaxf(v.w * sc.w + sh.w, 0.f));
+    }
+}
+
+// the ReLU's mask from the forward's own expression, then g and xhat
+__device__ __forceinline__ void bwd_terms(float4 v, float4 d, float4 sc, float4 sh, float4 mu, float4 is,
+                                          double (&g)[4], double (&xh)[4]) {
+    const float vv[4] = {v.x, v.y, v.z, v.w}, dd[4] = {d.x, d.y, d.z, d.w}, s[4] = {sc.x, sc.y, sc.z, sc.w},
+                h[4] = {sh.x, sh.y, sh.z, sh.w}, m[4] = {mu.x, mu.y, mu.z, mu.w}, iv[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        g[i] = vv[i] * s[i] + h[i] > 0.f ? (double)dd[i] : 0.0;
+        xh[i] = ((double)vv[i] - (double)m[i]) * (double)iv[i];
+    }
+}
+
+__global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const float4* __restrict__ x,
+                                                             const float4* __restrict__ dy,
+                                                             const float4* __restrict__ sv, long long rows, int C4,
+                                                             double* __restrict__ part) {
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    rows_of_block(rows, C4, [&](long long r, int q) {
+        double g[4], xh[4];
+        bwd_terms(x[r * C4 + q], dy[r * C4 + q], sv[q], sv[C4 + q], sv[2 * C4 + q], sv[3 * C4 + q], g, xh);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            a[i] += g[i];
+            a[4 + i] += g[i] * xh[i];
+        }
+    });
+    block_sum_store(a, C4, part);
+}
+
+// per channel: sum g, sum g xhat -> dbeta, dgamma and the apply's coefficients c1 = sum g / n,
+// c2 = sum g xhat / n (f32)
+__global__ __launch_bounds__(BN_T) void bn_bwd_final_kernel(const double* __restrict__ part, int nparts, int C,
+                                                            long long n, float* __restrict__ dgamma,
+                                                            float* __restrict__ dbeta, float* __restrict__ co) {
+    const int c = blockIdx.x * BN_T + threadIdx.x;
+    if (c >= C) return;
+    double s = 0, s2 = 0;
+#pragma unroll 8
+    for (int p = 0; p < nparts; ++p) {
+        s += part[(long long)p * 2 * C + c];
+        s2 += part[(long long)p * 2 * C + C + c];
+    }
+    dbeta[c] = (float)s;
+    dgamma[c] = (float)s2;
+    co[c] = (float)(s / (double)n);
+    co[C + c] = (float)(s2 / (double)n);
+}
+
+// dx = scale (g - c1 - xhat c2)
+__global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const float4* __restrict__ x, const float4* __restrict__ dy,
+                                                            const float4* __restrict__ sv,
+                                                            const float4* __restrict__ co, long long n4, int C4,
+                                                            float4* __restrict__ dx) {
+    for (long long i = (long long)blockIdx.x * BN_T + threadIdx.x; i < n4; i += (long long)gridDim.x * BN_T) {
+        const int q = (int)(i % C4);
+        const float4 sc = sv[q];
+        double g[4], xh[4];
+        bwd_terms(x[i], dy[i], sc, sv[C4 + q], sv[2 * C4 + q], sv[3 * C4 + q], g, xh);
+        const float4 c1 = co[q], c2 = co[C4 + q];
+        const float s[4] = {sc.x, sc.y, sc.z, sc.w}, a1[4] = {c1.x, c1.y, c1.z, c1.w}, a2[4] = {c2.x, c2.y, c2.z, c2.w};
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = s[k] * (float)(g[k] - (double)a1[k] - xh[k] * (double)a2[k]);
+        dx[i] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+unsigned stream_grid(long long n4) {
+    const long long b = (n4 + BN_T - 1) / BN_T;
+    return (unsigned)(b < 2048 ? b : 2048);
+}
+
+}  // namespace
+
+// Forward: y = relu(batchnorm(x)) with the batch's statistics; sv [4C] f32 receives scale, shift,
+// mean, invstd (the backward's input); run_mean / run_var updated in place (either may be null);
+// work >= 2 * 512 * C doubles.
+extern "C" int azg_bn_relu_fwd(const float* x, int64_t rows, int32_t C, const float* gamma, const float* beta,
+                               float eps, float momentum, float* run_mean, float* run_var, float* y, float* sv,
+                               double* work, void* stream) {
+    if (!x || !y || !gamma || !beta || !sv || !work || rows < 2 || C <= 0 || C % 4 || C / 4 > BN_T ||
+        ((uintptr_t)x & 15) || ((uintptr_t)y & 15) || ((uintptr_t)sv & 15))
+        return AZG_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const int C4 = C / 4;
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(BN_PARTS), dim3(BN_T), 0, st, (const float4*)x, (long long)rows, C4, work);
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((C + BN_T - 1) / BN_T), dim3(BN_T), 0, st, work, BN_PARTS, C,
+                       (long long)rows, gamma, beta, eps, momentum, run_mean, run_var, sv);
+    const long long n4 = rows * C4;
+    hipLaunchKernelGGL(bn_apply_relu_kernel, dim3(stream_grid(n4)), dim3(BN_T), 0, st, (const float4*)x,
+                       (const float4*)sv, n4, C4, (float4*)y);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+// Backward of azg_bn_relu_fwd: dx from dy (the gradient of y), x and the forward's sv; dgamma,
+// dbeta written (not accumulated); co >= 2C f32 and work >= 2 * 512 * C doubles scratch.
+extern "C" int azg_bn_relu_bwd(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv, float* dx,
+                               float* dgamma, float* dbeta, float* co, double* work, void* stream) {
+    if (!x || !dy || !sv || !dx || !dgamma || !dbeta || !co || !work || rows < 2 || C <= 0 || C % 4 ||
+        C / 4 > BN_T || ((uintptr_t)x & 15) || ((uintptr_t)dy & 15) || ((uintptr_t)dx & 15) ||
+        ((uintptr_t)sv & 15) || ((uintptr_t)co & 15))
+        return AZG_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const int C4 = C / 4;
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(BN_PARTS), dim3(BN_T), 0, st, (const float4*)x, (const float4*)dy,
+                       (const float4*)sv, (long long)rows, C4, work);
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + BN_T - 1) / BN_T), dim3(BN_T), 0, st, work, BN_PARTS, C,
+                       (long long)rows, dgamma, dbeta, co);
+    const long long n4 = rows * C4;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(n4)), dim3(BN_T), 0, st, (const float4*)x,
+                       (const float4*)dy, (const float4*)sv, (const float4*)co, n4, C4, (float4*)dx);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}

@@ -96,8 +96,25 @@ __device__ __forceinline__ void u_points(const float* __restrict__ w9, int h_out
     }
 }
 
-// max |x| of n floats (x % 4 == 0 handled by the caller) -> atomicMax on the bit pattern
-// (non-negative floats order as their bits); *out must be 0 before the launch
+// the block's max of m (non-negative) -> one atomicMax on the bit pattern (non-negative floats order as
+// their bits); one atomic per block, not per wave: 8192 waves' atomics on one word held wt_absmax at
+// 97 us for conv2's 51 MB gradient (profiles/r05_prof_train_probe_wino.md)
+template <int T>
+__device__ __forceinline__ void block_max_atomic(float m, unsigned* out) {
+    __shared__ float wm[T / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float b = wm[0];
+#pragma unroll
+        for (int q = 1; q < T / 64; ++q) b = fmaxf(b, wm[q]);
+        atomicMax(out, __float_as_uint(b));
+    }
+}
+
+// max |x| of n floats (x % 4 == 0 handled by the caller); *out must be 0 before the launch
 __global__ __launch_bounds__(256) void wt_absmax_kernel(const float4* __restrict__ x, long long n4,
                                                         unsigned* __restrict__ out) {
     float m = 0.f;
@@ -105,9 +122,7 @@ __global__ __launch_bounds__(256) void wt_absmax_kernel(const float4* __restrict
         const float4 v = x[i];
         m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+    block_max_atomic<256>(m, out);
 }
 
 // max |U| over every point and (c, k): one thread per (k, c)
@@ -116,31 +131,39 @@ __global__ __launch_bounds__(256) void wt_u_absmax_kernel(const float* __restric
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
     float m = 0.f;
     if (i < (long long)C * K) u_points(w + i * 9, h_out, [&](int, float u) { m = fmaxf(m, fabsf(u)); });
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+    block_max_atomic<256>(m, out);
 }
 
-// U 2^ku split into AZG_WINO_SPLIT2 rows: ROWS_K (the forward GEMM's B operand, U^T):
-// [P][K][2C], one thread per (k, c) with c fastest; else (the dV GEMM's B operand, U):
-// [P][C][2K], one thread per (c, k) with k fastest.  ku from max |U| (wt_u_absmax_kernel).
-template <bool ROWS_K>
-__global__ __launch_bounds__(256) void wt_u_split_kernel(const float* __restrict__ w, int C, int K, int h_out,
+// U 2^ku split into both AZG_WINO_SPLIT2 operand layouts at once: UT [P][K][2C] (the forward GEMM's
+// B operand, U^T) and UN [P][C][2K] (the dV GEMM's, U).  One 1024-thread block per 32 (k) x 32 (c)
+// tile, thread (k, c) computing its pair's U at every point in f64 (u_points); per point the tile's
+// [hi | lo] pairs go through LDS and out as 32 rows of 128 B in each layout (4-byte stores, whole
+// 32-channel blocks).  ku from max |U| (wt_u_absmax_kernel).  (Replaces one thread per pair storing
+// 2-byte halves per point in each layout: 112 us per layer and layout, r05_prof_train_probe_wino.md.)
+__global__ __launch_bounds__(1024) void wt_u_tile_kernel(const float* __restrict__ w, int C, int K, int h_out,
                                                          const unsigned* __restrict__ uamax,
-                                                         unsigned short* __restrict__ out) {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (long long)C * K) return;
-    const int k = ROWS_K ? (int)(i / C) : (int)(i % K), c = ROWS_K ? (int)(i % C) : (int)(i / K);
+                                                         unsigned* __restrict__ ut, unsigned* __restrict__ un) {
+    __shared__ unsigned tl[32][33];  // [k][c]: hi | lo << 16
+    const int t = threadIdx.x, cc = t & 31, kk = t >> 5;
+    const int c0 = blockIdx.x * 32, k0 = blockIdx.y * 32;
     const float sc = pow2_scale(*uamax, 1024.f);
-    const int R = ROWS_K ? K : C, W = ROWS_K ? C : K, r = ROWS_K ? k : c, x = ROWS_K ? c : k;
-    u_points(w + ((long long)k * C + c) * 9, h_out, [&](int e, float u) {
+    const int r = t >> 5, wd = t & 31, j = 2 * (wd & 15), sh = wd < 16 ? 0 : 16;  // the thread's output word
+    u_points(w + ((long long)(k0 + kk) * C + c0 + cc) * 9, h_out, [&](int e, float u) {
         const float us = u * sc;  // exact (a power of two)
         const _Float16 hi = (_Float16)us;
         const _Float16 lo = (_Float16)(us - (float)hi);
-        unsigned short* row = out + ((long long)e * R + r) * 2 * W;
-        const int o = 64 * (x >> 5) + (x & 31);
-        row[o] = __builtin_bit_cast(unsigned short, hi);
-        row[o + 32] = __builtin_bit_cast(unsigned short, lo);
+        tl[kk][cc] = (unsigned)__builtin_bit_cast(unsigned short, hi) |
+                     ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
+        __syncthreads();
+        if (ut) {  // row k0 + r, its 32-channel block of c0: words 0-15 the hi halves, 16-31 the lo
+            const unsigned a = (tl[r][j] >> sh) & 0xffffu, b = (tl[r][j + 1] >> sh) & 0xffffu;
+            ut[(((long long)e * K + k0 + r) * 2 * C + 2 * c0) / 2 + wd] = a | (b << 16);
+        }
+        if (un) {  // row c0 + r, its 32-channel block of k0
+            const unsigned a = (tl[j][r] >> sh) & 0xffffu, b = (tl[j + 1][r] >> sh) & 0xffffu;
+            un[(((long long)e * C + c0 + r) * 2 * K + 2 * k0) / 2 + wd] = a | (b << 16);
+        }
+        __syncthreads();
     });
 }
 
@@ -330,21 +353,22 @@ extern "C" int azg_absmax(const float* x, int64_t n, uint32_t* out, void* stream
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(out, 0, 4, st) != hipSuccess) return AZG_ERR_HIP;
     const long long n4 = n / 4;
-    const unsigned grid = (unsigned)std::min<long long>((n4 + 255) / 256, 2048);
+    const unsigned grid = (unsigned)std::min<long long>((n4 + 255) / 256, 1024);
     hipLaunchKernelGGL(wt_absmax_kernel, dim3(grid), dim3(256), 0, st, (const float4*)x, n4, out);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
 extern "C" int azg_wt_u_build(const float* w, int32_t c, int32_t k, int32_t h_out, uint32_t* uamax, void* ut,
                               void* un, void* stream) {
-    if (!w || !uamax || (!ut && !un) || c <= 0 || k <= 0 || c % 32 || k % 32 || h_out < 2 || h_out > 9)
+    if (!w || !uamax || (!ut && !un) || c <= 0 || k <= 0 || c % 32 || k % 32 || h_out < 2 || h_out > 9 ||
+        ((uintptr_t)ut & 3) || ((uintptr_t)un & 3))
         return AZG_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(uamax, 0, 4, st) != hipSuccess) return AZG_ERR_HIP;
     const dim3 grid((unsigned)(((long long)c * k + 255) / 256));
     hipLaunchKernelGGL(wt_u_absmax_kernel, grid, dim3(256), 0, st, w, c, k, h_out, uamax);
-    if (ut) hipLaunchKernelGGL(wt_u_split_kernel<true>, grid, dim3(256), 0, st, w, c, k, h_out, uamax, (unsigned short*)ut);
-    if (un) hipLaunchKernelGGL(wt_u_split_kernel<false>, grid, dim3(256), 0, st, w, c, k, h_out, uamax, (unsigned short*)un);
+    hipLaunchKernelGGL(wt_u_tile_kernel, dim3((unsigned)(c / 32), (unsigned)(k / 32)), dim3(1024), 0, st, w, c, k,
+                       h_out, uamax, (unsigned*)ut, (unsigned*)un);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 

@@ -16,9 +16,10 @@ transformed point one split-fp16 GEMM (f32-accurate products on the fp16 MFMA):
 (csrc/azg_wino_train.hip).  Operands are scaled by powers of two chosen on the device (U:
 max in (512, 1024]; dy: in (16, 32]) and unscaled exactly, so no step waits on the host.
 `train_forward` is InflexionNNet.forward with conv2-4 replaced when `applies` holds (a GPU
-batch, 512-style channel counts, the 7x7 board's layer sides); everything else -- conv1,
-BatchNorm (GlobalBatchNorm under the data-parallel trainer), ReLU, dropout, the FC layers,
-the losses and Adam -- is the reference's torch code.
+batch, 512-style channel counts, the 7x7 board's layer sides) and bn1-4 + ReLU on
+BatchNormReLU (NHWC, azg_train_bn.hip; the data-parallel trainer's GlobalBatchNorm stays
+torch's); everything else -- conv1, dropout, the FC layers and their BatchNorms, the losses and
+Adam -- is the reference's torch code.
 """
 import ctypes
 
@@ -144,6 +145,59 @@ class WinogradConv3x3(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class BatchNormReLU(torch.autograd.Function):
+    """relu(bn(x)) for a training-mode nn.BatchNorm2d on channels-last x, forward and backward on
+    libazg's NHWC kernels (azg_train_bn.hip: per-channel sums in f64 over fixed row ranges, the
+    ReLU fused, the running statistics updated on the device).  MIOpen's channels-last BatchNorm
+    kernels ran at ~1.3 TB/s on the trainer's activations (1.36 ms of a 512-example step,
+    profiles/r05_prof_train_probe_wino.md).  Returns y channels-last."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
+        L = _lib.lib()
+        dev = x.device
+        B, C, H, W = x.shape
+        rows = B * H * W
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        sv = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        work = torch.empty(1024 * C, dtype=torch.float64, device=dev)
+        _lib.check(L.azg_bn_relu_fwd(_p(x), rows, C, _p(weight.detach()), _p(bias.detach()), float(eps),
+                                     float(momentum), _p(running_mean), _p(running_var), _p(y), _p(sv), _p(work),
+                                     _stream(dev)))
+        ctx.save_for_backward(x, sv)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        x, sv = ctx.saved_tensors
+        dev = x.device
+        B, C, H, W = x.shape
+        dyc = dy.contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dg = torch.empty(C, dtype=torch.float32, device=dev)
+        db = torch.empty(C, dtype=torch.float32, device=dev)
+        co = torch.empty(2 * C, dtype=torch.float32, device=dev)
+        work = torch.empty(1024 * C, dtype=torch.float64, device=dev)
+        _lib.check(L.azg_bn_relu_bwd(_p(x), _p(dyc), B * H * W, C, _p(sv), _p(dx), _p(dg), _p(db), _p(co), _p(work),
+                                     _stream(dev)))
+        return dx, dg, db, None, None, None, None
+
+
+def bn_relu(bn, x):
+    """relu(bn(x)) as InflexionNNet.forward applies it (InflexionNNet.py:39-45): on
+    BatchNormReLU for a plain training-mode nn.BatchNorm2d (affine, running statistics, a
+    momentum) over channels-last CUDA f32 activations, else the module and F.relu (eval mode,
+    the data-parallel trainer's GlobalBatchNorm, other layouts)."""
+    if (type(bn) is torch.nn.BatchNorm2d and bn.training and bn.affine and bn.track_running_stats
+            and bn.momentum is not None and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 4 == 0
+            and x.shape[1] <= 1024 and x.numel() // x.shape[1] >= 2):
+        bn.num_batches_tracked.add_(1)
+        return BatchNormReLU.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps)
+    return F.relu(bn(x))
+
+
 def applies_net(net, s):
     """Whether train_forward puts conv2-4 of `net` on the training kernels for planes s: a CUDA
     batch of 64k leaves, the 7x7 board's layer sides (pads 1, 1, 0, 0), channel counts % 256.
@@ -166,9 +220,9 @@ def train_forward(net, s):
     x = s.view(-1, net.depth, net.n, net.n)
     if x.is_cuda:
         x = x.contiguous(memory_format=torch.channels_last)
-    x = F.relu(net.bn1(net.conv1(x)))
+    x = bn_relu(net.bn1, net.conv1(x))
     for i in range(2, 5):
-        x = F.relu(getattr(net, f"bn{i}")(conv3x3(x, getattr(net, f"conv{i}"))))
+        x = bn_relu(getattr(net, f"bn{i}"), conv3x3(x, getattr(net, f"conv{i}")))
     x = x.reshape(x.shape[0], -1)
     x = F.dropout(F.relu(net.fc_bn1(net.fc1(x))), p=net.dropout, training=net.training)
     x = F.dropout(F.relu(net.fc_bn2(net.fc2(x))), p=net.dropout, training=net.training)
@@ -226,4 +280,5 @@ def _flag(dev):
     return f
 
 
-__all__ = ["WinogradConv3x3", "applies", "applies_net", "check_range", "conv3x3", "take_flag", "train_forward"]
+__all__ = ["BatchNormReLU", "WinogradConv3x3", "applies", "applies_net", "bn_relu", "check_range", "conv3x3",
+           "take_flag", "train_forward"]

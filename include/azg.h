@@ -406,6 +406,17 @@ int  azg_examples(int32_t game_kind, int32_t n, int32_t max_turns, int32_t temp_
  *   azg_wt_split2_transpose: AZG_WINO_SPLIT2 [points][t][2c] -> [points][c][2t] (t, c % 64).
  *   azg_wt_pow2_scale   : *out = the power of two the kernels scale by for amax, target. */
 int  azg_absmax(const float* x, int64_t n, uint32_t* out, void* stream);
+/* The trainer's BatchNorm2d + ReLU on channels-last activations x [rows][C] (rows = batch x H x W;
+ * C % 4 == 0, C <= 1024), training mode (azg_train_bn.hip): azg_bn_relu_fwd writes y = relu(bn(x))
+ * with the batch's statistics, sv [4C] = (scale, shift, mean, invstd), and updates run_mean /
+ * run_var (momentum; unbiased variance; either may be null); azg_bn_relu_bwd writes dx, dgamma,
+ * dbeta from dy (the gradient of y), x and sv.  Sums in f64 over 512 fixed row ranges, reduced in
+ * order (deterministic); work >= 1024 C doubles, co >= 2C floats (scratch). */
+int  azg_bn_relu_fwd(const float* x, int64_t rows, int32_t C, const float* gamma, const float* beta, float eps,
+                     float momentum, float* run_mean, float* run_var, float* y, float* sv, double* work,
+                     void* stream);
+int  azg_bn_relu_bwd(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv, float* dx,
+                     float* dgamma, float* dbeta, float* co, double* work, void* stream);
 int  azg_wt_u_build(const float* w, int32_t c, int32_t k, int32_t h_out, uint32_t* uamax, void* ut, void* un,
                     void* stream);
 int  azg_wt_out(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,

@@ -82,3 +82,40 @@ def test_train_forward_matches_module():
         el = (gl[k] - g64[k]).abs().max().item() / scale
         print(f"{k}: winograd {ew:.3g}, library {el:.3g} of max |grad|")
         assert ew <= 5 * el + (5e-3 if k == "conv1.weight" else 1e-5), (k, ew, el)
+
+
+@pytest.mark.parametrize("B,H", [(512, 7), (512, 5), (64, 3), (2, 7)])
+def test_batchnorm_relu_matches_torch(B, H):
+    """wino_train.BatchNormReLU (azg_train_bn.hip, NHWC, f64 sums) against torch's training-mode
+    BatchNorm2d + ReLU in f64: y within 1e-5 of max |y|, the running statistics within 1e-6,
+    dx / dgamma / dbeta within 2e-5 of their largest magnitude (f32 storage of the inputs and
+    outputs; the library's f32 BatchNorm is held to the same bound)."""
+    import azg_amd  # noqa: F401
+    from azg_amd.wino_train import bn_relu
+    torch.manual_seed(13)
+    C = 512
+    bn = torch.nn.BatchNorm2d(C).cuda().train()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+        bn.running_mean.uniform_(-0.1, 0.1)
+    ref = torch.nn.BatchNorm2d(C).cuda().double().train()
+    ref.load_state_dict(bn.state_dict())
+    x = (torch.randn(B, C, H, H, device="cuda") * 2 + 0.3).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(B, C, H, H, device="cuda")
+    x1 = x.clone().requires_grad_()
+    y = bn_relu(bn, x1)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    x2 = x.double().clone().requires_grad_()
+    y2 = torch.relu(ref(x2))
+    y2.backward(dy.double())
+    for name, got, want, tol in (("y", y, y2, 1e-5), ("dx", x1.grad, x2.grad, 2e-5),
+                                 ("dgamma", bn.weight.grad, ref.weight.grad, 2e-5),
+                                 ("dbeta", bn.bias.grad, ref.bias.grad, 2e-5),
+                                 ("running_mean", bn.running_mean, ref.running_mean, 1e-6),
+                                 ("running_var", bn.running_var, ref.running_var, 1e-6)):
+        err = (got.double() - want).abs().max().item() / max(want.abs().max().item(), 1e-30)
+        print(f"B {B} H {H}: {name} max error {err:.3g}")
+        assert err < tol, (name, err)
+    assert int(bn.num_batches_tracked) == 1
