@@ -9,9 +9,9 @@
 //
 //   forward   stats  : per channel sum x, sum x^2 over the rows (f64, block partials reduced in a
 //                      fixed order), mean, biased var, invstd = 1/sqrt(var + eps); scale = gamma
-//                      invstd, shift = beta - mean scale; running stats (momentum, unbiased var)
-//             apply  : y = max(x scale + shift, 0)
-//   backward  reduce : g = dy where x scale + shift > 0 (the forward's own f32 expression, so the
+//                      invstd; running stats (momentum, unbiased var)
+//             apply  : y = max((x - mean) scale + beta, 0)
+//   backward  reduce : g = dy where (x - mean) scale + beta > 0 (the forward's own f32 expression, so the
 //                      same mask), per channel sum g and sum g xhat, xhat = (x - mean) invstd (f64)
 //             apply  : dx = scale (g - sum g / n - xhat sum(g xhat) / n); dgamma = sum g xhat,
 //                      dbeta = sum g
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(BN_T) void bn_stats_kernel(const float4* __restrict
     block_sum_store(a, C4, part);
 }
 
-// per channel: the parts in order -> mean, var, scale / shift (f32), running stats; one thread per channel
+// per channel: the parts in order -> mean, var, scale (f32), running stats; one thread per channel
 __global__ __launch_bounds__(BN_T) void bn_stats_final_kernel(const double* __restrict__ part, int nparts, int C,
                                                               long long n, const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float eps,
@@ -95,12 +95,21 @@ __global__ __launch_bounds__(BN_T) void bn_stats_final_kernel(const double* __re
     if (var < 0) var = 0;
     const double invstd = 1.0 / sqrt(var + (double)eps);
     const float scale = (float)((double)gamma[c] * invstd);
-    sv[c] = scale;                                                  // scale
-    sv[C + c] = (float)((double)beta[c] - mean * (double)scale);    // shift
+    sv[c] = scale;       // scale
+    sv[C + c] = beta[c];  // beta
     sv[2 * C + c] = (float)mean;                                    // mean
     sv[3 * C + c] = (float)invstd;                                  // invstd
     if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
     if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)(var * (double)n / (double)(n - 1));
+}
+
+// relu(bn(x)) = max((x - mean) scale + beta, 0) in f32: x - mean first (no cancellation against a
+// large mean, as x scale + (beta - mean scale) would have: conv3's weight gradient 4.5% off, r05f)
+__device__ __forceinline__ float bn_pre(float x, float mean, float scale, float beta) {
+    return (x - mean) * scale + beta;
+}
+__device__ __forceinline__ float bn_out(float x, float mean, float scale, float beta) {
+    return fmaxf(bn_pre(x, mean, scale, beta), 0.f);
 }
 
 __global__ __launch_bounds__(BN_T) void bn_apply_relu_kernel(const float4* __restrict__ x,
@@ -108,9 +117,9 @@ __global__ __launch_bounds__(BN_T) void bn_apply_relu_kernel(const float4* __res
                                                              float4* __restrict__ y) {
     for (long long i = (long long)blockIdx.x * BN_T + threadIdx.x; i < n4; i += (long long)gridDim.x * BN_T) {
         const int q = (int)(i % C4);
-        const float4 v = x[i], sc = sv[q], sh = sv[C4 + q];
-        y[i] = make_float4(fmaxf(v.x * sc.x + sh.x, 0.f), fmaxf(v.y * sc.y + sh.y, 0.f),
-                           fmaxf(v.z * sc.z + sh.z, 0.f), fmaxf(v.w * sc.w + sh.w, 0.f));
+        const float4 v = x[i], sc = sv[q], be = sv[C4 + q], mu = sv[2 * C4 + q];
+        y[i] = make_float4(bn_out(v.x, mu.x, sc.x, be.x), bn_out(v.y, mu.y, sc.y, be.y),
+                           bn_out(v.z, mu.z, sc.z, be.z), bn_out(v.w, mu.w, sc.w, be.w));
     }
 }
 
@@ -121,7 +130,7 @@ __device__ __forceinline__ void bwd_terms(float4 v, float4 d, float4 sc, float4 
                 h[4] = {sh.x, sh.y, sh.z, sh.w}, m[4] = {mu.x, mu.y, mu.z, mu.w}, iv[4] = {is.x, is.y, is.z, is.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        g[i] = vv[i] * s[i] + h[i] > 0.f ? (double)dd[i] : 0.0;
+        g[i] = bn_pre(vv[i], m[i], s[i], h[i]) > 0.f ? (double)dd[i] : 0.0;
         xh[i] = ((double)vv[i] - (double)m[i]) * (double)iv[i];
     }
 }
@@ -188,7 +197,7 @@ unsigned stream_grid(long long n4) {
 
 }  // namespace
 
-// Forward: y = relu(batchnorm(x)) with the batch's statistics; sv [4C] f32 receives scale, shift,
+// Forward: y = relu(batchnorm(x)) with the batch's statistics; sv [4C] f32 receives scale, beta,
 // mean, invstd (the backward's input); run_mean / run_var updated in place (either may be null);
 // work >= 2 * 512 * C doubles.
 extern "C" int azg_bn_relu_fwd(const float* x, int64_t rows, int32_t C, const float* gamma, const float* beta,

@@ -125,46 +125,58 @@ __global__ __launch_bounds__(256) void wt_absmax_kernel(const float4* __restrict
     block_max_atomic<256>(m, out);
 }
 
-// max |U| over every point and (c, k): one thread per (k, c)
-__global__ __launch_bounds__(256) void wt_u_absmax_kernel(const float* __restrict__ w, int C, int K, int h_out,
-                                                          unsigned* __restrict__ out) {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+// U of every point in f32, uf [P][K][C] (c fastest: coalesced 4-byte stores), and max |U| (block
+// reduced, one atomic per block): one thread per (k, c), f64 arithmetic (u_points)
+__global__ __launch_bounds__(256) void wt_u_f32_kernel(const float* __restrict__ w, int C, int K, int h_out,
+                                                       float* __restrict__ uf, unsigned* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x, CK = (long long)C * K;
     float m = 0.f;
-    if (i < (long long)C * K) u_points(w + i * 9, h_out, [&](int, float u) { m = fmaxf(m, fabsf(u)); });
+    if (i < CK)
+        u_points(w + i * 9, h_out, [&](int e, float u) {
+            uf[e * CK + i] = u;
+            m = fmaxf(m, fabsf(u));
+        });
     block_max_atomic<256>(m, out);
 }
 
-// U 2^ku split into both AZG_WINO_SPLIT2 operand layouts at once: UT [P][K][2C] (the forward GEMM's
-// B operand, U^T) and UN [P][C][2K] (the dV GEMM's, U).  One 1024-thread block per 32 (k) x 32 (c)
-// tile, thread (k, c) computing its pair's U at every point in f64 (u_points); per point the tile's
-// [hi | lo] pairs go through LDS and out as 32 rows of 128 B in each layout (4-byte stores, whole
-// 32-channel blocks).  ku from max |U| (wt_u_absmax_kernel).  (Replaces one thread per pair storing
-// 2-byte halves per point in each layout: 112 us per layer and layout, r05_prof_train_probe_wino.md.)
-__global__ __launch_bounds__(1024) void wt_u_tile_kernel(const float* __restrict__ w, int C, int K, int h_out,
-                                                         const unsigned* __restrict__ uamax,
-                                                         unsigned* __restrict__ ut, unsigned* __restrict__ un) {
-    __shared__ unsigned tl[32][33];  // [k][c]: hi | lo << 16
-    const int t = threadIdx.x, cc = t & 31, kk = t >> 5;
-    const int c0 = blockIdx.x * 32, k0 = blockIdx.y * 32;
+// U 2^ku split into both AZG_WINO_SPLIT2 operand layouts from uf: UT [P][K][2C] (the forward GEMM's B
+// operand, U^T) and UN [P][C][2K] (the dV GEMM's, U).  One block per (point, 64 k x 64 c tile): the
+// tile in LDS, then 64 rows of 256 B in each layout (4-byte words of two channels' halves).  Replaces
+// one thread per (k, c) recomputing U in f64 per layout and storing 2-byte halves (112 us per layer
+// and layout) and a one-pass tile kernel with two barriers per point (366 us),
+// profiles/r05_prof_train_probe_wino*.md.
+__global__ __launch_bounds__(256) void wt_u_split_tile_kernel(const float* __restrict__ uf, int C, int K,
+                                                              const unsigned* __restrict__ uamax,
+                                                              unsigned* __restrict__ ut, unsigned* __restrict__ un) {
+    __shared__ float tl[64][65];  // [k][c]
+    const int t = threadIdx.x, c0 = blockIdx.x * 64, k0 = blockIdx.y * 64, e = blockIdx.z;
     const float sc = pow2_scale(*uamax, 1024.f);
-    const int r = t >> 5, wd = t & 31, j = 2 * (wd & 15), sh = wd < 16 ? 0 : 16;  // the thread's output word
-    u_points(w + ((long long)(k0 + kk) * C + c0 + cc) * 9, h_out, [&](int e, float u) {
-        const float us = u * sc;  // exact (a power of two)
-        const _Float16 hi = (_Float16)us;
-        const _Float16 lo = (_Float16)(us - (float)hi);
-        tl[kk][cc] = (unsigned)__builtin_bit_cast(unsigned short, hi) |
-                     ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
-        __syncthreads();
-        if (ut) {  // row k0 + r, its 32-channel block of c0: words 0-15 the hi halves, 16-31 the lo
-            const unsigned a = (tl[r][j] >> sh) & 0xffffu, b = (tl[r][j + 1] >> sh) & 0xffffu;
-            ut[(((long long)e * K + k0 + r) * 2 * C + 2 * c0) / 2 + wd] = a | (b << 16);
+    const float* src = uf + ((long long)e * K + k0) * C + c0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {  // 64 rows of 64 floats: 16 per thread, rows of 256 B
+        const int r = q * 4 + (t >> 6), x = t & 63;
+        tl[r][x] = src[(long long)r * C + x] * sc;  // exact (a power of two)
+    }
+    __syncthreads();
+    // a row's 64 channels = two 32-channel blocks [hi 32 | lo 32] = 64 words; word wd of the row:
+    // block wd / 32, hi (wd % 32 < 16) or lo, channels 2 (wd % 16) and 2 (wd % 16) + 1 of the block
+    auto word = [&](float a, float b, bool lo) {
+        const _Float16 ha = (_Float16)a, hb = (_Float16)b;
+        unsigned short xa = __builtin_bit_cast(unsigned short, ha), xb = __builtin_bit_cast(unsigned short, hb);
+        if (lo) {
+            xa = __builtin_bit_cast(unsigned short, (_Float16)(a - (float)ha));
+            xb = __builtin_bit_cast(unsigned short, (_Float16)(b - (float)hb));
         }
-        if (un) {  // row c0 + r, its 32-channel block of k0
-            const unsigned a = (tl[j][r] >> sh) & 0xffffu, b = (tl[j + 1][r] >> sh) & 0xffffu;
-            un[(((long long)e * C + c0 + r) * 2 * K + 2 * k0) / 2 + wd] = a | (b << 16);
-        }
-        __syncthreads();
-    });
+        return (unsigned)xa | ((unsigned)xb << 16);
+    };
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int r = q * 4 + (t >> 6), wd = t & 63;
+        const int ch = 32 * (wd >> 5) + 2 * (wd & 15);
+        const bool lo = (wd & 31) >= 16;
+        if (ut) ut[(((long long)e * K + k0 + r) * 2 * C + 2 * c0) / 2 + wd] = word(tl[r][ch], tl[r][ch + 1], lo);
+        if (un) un[(((long long)e * C + c0 + r) * 2 * K + 2 * k0) / 2 + wd] = word(tl[ch][r], tl[ch + 1][r], lo);
+    }
 }
 
 // Forward output transform without ReLU (BatchNorm follows): y = bias + 2^-ku A^T M A,
@@ -359,16 +371,21 @@ extern "C" int azg_absmax(const float* x, int64_t n, uint32_t* out, void* stream
 }
 
 extern "C" int azg_wt_u_build(const float* w, int32_t c, int32_t k, int32_t h_out, uint32_t* uamax, void* ut,
-                              void* un, void* stream) {
-    if (!w || !uamax || (!ut && !un) || c <= 0 || k <= 0 || c % 32 || k % 32 || h_out < 2 || h_out > 9 ||
+                              void* un, float* work, void* stream) {
+    if (!w || !uamax || !work || (!ut && !un) || c <= 0 || k <= 0 || c % 64 || k % 64 || h_out < 2 || h_out > 9 ||
         ((uintptr_t)ut & 3) || ((uintptr_t)un & 3))
         return AZG_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(uamax, 0, 4, st) != hipSuccess) return AZG_ERR_HIP;
-    const dim3 grid((unsigned)(((long long)c * k + 255) / 256));
-    hipLaunchKernelGGL(wt_u_absmax_kernel, grid, dim3(256), 0, st, w, c, k, h_out, uamax);
-    hipLaunchKernelGGL(wt_u_tile_kernel, dim3((unsigned)(c / 32), (unsigned)(k / 32)), dim3(1024), 0, st, w, c, k,
-                       h_out, uamax, (unsigned*)ut, (unsigned*)un);
+    const WSeq S(h_out);
+    int P = 0;  // transformed points: sum over the tile types of (ma + 2)(mb + 2)
+    for (int i = 0; i < S.p; ++i)
+        for (int j = 0; j < S.p; ++j)
+            if (S.idx(i) == 0 && S.idx(j) == 0) P += (S.m(i) + 2) * (S.m(j) + 2);
+    hipLaunchKernelGGL(wt_u_f32_kernel, dim3((unsigned)(((long long)c * k + 255) / 256)), dim3(256), 0, st, w, c, k,
+                       h_out, work, uamax);
+    hipLaunchKernelGGL(wt_u_split_tile_kernel, dim3((unsigned)(c / 64), (unsigned)(k / 64), (unsigned)P), dim3(256), 0,
+                       st, work, c, k, uamax, (unsigned*)ut, (unsigned*)un);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 

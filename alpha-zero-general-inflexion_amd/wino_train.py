@@ -94,7 +94,9 @@ class WinogradConv3x3(torch.autograd.Function):
         uamax = torch.empty(1, dtype=torch.int32, device=dev)
         ut = torch.empty(P * K * 2 * C, dtype=torch.float16, device=dev)
         un = torch.empty(P * C * 2 * K, dtype=torch.float16, device=dev)
-        _lib.check(L.azg_wt_u_build(_p(wc), C, K, Ho, _p(uamax), _p(ut), _p(un), st))
+        uf = torch.empty(P * K * C, dtype=torch.float32, device=dev)  # U in f32 between the build's two passes
+        _lib.check(L.azg_wt_u_build(_p(wc), C, K, Ho, _p(uamax), _p(ut), _p(un), _p(uf), st))
+        del uf
         M = torch.empty(rows * K, dtype=torch.float32, device=dev)
         _gemm(V, ut, M, runs, C, K, dev)
         y = torch.empty((B, K, Ho, Ho), dtype=torch.float32, device=dev, memory_format=torch.channels_last)

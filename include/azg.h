@@ -397,7 +397,8 @@ int  azg_examples(int32_t game_kind, int32_t n, int32_t max_turns, int32_t temp_
  *                         output (nnet._winograd_u's point order), scaled by 2^ku (max |U| 2^ku
  *                         in (512, 1024], *uamax = bits of max |U|), split into AZG_WINO_SPLIT2
  *                         rows: ut [P][k][2c] (the forward GEMM's B operand) and/or un
- *                         [P][c][2k] (the input-gradient GEMM's).
+ *                         [P][c][2k] (the input-gradient GEMM's); c % 64 == k % 64 == 0; work:
+ *                         P k c floats (U in f32 between the two passes).
  *   azg_wt_out          : y NHWC = bias + 2^-ku A^T M A (no ReLU), h_out in {3, 5, 7}.
  *   azg_wt_dout         : dM [P][T][2k] AZG_WINO_SPLIT2 = 2^kd A dy A^T (dy NHWC; 2^kd puts
  *                         max |dy| in (16, 32]); |dM| > 65504 sets *overflow.
@@ -408,7 +409,7 @@ int  azg_examples(int32_t game_kind, int32_t n, int32_t max_turns, int32_t temp_
 int  azg_absmax(const float* x, int64_t n, uint32_t* out, void* stream);
 /* The trainer's BatchNorm2d + ReLU on channels-last activations x [rows][C] (rows = batch x H x W;
  * C % 4 == 0, C <= 1024), training mode (azg_train_bn.hip): azg_bn_relu_fwd writes y = relu(bn(x))
- * with the batch's statistics, sv [4C] = (scale, shift, mean, invstd), and updates run_mean /
+ * with the batch's statistics, sv [4C] = (scale, beta, mean, invstd), and updates run_mean /
  * run_var (momentum; unbiased variance; either may be null); azg_bn_relu_bwd writes dx, dgamma,
  * dbeta from dy (the gradient of y), x and sv.  Sums in f64 over 512 fixed row ranges, reduced in
  * order (deterministic); work >= 1024 C doubles, co >= 2C floats (scratch). */
@@ -418,7 +419,7 @@ int  azg_bn_relu_fwd(const float* x, int64_t rows, int32_t C, const float* gamma
 int  azg_bn_relu_bwd(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv, float* dx,
                      float* dgamma, float* dbeta, float* co, double* work, void* stream);
 int  azg_wt_u_build(const float* w, int32_t c, int32_t k, int32_t h_out, uint32_t* uamax, void* ut, void* un,
-                    void* stream);
+                    float* work, void* stream);
 int  azg_wt_out(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,
                 const uint32_t* uamax, void* stream);
 int  azg_wt_dout(const float* dy, void* dM, int32_t batch, int32_t h_out, int32_t k, const uint32_t* dyamax,

@@ -64,7 +64,7 @@ for task in "$@"; do
         kk=()
         [ -n "$k" ] && kk=(-k "$k")
         rc=0
-        timeout -k 10 1100 python -u -m pytest "$path" -m gpu -x -v -s --timeout 300 --timeout-method thread \
+        timeout -k 10 1100 python -u -m pytest "$path" -m gpu -v -s --timeout 170 --timeout-method thread \
             --durations 10 "${kk[@]}" > "$log" 2>&1 || rc=$?
         # exit 1 = assertion failures only: the run goes on to its other tasks unless the log shows
         # a device error; any other status (abort, fault, time limit) ends the run here
