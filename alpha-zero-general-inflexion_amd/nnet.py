@@ -1068,9 +1068,13 @@ class NNetWrapper:
         return self.nnet(x)
 
     def _adam(self):
+        """torch.optim.Adam() as NNet.py:37 builds it; on the GPU in its capturable form (step count
+        and bias corrections on the device), the form _train_graph replays, so the eager and the
+        graph-replayed trainer take the same update (the CPU keeps the reference's exact Adam)."""
+        kw = {"capturable": True} if self.device.type == "cuda" else {}
         if self.args["fused_adam"]:
-            return torch.optim.Adam(self.nnet.parameters(), fused=True)
-        return torch.optim.Adam(self.nnet.parameters())
+            kw["fused"] = True
+        return torch.optim.Adam(self.nnet.parameters(), **kw)
 
     def _autocast(self, cache=True):
         dt = self.args["train_dtype"]
@@ -1208,16 +1212,12 @@ class NNetWrapper:
         stream; the first _GRAPH_EAGER_STEPS steps run eagerly on a side stream (real
         steps, which also warm up every kernel's one-time queries and the allocator), then
         one step is captured and replayed, each replay reading the batch's indices from a
-        static buffer.  Adam is torch's capturable form (its step count and bias
-        corrections on the device: the same update up to rounding); dropout draws from
-        torch's graph-safe philox offsets."""
+        static buffer.  Adam is torch's capturable form, as in the eager GPU loop (_adam);
+        dropout draws from torch's graph-safe philox offsets."""
         bs = self.args["batch_size"]
         dev = self.device
         E = planes.shape[0]
-        kw = dict(capturable=True)
-        if self.args["fused_adam"]:
-            kw["fused"] = True
-        opt = torch.optim.Adam(self.nnet.parameters(), **kw)
+        opt = self._adam()
         ids_buf = torch.zeros(bs, dtype=torch.int64, device=dev)
         loss_buf = torch.zeros(2, dtype=torch.float32, device=dev)
 
