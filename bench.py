@@ -455,13 +455,13 @@ def main():
     net = InflexionNNet(n=args.n, depth=depth, action_size=A).cuda().eval()
     if args.fc_kparts:
         import azg_amd.nnet as nn_mod
-        nn_mod.FC2_KPARTS, nn_mod.FC34_KPARTS = (int(x) for x in args.fc_kparts.split(","))
+        nn_mod.FC2_KPARTS, nn_mod.FC34_KPARTS = (int(x) for x in args.fc_kparts.replace("+", ",").split(","))
     if args.fc1_split_min is not None:
         import azg_amd.nnet as nn_mod
         nn_mod.FC1_SPLIT_MIN_BATCH = args.fc1_split_min
     if args.fc_small_kparts:
         import azg_amd.nnet as nn_mod
-        nn_mod.FC1T_KPARTS, nn_mod.FCS_KPARTS2, nn_mod.FCS_KPARTS3 = (int(x) for x in args.fc_small_kparts.split(","))
+        nn_mod.FC1T_KPARTS, nn_mod.FCS_KPARTS2, nn_mod.FCS_KPARTS3 = (int(x) for x in args.fc_small_kparts.replace("+", ",").split(","))
     ev = ((InferenceNet(net, conv=args.conv, gemm=args.gemm) if args.net == "inference" else net)
           if args.evaluator == "net" else "stub")
     if args.fc_tail == "blas" and hasattr(ev, "fc_tail_azg"):
