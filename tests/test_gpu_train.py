@@ -136,10 +136,12 @@ def test_graph_trainer_matches_eager():
     """train_examples' captured-graph form (NNetWrapper._train_graph: the step after the first
     _GRAPH_EAGER_STEPS replayed as one HIP graph) against the eager loop on the same examples and
     batch draws, dropout 0, 512 channels (conv2-4 on the Winograd training kernels, bn1-4 on the
-    NHWC kernels in both; Adam in its capturable form in both, NNetWrapper._adam): the same
-    kernels on the same inputs, so the losses of all 8 steps and the trained weights agree to
-    1e-6 (a replay is not required to be bitwise: no kernel relies on it); numpy's stream ends at
-    the same position."""
+    NHWC kernels in both; Adam in its capturable form in both, NNetWrapper._adam), MIOpen in its
+    deterministic mode.  Two eager runs give the run-to-run spread of the GPU trainer (a library
+    kernel that does not sum in a fixed order shows there; Adam's normalised first steps amplify
+    one ulp to percents within 8 steps); the graph run must agree with the first eager run within
+    4x that spread (1e-6 when the eager runs agree), losses and trained weights; numpy's stream
+    ends at the same position."""
     import azg_amd  # noqa: F401
     from azg_amd.examples import ExampleSet
     from azg_amd.inflexion import InflexionGame
@@ -150,23 +152,33 @@ def test_graph_trainer_matches_eager():
     planes = (torch.rand((E, 4, 7, 7), generator=gen) < 0.3).float()
     pis = torch.softmax(torch.randn((E, 343), generator=gen), 1)
     vs = torch.randint(0, 2, (E,), generator=gen).float() * 2 - 1
-    out = {}
-    for graph in (False, True):
-        torch.manual_seed(0)
-        w = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0, train_graph=graph), device="cuda")
-        np.random.seed(5)
-        st = {}
-        losses = w.train_examples(ExampleSet(planes.cuda(), pis.cuda(), vs.cuda()), stats=st)
-        out[graph] = (losses.cpu().numpy(), np.random.get_state()[2],
-                      {k: v.detach().cpu() for k, v in w.nnet.state_dict().items()}, st)
-    assert out[True][3].get("graph") and not out[False][3].get("graph")
-    assert out[True][1] == out[False][1]
-    le, lg = out[False][0], out[True][0]
-    np.testing.assert_allclose(lg, le, rtol=1e-6)
-    for k in ("conv1.weight", "conv2.weight", "conv4.weight", "fc1.weight", "fc3.weight"):
-        a, b = out[False][2][k], out[True][2][k]
-        d0 = ((a - b).norm() / a.norm()).item()
-        assert d0 <= 1e-6, (k, d0)
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    out = []
+    try:
+        for graph in (False, False, True):
+            torch.manual_seed(0)
+            w = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0, train_graph=graph), device="cuda")
+            np.random.seed(5)
+            st = {}
+            losses = w.train_examples(ExampleSet(planes.cuda(), pis.cuda(), vs.cuda()), stats=st)
+            out.append((losses.cpu().numpy().astype(np.float64), np.random.get_state()[2],
+                        {k: v.detach().cpu().double() for k, v in w.nnet.state_dict().items()}, st))
+    finally:
+        torch.backends.cudnn.deterministic = det
+    (la, pa, wa, sa), (lb, pb, wb, sb), (lg, pg, wg, sg) = out
+    assert sg.get("graph") and not sa.get("graph") and pa == pb == pg
+    keys = ("conv1.weight", "conv2.weight", "conv4.weight", "fc1.weight", "fc3.weight")
+
+    def wdiff(x, y):
+        return max(((x[k] - y[k]).norm() / x[k].norm()).item() for k in keys)
+    spread_l = float(np.max(np.abs(lb - la) / np.abs(la)))
+    spread_w = wdiff(wa, wb)
+    gl = float(np.max(np.abs(lg - la) / np.abs(la)))
+    gw = wdiff(wa, wg)
+    print(f"eager-eager spread: losses {spread_l:.3g}, weights {spread_w:.3g}; graph-eager: {gl:.3g}, {gw:.3g}")
+    assert gl <= max(4 * spread_l, 1e-6), (gl, spread_l)
+    assert gw <= max(4 * spread_w, 1e-6), (gw, spread_w)
 
 
 def test_out_of_range_training_replays_on_library():
