@@ -59,6 +59,11 @@ FC34_KPARTS = 2
 FC1T_KPARTS = 18
 FCS_KPARTS2 = 16
 FCS_KPARTS3 = 8
+# ... opt-in (InferenceNet.fc_tail_small = True): at C2 it measured 1.02-1.06M exp/s over K-part choices
+# (18/16/8, 18/8/4, 18/16/4, 24/8/4, 12/8/4, 18/8/2, 18/4/2) against 1.10M for the f32 hipBLASLt tail
+# on the same box (profiles/r05_bench_C2_*.json): its three split GEMMs alone take 49 us per 256-leaf
+# forward, the library's three GEMMs 41 us -- the split GEMM's tiles are built for thousands of rows
+FC_SMALL_TAIL = False
 
 
 class InflexionNNet(nn.Module):
@@ -405,9 +410,10 @@ class InferenceNet(nn.Module):
             self.register_buffer("fw34_sk", self._split_k_weights(w34, FC34_KPARTS, self.fc34_scale))
             # the small-batch tail (FC1T_KPARTS, FCS_KPARTS2 / 3; _fc_split_small)
             w1w = w1.shape[1]
-            self.fc_tail_small = (w1w % (64 * FC1T_KPARTS) == 0 and w1.shape[0] % 64 == 0
-                                  and w2.shape[1] % (64 * FCS_KPARTS2) == 0 and n2 % (64 * FCS_KPARTS3) == 0)
-            if self.fc_tail_small:
+            small_ok = (w1w % (64 * FC1T_KPARTS) == 0 and w1.shape[0] % 64 == 0
+                        and w2.shape[1] % (64 * FCS_KPARTS2) == 0 and n2 % (64 * FCS_KPARTS3) == 0)
+            self.fc_tail_small = small_ok and FC_SMALL_TAIL
+            if small_ok:
                 self.register_buffer("fw1_skT", self._split_k_weights(w1, FC1T_KPARTS, self.fc1_scale))
                 self.register_buffer("fw2_skS", self._split_k_weights(w2, FCS_KPARTS2, self.fc2_scale))
                 self.register_buffer("fw34_skS", self._split_k_weights(w34, FCS_KPARTS3, self.fc34_scale))

@@ -186,9 +186,9 @@ def test_out_of_range_training_replays_on_library():
     training convolutions flag it, and train_examples undoes the call (weights, BatchNorm
     buffers, numpy's and torch's streams) and runs it again on the library convolutions, so
     the result is the library trainer's from the same start: the same batches, the first forward
-    within 1e-6, then within the GPU trainer's 2e-3 (MIOpen picks its algorithms on a process's
-    first call and its weight-gradient kernels do not sum in a fixed order from one run to the
-    next: measured 1 ulp at the first step, 1.2e-3 relative by the fifth)."""
+    within 1e-6, then within the GPU trainer's 2e-3 (with MIOpen in its deterministic mode; its
+    default weight-gradient kernels do not sum in a fixed order from one run to the next, 3.8e-3
+    relative by the fifth step)."""
     import azg_amd  # noqa: F401
     from azg_amd.examples import ExampleSet
     from azg_amd.inflexion import InflexionGame
@@ -200,15 +200,20 @@ def test_out_of_range_training_replays_on_library():
                     torch.softmax(torch.randn((E, 343), generator=gen), 1).cuda(),
                     (torch.randint(0, 2, (E,), generator=gen).float() * 2 - 1).cuda())
     out = {}
-    for conv in ("winograd", "library"):
-        torch.manual_seed(0)
-        w = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0, train_conv=conv), device="cuda")
-        with torch.no_grad():
-            w.nnet.bn1.weight.fill_(1e6)
-        np.random.seed(9)
-        st = {}
-        losses = w.train_examples(ex, stats=st).cpu().numpy()
-        out[conv] = (losses, np.random.get_state()[2], w.nnet.state_dict()["fc3.weight"].cpu(), st)
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True  # MIOpen's deterministic solvers (no run-to-run spread)
+    try:
+        for conv in ("winograd", "library"):
+            torch.manual_seed(0)
+            w = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0, train_conv=conv), device="cuda")
+            with torch.no_grad():
+                w.nnet.bn1.weight.fill_(1e6)
+            np.random.seed(9)
+            st = {}
+            losses = w.train_examples(ex, stats=st).cpu().numpy()
+            out[conv] = (losses, np.random.get_state()[2], w.nnet.state_dict()["fc3.weight"].cpu(), st)
+    finally:
+        torch.backends.cudnn.deterministic = det
     assert out["winograd"][3].get("replayed_library") and not out["library"][3].get("replayed_library")
     assert out["winograd"][1] == out["library"][1]
     np.testing.assert_allclose(out["winograd"][0][:1], out["library"][0][:1], rtol=1e-6)
