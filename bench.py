@@ -120,6 +120,8 @@ def load_pmc(G, game, impl, gemm="split"):
     if per_fwd("split_gemm"):
         # per forward over the calls' launches (one per call)
         out["split_gemm_per_forward"] = per_fwd("split_gemm")
+    # every kernel of a simulation step (network forward, tree, move end amortised): the games/s roofline
+    out["step_total"] = sum(per_fwd(k) for k in d if not k.startswith("_"))
     return out
 
 
@@ -825,6 +827,19 @@ def main():
                 if k in out:
                     out[k]["traffic_note"] = pmc["note"]
             out["roofline_tree"]["traffic"] = pmc["tree"]
+            # north_star's "games/s as a fraction of HBM roofline": the games/s the step's measured HBM
+            # bytes would allow at the 8 TB/s peak (bytes per leaf x expansions per game), against games_per_s
+            if out.get("games_per_s") and args.game == "inflexion":
+                per_game = pmc["step_total"] / G * EXPANSIONS_PER_GAME_REF
+                peak_gps = HBM_PEAK_GBS * 1e9 / per_game * world
+                out["games_roofline"] = {
+                    "bound": "hbm", "achieved": out["games_per_s"], "peak": peak_gps, "unit": "games/s",
+                    "frac": out["games_per_s"] / peak_gps, "bytes_per_game": per_game,
+                    "note": f"PMC HBM bytes of every kernel per simulation step ({pmc['step_total'] / 1e9:.2f} GB at "
+                            f"{G} leaves, {os.path.relpath(PMC_FILE_WINOGRAD['split'], ROOT)}) / {G} leaves x "
+                            f"{EXPANSIONS_PER_GAME_REF} expansions per game, at {HBM_PEAK_GBS / 1e3:.0f} TB/s x "
+                            f"{world} GPU(s); the step is MFMA-bound (roofline), so this is a traffic ceiling, not "
+                            "the step's bound"}
         if split and getattr(ev, "gemm", "") == "split" and os.path.exists(GEMM_PMC_FILE):
             d = json.load(open(GEMM_PMC_FILE))
             out["roofline"]["mfma_busy_frac"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * d["GRBM_GUI_ACTIVE"] / 8)

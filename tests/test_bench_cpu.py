@@ -32,6 +32,18 @@ def test_tree_bytes_per_expansion():
     assert 4700 < b < 4800
 
 
+def test_committed_pmc_traffic():
+    """The committed round-5 PMC pass the bench line's `traffic` fields and games/s HBM roofline read:
+    the split GEMM near its algorithmic ~0.91 GB per launch (4 launches per forward), a whole
+    simulation step at 4096 leaves between the GEMMs + transforms and 10 GB."""
+    pmc = bench.load_pmc(4096, "inflexion", "winograd")
+    assert pmc is not None
+    assert 3.4e9 < pmc["split_gemm_per_forward"] < 4.2e9
+    assert 3.0e9 < pmc["transforms"] < 3.8e9
+    assert pmc["split_gemm_per_forward"] + pmc["transforms"] < pmc["step_total"] < 10e9
+    assert bench.load_pmc(256, "inflexion", "winograd") is None  # measured at G = 4096 only
+
+
 def test_presets_are_the_baseline_configs():
     assert bench.PRESETS["C4"] == dict(game="inflexion", n=7, games=4096, sims=25)
     assert bench.PRESETS["C2"]["games"] == 256 and bench.PRESETS["C3"]["sims"] == 100
