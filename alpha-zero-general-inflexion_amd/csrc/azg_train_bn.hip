@@ -16,7 +16,7 @@
 //             apply  : dx = scale (g - sum g / n - xhat sum(g xhat) / n); dgamma = sum g xhat,
 //                      dbeta = sum g
 //
-// Deterministic (fixed partial order).  Tolerance-equal to torch's f32 BatchNorm (the sums are
+// Deterministic (fixed partial and butterfly order).  Tolerance-equal to torch's f32 BatchNorm (the sums are
 // f64 here); the trainer's tests bound the whole step against the reference trainer.
 #include <hip/hip_runtime.h>
 
@@ -76,20 +76,35 @@ __global__ __launch_bounds__(BN_T) void bn_stats_kernel(const float4* __restrict
     block_sum_store(a, C4, part);
 }
 
-// per channel: the parts in order -> mean, var, scale (f32), running stats; one thread per channel
+// the nparts partial (sum, second sum) pairs of channel c: one 64-lane wave per channel, lane l summing
+// parts l, l + 64, ... in order, then a fixed butterfly (deterministic); every lane returns the totals.
+// (One thread per channel summing the 512 parts serially took 36 us per call: a dependent f64 chain.)
+__device__ __forceinline__ void channel_sums(const double* __restrict__ part, int nparts, int C, int c, double& s,
+                                             double& s2) {
+    const int lane = threadIdx.x & 63;
+    s = 0, s2 = 0;
+    for (int p = lane; p < nparts; p += 64) {
+        s += part[(long long)p * 2 * C + c];
+        s2 += part[(long long)p * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o);
+        s2 += __shfl_xor(s2, o);
+    }
+}
+
+// per channel: the parts -> mean, var, scale (f32), running stats; one wave per channel
 __global__ __launch_bounds__(BN_T) void bn_stats_final_kernel(const double* __restrict__ part, int nparts, int C,
                                                               long long n, const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float eps,
                                                               float momentum, float* __restrict__ run_mean,
                                                               float* __restrict__ run_var, float* __restrict__ sv) {
-    const int c = blockIdx.x * BN_T + threadIdx.x;
-    if (c >= C) return;
-    double s = 0, s2 = 0;
-#pragma unroll 8
-    for (int p = 0; p < nparts; ++p) {
-        s += part[(long long)p * 2 * C + c];
-        s2 += part[(long long)p * 2 * C + C + c];
-    }
+    const int c = blockIdx.x * (BN_T / 64) + (int)(threadIdx.x >> 6);
+    if (c >= C) return;  // wave-uniform
+    double s, s2;
+    channel_sums(part, nparts, C, c, s, s2);
+    if ((threadIdx.x & 63) != 0) return;
     const double mean = s / (double)n;
     double var = s2 / (double)n - mean * mean;
     if (var < 0) var = 0;
@@ -157,14 +172,11 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const float4* __res
 __global__ __launch_bounds__(BN_T) void bn_bwd_final_kernel(const double* __restrict__ part, int nparts, int C,
                                                             long long n, float* __restrict__ dgamma,
                                                             float* __restrict__ dbeta, float* __restrict__ co) {
-    const int c = blockIdx.x * BN_T + threadIdx.x;
-    if (c >= C) return;
-    double s = 0, s2 = 0;
-#pragma unroll 8
-    for (int p = 0; p < nparts; ++p) {
-        s += part[(long long)p * 2 * C + c];
-        s2 += part[(long long)p * 2 * C + C + c];
-    }
+    const int c = blockIdx.x * (BN_T / 64) + (int)(threadIdx.x >> 6);
+    if (c >= C) return;  // wave-uniform
+    double s, s2;
+    channel_sums(part, nparts, C, c, s, s2);
+    if ((threadIdx.x & 63) != 0) return;
     dbeta[c] = (float)s;
     dgamma[c] = (float)s2;
     co[c] = (float)(s / (double)n);
@@ -209,7 +221,7 @@ extern "C" int azg_bn_relu_fwd(const float* x, int64_t rows, int32_t C, const fl
     hipStream_t st = (hipStream_t)stream;
     const int C4 = C / 4;
     hipLaunchKernelGGL(bn_stats_kernel, dim3(BN_PARTS), dim3(BN_T), 0, st, (const float4*)x, (long long)rows, C4, work);
-    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((C + BN_T - 1) / BN_T), dim3(BN_T), 0, st, work, BN_PARTS, C,
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((C + BN_T / 64 - 1) / (BN_T / 64)), dim3(BN_T), 0, st, work, BN_PARTS, C,
                        (long long)rows, gamma, beta, eps, momentum, run_mean, run_var, sv);
     const long long n4 = rows * C4;
     hipLaunchKernelGGL(bn_apply_relu_kernel, dim3(stream_grid(n4)), dim3(BN_T), 0, st, (const float4*)x,
@@ -229,7 +241,7 @@ extern "C" int azg_bn_relu_bwd(const float* x, const float* dy, int64_t rows, in
     const int C4 = C / 4;
     hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(BN_PARTS), dim3(BN_T), 0, st, (const float4*)x, (const float4*)dy,
                        (const float4*)sv, (long long)rows, C4, work);
-    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + BN_T - 1) / BN_T), dim3(BN_T), 0, st, work, BN_PARTS, C,
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + BN_T / 64 - 1) / (BN_T / 64)), dim3(BN_T), 0, st, work, BN_PARTS, C,
                        (long long)rows, dgamma, dbeta, co);
     const long long n4 = rows * C4;
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(n4)), dim3(BN_T), 0, st, (const float4*)x,
