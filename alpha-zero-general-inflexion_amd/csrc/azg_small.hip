@@ -668,87 +668,88 @@ __global__ __launch_bounds__(SC_T) void small_net_kernel(SmallNetArgs a) {
                                            nrow, bias, relu, y, ldy, hb, P, V, ticket);
     };
 
+    // One loop per layer, in layer order (the queue's order): a block runs the items it takes while
+    // they belong to layer L, and carries the first item past it to the next layer's loop.  The layers'
+    // code sits in separate loops, so their hoisted invariants are live in their own loop only (one
+    // loop with a switch over the six bodies spilled 464 B per thread).
     if (tid == 0) s_next = (int)__hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    int known = 0;  // layers [0, known) are complete as far as this block has seen
-    for (;;) {
-        const int item = s_next;
-        __syncthreads();  // every thread has read s_next before it is overwritten below
-        if (item >= e5) break;
-        unsigned nxt = 0;  // the next item, fetched while this one runs (thread 0)
-        if (tid == 0) nxt = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int L = item < e0 ? 0 : item < e1 ? 1 : item < e2 ? 2 : item < e3 ? 3 : item < e4 ? 4 : 5;
-        const int lo = L == 0 ? 0 : L == 1 ? e0 : L == 2 ? e1 : L == 3 ? e2 : L == 4 ? e3 : e4;
-        const int i = item - lo;
-        if (known < L) {  // layer L-1 done (and so every layer before it: its items waited in turn)
-            if (tid == 0) {
-                // layer L-1's item count
-                const unsigned target = (unsigned)(lo - (L == 1 ? 0 : L == 2 ? e0 : L == 3 ? e1 : L == 4 ? e2 : e3));
-                // polls back off (64 .. 512 clocks apart): up to 256 blocks poll one counter, and the
-                // blocks still working on layer L-1 increment it through the same memory channel
-                for (unsigned spins = 0;
-                     __hip_atomic_load(q + 2 + (L - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
-                    if (spins < 4) __builtin_amdgcn_s_sleep(1);
-                    else if (spins < 16) __builtin_amdgcn_s_sleep(4);
-                    else __builtin_amdgcn_s_sleep(8);
-                    if (++spins > (1u << 22)) {  // an item never finished: report instead of hanging the GPU
-                        atomicOr(a.err, 1);
-                        break;
-                    }
+    int item = s_next;
+    // wait until layer L-1's `target` items are done (and so every layer before it: its items waited in turn)
+    auto wait_layer = [&](int L, int target) {
+        if (tid == 0) {
+            // polls back off (64 .. 512 clocks apart): up to 256 blocks poll one counter, and the blocks
+            // still working on layer L-1 increment it through the same memory channel
+            for (unsigned spins = 0;
+                 __hip_atomic_load(q + 2 + (L - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)target;) {
+                if (spins < 4) __builtin_amdgcn_s_sleep(1);
+                else if (spins < 16) __builtin_amdgcn_s_sleep(4);
+                else __builtin_amdgcn_s_sleep(8);
+                if (++spins > (1u << 22)) {  // an item never finished: report instead of hanging the GPU
+                    atomicOr(a.err, 1);
+                    break;
                 }
             }
+        }
+        __syncthreads();
+    };
+    // run the items of layer L in [lo, hi): body(i) per item, each counted done after its stores landed
+    auto layer = [&](int L, int lo, int hi, auto&& body) {
+        if (item >= hi) return;
+        if (L > 0) wait_layer(L, lo - (L == 1 ? 0 : L == 2 ? e0 : L == 3 ? e1 : L == 4 ? e2 : e3));
+        while (item < hi) {
+            unsigned nxt = 0;  // the next item, fetched while this one runs (thread 0)
+            if (tid == 0) nxt = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            body(item - lo);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this item's write-through stores have landed
             __syncthreads();
-            known = L;
+            if (tid == 0) {
+                if (L < 5) __hip_atomic_fetch_add(q + 2 + L, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_next = (int)nxt;
+            }
+            __syncthreads();
+            item = s_next;
+            __syncthreads();  // every thread has read s_next before thread 0 writes it again
         }
-        switch (L) {
-            case 0:
-                small_conv_sk_body<P12, NB, SK_KG1, true>(i, nsk, pool, s_last, a.planes, (long long)a.D * NB * NB, 0,
-                                                          0, B, NB, 1, a.w2, C, a.b2, 1, a.y2, C, a.part, a.tickets,
-                                                          a.w1, a.b1, a.D);
-                break;
-            case 1:
-                if constexpr (H3 * H3 > 16)  // conv3 as the per-layer path runs it: split-K in 8 K-parts ...
-                    small_conv_sk_body<P3, 0, SK_KG, true>(i, n3, pool, s_last, a.y2, (long long)NB * NB * C, NB * C,
-                                                           C, B, NB, 0, a.w3, C, a.b3, 1, a.y3, C, a.part, a.tickets,
-                                                           nullptr, nullptr, 0);
-                else  // ... or, for <= 16 output pixels (6x6 boards), in 2-channel blocks
-                    small_conv_body<P3, 2, true, WLDS3, true>(i, pool, a.y2, (long long)NB * NB * C, NB * C, C, 1, B,
-                                                              NB, 0, a.w3, C, C, a.b3, 1, a.y3, C);
-                break;
-            case 2:
-                small_conv_body<P4, 2, true, WLDS4, true>(i, pool, a.y3, (long long)H3 * H3 * C, H3 * C, C, 1, B, H3,
-                                                          0, a.w4, C, C, a.b4, 1, a.y4, C);
-                break;
-            case 3:
-                if (npb1 == 4) fc(std::integral_constant<int, 4>{}, std::false_type{}, 2 * i, a.N1, a.y4, K1, a.fw1, K1,
-                                  a.fb1, 1, a.h1, a.N1, nullptr, nullptr, nullptr, nullptr);
-                else if (npb1 == 2) fc(std::integral_constant<int, 2>{}, std::false_type{}, 2 * i, a.N1, a.y4, K1,
-                                       a.fw1, K1, a.fb1, 1, a.h1, a.N1, nullptr, nullptr, nullptr, nullptr);
-                else fc(std::integral_constant<int, 1>{}, std::false_type{}, 2 * i, a.N1, a.y4, K1, a.fw1, K1, a.fb1, 1,
-                        a.h1, a.N1, nullptr, nullptr, nullptr, nullptr);
-                break;
-            case 4:
-                if (npb2 == 4) fc(std::integral_constant<int, 4>{}, std::false_type{}, 2 * i, a.N2, a.h1, a.N1, a.fw2,
-                                  a.N1, a.fb2, 1, a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
-                else if (npb2 == 2) fc(std::integral_constant<int, 2>{}, std::false_type{}, 2 * i, a.N2, a.h1, a.N1,
-                                       a.fw2, a.N1, a.fb2, 1, a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
-                else fc(std::integral_constant<int, 1>{}, std::false_type{}, 2 * i, a.N2, a.h1, a.N1, a.fw2, a.N1,
-                        a.fb2, 1, a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
-                break;
-            default:
-                fc(std::integral_constant<int, 4>{}, std::true_type{}, 2 * i, a.A + 1, a.h2, a.N2, a.fw34, a.N2, nullptr,
-                   0, a.logits, a.A + 1, a.fb34, a.P, a.v, a.heads_ticket);
-                break;
-        }
-        // this item's write-through stores have landed (every wave), then it counts as done
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            if (L < 5) __hip_atomic_fetch_add(q + 2 + L, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_next = (int)nxt;
-        }
-        __syncthreads();
-    }
+    };
+    layer(0, 0, e0, [&](int i) {
+        small_conv_sk_body<P12, NB, SK_KG1, true>(i, nsk, pool, s_last, a.planes, (long long)a.D * NB * NB, 0, 0, B,
+                                                  NB, 1, a.w2, C, a.b2, 1, a.y2, C, a.part, a.tickets, a.w1, a.b1,
+                                                  a.D);
+    });
+    layer(1, e0, e1, [&](int i) {
+        if constexpr (H3 * H3 > 16)  // conv3 as the per-layer path runs it: split-K in 8 K-parts ...
+            small_conv_sk_body<P3, 0, SK_KG, true>(i, n3, pool, s_last, a.y2, (long long)NB * NB * C, NB * C, C, B,
+                                                   NB, 0, a.w3, C, a.b3, 1, a.y3, C, a.part, a.tickets, nullptr,
+                                                   nullptr, 0);
+        else  // ... or, for <= 16 output pixels (6x6 boards), in 2-channel blocks
+            small_conv_body<P3, 2, true, WLDS3, true>(i, pool, a.y2, (long long)NB * NB * C, NB * C, C, 1, B, NB, 0,
+                                                      a.w3, C, C, a.b3, 1, a.y3, C);
+    });
+    layer(2, e1, e2, [&](int i) {
+        small_conv_body<P4, 2, true, WLDS4, true>(i, pool, a.y3, (long long)H3 * H3 * C, H3 * C, C, 1, B, H3, 0, a.w4,
+                                                  C, C, a.b4, 1, a.y4, C);
+    });
+    layer(3, e2, e3, [&](int i) {
+        if (npb1 == 4) fc(std::integral_constant<int, 4>{}, std::false_type{}, 2 * i, a.N1, a.y4, K1, a.fw1, K1, a.fb1,
+                          1, a.h1, a.N1, nullptr, nullptr, nullptr, nullptr);
+        else if (npb1 == 2) fc(std::integral_constant<int, 2>{}, std::false_type{}, 2 * i, a.N1, a.y4, K1, a.fw1, K1,
+                               a.fb1, 1, a.h1, a.N1, nullptr, nullptr, nullptr, nullptr);
+        else fc(std::integral_constant<int, 1>{}, std::false_type{}, 2 * i, a.N1, a.y4, K1, a.fw1, K1, a.fb1, 1, a.h1,
+                a.N1, nullptr, nullptr, nullptr, nullptr);
+    });
+    layer(4, e3, e4, [&](int i) {
+        if (npb2 == 4) fc(std::integral_constant<int, 4>{}, std::false_type{}, 2 * i, a.N2, a.h1, a.N1, a.fw2, a.N1,
+                          a.fb2, 1, a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
+        else if (npb2 == 2) fc(std::integral_constant<int, 2>{}, std::false_type{}, 2 * i, a.N2, a.h1, a.N1, a.fw2,
+                               a.N1, a.fb2, 1, a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
+        else fc(std::integral_constant<int, 1>{}, std::false_type{}, 2 * i, a.N2, a.h1, a.N1, a.fw2, a.N1, a.fb2, 1,
+                a.h2, a.N2, nullptr, nullptr, nullptr, nullptr);
+    });
+    layer(5, e4, e5, [&](int i) {
+        fc(std::integral_constant<int, 4>{}, std::true_type{}, 2 * i, a.A + 1, a.h2, a.N2, a.fw34, a.N2, nullptr, 0,
+           a.logits, a.A + 1, a.fb34, a.P, a.v, a.heads_ticket);
+    });
     // the last block to leave resets the queue for the next launch (every block has taken its last item)
     if (tid == 0 &&
         __hip_atomic_fetch_add(q + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u)
