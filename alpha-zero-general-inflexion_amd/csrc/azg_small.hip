@@ -66,7 +66,10 @@ __host__ __device__ constexpr int sc_pitch(int cin) { return ((cin + 3) & ~3) + 
 // are read with device-scope (sc1) loads and written with agent-scope (write-through) stores -- the
 // split-K hand-off's rule (see above) applied to every layer boundary inside the launch.  The loads
 // are 128-bit buffer loads with the sc1 cache policy from a wave-uniform base (one instruction per
-// float4; relaxed agent-scope atomic loads are 32-bit, four instructions per float4)
+// float4; relaxed agent-scope atomic loads are 32-bit, four instructions per float4).  (Ordinary loads
+// after an agent-scope acquire fence instead -- buffer_inv sc1 per wave at each layer, dropping the
+// XCD's L2 weights with the stale lines -- measured 192 us per forward against these loads' 130 us,
+// profiles/r05_small_net_probe_*.json.)
 constexpr int BUF_SC1 = 16;  // cache-policy bit of sc1 in the buffer intrinsics' aux operand (gfx940+)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t coh_rsrc(const float* base) {

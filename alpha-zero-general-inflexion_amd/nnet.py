@@ -38,9 +38,10 @@ SMALL_PATH = True
 SMALL_MAX_B = 4
 # the small-batch forward as ONE launch (azg_small_net: the per-layer kernels' block bodies as items of
 # an in-order work queue, an item waiting for the previous layer's done count; bit-identical results),
-# else one launch per layer (the default: the one-launch form measured 134.5 us per one-leaf forward
-# against the per-layer kernels' 68.9 us in one HIP graph -- its six bodies in one function spill 464 B
-# of registers per thread, profiles/r05_small_net_probe.json -- opt in with small_fused / SMALL_FUSED)
+# else one launch per layer (the default: the one-launch form measured 130 us per one-leaf forward
+# against the per-layer kernels' 68.9 us in one HIP graph -- cross-XCD activation reads and per-item
+# queue atomics cost more than the five kernel boundaries they replace, DESIGN.md 4.1,
+# profiles/r05_small_net_probe_loops.json -- opt in with small_fused / SMALL_FUSED)
 SMALL_FUSED = False
 FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
 # NNetWrapper.train_examples on the GPU: steps run eagerly before the step is captured as a HIP graph
