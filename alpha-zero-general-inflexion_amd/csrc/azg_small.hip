@@ -119,8 +119,11 @@ __device__ __forceinline__ void small_conv_body(int bid, float* __restrict__ lds
     const int KS = K / STEP;
     const int per = (KS + KSL - 1) / KSL;
     const int k0 = s * per, k1 = min(KS, k0 + per);
-    // staging: every thread's loads are issued together (SC_UNR float4 in flight per thread,
-    // one memory round trip per SC_UNR x 8 KB), then stored to LDS
+    // staging: every thread's loads are issued together (UNR float4 in flight per thread, one memory
+    // round trip per UNR x 8 KB), then stored to LDS.  UNR: SC_UNR, or 8 for <= 16 output pixels
+    // (conv4: a 5 x 5 x 512 plane is 6.25 vectors per thread; 16 in flight held 256 VGPRs + 48 B of
+    // scratch, 8 fit)
+    constexpr int UNR = PXL <= 16 ? 8 : SC_UNR;
     const int nw4 = WLDS ? CO_PB * K / 4 : 0;  // the block's weights: CO_PB contiguous rows
     const float4* __restrict__ w4 = (const float4*)(w + (long long)co0 * K);
     int oy = 0, ox = 0;
@@ -140,9 +143,9 @@ __device__ __forceinline__ void small_conv_body(int bid, float* __restrict__ lds
 #pragma unroll
                     for (int u = 0; u < SC_UNRW; ++u) rw[u] = w4[min(tid + u * SC_T, nw4 - 1)];
                 }
-                float4 r[SC_UNR];
+                float4 r[UNR];
 #pragma unroll
-                for (int u = 0; u < SC_UNR; ++u) {  // past the end: a duplicate load, not stored
+                for (int u = 0; u < UNR; ++u) {  // past the end: a duplicate load, not stored
                     const int i = min(base + u * SC_T, nx4 - 1);
                     const int pix = i / c4, c = (i - pix * c4) * 4, iy = pix / H, ix = pix - iy * H;
                     r[u] = ld4<COH>(xb, (long long)iy * sY + (long long)ix * sX + c);
@@ -154,7 +157,7 @@ __device__ __forceinline__ void small_conv_body(int bid, float* __restrict__ lds
                     for (int i = tid + SC_UNRW * SC_T; i < nw4; i += SC_T) ((float4*)ws)[i] = w4[i];
                 }
 #pragma unroll
-                for (int u = 0; u < SC_UNR; ++u) {
+                for (int u = 0; u < UNR; ++u) {
                     const int i = base + u * SC_T;
                     if (i < nx4) {
                         const int pix = i / c4, c = (i - pix * c4) * 4;
@@ -164,7 +167,7 @@ __device__ __forceinline__ void small_conv_body(int bid, float* __restrict__ lds
             };
             if (WLDS && b == 0) batch(tid, std::true_type{});
             else batch(tid, std::false_type{});
-            for (int base = tid + SC_T * SC_UNR; base < nx4; base += SC_T * SC_UNR) batch(base, std::false_type{});
+            for (int base = tid + SC_T * UNR; base < nx4; base += SC_T * UNR) batch(base, std::false_type{});
         } else {
             if (b == 0)
                 for (int i = tid; i < nw4; i += SC_T) ((float4*)ws)[i] = w4[i];
