@@ -1242,13 +1242,29 @@ class NNetWrapper:
         cur = torch.cuda.current_stream(dev)
         side = torch.cuda.Stream(dev)
         graph = None
+        eager = False  # set when the capture failed: the remaining steps run eagerly
         k = 0
         self.nnet.train()
         try:
             for _ in range(self.args["epochs"]):
                 ids_all = torch.from_numpy(np.random.randint(E, size=(nb, bs))).to(dev) if nb else None
                 for j in range(nb):
-                    if graph is None and k < _GRAPH_EAGER_STEPS:
+                    if graph is None and not eager and k >= _GRAPH_EAGER_STEPS:
+                        # capture the step (nothing executes during a capture; a failed one leaves the
+                        # weights, the optimizer's device state and the RNG where they were)
+                        try:
+                            g = torch.cuda.CUDAGraph()
+                            opt.zero_grad(set_to_none=True)
+                            with torch.cuda.graph(g):
+                                step()
+                            graph = g
+                        except RuntimeError as err:
+                            import warnings
+                            warnings.warn(f"train_examples: the training step could not be captured as a HIP "
+                                          f"graph ({err}); the remaining steps run eagerly")
+                            eager = True
+                            torch.cuda.synchronize(dev)
+                    if graph is None:
                         side.wait_stream(cur)
                         with torch.cuda.stream(side):
                             ids_buf.copy_(ids_all[j])
@@ -1257,11 +1273,6 @@ class NNetWrapper:
                             losses[k].copy_(loss_buf)
                         cur.wait_stream(side)
                     else:
-                        if graph is None:
-                            graph = torch.cuda.CUDAGraph()
-                            opt.zero_grad(set_to_none=True)
-                            with torch.cuda.graph(graph):
-                                step()
                         ids_buf.copy_(ids_all[j])
                         graph.replay()
                         losses[k].copy_(loss_buf)

@@ -220,3 +220,50 @@ def test_out_of_range_training_replays_on_library():
     np.testing.assert_allclose(out["winograd"][0], out["library"][0], rtol=2e-3)
     a, b = out["winograd"][2], out["library"][2]
     assert ((a - b).norm() / a.norm()).item() < 1e-2
+
+
+def test_graph_capture_failure_runs_eagerly(monkeypatch):
+    """If the training step cannot be captured (a torch build or an op that refuses capture), the
+    steps from there on run eagerly with a warning: the same losses and weights as the eager loop
+    (MIOpen deterministic mode), numpy's stream at the same position."""
+    import azg_amd  # noqa: F401
+    from azg_amd.examples import ExampleSet
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.nnet import NNetWrapper
+
+    gen = torch.Generator().manual_seed(8)
+    E = 512 * 5
+    ex = ExampleSet((torch.rand((E, 4, 7, 7), generator=gen) < 0.3).float().cuda(),
+                    torch.softmax(torch.randn((E, 343), generator=gen), 1).cuda(),
+                    (torch.randint(0, 2, (E,), generator=gen).float() * 2 - 1).cuda())
+
+    class Refuse:
+        def __init__(self, *a, **k):
+            raise RuntimeError("capture refused (test)")
+
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    out = []
+    try:
+        for refuse in (False, True):
+            if refuse:
+                monkeypatch.setattr(torch.cuda, "graph", Refuse)
+            torch.manual_seed(0)
+            w = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0, train_graph=refuse), device="cuda")
+            np.random.seed(2)
+            with pytest.warns(UserWarning, match="could not be captured") if refuse else _nullcontext():
+                losses = w.train_examples(ex).cpu().numpy()
+            out.append((losses, np.random.get_state()[2], w.nnet.state_dict()["conv2.weight"].cpu()))
+    finally:
+        torch.backends.cudnn.deterministic = det
+    np.testing.assert_allclose(out[1][0], out[0][0], rtol=1e-6)
+    assert out[1][1] == out[0][1]
+    torch.testing.assert_close(out[1][2], out[0][2], rtol=1e-6, atol=1e-8)
+
+
+class _nullcontext:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
