@@ -51,7 +51,11 @@ def test_train_forward_matches_module():
     conv1.weight's gradient sits behind conv2's input gradient and BatchNorm 1's backward, which
     cancels it further (its inputs include the planes constant over each image): the Winograd
     input gradient's error (<= 2e-5 of its size, test_winograd_conv_forward_backward) comes out
-    at 2.8e-3 of max |grad| there, the library's (~1e-7) at 2e-6 -- bounded here at 5e-3."""
+    at 0.7-2.8e-3 of max |grad| there.  The library's own distance is not stable from run to run:
+    MIOpen picks a Winograd solver (miopenSp3AsmConv F(2,3)) for some calls, 3.4e-3 on conv2.weight,
+    and an implicit GEMM for others, 1.8e-6.  So the conv weights (conv1-4) are held to 5e-3 of max
+    |grad| or 5x the library's distance, whichever is larger (measured: <= 2.9e-3; a wrong BatchNorm
+    backward put conv3.weight at 4.5e-2, round 5); every other gradient to 5x the library's + 1e-5."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InflexionNNet
     from azg_amd.wino_train import train_forward
@@ -81,7 +85,9 @@ def test_train_forward_matches_module():
         ew = (gw[k] - g64[k]).abs().max().item() / scale
         el = (gl[k] - g64[k]).abs().max().item() / scale
         print(f"{k}: winograd {ew:.3g}, library {el:.3g} of max |grad|")
-        assert ew <= 5 * el + (5e-3 if k == "conv1.weight" else 1e-5), (k, ew, el)
+        # conv weights behind a training-mode BatchNorm: at most 5e-3 of max |grad| (or 5x the library's)
+        conv_w = k in ("conv1.weight", "conv2.weight", "conv3.weight", "conv4.weight")
+        assert ew <= max(5 * el + 1e-5, 5e-3 if conv_w else 0.0), (k, ew, el)
 
 
 @pytest.mark.parametrize("B,H", [(512, 7), (512, 5), (64, 3), (2, 7)])
