@@ -1091,7 +1091,11 @@ class NNetWrapper:
 
     def train(self, examples):
         """Reference training loop (NNet.py:36-76): Adam, 10 epochs of batches
-        sampled with replacement from numpy's global RNG."""
+        sampled with replacement from numpy's global RNG (examples as the reference's list of
+        (planes, pi, v)); on the GPU with train_examples' out-of-range rule (_overflow_replay)."""
+        return self._overflow_replay(lambda: self._train_list(examples))
+
+    def _train_list(self, examples):
         opt = self._adam()
         bs = self.args["batch_size"]
         for _ in range(self.args["epochs"]):
@@ -1141,6 +1145,19 @@ class NNetWrapper:
                 return train_examples_dp(self, ex, group, stats=stats)
             return self._train_single(ex, stats)
 
+        losses = self._overflow_replay(run, group if dp is not None else None)
+        if stats is not None and self.last_replayed_library:
+            stats["replayed_library"] = True
+        return losses
+
+    def _overflow_replay(self, run, group=None):
+        """run() (a training call); if the Winograd training convolutions met an operand fp16
+        cannot hold, undo it -- weights, BatchNorm buffers, numpy's and torch's streams -- and
+        run it again on the library convolutions (every rank of `group` when one saw it)."""
+        self.last_replayed_library = False
+        dp = None
+        if group is not None:
+            import torch.distributed as dp
         wino = (self.device.type == "cuda" and self.args.get("train_conv", "winograd") == "winograd"
                 and self.args["train_dtype"] == "f32")
         if not wino:
@@ -1168,8 +1185,7 @@ class NNetWrapper:
                 losses = run()
             finally:
                 self.args["train_conv"] = conv
-            if stats is not None:
-                stats["replayed_library"] = True
+            self.last_replayed_library = True
         return losses
 
     def _train_single(self, ex, stats):

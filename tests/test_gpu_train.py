@@ -267,3 +267,28 @@ class _nullcontext:
 
     def __exit__(self, *a):
         return False
+
+
+def test_out_of_range_train_list_replays():
+    """NNetWrapper.train (the reference's list-of-examples entry, NNet.py:36-76) follows the same rule:
+    an out-of-range Winograd operand undoes the call and reruns it on the library convolutions."""
+    import azg_amd  # noqa: F401
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.nnet import NNetWrapper
+
+    rs = np.random.RandomState(5)
+    ex = [((rs.rand(4, 7, 7) < 0.3).astype(np.int64), list(np.full(343, 1 / 343)), float(rs.choice([-1, 1])))
+          for _ in range(1024)]
+    torch.manual_seed(0)
+    w = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0), device="cuda")
+    with torch.no_grad():
+        w.nnet.bn1.weight.fill_(1e6)
+    np.random.seed(1)
+    w.train(ex)
+    assert w.last_replayed_library
+    assert all(torch.isfinite(p).all() for p in w.nnet.parameters())
+    torch.manual_seed(0)
+    w2 = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0), device="cuda")
+    np.random.seed(1)
+    w2.train(ex)
+    assert not w2.last_replayed_library
