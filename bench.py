@@ -170,6 +170,9 @@ def parse():
                         "learn_iteration (self-play / exchange / train seconds, collective bytes and time per step). "
                         "auto: whenever the generation pass runs")
     p.add_argument("--train-epochs", type=int, default=10, help="--learn-iteration: epochs (NNet.py:19: 10)")
+    p.add_argument("--rank0-train", type=int, default=1,
+                   help="--learn-iteration with several ranks: also time the training on rank 0 alone + a weight "
+                        "broadcast (train_rank0_s; 0 = skip)")
     p.add_argument("--train-window", type=int, default=200000,
                    help="--learn-iteration: examples kept from the iteration (main.py:19 maxlenOfQueue)")
     p.add_argument("--timer-every", type=int, default=25,
@@ -393,6 +396,22 @@ def learn_iteration(args, eng, net, rank, world, gen):
             out["grad_allreduce_ms_per_step"] = stats["grad_allreduce_ms"] / stats["grad_allreduce_timed"]
             out["grad_allreduce_note"] = ("HIP events on the compute stream around the gradient all-reduce, every "
                                           f"{stats['every']}th step, rank {rank}")
+    if world > 1 and args.rank0_train:
+        # north_star's arrangement for comparison: the same training on rank 0 alone (the one-GPU
+        # trainer: Winograd convolutions, NHWC BatchNorm, graph-replayed steps), then its weights
+        # broadcast to every rank -- one collective of the state_dict instead of one all-reduce per step
+        w0 = NNetWrapper(game, {"epochs": args.train_epochs}, device=dev)
+        w0.nnet.load_state_dict(net.state_dict())
+        np.random.seed(0)
+        t0 = time.perf_counter()
+        if rank == 0:
+            w0.train_examples(ex)
+        flat = torch.cat([t.detach().reshape(-1).float() for t in w0.nnet.state_dict().values()])
+        dist.broadcast(flat, src=0)
+        out["train_rank0_s"] = wall(t0)
+        out["rank0_broadcast_bytes"] = flat.numel() * 4
+        out["train_rank0_note"] = ("the iteration's training on rank 0 alone + one broadcast of its weights "
+                                   "(north_star: examples gathered, weights broadcast), same examples and draws")
     return out
 
 

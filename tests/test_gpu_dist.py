@@ -245,3 +245,4 @@ def test_bench_two_ranks_learn_iteration():
     assert li["grad_allreduce_bytes_per_step"] > 4 * 10e6
     assert li["bn_allreduce_calls_per_step"] == 12  # 6 BatchNorm layers, forward + backward
     assert li["grad_allreduce_ms_per_step"] > 0
+    assert li["train_rank0_s"] > 0 and li["rank0_broadcast_bytes"] > 4 * 10e6
