@@ -10,8 +10,10 @@ unchanged, and modules are created in the same order so that
 `predict(planes) -> (P f32[A], v f32[1])` batch-1 as the reference does,
 `predict_batch(planes[B,4,n,n]) -> (P [B,A], v [B])` for the engine,
 `save_checkpoint` / `load_checkpoint` with the same file format.  Training
-(`train`) is outside the accelerated hot path and kept on the reference
-algorithm for compatibility.
+(`train`, `train_examples`) runs the reference's loop (batches, losses, Adam):
+on the CPU with the reference's arithmetic (bit-identical), on the GPU with
+conv2-4 in the Winograd domain and bn1-4 + ReLU on libazg's kernels
+(wino_train.py), each step after the third replayed from a captured HIP graph.
 """
 import os
 
