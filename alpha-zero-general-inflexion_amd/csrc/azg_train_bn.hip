@@ -94,26 +94,37 @@ __device__ __forceinline__ void channel_sums(const double* __restrict__ part, in
     }
 }
 
-// per channel: the parts -> mean, var, scale (f32), running stats; one wave per channel
-__global__ __launch_bounds__(BN_T) void bn_stats_final_kernel(const double* __restrict__ part, int nparts, int C,
-                                                              long long n, const float* __restrict__ gamma,
-                                                              const float* __restrict__ beta, float eps,
-                                                              float momentum, float* __restrict__ run_mean,
-                                                              float* __restrict__ run_var, float* __restrict__ sv) {
+// per channel: the parts -> sums [2C] f64 (the first sums, then the second); one wave per channel
+__global__ __launch_bounds__(BN_T) void bn_sums_kernel(const double* __restrict__ part, int nparts, int C,
+                                                       double* __restrict__ sums) {
     const int c = blockIdx.x * (BN_T / 64) + (int)(threadIdx.x >> 6);
     if (c >= C) return;  // wave-uniform
     double s, s2;
     channel_sums(part, nparts, C, c, s, s2);
     if ((threadIdx.x & 63) != 0) return;
+    sums[c] = s;
+    sums[C + c] = s2;
+}
+
+// per channel, from (sum x, sum x^2) over n rows (every rank's, data-parallel): mean, var, scale (f32),
+// running stats
+__global__ __launch_bounds__(BN_T) void bn_finalize_kernel(const double* __restrict__ sums, int C, long long n,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float eps, float momentum,
+                                                           float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                           float* __restrict__ sv) {
+    const int c = blockIdx.x * BN_T + threadIdx.x;
+    if (c >= C) return;
+    const double s = sums[c], s2 = sums[C + c];
     const double mean = s / (double)n;
     double var = s2 / (double)n - mean * mean;
     if (var < 0) var = 0;
     const double invstd = 1.0 / sqrt(var + (double)eps);
     const float scale = (float)((double)gamma[c] * invstd);
-    sv[c] = scale;       // scale
-    sv[C + c] = beta[c];  // beta
-    sv[2 * C + c] = (float)mean;                                    // mean
-    sv[3 * C + c] = (float)invstd;                                  // invstd
+    sv[c] = scale;                  // scale
+    sv[C + c] = beta[c];            // beta
+    sv[2 * C + c] = (float)mean;    // mean
+    sv[3 * C + c] = (float)invstd;  // invstd
     if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
     if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)(var * (double)n / (double)(n - 1));
 }
@@ -167,18 +178,19 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const float4* __res
     block_sum_store(a, C4, part);
 }
 
-// per channel: sum g, sum g xhat -> dbeta, dgamma and the apply's coefficients c1 = sum g / n,
-// c2 = sum g xhat / n (f32)
-__global__ __launch_bounds__(BN_T) void bn_bwd_final_kernel(const double* __restrict__ part, int nparts, int C,
-                                                            long long n, float* __restrict__ dgamma,
-                                                            float* __restrict__ dbeta, float* __restrict__ co) {
-    const int c = blockIdx.x * (BN_T / 64) + (int)(threadIdx.x >> 6);
-    if (c >= C) return;  // wave-uniform
-    double s, s2;
-    channel_sums(part, nparts, C, c, s, s2);
-    if ((threadIdx.x & 63) != 0) return;
-    dbeta[c] = (float)s;
-    dgamma[c] = (float)s2;
+// per channel, from (sum g, sum g xhat) over n rows (every rank's, data-parallel): the apply's
+// coefficients c1 = sum g / n, c2 = sum g xhat / n (f32), and -- when dgamma is given -- dbeta = sum g,
+// dgamma = sum g xhat
+__global__ __launch_bounds__(BN_T) void bn_bwd_coef_kernel(const double* __restrict__ sums, int C, long long n,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                           float* __restrict__ co) {
+    const int c = blockIdx.x * BN_T + threadIdx.x;
+    if (c >= C) return;
+    const double s = sums[c], s2 = sums[C + c];
+    if (dgamma) {
+        dbeta[c] = (float)s;
+        dgamma[c] = (float)s2;
+    }
     co[c] = (float)(s / (double)n);
     co[C + c] = (float)(s2 / (double)n);
 }
@@ -209,42 +221,92 @@ unsigned stream_grid(long long n4) {
 
 }  // namespace
 
-// Forward: y = relu(batchnorm(x)) with the batch's statistics; sv [4C] f32 receives scale, beta,
-// mean, invstd (the backward's input); run_mean / run_var updated in place (either may be null);
-// work >= 2 * 512 * C doubles.
-extern "C" int azg_bn_relu_fwd(const float* x, int64_t rows, int32_t C, const float* gamma, const float* beta,
-                               float eps, float momentum, float* run_mean, float* run_var, float* y, float* sv,
-                               double* work, void* stream) {
-    if (!x || !y || !gamma || !beta || !sv || !work || rows < 2 || C <= 0 || C % 4 || C / 4 > BN_T ||
-        ((uintptr_t)x & 15) || ((uintptr_t)y & 15) || ((uintptr_t)sv & 15))
+static bool bn_args_ok(const float* x, int64_t rows, int32_t C) {
+    return x && rows >= 2 && C > 0 && C % 4 == 0 && C / 4 <= BN_T && ((uintptr_t)x & 15) == 0;
+}
+
+// sums [2C] f64 = per channel (sum x, sum x^2) over the rows of x [rows][C]; work >= 2 * 512 * C doubles
+extern "C" int azg_bn_sums(const float* x, int64_t rows, int32_t C, double* sums, double* work, void* stream) {
+    if (!bn_args_ok(x, rows, C) || !sums || !work) return AZG_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(BN_PARTS), dim3(BN_T), 0, st, (const float4*)x, (long long)rows, C / 4,
+                       work);
+    hipLaunchKernelGGL(bn_sums_kernel, dim3((C + BN_T / 64 - 1) / (BN_T / 64)), dim3(BN_T), 0, st, work, BN_PARTS, C,
+                       sums);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+// y = relu(batchnorm(x)) from azg_bn_sums' sums over n_total rows (this call's x, or every rank's
+// when the caller all-reduced them); sv [4C] f32 receives scale, beta, mean, invstd; run_mean /
+// run_var updated in place (either may be null)
+extern "C" int azg_bn_relu_fwd_from_sums(const float* x, int64_t rows, int32_t C, const double* sums, int64_t n_total,
+                                         const float* gamma, const float* beta, float eps, float momentum,
+                                         float* run_mean, float* run_var, float* y, float* sv, void* stream) {
+    if (!bn_args_ok(x, rows, C) || !sums || n_total < 2 || !gamma || !beta || !y || !sv || ((uintptr_t)y & 15) ||
+        ((uintptr_t)sv & 15))
         return AZG_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     const int C4 = C / 4;
-    hipLaunchKernelGGL(bn_stats_kernel, dim3(BN_PARTS), dim3(BN_T), 0, st, (const float4*)x, (long long)rows, C4, work);
-    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((C + BN_T / 64 - 1) / (BN_T / 64)), dim3(BN_T), 0, st, work, BN_PARTS, C,
-                       (long long)rows, gamma, beta, eps, momentum, run_mean, run_var, sv);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + BN_T - 1) / BN_T), dim3(BN_T), 0, st, sums, C,
+                       (long long)n_total, gamma, beta, eps, momentum, run_mean, run_var, sv);
     const long long n4 = rows * C4;
     hipLaunchKernelGGL(bn_apply_relu_kernel, dim3(stream_grid(n4)), dim3(BN_T), 0, st, (const float4*)x,
                        (const float4*)sv, n4, C4, (float4*)y);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
-// Backward of azg_bn_relu_fwd: dx from dy (the gradient of y), x and the forward's sv; dgamma,
-// dbeta written (not accumulated); co >= 2C f32 and work >= 2 * 512 * C doubles scratch.
-extern "C" int azg_bn_relu_bwd(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv, float* dx,
-                               float* dgamma, float* dbeta, float* co, double* work, void* stream) {
-    if (!x || !dy || !sv || !dx || !dgamma || !dbeta || !co || !work || rows < 2 || C <= 0 || C % 4 ||
-        C / 4 > BN_T || ((uintptr_t)x & 15) || ((uintptr_t)dy & 15) || ((uintptr_t)dx & 15) ||
-        ((uintptr_t)sv & 15) || ((uintptr_t)co & 15))
+// sums [2C] f64 = per channel (sum g, sum g xhat) over the rows of x / dy (g = dy where the forward's ReLU
+// passed); work >= 2 * 512 * C doubles
+extern "C" int azg_bn_relu_bwd_sums(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv,
+                                    double* sums, double* work, void* stream) {
+    if (!bn_args_ok(x, rows, C) || !dy || !sv || !sums || !work || ((uintptr_t)dy & 15) || ((uintptr_t)sv & 15))
+        return AZG_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(BN_PARTS), dim3(BN_T), 0, st, (const float4*)x, (const float4*)dy,
+                       (const float4*)sv, (long long)rows, C / 4, work);
+    hipLaunchKernelGGL(bn_sums_kernel, dim3((C + BN_T / 64 - 1) / (BN_T / 64)), dim3(BN_T), 0, st, work, BN_PARTS, C,
+                       sums);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+// dx from azg_bn_relu_bwd_sums' sums over n_total rows (every rank's, data-parallel); dgamma / dbeta
+// (may be null) = the sums themselves; co >= 2C f32 scratch
+extern "C" int azg_bn_relu_bwd_from_sums(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv,
+                                         const double* sums, int64_t n_total, float* dx, float* dgamma, float* dbeta,
+                                         float* co, void* stream) {
+    if (!bn_args_ok(x, rows, C) || !dy || !sv || !sums || n_total < 2 || !dx || !co || (!dgamma) != (!dbeta) ||
+        ((uintptr_t)dy & 15) || ((uintptr_t)dx & 15) || ((uintptr_t)sv & 15) || ((uintptr_t)co & 15))
         return AZG_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     const int C4 = C / 4;
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(BN_PARTS), dim3(BN_T), 0, st, (const float4*)x, (const float4*)dy,
-                       (const float4*)sv, (long long)rows, C4, work);
-    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + BN_T / 64 - 1) / (BN_T / 64)), dim3(BN_T), 0, st, work, BN_PARTS, C,
-                       (long long)rows, dgamma, dbeta, co);
+    hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + BN_T - 1) / BN_T), dim3(BN_T), 0, st, sums, C,
+                       (long long)n_total, dgamma, dbeta, co);
     const long long n4 = rows * C4;
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(n4)), dim3(BN_T), 0, st, (const float4*)x,
                        (const float4*)dy, (const float4*)sv, (const float4*)co, n4, C4, (float4*)dx);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+// One process: azg_bn_sums + azg_bn_relu_fwd_from_sums (work >= 2 * 512 * C + 2 C doubles: the partials,
+// then the sums)
+extern "C" int azg_bn_relu_fwd(const float* x, int64_t rows, int32_t C, const float* gamma, const float* beta,
+                               float eps, float momentum, float* run_mean, float* run_var, float* y, float* sv,
+                               double* work, void* stream) {
+    if (!work) return AZG_ERR_ARG;
+    double* sums = work + (size_t)2 * BN_PARTS * C;
+    int rc = azg_bn_sums(x, rows, C, sums, work, stream);
+    if (rc) return rc;
+    return azg_bn_relu_fwd_from_sums(x, rows, C, sums, rows, gamma, beta, eps, momentum, run_mean, run_var, y, sv,
+                                     stream);
+}
+
+// One process: azg_bn_relu_bwd_sums + azg_bn_relu_bwd_from_sums (dgamma, dbeta written, not accumulated;
+// work as azg_bn_relu_fwd's)
+extern "C" int azg_bn_relu_bwd(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv, float* dx,
+                               float* dgamma, float* dbeta, float* co, double* work, void* stream) {
+    if (!work || !dgamma || !dbeta) return AZG_ERR_ARG;
+    double* sums = work + (size_t)2 * BN_PARTS * C;
+    int rc = azg_bn_relu_bwd_sums(x, dy, rows, C, sv, sums, work, stream);
+    if (rc) return rc;
+    return azg_bn_relu_bwd_from_sums(x, dy, rows, C, sv, sums, rows, dx, dgamma, dbeta, co, stream);
 }

@@ -17,8 +17,8 @@ transformed point one split-fp16 GEMM (f32-accurate products on the fp16 MFMA):
 max in (512, 1024]; dy: in (16, 32]) and unscaled exactly, so no step waits on the host.
 `train_forward` is InflexionNNet.forward with conv2-4 replaced when `applies` holds (a GPU
 batch, 512-style channel counts, the 7x7 board's layer sides) and bn1-4 + ReLU on
-BatchNormReLU (NHWC, azg_train_bn.hip; the data-parallel trainer's GlobalBatchNorm stays
-torch's); everything else -- conv1, dropout, the FC layers and their BatchNorms, the losses and
+BatchNormReLU (NHWC, azg_train_bn.hip; BatchNormReLUDP under the data-parallel trainer's
+GlobalBatchNorm, its sums all-reduced); everything else -- conv1, dropout, the FC layers and their BatchNorms, the losses and
 Adam -- is the reference's torch code.
 """
 import ctypes
@@ -162,7 +162,7 @@ class BatchNormReLU(torch.autograd.Function):
         rows = B * H * W
         y = torch.empty_like(x, memory_format=torch.channels_last)
         sv = torch.empty(4 * C, dtype=torch.float32, device=dev)
-        work = torch.empty(1024 * C, dtype=torch.float64, device=dev)
+        work = torch.empty(1026 * C, dtype=torch.float64, device=dev)
         _lib.check(L.azg_bn_relu_fwd(_p(x), rows, C, _p(weight.detach()), _p(bias.detach()), float(eps),
                                      float(momentum), _p(running_mean), _p(running_var), _p(y), _p(sv), _p(work),
                                      _stream(dev)))
@@ -180,23 +180,83 @@ class BatchNormReLU(torch.autograd.Function):
         dg = torch.empty(C, dtype=torch.float32, device=dev)
         db = torch.empty(C, dtype=torch.float32, device=dev)
         co = torch.empty(2 * C, dtype=torch.float32, device=dev)
-        work = torch.empty(1024 * C, dtype=torch.float64, device=dev)
+        work = torch.empty(1026 * C, dtype=torch.float64, device=dev)
         _lib.check(L.azg_bn_relu_bwd(_p(x), _p(dyc), B * H * W, C, _p(sv), _p(dx), _p(dg), _p(db), _p(co), _p(work),
                                      _stream(dev)))
         return dx, dg, db, None, None, None, None
 
 
+class BatchNormReLUDP(torch.autograd.Function):
+    """BatchNormReLU with the statistics of the whole data-parallel batch (ddp.GlobalBatchNorm's
+    arithmetic: every rank holds an equal slice): the per-channel f64 sums of this rank's rows are
+    SUM-all-reduced before the finish, forward and backward; dgamma / dbeta are this rank's own
+    share (the trainer's gradient all-reduce sums them), dx uses the whole batch's sums."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, group, world):
+        import torch.distributed as dist
+        from . import ddp
+        L = _lib.lib()
+        dev = x.device
+        B, C, H, W = x.shape
+        rows = B * H * W
+        work = torch.empty(1024 * C, dtype=torch.float64, device=dev)
+        sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
+        _lib.check(L.azg_bn_sums(_p(x), rows, C, _p(sums), _p(work), _stream(dev)))
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+        ddp._count("bn_allreduce", sums.numel() * 8)
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        sv = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        _lib.check(L.azg_bn_relu_fwd_from_sums(_p(x), rows, C, _p(sums), rows * world, _p(weight.detach()),
+                                               _p(bias.detach()), float(eps), float(momentum), _p(running_mean),
+                                               _p(running_var), _p(y), _p(sv), _stream(dev)))
+        ctx.save_for_backward(x, sv)
+        ctx.group, ctx.world = group, world
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        import torch.distributed as dist
+        from . import ddp
+        L = _lib.lib()
+        x, sv = ctx.saved_tensors
+        dev = x.device
+        B, C, H, W = x.shape
+        rows = B * H * W
+        dyc = dy.contiguous(memory_format=torch.channels_last)
+        work = torch.empty(1024 * C, dtype=torch.float64, device=dev)
+        sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
+        _lib.check(L.azg_bn_relu_bwd_sums(_p(x), _p(dyc), rows, C, _p(sv), _p(sums), _p(work), _stream(dev)))
+        db, dg = sums[:C].float(), sums[C:].float()  # this rank's share (before the reduction)
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=ctx.group)
+        ddp._count("bn_allreduce", sums.numel() * 8)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        co = torch.empty(2 * C, dtype=torch.float32, device=dev)
+        _lib.check(L.azg_bn_relu_bwd_from_sums(_p(x), _p(dyc), rows, C, _p(sv), _p(sums), rows * ctx.world, _p(dx),
+                                               None, None, _p(co), _stream(dev)))
+        return dx, dg, db, None, None, None, None, None, None
+
+
+def _bn_relu_ok(bn, x):
+    return (type(bn) is torch.nn.BatchNorm2d and bn.training and bn.affine and bn.track_running_stats
+            and bn.momentum is not None and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 4 == 0
+            and x.shape[1] <= 1024 and x.numel() // x.shape[1] >= 2)
+
+
 def bn_relu(bn, x):
     """relu(bn(x)) as InflexionNNet.forward applies it (InflexionNNet.py:39-45): on
     BatchNormReLU for a plain training-mode nn.BatchNorm2d (affine, running statistics, a
-    momentum) over channels-last CUDA f32 activations, else the module and F.relu (eval mode,
-    the data-parallel trainer's GlobalBatchNorm, other layouts)."""
-    if (type(bn) is torch.nn.BatchNorm2d and bn.training and bn.affine and bn.track_running_stats
-            and bn.momentum is not None and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
-            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 4 == 0
-            and x.shape[1] <= 1024 and x.numel() // x.shape[1] >= 2):
+    momentum) over channels-last CUDA f32 activations, on BatchNormReLUDP for the data-parallel
+    trainer's GlobalBatchNorm around one, else the module and F.relu (eval mode, other layouts)."""
+    if _bn_relu_ok(bn, x):
         bn.num_batches_tracked.add_(1)
         return BatchNormReLU.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps)
+    inner = getattr(bn, "bn", None)  # ddp.GlobalBatchNorm: the whole data-parallel batch's statistics
+    if inner is not None and type(bn).__name__ == "GlobalBatchNorm" and _bn_relu_ok(inner, x):
+        inner.num_batches_tracked.add_(1)
+        return BatchNormReLUDP.apply(x, inner.weight, inner.bias, inner.running_mean, inner.running_var,
+                                     inner.momentum, inner.eps, bn.group, bn.world)
     return F.relu(bn(x))
 
 
@@ -282,5 +342,5 @@ def _flag(dev):
     return f
 
 
-__all__ = ["BatchNormReLU", "WinogradConv3x3", "applies", "applies_net", "bn_relu", "check_range", "conv3x3",
+__all__ = ["BatchNormReLU", "BatchNormReLUDP", "WinogradConv3x3", "applies", "applies_net", "bn_relu", "check_range", "conv3x3",
            "take_flag", "train_forward"]

@@ -412,12 +412,26 @@ int  azg_absmax(const float* x, int64_t n, uint32_t* out, void* stream);
  * with the batch's statistics, sv [4C] = (scale, beta, mean, invstd), and updates run_mean /
  * run_var (momentum; unbiased variance; either may be null); azg_bn_relu_bwd writes dx, dgamma,
  * dbeta from dy (the gradient of y), x and sv.  Sums in f64 over 512 fixed row ranges, reduced in
- * order (deterministic); work >= 1024 C doubles, co >= 2C floats (scratch). */
+ * order (deterministic); work >= 1026 C doubles, co >= 2C floats (scratch). */
 int  azg_bn_relu_fwd(const float* x, int64_t rows, int32_t C, const float* gamma, const float* beta, float eps,
                      float momentum, float* run_mean, float* run_var, float* y, float* sv, double* work,
                      void* stream);
 int  azg_bn_relu_bwd(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv, float* dx,
                      float* dgamma, float* dbeta, float* co, double* work, void* stream);
+/* The same in two halves around a caller's reduction over data-parallel ranks: azg_bn_sums writes
+ * sums [2C] f64 = (sum x, sum x^2) of this rank's rows, azg_bn_relu_fwd_from_sums finishes from the
+ * (all-reduced) sums over n_total rows; azg_bn_relu_bwd_sums writes (sum g, sum g xhat), and
+ * azg_bn_relu_bwd_from_sums writes dx from the all-reduced ones (dgamma / dbeta may be null: a rank's
+ * own share comes from its un-reduced sums).  work >= 1024 C doubles (azg_bn_relu_fwd / _bwd: 1026 C). */
+int  azg_bn_sums(const float* x, int64_t rows, int32_t C, double* sums, double* work, void* stream);
+int  azg_bn_relu_fwd_from_sums(const float* x, int64_t rows, int32_t C, const double* sums, int64_t n_total,
+                               const float* gamma, const float* beta, float eps, float momentum, float* run_mean,
+                               float* run_var, float* y, float* sv, void* stream);
+int  azg_bn_relu_bwd_sums(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv, double* sums,
+                          double* work, void* stream);
+int  azg_bn_relu_bwd_from_sums(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv,
+                               const double* sums, int64_t n_total, float* dx, float* dgamma, float* dbeta,
+                               float* co, void* stream);
 int  azg_wt_u_build(const float* w, int32_t c, int32_t k, int32_t h_out, uint32_t* uamax, void* ut, void* un,
                     float* work, void* stream);
 int  azg_wt_out(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,

@@ -246,3 +246,81 @@ def test_bench_two_ranks_learn_iteration():
     assert li["bn_allreduce_calls_per_step"] == 12  # 6 BatchNorm layers, forward + backward
     assert li["grad_allreduce_ms_per_step"] > 0
     assert li["train_rank0_s"] > 0 and li["rank0_broadcast_bytes"] > 4 * 10e6
+
+
+def _dp_train_worker(rank, world, port, q, E):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import azg_amd  # noqa: F401
+        from azg_amd.examples import ExampleSet
+        from azg_amd.inflexion import InflexionGame
+        from azg_amd.nnet import NNetWrapper
+        torch.cuda.set_device(0)
+        torch.backends.cudnn.deterministic = True
+        gen = torch.Generator().manual_seed(21)
+        ex = ExampleSet((torch.rand((E, 4, 7, 7), generator=gen) < 0.3).float().cuda(),
+                        torch.softmax(torch.randn((E, 343), generator=gen), 1).cuda(),
+                        (torch.randint(0, 2, (E,), generator=gen).float() * 2 - 1).cuda())
+        torch.manual_seed(0)
+        w = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0), device="cuda")
+        np.random.seed(4)
+        st = {}
+        losses = w.train_examples(ex, group=dist.group.WORLD, stats=st).cpu().numpy()
+        q.put((rank, losses, {k: v.detach().cpu().numpy() for k, v in w.nnet.state_dict().items()
+                              if k in ("conv2.weight", "conv4.weight", "bn2.running_var", "fc1.weight")},
+               st.get("bn_allreduce_calls", 0) / max(st.get("steps", 1), 1)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_trainer_on_the_training_kernels():
+    """The data-parallel trainer at the real network's size (512 channels: conv2-4 on the Winograd
+    training kernels, bn1-4 + ReLU on BatchNormReLUDP -- the NHWC kernels with the ranks' f64 sums
+    all-reduced), two gloo ranks on one GPU, against the one-process GPU trainer on the same
+    examples and draws (dropout 0, MIOpen deterministic): per-batch losses within the GPU trainer's
+    2e-3, the weights' update (in norm) within 5e-2 of its size, the running variance within 1e-5 --
+    and 12 BatchNorm all-reduces per step (4 conv BatchNorms + 2 FC ones, forward and backward)."""
+    import azg_amd  # noqa: F401
+    from azg_amd.examples import ExampleSet
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.nnet import NNetWrapper
+    E = 512 * 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_train_worker, args=(r, 2, port, q, E)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, losses, w, calls = q.get(timeout=150)
+        res[r] = (losses, w, calls)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        gen = torch.Generator().manual_seed(21)
+        ex = ExampleSet((torch.rand((E, 4, 7, 7), generator=gen) < 0.3).float().cuda(),
+                        torch.softmax(torch.randn((E, 343), generator=gen), 1).cuda(),
+                        (torch.randint(0, 2, (E,), generator=gen).float() * 2 - 1).cuda())
+        torch.manual_seed(0)
+        w0 = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0, train_graph=False), device="cuda")
+        init = {k: v.detach().cpu().numpy().copy() for k, v in w0.nnet.state_dict().items()}
+        np.random.seed(4)
+        ref = w0.train_examples(ex).cpu().numpy()
+        sd = {k: v.detach().cpu().numpy() for k, v in w0.nnet.state_dict().items()}
+    finally:
+        torch.backends.cudnn.deterministic = det
+    for r in (0, 1):
+        losses, w, calls = res[r]
+        np.testing.assert_allclose(losses, ref, rtol=2e-3)
+        assert calls == 12, calls
+        for k in ("conv2.weight", "conv4.weight", "fc1.weight"):
+            d = np.linalg.norm(w[k] - sd[k]) / np.linalg.norm(sd[k] - init[k])
+            assert d < 5e-2, (r, k, d)
+        np.testing.assert_allclose(w["bn2.running_var"], sd["bn2.running_var"], rtol=1e-5, atol=1e-6)
+    for k in res[0][1]:  # the ranks' weights stay bitwise equal
+        assert np.array_equal(res[0][1][k], res[1][1][k]), k
