@@ -29,7 +29,9 @@
 
 namespace {
 
-template <int FMT>
+// PM > 1: up to PM split-K parts, every part's load issued before the in-order sum (one memory
+// round trip, not one per part: C2's fc2 sums 16 parts); PM = 0: any number, one part at a time
+template <int FMT, int PM>
 __global__ __launch_bounds__(256) void fc_act_split_kernel(const float4* __restrict__ m, int parts,
                                                            long long pstride4, const float4* __restrict__ bias,
                                                            float scale, ushort4* __restrict__ out, long long rows,
@@ -39,9 +41,18 @@ __global__ __launch_bounds__(256) void fc_act_split_kernel(const float4* __restr
     const long long r = i / n4;
     const int c4 = (int)(i - r * n4);
     float4 x = m[i];
-    for (int p = 1; p < parts; ++p) {  // split-K parts, summed in order
-        const float4 t = m[p * pstride4 + i];
-        x = make_float4(x.x + t.x, x.y + t.y, x.z + t.z, x.w + t.w);
+    if constexpr (PM > 1) {
+        float4 t[PM - 1];
+#pragma unroll
+        for (int p = 1; p < PM; ++p) t[p - 1] = p < parts ? m[p * pstride4 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int p = 1; p < PM; ++p)  // split-K parts, summed in order
+            if (p < parts) x = make_float4(x.x + t[p - 1].x, x.y + t[p - 1].y, x.z + t[p - 1].z, x.w + t[p - 1].w);
+    } else {
+        for (int p = 1; p < parts; ++p) {  // split-K parts, summed in order
+            const float4 t = m[p * pstride4 + i];
+            x = make_float4(x.x + t.x, x.y + t.y, x.z + t.z, x.w + t.w);
+        }
     }
     const float4 b = bias[c4];
     float y[4] = {b.x + scale * x.x, b.y + scale * x.y, b.z + scale * x.z, b.w + scale * x.w};
@@ -131,8 +142,12 @@ __global__ __launch_bounds__(256) void fc_act_t_kernel(const float* __restrict__
 }
 
 constexpr int PV_MAX_PER_LANE = 16;  // up to 1024 actions per leaf (9x9 Inflexion: 567)
+constexpr int PV_PMAX = 16;          // split-K parts of the [fc3 | fc4] GEMM
 
-template <int PV_PER_LANE>
+// PM > 1 (the split-K [fc3 | fc4] GEMM's parts, <= PM): every part's loads issued before the
+// in-order sums, one memory round trip (C2's 8 parts: 14.8 us with one round trip per part);
+// PM = 1: one part
+template <int PV_PER_LANE, int PM>
 __global__ __launch_bounds__(256) void policy_value_kernel(const float* __restrict__ m, int ldm, int parts,
                                                            long long pstride, const float* __restrict__ bias,
                                                            float scale, float* __restrict__ P,
@@ -143,15 +158,25 @@ __global__ __launch_bounds__(256) void policy_value_kernel(const float* __restri
     const float* mr = m + (long long)r * ldm;
     float x[PV_PER_LANE];
     float mx = -INFINITY;
+    float t[PM][PV_PER_LANE];
+#pragma unroll
+    for (int p = 0; p < PM; ++p)
+#pragma unroll
+        for (int j = 0; j < PV_PER_LANE; ++j) {
+            const int a = lane + 64 * j;
+            t[p][j] = (a < A && p < parts) ? mr[p * pstride + a] : 0.f;
+        }
+    float tv[PM];  // the value column, lane 0, loaded with the rest
+#pragma unroll
+    for (int p = 0; p < PM; ++p) tv[p] = (lane == 0 && p < parts) ? mr[p * pstride + A] : 0.f;
 #pragma unroll
     for (int j = 0; j < PV_PER_LANE; ++j) {
         const int a = lane + 64 * j;
-        float t = 0.f;
-        if (a < A) {
-            t = mr[a];
-            for (int p = 1; p < parts; ++p) t += mr[p * pstride + a];  // split-K parts, in order
-        }
-        x[j] = a < A ? bias[a] + scale * t : -INFINITY;
+        float s = t[0][j];
+#pragma unroll
+        for (int p = 1; p < PM; ++p)
+            if (p < parts) s += t[p][j];  // split-K parts, in order
+        x[j] = a < A ? bias[a] + scale * s : -INFINITY;
         mx = fmaxf(mx, x[j]);
     }
 #pragma unroll
@@ -172,8 +197,10 @@ __global__ __launch_bounds__(256) void policy_value_kernel(const float* __restri
         if (a < A) pr[a] = x[j] * inv;
     }
     if (lane == 0) {
-        float t = mr[A];
-        for (int p = 1; p < parts; ++p) t += mr[p * pstride + A];
+        float t = tv[0];
+#pragma unroll
+        for (int p = 1; p < PM; ++p)
+            if (p < parts) t += tv[p];
         v[r] = tanhf(bias[A] + scale * t);
     }
 }
@@ -191,14 +218,19 @@ extern "C" int azg_fc_act(const float* m, int32_t parts, int64_t part_stride, co
         return AZG_ERR_ARG;
     const long long items = (long long)rows * (n / 4);
     const dim3 grid((unsigned)((items + 255) / 256));
+    auto launch = [&](auto kern, int op) {
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, (const float4*)m, parts,
+                           (long long)(part_stride / 4), (const float4*)bias, scale, (ushort4*)out, (long long)rows,
+                           n / 4, relu, op, overflow);
+    };
     if (fmt == AZG_WINO_SPLIT)
-        hipLaunchKernelGGL(fc_act_split_kernel<AZG_WINO_SPLIT>, grid, dim3(256), 0, (hipStream_t)stream,
-                           (const float4*)m, parts, (long long)(part_stride / 4), (const float4*)bias, scale,
-                           (ushort4*)out, (long long)rows, n / 4, relu, 1, overflow);
+        launch(fc_act_split_kernel<AZG_WINO_SPLIT, 0>, 1);
+    else if (parts <= 4)
+        launch(fc_act_split_kernel<AZG_WINO_SPLIT2, 4>, out_parts);
+    else if (parts <= 16)
+        launch(fc_act_split_kernel<AZG_WINO_SPLIT2, 16>, out_parts);
     else
-        hipLaunchKernelGGL(fc_act_split_kernel<AZG_WINO_SPLIT2>, grid, dim3(256), 0, (hipStream_t)stream,
-                           (const float4*)m, parts, (long long)(part_stride / 4), (const float4*)bias, scale,
-                           (ushort4*)out, (long long)rows, n / 4, relu, out_parts, overflow);
+        launch(fc_act_split_kernel<AZG_WINO_SPLIT2, 0>, out_parts);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
@@ -223,15 +255,26 @@ extern "C" int azg_policy_value_parts(const float* m, int32_t parts, int64_t par
                                       const float* bias, float scale, float* P, float* v, int32_t rows,
                                       int32_t actions, void* stream) {
     if (!m || !bias || !P || !v || rows <= 0 || actions <= 0 || actions > 64 * PV_MAX_PER_LANE ||
-        ldm < actions + 1 || parts < 1 || (parts > 1 && part_stride < (int64_t)rows * ldm))
+        ldm < actions + 1 || parts < 1 || parts > PV_PMAX || (parts > 1 && part_stride < (int64_t)rows * ldm))
         return AZG_ERR_ARG;
     const dim3 grid((unsigned)((rows + 3) / 4));
-    if (actions <= 64 * 8)
-        hipLaunchKernelGGL(policy_value_kernel<8>, grid, dim3(256), 0, (hipStream_t)stream, m, ldm, parts,
-                           (long long)part_stride, bias, scale, P, v, rows, actions);
-    else
-        hipLaunchKernelGGL(policy_value_kernel<PV_MAX_PER_LANE>, grid, dim3(256), 0, (hipStream_t)stream, m, ldm,
-                           parts, (long long)part_stride, bias, scale, P, v, rows, actions);
+    auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, m, ldm, parts, (long long)part_stride,
+                           bias, scale, P, v, rows, actions);
+    };
+    if (actions <= 64 * 8) {
+        if (parts == 1)
+            launch(policy_value_kernel<8, 1>);
+        else if (parts <= 8)
+            launch(policy_value_kernel<8, 8>);
+        else
+            launch(policy_value_kernel<8, PV_PMAX>);
+    } else {
+        if (parts == 1)
+            launch(policy_value_kernel<PV_MAX_PER_LANE, 1>);
+        else
+            launch(policy_value_kernel<PV_MAX_PER_LANE, PV_PMAX>);
+    }
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 

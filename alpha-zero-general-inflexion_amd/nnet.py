@@ -62,11 +62,12 @@ FC34_KPARTS = 2
 FC1T_KPARTS = 18
 FCS_KPARTS2 = 16
 FCS_KPARTS3 = 8
-# ... opt-in (InferenceNet.fc_tail_small = True): at C2 it measured 1.02-1.06M exp/s over K-part choices
-# (18/16/8, 18/8/4, 18/16/4, 24/8/4, 12/8/4, 18/8/2, 18/4/2) against 1.10M for the f32 hipBLASLt tail
-# on the same box (profiles/r05_bench_C2_*.json): its three split GEMMs alone take 49 us per 256-leaf
-# forward, the library's three GEMMs 41 us -- the split GEMM's tiles are built for thousands of rows
-FC_SMALL_TAIL = False
+# ... the default (InferenceNet.fc_tail_small): with its epilogues loading every split-K part in flight
+# (policy_value 14.8 -> 6.9 us, fc_act 6.1 -> 4.8 us per 256-leaf forward) it measured 1.037M exp/s at C2
+# against 1.005M for the f32 hipBLASLt tail eager and 1.078M / 1.082M in graph replay, the same box
+# (profiles/r05_bench_C2_tail_ab_*.json); before that, 1.02-1.06M over seven K-part choices against
+# 1.10M.  No library GEMM is left in the C2 forward.
+FC_SMALL_TAIL = True
 
 
 class InflexionNNet(nn.Module):

@@ -147,7 +147,7 @@ def parse():
                    help="fc2 and [fc3 | fc4] at >= 1024 leaves: libazg split-K split GEMMs (azg) or the round-2 "
                         "hipBLASLt fp16 GEMMs (blas)")
     p.add_argument("--fc-kparts", default=None, help="with --fc-tail azg: split-K parts of fc2,fc3|fc4 (e.g. 4,2)")
-    p.add_argument("--fc-small", default="off", choices=["on", "off"],
+    p.add_argument("--fc-small", default="on", choices=["on", "off"],
                    help="below --fc1-split-min leaves (leaves % 256 == 0): the FC tail on libazg's split GEMM, fc1 "
                         "transposed (on, nnet._fc_split_small) or the f32 hipBLASLt tail (off)")
     p.add_argument("--fc-small-kparts", default=None, help="--fc-small on: K-parts of fc1,fc2,fc3|fc4 (e.g. 18,16,8)")

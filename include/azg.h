@@ -324,7 +324,7 @@ int  azg_policy_value(const float* m, int32_t ldm, const float* bias, float scal
  * = azg_fc_act_split) or AZG_WINO_SPLIT2: out_parts K-parts of 32-channel [hi | lo]
  * blocks, [part][rows][2 n / out_parts] fp16 -- the A operand of the next layer's
  * split-K azg_split_gemm (its parts as the GEMM's points); (n / out_parts) % 32 == 0.
- * azg_policy_value_parts sums `parts` partial [fc3 | fc4] products (part p at m + p *
+ * azg_policy_value_parts sums `parts` (1..16) partial [fc3 | fc4] products (part p at m + p *
  * part_stride floats, in order) first; azg_policy_value = parts 1. */
 int  azg_fc_act(const float* m, int32_t parts, int64_t part_stride, const float* bias, float scale, void* out,
                 int32_t rows, int32_t n, int32_t relu, int32_t fmt, int32_t out_parts, int32_t* overflow,

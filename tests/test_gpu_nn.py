@@ -487,15 +487,17 @@ def test_fc_act_split_kernel():
         assert int(ovf.item()) == 1
 
 
-@pytest.mark.parametrize("n,out_parts", [(1024, 8), (512, 4), (512, 1), (256, 2)])
-def test_fc_act_split2_layout(n, out_parts):
+@pytest.mark.parametrize("n,out_parts,parts", [(1024, 8, 3), (512, 4, 3), (512, 1, 3), (256, 2, 3), (512, 8, 9),
+                                                (512, 8, 16), (256, 4, 20)])
+def test_fc_act_split2_layout(n, out_parts, parts):
     """azg_fc_act with AZG_WINO_SPLIT2 output: the same hi / lo values as the [hi | lo | hi]
     form, laid out as out_parts K-parts of 32-channel [hi | lo] blocks (nnet.split2_rows of
-    each part), the A operand of the next split-K split GEMM."""
+    each part), the A operand of the next split-K split GEMM.  Input parts summed in order,
+    bit-exact: <= 4 and <= 16 parts (every part's load in flight) and 20 (one at a time)."""
     import ctypes
     from azg_amd import _lib
     from azg_amd.nnet import split2_rows
-    B, scale, parts = 257, 2.0 ** -5, 3
+    B, scale = 257, 2.0 ** -5
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     m = torch.randn(parts, B, n, device="cuda") * 50
     b = torch.randn(n, device="cuda")
@@ -504,7 +506,10 @@ def test_fc_act_split2_layout(n, out_parts):
     _lib.check(_lib.lib().azg_fc_act(ctypes.c_void_p(m.data_ptr()), parts, B * n, ctypes.c_void_p(b.data_ptr()),
                                      scale, ctypes.c_void_p(out.data_ptr()), B, n, 1, 2, out_parts,
                                      ctypes.c_void_p(ovf.data_ptr()), st))
-    y = torch.relu(b + scale * (m[0] + m[1] + m[2]))
+    acc = m[0].clone()
+    for p in range(1, parts):
+        acc = acc + m[p]
+    y = torch.relu(b + scale * acc)
     hi = y.half()
     lo = (y - hi.float()).half()
     want = split2_rows(hi.reshape(B, out_parts, n // out_parts).transpose(0, 1),
@@ -518,12 +523,13 @@ def test_fc_act_split2_layout(n, out_parts):
                                  ctypes.c_void_p(host_flag.data_ptr()), st) == -1
 
 
-@pytest.mark.parametrize("parts", [1, 4])
-def test_policy_value_parts_kernel(parts):
-    """azg_policy_value_parts: the split-K parts of [fc3 | fc4] summed in order, then softmax / tanh."""
+@pytest.mark.parametrize("parts,A", [(1, 343), (4, 343), (8, 343), (13, 343), (16, 343), (5, 567)])
+def test_policy_value_parts_kernel(parts, A):
+    """azg_policy_value_parts: the split-K parts of [fc3 | fc4] summed in order, then softmax / tanh
+    (up to 8 parts / up to 16 parts, every part's load in flight; 17 parts refused)."""
     import ctypes
     from azg_amd import _lib
-    B, A, ld, scale = 333, 343, 512, 0.25
+    B, ld, scale = 333, 512 if A < 512 else 640, 0.25
     m = torch.randn(parts, B, ld, device="cuda") * 4
     b = torch.randn(A + 1, device="cuda")
     P = torch.empty(B, A, device="cuda")
@@ -538,6 +544,9 @@ def test_policy_value_parts_kernel(parts):
     x = b + scale * acc[:, :A + 1]
     torch.testing.assert_close(P, torch.softmax(x[:, :A], dim=1), rtol=2e-6, atol=1e-8)
     torch.testing.assert_close(v, torch.tanh(x[:, A]), rtol=2e-6, atol=1e-7)
+    assert _lib.lib().azg_policy_value_parts(ctypes.c_void_p(m.data_ptr()), 17, B * ld, ld,
+                                             ctypes.c_void_p(b.data_ptr()), scale, ctypes.c_void_p(P.data_ptr()),
+                                             ctypes.c_void_p(v.data_ptr()), B, A, None) == -1
 
 
 @pytest.mark.parametrize("A", [343, 65, 36, 512, 567, 1024])
@@ -827,15 +836,14 @@ def test_small_path_gate_falls_back(A, C):
 def test_small_fc_tail_matches_reference(B):
     """The FC tail below FC1_SPLIT_MIN_BATCH leaves on libazg only (InferenceNet._fc_split_small:
     fc1 as the transposed split-K GEMM W1 A^T, azg_fc_act_t, then fc2 / [fc3 | fc4] split-K; C2's
-    256 leaves; opt-in, the f32 hipBLASLt tail measured faster) against the reference module (1e-5)
-    and the f32 tail."""
+    256 leaves; the default since the epilogues load every part in flight) against the reference
+    module (1e-5) and the f32 hipBLASLt tail."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InferenceNet, InflexionNNet
     torch.manual_seed(13)
     net = InflexionNNet().cuda().eval()
     fast = InferenceNet(net).cuda()
-    assert not fast.fc_tail_small and hasattr(fast, "fw1_skT")  # opt-in (nnet.FC_SMALL_TAIL)
-    fast.fc_tail_small = True
+    assert fast.fc_tail_small and hasattr(fast, "fw1_skT")  # the default (nnet.FC_SMALL_TAIL)
     x = (torch.rand(B, 4, 7, 7, device="cuda") < 0.3).float()
     x[:, 2:] = x[:, 2:, :1, :1]
     with torch.no_grad():
