@@ -111,6 +111,8 @@ SIGNATURES = [
                                                  ctypes.c_float, _VP, _VP, _VP, _VP, _VP]),
     ("azg_bn_relu_bwd_sums", ctypes.c_int, [_VP, _VP, _I64, _I32, _VP, _VP, _VP, _VP]),
     ("azg_bn_relu_bwd_from_sums", ctypes.c_int, [_VP, _VP, _I64, _I32, _VP, _VP, _I64, _VP, _VP, _VP, _VP, _VP]),
+    ("azg_conv1_train_fwd", ctypes.c_int, [_VP, _I64, _I32, _I32, _VP, _VP, _I32, _VP, _VP]),
+    ("azg_conv1_train_wgrad", ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
     ("azg_wt_u_build", ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP]),
     ("azg_wt_out", ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _VP, _VP]),
     ("azg_wt_dout", ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _VP, _VP, _VP]),

@@ -18,8 +18,9 @@ max in (512, 1024]; dy: in (16, 32]) and unscaled exactly, so no step waits on t
 `train_forward` is InflexionNNet.forward with conv2-4 replaced when `applies` holds (a GPU
 batch, 512-style channel counts, the 7x7 board's layer sides) and bn1-4 + ReLU on
 BatchNormReLU (NHWC, azg_train_bn.hip; BatchNormReLUDP under the data-parallel trainer's
-GlobalBatchNorm, its sums all-reduced); everything else -- conv1, dropout, the FC layers and their BatchNorms, the losses and
-Adam -- is the reference's torch code.
+GlobalBatchNorm, its sums all-reduced) and conv1 on Conv1Train (azg_train_conv1.hip); everything
+else -- dropout, the FC layers and their BatchNorms, the losses and Adam -- is the reference's
+torch code.
 """
 import ctypes
 
@@ -145,6 +146,56 @@ class WinogradConv3x3(torch.autograd.Function):
             _lib.check(L.azg_wt_dw(_p(dU), C, K, Ho, _p(dyamax), _p(dw), st))
         db = dy.sum(dim=(0, 2, 3)) if ctx.needs_input_grad[2] else None
         return dx, dw, db, None
+
+
+class Conv1Train(torch.autograd.Function):
+    """conv1 (InflexionNNet.py:39: 3x3, stride 1, padding 1) on the board planes, forward and the
+    weight / bias gradients on libazg (azg_train_conv1.hip), so no training step reaches MIOpen
+    (whose conv1 kernels were compiled on a process's first step: 2.2 s, tools/train_first_use.py).
+    x: channels-last planes [B, D, n, n] (no gradient), w: [K, D, 3, 3], b: [K].  Returns y
+    channels-last."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        dev = x.device
+        B, D, n, _ = x.shape
+        K = w.shape[0]
+        y = torch.empty((B, K, n, n), dtype=torch.float32, device=dev, memory_format=torch.channels_last)
+        _lib.check(_lib.lib().azg_conv1_train_fwd(_p(x), B, D, n, _p(w.detach().contiguous()), _p(b.detach()), K,
+                                                  _p(y), _stream(dev)))
+        ctx.save_for_backward(x)
+        ctx.K = K
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dev = x.device
+        B, D, n, _ = x.shape
+        K = ctx.K
+        dyc = dy.contiguous(memory_format=torch.channels_last)
+        dw = torch.empty((K, D, 3, 3), dtype=torch.float32, device=dev)
+        db = torch.empty(K, dtype=torch.float32, device=dev)
+        work = torch.empty(64 * K * (9 * D + 1), dtype=torch.float64, device=dev)
+        _lib.check(_lib.lib().azg_conv1_train_wgrad(_p(x), _p(dyc), B, D, n, K, _p(dw), _p(db), _p(work),
+                                                    _stream(dev)))
+        return None, dw, db
+
+
+def _conv1_ok(conv, x):
+    return (type(conv) is torch.nn.Conv2d and conv.kernel_size == (3, 3) and conv.stride == (1, 1)
+            and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is not None
+            and conv.padding_mode == "zeros" and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and not x.requires_grad and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[1] == conv.in_channels and x.shape[1] <= 8 and x.shape[2] == x.shape[3] <= 8
+            and conv.out_channels % 64 == 0)
+
+
+def conv1_train(conv, x):
+    """conv(x) for the first layer: on Conv1Train when its shapes allow, else the module."""
+    if _conv1_ok(conv, x):
+        return Conv1Train.apply(x, conv.weight, conv.bias)
+    return conv(x)
 
 
 class BatchNormReLU(torch.autograd.Function):
@@ -282,7 +333,7 @@ def train_forward(net, s):
     x = s.view(-1, net.depth, net.n, net.n)
     if x.is_cuda:
         x = x.contiguous(memory_format=torch.channels_last)
-    x = bn_relu(net.bn1, net.conv1(x))
+    x = bn_relu(net.bn1, conv1_train(net.conv1, x))
     for i in range(2, 5):
         x = bn_relu(getattr(net, f"bn{i}"), conv3x3(x, getattr(net, f"conv{i}")))
     x = x.reshape(x.shape[0], -1)
@@ -342,5 +393,5 @@ def _flag(dev):
     return f
 
 
-__all__ = ["BatchNormReLU", "BatchNormReLUDP", "WinogradConv3x3", "applies", "applies_net", "bn_relu", "check_range", "conv3x3",
-           "take_flag", "train_forward"]
+__all__ = ["BatchNormReLU", "BatchNormReLUDP", "Conv1Train", "WinogradConv3x3", "applies", "applies_net", "bn_relu",
+           "check_range", "conv1_train", "conv3x3", "take_flag", "train_forward"]

@@ -432,6 +432,16 @@ int  azg_bn_relu_bwd_sums(const float* x, const float* dy, int64_t rows, int32_t
 int  azg_bn_relu_bwd_from_sums(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv,
                                const double* sums, int64_t n_total, float* dx, float* dgamma, float* dbeta,
                                float* co, void* stream);
+/* The trainer's conv1 (InflexionNNet.py:39: 3x3, stride 1, padding 1, on the board planes;
+ * azg_train_conv1.hip): x NHWC [batch][n][n][depth] (the planes channels_last), w [K][depth][3][3],
+ * depth <= 8, n <= 8, K % 64 == 0.  azg_conv1_train_fwd writes y NHWC [batch][n][n][K] = conv + bias
+ * (bias may be null); azg_conv1_train_wgrad writes dw [K][depth][3][3] and db [K] (may be null) from
+ * dy NHWC [batch][n][n][K], f64 partials in a fixed order (deterministic); work >= 64 K (9 depth + 1)
+ * doubles.  (No input gradient: the planes need none.) */
+int  azg_conv1_train_fwd(const float* x, int64_t batch, int32_t depth, int32_t n, const float* w, const float* bias,
+                         int32_t K, float* y, void* stream);
+int  azg_conv1_train_wgrad(const float* x, const float* dy, int64_t batch, int32_t depth, int32_t n, int32_t K,
+                           float* dw, float* db, double* work, void* stream);
 int  azg_wt_u_build(const float* w, int32_t c, int32_t k, int32_t h_out, uint32_t* uamax, void* ut, void* un,
                     float* work, void* stream);
 int  azg_wt_out(const float* M, const float* bias, float* y, int32_t batch, int32_t h_out, int32_t k,

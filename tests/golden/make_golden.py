@@ -25,6 +25,7 @@ Fixtures written (all small, gzip'd JSON or npz):
   nnet_golden.npz        InflexionNNet(manual_seed 0) checksum + (planes -> P, v)
   train_golden.json.gz   NNetWrapper.train (32 channels, 2 epochs): losses + weight digests
   train_full_golden.json.gz  the same at 512 channels, 1 epoch (2 steps), dropout 0, + digests after step 1
+  train_full_sensitivity.json.gz  train_full again from initial weights moved by a few ulps (3 seeds)
   realnet_sensitivity.json.gz  first divergent move of the reference's real-net traces when its network's
                          weights, or its outputs, move by 1e-7 / 1e-6 relative
   realnet_branches.json.gz     the perturbed reference's traces past those divergent moves
@@ -881,6 +882,84 @@ def gen_train_full(np):
     _dump("train_full_golden.json.gz", out)
 
 
+def gen_train_full_sensitivity(np, seeds=(1, 2, 3)):
+    """The reference trainer's own rounding sensitivity at the full size: gen_train_full's run
+    again from initial weights moved by a few ulps (every parameter element times 1 + 2^-22 s,
+    s uniform in {-1, 0, 1}, per seed), same examples and batch draws.  Adam's first step moves
+    each weight by lr sign(g), so an element whose gradient sits at rounding level can step
+    either way; the spread of the update digests over these runs is the reference's own noise,
+    against which a GPU-order trainer is judged (tests/test_gpu_train.py)."""
+    import torch
+    import MCTS as mcts_mod
+    from Coach import Coach
+    from inflexion.InflexionGame import InflexionGame
+    import inflexion.pytorch.NNet as nn_mod
+    from inflexion.pytorch.NNet import NNetWrapper
+    from utils import dotdict
+    from stubnet import stub_eval
+    c = TRAIN_FULL_CFG
+
+    class StubNNet(NNetWrapper):
+        def __init__(self, game):
+            self.n_actions = game.max_actions
+
+        def predict(self, board):
+            return stub_eval(board, self.n_actions)
+
+    class RecNNet(NNetWrapper):
+        losses = []
+        step1 = None
+
+        def loss_pi(self, targets, outputs):
+            lp = super().loss_pi(targets, outputs)
+            self.losses.append([float(lp.item()), None])
+            if len(self.losses) == 2:
+                RecNNet.step1 = state_digest(np, self.nnet.state_dict(), c["proj_seed"])
+            return lp
+
+        def loss_v(self, targets, outputs):
+            lv = super().loss_v(targets, outputs)
+            self.losses[-1][1] = float(lv.item())
+            return lv
+
+    game = InflexionGame(7, max_turns=c["max_turns"], max_power=6)
+    args = dotdict({"numMCTSSims": c["sims"], "cpuct": c["cpuct"], "tempThreshold": c["temp_threshold"]})
+    stub = StubNNet(game)
+    np.random.seed(c["seed"])
+    ex = Coach(game, stub, args).executeEpisode((game.restarted(), mcts_mod.MCTS(stub, args)))
+    saved = dict(nn_mod.args)
+    out = {"config": c, "n_examples": len(ex), "perturbation": "p * (1 + 2^-22 s), s in {-1, 0, 1}", "runs": {}}
+    try:
+        nn_mod.args.num_channels = c["num_channels"]
+        nn_mod.args.epochs = c["epochs"]
+        nn_mod.args.dropout = 0.0
+        for seed in seeds:
+            torch.manual_seed(c["init_seed"])
+            w = RecNNet(game)
+            gen = torch.Generator().manual_seed(1000 + seed)
+            with torch.no_grad():
+                for prm in w.nnet.parameters():
+                    sgn = torch.randint(-1, 2, prm.shape, generator=gen).to(prm.dtype)
+                    prm.mul_(1 + sgn * 2.0 ** -22)
+            init = state_digest(np, w.nnet.state_dict(), c["proj_seed"])
+            RecNNet.losses = []
+            np.random.seed(c["batch_seed"])
+            torch.manual_seed(c["torch_seed"])
+            w.train(ex)
+            out["runs"][str(seed)] = {"init": init, "losses": RecNNet.losses, "step1": RecNNet.step1,
+                                      "final": state_digest(np, w.nnet.state_dict(), c["proj_seed"])}
+            print(f"  train_full_sensitivity {seed}: losses {RecNNet.losses}", flush=True)
+    finally:
+        nn_mod.args.clear()
+        nn_mod.args.update(saved)
+    # keep only what the test reads: the projections of the trained layers
+    keep = ("conv2.weight", "conv3.weight", "conv4.weight", "fc1.weight", "fc2.weight", "fc3.weight")
+    for r in out["runs"].values():
+        for ph in ("init", "step1", "final"):
+            r[ph] = {k: {"proj": v["proj"]} for k, v in r[ph].items() if k in keep}
+    _dump("train_full_sensitivity.json.gz", out)
+
+
 def main():
     _need_reference()
     import numpy as np
@@ -903,6 +982,7 @@ def main():
         "arena": lambda: gen_arena(np),
         "train": lambda: gen_train(np),
         "train_full": lambda: gen_train_full(np),
+        "train_full_sensitivity": lambda: gen_train_full_sensitivity(np),
         "sensitivity": lambda: gen_realnet_sensitivity(np),
         "sensitivity_othello": lambda: gen_realnet_sensitivity(np, othello=True),
         "branches": lambda: gen_realnet_branches(np),

@@ -80,11 +80,15 @@ def test_trainer_gpu_full_size(path):
     initial weights' forward on the reference's batch) within 2e-5 relative, the second batch's
     (the forward after the first Adam step) within 1e-3, and the update of every weight matrix
     whose gradient no BatchNorm cancels (conv2-4, fc1-3) after the first step and after the
-    second within 5e-2 of its size.  Adam's first step moves every weight by lr times the SIGN of
-    its gradient (m / sqrt(v) = g / |g|), so an element whose gradient is near the rounding noise
-    of a GPU-order sum can take the opposite step.  Measured on MI355X: first losses equal to
-    the printed digits, second within 1.9e-4; updates 3.5e-5 (fc3) to 1.3e-2 (conv3) after one
-    step, 4.5e-4 to 2.5e-2 after two (the printed errors list every layer)."""
+    second within 5e-2 of its size -- or within 1.25x the reference's own spread where that is
+    larger.  Adam's first step moves every weight by lr times the SIGN of its gradient (m / sqrt(v)
+    = g / |g|), so an element whose gradient is near the rounding noise of a sum can take the
+    opposite step: the reference itself, rerun from initial weights moved by a few ulps
+    (tests/golden/train_full_sensitivity.json.gz, 3 seeds, make_golden.py train_full_sensitivity),
+    moves conv3.weight's two-step update by 3.8-6.6e-2 of its size and the others by <= 2.9e-2.
+    Measured on MI355X (Winograd training kernels): first losses equal to the printed digits, second
+    within 1.9e-4; conv3.weight 3.1e-2 after one step, 4.1-5.2e-2 after two, every other layer
+    <= 3.2e-2 (the printed errors list every layer)."""
     import azg_amd  # noqa: F401
     from azg_amd.examples import ExampleSet
     from azg_amd.nnet import NNetWrapper
@@ -122,14 +126,20 @@ def test_trainer_gpu_full_size(path):
         np.testing.assert_allclose(losses[0], np.array(r["losses"][0]), rtol=2e-5)
         np.testing.assert_allclose(losses[1], np.array(r["losses"][1]), rtol=1e-3)
     final = _proj(w.nnet.state_dict(), c["proj_seed"])
-    errs = {}
+    sens = ol.load_json("train_full_sensitivity.json.gz")["runs"]
+    errs, tol = {}, {}
     for k in ("conv2.weight", "conv3.weight", "conv4.weight", "fc1.weight", "fc2.weight", "fc3.weight"):
         for name, got in (("step1", seen["step1"]), ("final", final)):
             d_ref = np.array(r[name][k]["proj"]) - np.array(r["init"][k]["proj"])
             d_gpu = got[k] - init[k]
             errs[f"{k} {name}"] = float(np.abs(d_gpu - d_ref).max() / np.abs(d_ref).max())
+            spread = max(float(np.abs(np.array(q[name][k]["proj"]) - np.array(q["init"][k]["proj"]) - d_ref).max()
+                               / np.abs(d_ref).max()) for q in sens.values())
+            tol[f"{k} {name}"] = max(5e-2, 1.25 * spread)
     print("update errors:", {k: f"{v:.1e}" for k, v in errs.items()})
-    assert max(errs.values()) < 5e-2, errs
+    print("tolerances:", {k: f"{v:.1e}" for k, v in tol.items()})
+    bad = {k: (v, tol[k]) for k, v in errs.items() if not v < tol[k]}
+    assert not bad, bad
 
 
 def test_graph_trainer_matches_eager():

@@ -98,6 +98,38 @@ def test_train_forward_matches_module():
         assert ew <= max(5 * el + 1e-5, 2e-2 if cancelled else 0.0), (k, ew, el)
 
 
+@pytest.mark.parametrize("B,D,n,K", [(512, 4, 7, 512), (3, 2, 6, 64), (130, 8, 8, 128), (1, 1, 5, 64), (67, 4, 7, 192)])
+def test_conv1_train_matches_torch(B, D, n, K):
+    """wino_train.Conv1Train (azg_train_conv1.hip) against torch's conv2d in f64: y within 1e-6 of
+    max |y|, dw and db within 1e-6 of their largest magnitude (f32 products, f64 partial sums),
+    deterministic (two backward passes bit-equal); board planes as the trainer feeds them (0/1 planes
+    and constant planes, channels_last)."""
+    import azg_amd  # noqa: F401
+    from azg_amd.wino_train import Conv1Train, conv1_train
+    torch.manual_seed(B + D + n + K)
+    conv = torch.nn.Conv2d(D, K, 3, stride=1, padding=1).cuda()
+    x = (torch.rand(B, D, n, n, device="cuda") < 0.3).float()
+    if D > 1:
+        x[:, D // 2:] = x[:, D // 2:, :1, :1]
+    x[0, 0, 0, 0] = 1.0
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = conv1_train(conv, x)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    g = torch.randn(B, K, n, n, device="cuda")
+    y.backward(g)
+    dw, db = conv.weight.grad.clone(), conv.bias.grad.clone()
+    conv.weight.grad = None
+    conv.bias.grad = None
+    Conv1Train.apply(x, conv.weight, conv.bias).backward(g)
+    assert torch.equal(conv.weight.grad, dw) and torch.equal(conv.bias.grad, db)
+    w64, b64 = conv.weight.detach().double().requires_grad_(), conv.bias.detach().double().requires_grad_()
+    y64 = torch.nn.functional.conv2d(x.double(), w64, b64, padding=1)
+    y64.backward(g.double())
+    for got, want in ((y, y64), (dw, w64.grad), (db, b64.grad)):
+        err = (got.double() - want).abs().max().item() / want.abs().max().item()
+        assert err <= 1e-6, err
+
+
 @pytest.mark.parametrize("B,H", [(512, 7), (512, 5), (64, 3), (2, 7)])
 def test_batchnorm_relu_matches_torch(B, H):
     """wino_train.BatchNormReLU (azg_train_bn.hip, NHWC, f64 sums) against torch's training-mode
