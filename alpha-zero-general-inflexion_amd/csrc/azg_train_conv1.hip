@@ -162,8 +162,9 @@ struct Wgrad {
 };
 
 bool c1_args_ok(const float* x, int64_t batch, int32_t depth, int32_t n, int32_t K) {
+    // (the forward's grid.y = batch / C1_IMG stays within the 65535 a launch dimension allows)
     return x && batch > 0 && depth >= 1 && depth <= C1_DMAX && n >= 1 && n <= C1_NMAX && K > 0 && K % 64 == 0 &&
-           batch <= (int64_t)1 << 31;
+           batch <= (int64_t)65535 * C1_IMG;
 }
 
 }  // namespace

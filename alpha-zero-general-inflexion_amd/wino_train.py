@@ -188,7 +188,7 @@ def _conv1_ok(conv, x):
             and conv.padding_mode == "zeros" and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
             and not x.requires_grad and x.is_contiguous(memory_format=torch.channels_last)
             and x.shape[1] == conv.in_channels and x.shape[1] <= 8 and x.shape[2] == x.shape[3] <= 8
-            and conv.out_channels % 64 == 0)
+            and conv.out_channels % 64 == 0 and 0 < x.shape[0] <= 262140)
 
 
 def conv1_train(conv, x):

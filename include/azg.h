@@ -434,7 +434,7 @@ int  azg_bn_relu_bwd_from_sums(const float* x, const float* dy, int64_t rows, in
                                float* co, void* stream);
 /* The trainer's conv1 (InflexionNNet.py:39: 3x3, stride 1, padding 1, on the board planes;
  * azg_train_conv1.hip): x NHWC [batch][n][n][depth] (the planes channels_last), w [K][depth][3][3],
- * depth <= 8, n <= 8, K % 64 == 0.  azg_conv1_train_fwd writes y NHWC [batch][n][n][K] = conv + bias
+ * depth <= 8, n <= 8, K % 64 == 0, batch <= 262140.  azg_conv1_train_fwd writes y NHWC [batch][n][n][K] = conv + bias
  * (bias may be null); azg_conv1_train_wgrad writes dw [K][depth][3][3] and db [K] (may be null) from
  * dy NHWC [batch][n][n][K], f64 partials in a fixed order (deterministic); work >= 64 K (9 depth + 1)
  * doubles.  (No input gradient: the planes need none.) */
