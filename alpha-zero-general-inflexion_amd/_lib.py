@@ -27,8 +27,16 @@ ERR = {0: "ok", -1: "bad argument", -2: "HIP error", -3: "node pool full", -4: "
        -5: "no valid action", -6: "bad call order"}
 
 
+ERR_NODE_POOL = -3
+ERR_PATH = -4
+
+
 class AzgError(RuntimeError):
-    pass
+    """A libazg call failed; `code` is its AZG_ERR_* value (None for errors raised in Python)."""
+
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 class Config(ctypes.Structure):
@@ -120,6 +128,9 @@ SIGNATURES = [
     ("azg_wt_split2_transpose", ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _VP]),
     ("azg_wt_pow2_scale", ctypes.c_int, [_VP, ctypes.c_float, _VP, _VP]),
     ("azg_wt_dw", ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _VP, _VP]),
+    ("azg_py_shuffle", ctypes.c_int, [_VP, _I64, _VP, ctypes.POINTER(_I32)]),
+    ("azg_adam_step", ctypes.c_int, [_I32, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_double, _VP]),
 ]
 
 _lib = None
@@ -181,5 +192,5 @@ def probes():
 def check(rc):
     if rc != 0:
         msg = lib().azg_last_error().decode(errors="replace")
-        raise AzgError(f"libazg: {ERR.get(rc, rc)} ({rc}): {msg}")
+        raise AzgError(f"libazg: {ERR.get(rc, rc)} ({rc}): {msg}", rc)
     return rc

@@ -21,8 +21,6 @@ GPU (examples.py) and `learn` runs the reference's iteration loop
 """
 import logging
 import os
-import pickle
-import random
 from collections import deque
 
 import numpy as np
@@ -89,13 +87,46 @@ class Coach:
             if not ongoing(game.outcome):
                 return build_examples(game, planes, pis, players, game, self.label_mode)
 
-    def _engine(self, num_games, evaluator, seed_base, first_game):
+    def _engine(self, num_games, evaluator, seed_base, first_game, node_capacity=0, max_depth=0):
         from .engine import SelfPlayEngine, game_spec
         name, n, max_turns = game_spec(self.game)
         return SelfPlayEngine(num_games, sims=int(self.args.numMCTSSims), cpuct=self.args.cpuct,
                               temp_threshold=int(self.args.tempThreshold), max_turns=max_turns, game=name, n=n,
                               seed_base=seed_base, first_game=first_game,
-                              evaluator=evaluator if evaluator is not None else self.evaluator())
+                              evaluator=evaluator if evaluator is not None else self.evaluator(),
+                              node_capacity=node_capacity, max_depth=max_depth)
+
+    def _capacity(self):
+        """The engine's per-game tree capacity for self-play: args.nodeCapacity / args.maxDepth
+        (0 or absent: the engine's defaults, 16 numMCTSSims + 128 nodes and a 256-node path)."""
+        get = self.args.get if hasattr(self.args, "get") else (lambda k, d=None: d)
+        return {"node_capacity": int(get("nodeCapacity", 0) or 0), "max_depth": int(get("maxDepth", 0) or 0)}
+
+    def _grow(self, cap, code):
+        """The capacity after a run that filled it: a full node pool (AZG_ERR_NODE_POOL) doubles the
+        nodes per game, a path deeper than max_depth (AZG_ERR_PATH) doubles the path.  Games are
+        seeded by their index and the tree's contents do not depend on the capacity (nodes are
+        found by key; GC frees by turn), so the rerun's records are those a large-enough first
+        run gives."""
+        from ._lib import ERR_NODE_POOL, ERR_PATH, AzgError
+        cap = dict(cap)
+        if code == ERR_NODE_POOL:
+            cur = cap["node_capacity"] or 16 * int(self.args.numMCTSSims) + 128
+            if 2 * cur >= 1 << 21:
+                raise AzgError(f"self-play: node pool full at {cur} nodes per game (the engine's limit is 2^21)",
+                               code)
+            cap["node_capacity"] = 2 * cur
+            log.warning("self-play: a game's node pool filled up; replaying with %d nodes per game", 2 * cur)
+        elif code == ERR_PATH:
+            cur = cap["max_depth"] or 256
+            if 2 * cur > 1 << 16:
+                raise AzgError(f"self-play: search path deeper than {cur}", code)
+            cap["max_depth"] = 2 * cur
+            log.warning("self-play: a search path outgrew max_depth; replaying with max_depth %d", 2 * cur)
+        else:
+            raise ValueError(code)
+        self.last_capacity = cap
+        return cap
 
     def evaluator(self, gemm="split"):
         """The leaf evaluator for the engine: an NNetWrapper's current weights as
@@ -108,18 +139,28 @@ class Coach:
         return self.nnet
 
     def _range_checked(self, run, evaluator):
-        """run(evaluator) -> result; if the split-fp16 network met an operand out of
-        fp16 range (FloatingPointError from SelfPlayEngine.check_evaluator), rerun
-        with nnet.replay_form.  Games are seeded by their index, so the rerun's
-        records are the ones a first f32 run would have produced."""
+        """run(evaluator, **capacity) -> result, rerun until it fits: if the split-fp16 network
+        met an operand out of fp16 range (FloatingPointError from SelfPlayEngine.check_evaluator),
+        with nnet.replay_form; if a game's tree outgrew the engine's node pool or path
+        (AzgError AZG_ERR_NODE_POOL / AZG_ERR_PATH), with twice that capacity (_grow).  Games are
+        seeded by their index, so the rerun's records are the ones a first run with that
+        evaluator and capacity would have produced."""
+        from ._lib import ERR_NODE_POOL, ERR_PATH, AzgError
         ev = evaluator if evaluator is not None else self.evaluator()
-        try:
-            return run(ev)
-        except FloatingPointError:
-            if evaluator is not None or ev is self.nnet:
-                raise
-            log.warning("self-play: split-fp16 operand out of range; replaying with the f32 replay form")
-            return run(self.evaluator(gemm="f32"))
+        cap = self._capacity()
+        self.last_capacity = cap
+        while True:
+            try:
+                return run(ev, **cap)
+            except FloatingPointError:
+                if evaluator is not None or ev is self.nnet or getattr(ev, "gemm", None) == "f32":
+                    raise
+                log.warning("self-play: split-fp16 operand out of range; replaying with the f32 replay form")
+                ev = self.evaluator(gemm="f32")
+            except AzgError as e:
+                if e.code not in (ERR_NODE_POOL, ERR_PATH):
+                    raise
+                cap = self._grow(cap, e.code)
 
     def native(self):
         """Whether the engine has rules kernels for self.game (else the generic host path)."""
@@ -145,8 +186,8 @@ class Coach:
             examples = [e for ex, _ in res for e in ex]
             return (examples, [r for _, r in res]) if return_records else examples
 
-        def run(ev):
-            eng = self._engine(num_games, ev, seed_base, first_game)
+        def run(ev, **cap):
+            eng = self._engine(num_games, ev, seed_base, first_game, **cap)
             try:
                 eng.play()
                 return eng.read_moves()
@@ -175,8 +216,8 @@ class Coach:
         if 0 < slots < num_games:
             # continuous batching: num_games games through `slots` engine slots
             # (azg_refill); same examples, game for game, as one slot per game
-            def run(ev):
-                eng = self._engine(slots, ev, seed_base, first_game)
+            def run(ev, **cap):
+                eng = self._engine(slots, ev, seed_base, first_game, **cap)
                 try:
                     return eng.play_games(num_games, first_game=first_game)
                 finally:
@@ -186,8 +227,8 @@ class Coach:
             return examples_from_records(name, n, max_turns, int(self.args.tempThreshold), r["moves"],
                                          r["actions"], r["counts"], self.label_mode, maxlen)
 
-        def run(ev):
-            eng = self._engine(num_games, ev, seed_base, first_game)
+        def run(ev, **cap):
+            eng = self._engine(num_games, ev, seed_base, first_game, **cap)
             try:
                 eng.play()
                 return engine_examples(eng, int(self.args.tempThreshold), self.label_mode, maxlen)
@@ -222,8 +263,8 @@ class Coach:
         if not self.native():
             return self._host_selfplay_iteration(first, eps, group, all_ranks)
 
-        def run(ev):
-            eng = self._engine(eps, ev, 0, first)
+        def run(ev, **cap):
+            eng = self._engine(eps, ev, 0, first, **cap)
             try:
                 eng.play()
             except BaseException:
@@ -231,37 +272,58 @@ class Coach:
                 raise
             return eng
         # The ranks agree on how self-play went before any of them enters the record
-        # exchange (flag: 0 ok, 1 a split-fp16 operand out of fp16 range, 2 any other
-        # error).  On 1 EVERY rank replays its games with nnet.replay_form, together: no
-        # rank waits in the gather while another replays (which could outlast the process
-        # group's timeout), and the iteration's records are those of an all-f32 run
-        # whatever the sharding.  On 2 every rank raises, instead of the healthy ranks
-        # blocking in the gather until the timeout.
+        # exchange: flags [fp16, pool, path, error] MAX-reduced (a split-fp16 operand out of
+        # fp16 range; a game's tree outgrew the node pool / the search path, AZG_ERR_NODE_POOL /
+        # AZG_ERR_PATH; anything else).  On fp16 or capacity EVERY rank
+        # replays its games -- with nnet.replay_form and / or twice the capacity -- together:
+        # no rank waits in the gather while another replays (which could outlast the process
+        # group's timeout), and the iteration's records are those of a first run with that
+        # evaluator and capacity whatever the sharding.  On an error every rank raises,
+        # instead of the healthy ranks blocking in the gather until the timeout.
+        from ._lib import ERR_NODE_POOL, ERR_PATH, AzgError
         ev = self.evaluator()
-        eng, flag_v, err = None, 0, None
-        try:
-            eng = run(ev)
-        except FloatingPointError as e:
-            flag_v, err = (2, e) if ev is self.nnet else (1, None)
-        except Exception as e:  # noqa: BLE001 -- reported to every rank, re-raised below
-            flag_v, err = 2, e
+        cap = self._capacity()
         dev = (torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl"
                else torch.device("cpu"))
-        flag = torch.tensor([flag_v], dtype=torch.int64, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-        flag_v = int(flag.item())
-        if flag_v == 2:
+        replayed_f32 = False
+        while True:
+            eng, flags, err = None, [0, 0, 0, 0], None
+            try:
+                eng = run(ev, **cap)
+            except FloatingPointError as e:
+                if ev is self.nnet or replayed_f32:
+                    flags[3], err = 1, e
+                else:
+                    flags[0] = 1
+            except AzgError as e:
+                if e.code == ERR_NODE_POOL:
+                    flags[1] = 1
+                elif e.code == ERR_PATH:
+                    flags[2] = 1
+                else:
+                    flags[3], err = 1, e
+            except Exception as e:  # noqa: BLE001 -- reported to every rank, re-raised below
+                flags[3], err = 1, e
+            flag = torch.tensor(flags, dtype=torch.int64, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+            f16, pool, path, bad = (int(x) for x in flag.tolist())
+            if not (f16 or pool or path or bad):
+                break
             if eng is not None:
                 eng.close()
-            if err is not None:
-                raise err
-            raise RuntimeError("self-play failed on another rank; this rank stops with it")
-        if flag_v == 1:
-            log.warning("self-play: split-fp16 operand out of range on a rank; all ranks replay with "
-                        "the f32 replay form")
-            if eng is not None:
-                eng.close()
-            eng = run(self.evaluator(gemm="f32"))
+            if bad:
+                if err is not None:
+                    raise err
+                raise RuntimeError("self-play failed on another rank; this rank stops with it")
+            if f16:
+                log.warning("self-play: split-fp16 operand out of range on a rank; all ranks replay with "
+                            "the f32 replay form")
+                ev, replayed_f32 = self.evaluator(gemm="f32"), True
+            if pool:
+                cap = self._grow(cap, ERR_NODE_POOL)
+            if path:
+                cap = self._grow(cap, ERR_PATH)
+        flag_v = int(replayed_f32)
         self.last_replayed_f32 = flag_v == 1
         try:
             rec, self.last_sent_bytes = gather_records(eng, dst=None if all_ranks else 0, group=group,
@@ -324,7 +386,7 @@ class Coach:
         weights need no broadcast; "rank0" gathers the records to rank 0, which trains
         alone and broadcasts its weights at the start of the next iteration."""
         import torch.distributed as dist
-        from .examples import ExampleSet
+        from .examples import ExampleSet, shuffle_perm
         distributed = group is not None or (dist.is_available() and dist.is_initialized()
                                             and dist.get_world_size() > 1)
         trainer = not distributed or dist.get_rank(group) == 0
@@ -357,9 +419,11 @@ class Coach:
             if trainer and self.args.get("saveExamples", True):
                 self.saveTrainExamples(i - 1)
             train = ExampleSet.cat(self.trainExamplesHistory)
-            perm = list(range(len(train)))
+            perm = np.arange(len(train), dtype=np.int64)
             if trainer:
-                random.shuffle(perm)  # shuffle(trainExamples), Coach.py:149
+                # shuffle(trainExamples), Coach.py:149: random.shuffle's permutation and stream
+                # position, drawn natively (examples.shuffle_perm; 4M examples: ~2.2 s in Python)
+                perm = shuffle_perm(len(train))
             if ddp:  # the trainer's shuffle on every rank
                 from .ddp import broadcast_perm
                 dev = self.nnet.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
@@ -409,31 +473,51 @@ class Coach:
         return "checkpoint_" + str(iteration) + ".pth.tar"
 
     def saveTrainExamples(self, iteration):
-        """Coach.py:170-176: the history as a pickled list of deques of
-        (board, pi, z) tuples in checkpoint_{iteration}.pth.tar.examples."""
+        """Coach.py:170-176: the history in checkpoint_{iteration}.pth.tar.examples.
+
+        args.examplesFormat "azg" (default): a JSON manifest naming one array file per window,
+        each window written once, when it is first saved (examples.write_manifest): a save
+        costs O(the iteration's new window) instead of re-pickling every window's Python
+        tuples (the reference's 20 x 200,000-example history is ~1.4e9 Python floats per
+        save).  "reference": the reference's own pickle of a list of deques of (board, pi, z)
+        tuples, streamed (examples.export_reference_examples), for a reference Coach to load.
+        loadTrainExamples reads both."""
+        from .examples import export_reference_examples, write_manifest
         folder = self.args.checkpoint
         os.makedirs(folder, exist_ok=True)
         filename = os.path.join(folder, self.getCheckpointFile(iteration) + ".examples")
-        hist = [deque(h.to_list() if hasattr(h, "to_list") else h, maxlen=int(self.args.maxlenOfQueue))
+        fmt = self.args.get("examplesFormat", "azg") if hasattr(self.args, "get") else "azg"
+        hist = [h if not isinstance(h, (list, deque)) else _as_example_set(h, self.nnet.device)
                 for h in self.trainExamplesHistory]
-        with open(filename, "wb+") as f:
-            pickle.Pickler(f).dump(hist)
+        if fmt == "reference":
+            export_reference_examples(hist, filename, int(self.args.maxlenOfQueue))
+        elif fmt == "azg":
+            self.last_windows_written = write_manifest(hist, filename, int(self.args.maxlenOfQueue), iteration)
+        else:
+            raise ValueError(f"examplesFormat must be 'azg' or 'reference', got {fmt!r}")
+
+    def export_reference_examples(self, filename):
+        """Write the current history as the reference's examples pickle (Coach.py:170-176)."""
+        from .examples import export_reference_examples
+        export_reference_examples([_as_example_set(h, self.nnet.device) for h in self.trainExamplesHistory],
+                                  filename, int(self.args.maxlenOfQueue))
 
     def loadTrainExamples(self, device=None):
-        """Coach.py:178-193 for a file this Coach (or the reference) wrote: the
-        history comes back as device ExampleSets; self-play of iteration 1 is
-        skipped.  A missing file raises FileNotFoundError (the reference asks on
-        stdin)."""
-        from .examples import ExampleSet
+        """Coach.py:178-193 for a file this Coach (either format) or the reference wrote: the
+        history comes back as device ExampleSets; self-play of iteration 1 is skipped.  A
+        missing file raises FileNotFoundError (the reference asks on stdin)."""
+        from .examples import read_examples_file
         model_file = os.path.join(self.args.load_folder_file[0], self.args.load_folder_file[1])
         examples_file = model_file + ".examples"
         if not os.path.isfile(examples_file):
             raise FileNotFoundError(f'File "{examples_file}" with trainExamples not found')
-        with open(examples_file, "rb") as f:
-            hist = pickle.Unpickler(f).load()
-        dev = device or self.nnet.device
-        self.trainExamplesHistory = [ExampleSet.from_list(list(h), dev) for h in hist if len(h)]
+        self.trainExamplesHistory = read_examples_file(examples_file, device or self.nnet.device)
         self.skipFirstSelfPlay = True
+
+
+def _as_example_set(h, device):
+    from .examples import ExampleSet
+    return h if isinstance(h, ExampleSet) else ExampleSet.from_list(list(h), device)
 
 
 def examples_from_record(template, actions, temps, counts, moves, label_mode="reference"):

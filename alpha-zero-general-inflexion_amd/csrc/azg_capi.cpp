@@ -39,6 +39,9 @@ int next_pow2(int x) {
 }
 }  // namespace
 
+// the thread-local error message for the host-only helpers (azg_host.cpp)
+int azg_host_fail(int code, const std::string& msg) { return fail(code, msg); }
+
 struct azg_engine {
     azg_config cfg;
     Dev d;

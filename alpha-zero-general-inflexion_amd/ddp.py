@@ -201,9 +201,10 @@ def train_examples_dp(wrapper, ex, group=None, stats=None):
     all-reduce's time on the compute stream (HIP events on every `stats["every"]`-th step,
     default 10, milliseconds summed in grad_allreduce_ms over grad_allreduce_timed steps)."""
     dev = wrapper.device
-    seed = rank_dropout_seed(group, dev if dist.get_backend(group) == "nccl" else None)
     devices = [dev.index if dev.index is not None else torch.cuda.current_device()] if dev.type == "cuda" else []
     with torch.random.fork_rng(devices=devices):
+        # drawn inside the fork (ADVICE r5): rank 0's draw does not move its restored generator
+        seed = rank_dropout_seed(group, dev if dist.get_backend(group) == "nccl" else None)
         torch.default_generator.manual_seed(seed)
         if dev.type == "cuda":
             with torch.cuda.device(devices[0]):
@@ -217,6 +218,7 @@ def train_examples_dp(wrapper, ex, group=None, stats=None):
 
 
 def _train_examples_dp(wrapper, ex, group, stats=None):
+    from .optim import FusedAdam
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     a = wrapper.args
@@ -265,12 +267,15 @@ def _train_examples_dp(wrapper, ex, group, stats=None):
                     ev1.record()
                     stats.setdefault("_events", []).append((ev0, ev1))
                 parts = _unflatten_dense_tensors(flat, grads + [losses[k]])
-                for p, g in zip(params, parts[:-1]):
-                    if p.grad is None:
-                        p.grad = g.clone()
-                    else:
-                        p.grad.copy_(g)
-                opt.step()
+                if isinstance(opt, FusedAdam):
+                    opt.step(grads=list(parts[:-1]))  # straight from the all-reduced buffer
+                else:
+                    for p, g in zip(params, parts[:-1]):
+                        if p.grad is None:
+                            p.grad = g.clone()
+                        else:
+                            p.grad.copy_(g)
+                    opt.step()
                 losses[k] = parts[-1]
                 k += 1
     finally:

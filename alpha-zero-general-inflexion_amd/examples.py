@@ -18,8 +18,26 @@ torch.FloatTensor(np.array(...)).  Nothing goes through host memory.
 (board int64 ndarray, pi list, z) tuples (Coach.py:89-90), e.g. for the
 `checkpoint_{i}.pth.tar.examples` pickle (Coach.py:170-176); pi values there
 are the f32 values the trainer sees.
+
+The examples file (Coach.saveTrainExamples, Coach.py:170-176).  The reference pickles the
+whole history -- numItersForTrainExamplesHistory windows of up to maxlenOfQueue examples
+(main.py:19,27: 20 x 200,000) -- as Python tuples every iteration: at 4096 games per
+iteration 1.37e9 Python floats (~44 GB of objects, ~19 GB pickled) per save.  Here each
+window is written ONCE, when it is first saved, as its own array file (`save_window`: planes
+in the smallest integer type that holds them exactly, pis as CSR rows -- at most
+numMCTSSims nonzeros per self-play row --, vs f32; numpy .npz, no pickle), and the examples
+file is a small JSON manifest naming the history's windows in order (`write_manifest`), so a
+save costs O(the new window).  `read_examples_file` loads a manifest or a reference-written
+pickle; `export_reference_examples` writes the reference's pickle (a list of deques of
+tuples) streamed window by window, for a reference Coach to load.
 """
 import ctypes
+import json
+import os
+import pickle
+import random
+import uuid
+from collections import deque
 
 import numpy as np
 import torch
@@ -60,13 +78,16 @@ class ExampleSet:
 
     def to_list(self):
         """Reference example tuples (board int64 [planes, n, n], pi list, z)."""
-        b = self.planes.cpu().numpy().astype(np.int64)
-        p = self.pis.cpu().numpy().astype(np.float64)
-        v = self.vs.cpu().numpy()
-        # z is +-result.value: int +-1 or float +-1e-4 (flags.py:32-36), restored exactly
-        z = [int(x) if abs(x) == 1.0 else (1e-4 if x > 0 else -1e-4) if abs(x) == np.float32(1e-4) else float(x)
-             for x in v.tolist()]
-        return [(b[i], p[i].tolist(), z[i]) for i in range(len(z))]
+        return list(self.iter_tuples())
+
+    def iter_tuples(self, chunk=8192):
+        """to_list()'s tuples generated `chunk` examples at a time (host memory O(chunk))."""
+        for c0 in range(0, len(self), chunk):
+            b = self.planes[c0:c0 + chunk].cpu().numpy().astype(np.int64)
+            p = self.pis[c0:c0 + chunk].cpu().numpy().astype(np.float64)
+            z = [_z_value(x) for x in self.vs[c0:c0 + chunk].cpu().numpy().tolist()]
+            for i in range(len(z)):
+                yield b[i], p[i].tolist(), z[i]
 
     @staticmethod
     def from_list(examples, device):
@@ -75,6 +96,172 @@ class ExampleSet:
         return ExampleSet(torch.as_tensor(np.array(boards).astype(np.float64), dtype=torch.float32, device=device),
                           torch.as_tensor(np.array(pis), dtype=torch.float32, device=device),
                           torch.as_tensor(np.array(vs).astype(np.float64), dtype=torch.float32, device=device))
+
+
+def _z_value(x):
+    """z as the reference stores it: +-result.value, an int +-1 or a float +-1e-4 (flags.py:32-36)."""
+    if abs(x) == 1.0:
+        return int(x)
+    if abs(x) == np.float32(1e-4):
+        return 1e-4 if x > 0 else -1e-4
+    return float(x)
+
+
+# ---------------------------------------------------------------- examples file
+FILE_FORMAT = "azg-examples"
+FILE_VERSION = 1
+WINDOW_DIR = "examples_windows"
+
+
+def shuffle_perm(n):
+    """Coach.py:149's shuffle(trainExamples) as an index permutation: the order
+    random.shuffle(list(range(n))) gives, drawn on the `random` module's global stream, which
+    is left where random.shuffle would leave it (libazg azg_py_shuffle, host code).  Returns
+    an int64 ndarray."""
+    version, internal, gauss = random.getstate()
+    mt = np.array(internal[:624], dtype=np.uint32)
+    pos = ctypes.c_int32(internal[624])
+    perm = np.arange(n, dtype=np.int64)
+    check(_lib.lib().azg_py_shuffle(perm.ctypes.data, int(n), mt.ctypes.data, ctypes.byref(pos)))
+    random.setstate((version, tuple(int(x) for x in mt) + (pos.value,), gauss))
+    return perm
+
+
+def _planes_int_dtype(planes):
+    """The smallest integer type holding every plane value exactly (planes are counts and 0/1
+    masks: the turn plane reaches max_turns), or None (then kept as f32)."""
+    if planes.numel() == 0:
+        return torch.int8
+    if not torch.equal(planes, planes.round()):
+        return None
+    lo, hi = (float(x) for x in torch.aminmax(planes))
+    for dt, lim in ((torch.int8, 127), (torch.int16, 32767), (torch.int32, 2 ** 31 - 1)):
+        if -lim - 1 <= lo and hi <= lim:
+            return dt
+    return None
+
+
+def save_window(ex, path):
+    """One history window as an array file: planes (smallest exact integer type), pis as CSR
+    (row_nnz u16, cols i16/i32, vals f32: the exact f32 values), vs f32.  Written to a
+    temporary name and renamed, so a reader never sees half a window."""
+    dev_planes = ex.planes
+    pdt = _planes_int_dtype(dev_planes)
+    planes = (dev_planes.to(pdt) if pdt is not None else dev_planes).cpu().numpy()
+    pis = ex.pis
+    A = int(pis.shape[1]) if pis.dim() == 2 else 0
+    nz = pis != 0
+    row_nnz = nz.sum(dim=1).to(torch.int32)
+    cols = nz.nonzero()[:, 1].to(torch.int16 if A <= 32767 else torch.int32)
+    vals = pis[nz]
+    arrays = dict(planes=planes, planes_shape=np.array(dev_planes.shape, dtype=np.int64),
+                  pis_shape=np.array(pis.shape, dtype=np.int64),
+                  row_nnz=row_nnz.cpu().numpy().astype(np.uint16 if A < 65536 else np.uint32),
+                  cols=cols.cpu().numpy(), vals=vals.cpu().numpy(), vs=ex.vs.cpu().numpy())
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        np.savez(f, **arrays)
+    os.replace(tmp, path)
+
+
+def load_window(path, device):
+    """save_window's file -> ExampleSet on `device` (f32, the trainer's layout)."""
+    with np.load(path, allow_pickle=False) as z:
+        planes = torch.as_tensor(z["planes"]).to(device).float().reshape(tuple(z["planes_shape"].tolist()))
+        E, A = (int(x) for x in z["pis_shape"])
+        row_nnz = torch.as_tensor(z["row_nnz"].astype(np.int64)).to(device)
+        cols = torch.as_tensor(z["cols"].astype(np.int64)).to(device)
+        vals = torch.as_tensor(z["vals"]).to(device)
+        vs = torch.as_tensor(z["vs"]).to(device)
+    pis = torch.zeros((E, A), dtype=torch.float32, device=device)
+    rows = torch.repeat_interleave(torch.arange(E, device=device), row_nnz)
+    pis[rows, cols] = vals
+    return ExampleSet(planes, pis, vs)
+
+
+def write_manifest(history, filename, maxlen=None, iteration=None):
+    """The examples file: a JSON manifest of the history's windows in order, each window saved
+    under <folder>/examples_windows/ the first time it is written (later saves name the same
+    file: O(new windows) per save).  history: ExampleSets (a loaded or saved one remembers its
+    file in `saved_path`).  Returns the number of windows written by this call."""
+    folder = os.path.dirname(os.path.abspath(filename))
+    wdir = os.path.join(folder, WINDOW_DIR)
+    os.makedirs(wdir, exist_ok=True)
+    written, entries = 0, []
+    for h in history:
+        if not isinstance(h, ExampleSet):
+            raise TypeError("write_manifest: the history holds ExampleSets (Coach.trainExamplesHistory)")
+        path = getattr(h, "saved_path", None)
+        if path is None or not os.path.isfile(path):
+            path = os.path.join(wdir, f"w_{uuid.uuid4().hex}.npz")
+            save_window(h, path)
+            h.saved_path = path
+            written += 1
+        entries.append({"file": os.path.relpath(path, folder), "examples": len(h)})
+    doc = {"format": FILE_FORMAT, "version": FILE_VERSION, "iteration": iteration, "maxlen": maxlen,
+           "windows": entries}
+    tmp = filename + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(doc, f)
+    os.replace(tmp, filename)
+    return written
+
+
+def is_manifest(filename):
+    with open(filename, "rb") as f:
+        head = f.read(1)
+    return head == b"{"
+
+
+def read_examples_file(filename, device, maxlen=None):
+    """An examples file -> list of device ExampleSets (empty windows dropped): a manifest
+    (write_manifest) or the reference's pickle (Coach.py:175-176, a list of deques of
+    (board, pi, z) tuples).  A reference pickle is unpickled as the reference's own
+    loadTrainExamples does (Coach.py:189) -- open only files you or a reference Coach wrote."""
+    if is_manifest(filename):
+        with open(filename) as f:
+            doc = json.load(f)
+        if doc.get("format") != FILE_FORMAT or int(doc.get("version", 0)) > FILE_VERSION:
+            raise ValueError(f"{filename}: not an {FILE_FORMAT} v{FILE_VERSION} manifest")
+        folder = os.path.dirname(os.path.abspath(filename))
+        out = []
+        for w in doc["windows"]:
+            path = os.path.join(folder, w["file"])
+            ex = load_window(path, device)
+            if len(ex) != int(w["examples"]):
+                raise ValueError(f"{path}: {len(ex)} examples, the manifest says {w['examples']}")
+            ex.saved_path = path
+            if len(ex):
+                out.append(ex)
+        return out
+    with open(filename, "rb") as f:
+        hist = pickle.Unpickler(f).load()
+    return [ExampleSet.from_list(list(h), device) for h in hist if len(h)]
+
+
+class _StreamedDeque:
+    """Pickles as deque(window's tuples, maxlen) -- the deque's own reduce form (type, ((),
+    maxlen), None, item iterator) -- with the items generated chunk by chunk."""
+
+    def __init__(self, ex, maxlen):
+        self.ex, self.maxlen = ex, maxlen
+
+    def __reduce_ex__(self, protocol):
+        return (deque, ((), self.maxlen), None, self.ex.iter_tuples())
+
+
+def export_reference_examples(history, filename, maxlen):
+    """The reference's examples file (Coach.py:170-176: Pickler(f).dump(trainExamplesHistory), a
+    list of deques of (board int64 ndarray, pi list, z) tuples) from device ExampleSets, for a
+    reference Coach's loadTrainExamples.  Streamed: the pickler runs in fast mode (no memo, so
+    written tuples are freed) over windows whose tuples are generated in chunks, so host memory
+    stays O(chunk) instead of the whole history's Python objects."""
+    tmp = filename + ".tmp"
+    with open(tmp, "wb", buffering=1 << 24) as f:
+        p = pickle.Pickler(f)
+        p.fast = True
+        p.dump([_StreamedDeque(h, maxlen) for h in history])
+    os.replace(tmp, filename)
 
 
 def examples_from_records(game_name, n, max_turns, temp_threshold, moves, actions, counts,

@@ -1078,9 +1078,15 @@ class NNetWrapper:
         return self.nnet(x)
 
     def _adam(self):
-        """torch.optim.Adam() as NNet.py:37 builds it; on the GPU in its capturable form (step count
-        and bias corrections on the device), the form _train_graph replays, so the eager and the
-        graph-replayed trainer take the same update (the CPU keeps the reference's exact Adam)."""
+        """torch.optim.Adam() as NNet.py:37 builds it.  On the GPU: args["optimizer"] "azg" (default)
+        is optim.FusedAdam, the capturable foreach form's arithmetic in one libazg launch per step;
+        "torch" is torch's own capturable form (step count and bias corrections on the device) --
+        either way the form _train_graph replays, so the eager and the graph-replayed trainer take
+        the same update.  The CPU keeps the reference's exact Adam."""
+        if (self.device.type == "cuda" and self.args.get("optimizer", "azg") == "azg"
+                and not self.args["fused_adam"]):
+            from .optim import FusedAdam
+            return FusedAdam(self.nnet.parameters())
         kw = {"capturable": True} if self.device.type == "cuda" else {}
         if self.args["fused_adam"]:
             kw["fused"] = True
@@ -1278,6 +1284,9 @@ class NNetWrapper:
                                 step()
                             graph = g
                         except RuntimeError as err:
+                            from ._lib import AzgError
+                            if isinstance(err, AzgError):  # a libazg argument / HIP error is not a refused capture
+                                raise
                             import warnings
                             warnings.warn(f"train_examples: the training step could not be captured as a HIP "
                                           f"graph ({err}); the remaining steps run eagerly")

@@ -455,6 +455,27 @@ int  azg_wt_pow2_scale(const uint32_t* amax, float target, float* out, void* str
 /* dw [k][c][3][3] = 2^-kd sum_e G_a^T dU_e G_b from dU [P][c][k] (the weights' adjoint transform). */
 int  azg_wt_dw(const float* dU, int32_t c, int32_t k, int32_t h_out, const uint32_t* dyamax, float* dw, void* stream);
 
+/* ---- the trainer's optimizer (azg_adam.hip) -------------------------------------------------
+ * azg_adam_step: torch.optim.Adam's step (NNet.py:37; the capturable foreach arithmetic of
+ * torch/optim/adam.py in f32, no weight decay / amsgrad) over nseg parameter tensors in one launch:
+ * params[i] / grads[i] device f32 pointers of counts[i] elements (host arrays of pointers); m, v
+ * flat f32 state buffers, 16-B aligned, segment i at offset sum_{j<i} round_up(counts[j], 4);
+ * *step a device f32 step counter, incremented by this call before the update (t = *step + 1).
+ * 1 <= nseg <= AZG_ADAM_MAX_SEG.  The segment table is a by-value kernel argument: a launch
+ * captured in a HIP graph replays with the pointers it was captured with. */
+#define AZG_ADAM_MAX_SEG 48
+int  azg_adam_step(int32_t nseg, float* const* params, const float* const* grads, const int64_t* counts,
+                   float* m, float* v, float* step, double lr, double beta1, double beta2, double eps,
+                   void* stream);
+
+/* ---- learn-loop host helpers (azg_host.cpp; no device work) ---------------------------------
+ * azg_py_shuffle: Python's random.shuffle (Lib/random.py: for i from n-1 down to 1, j =
+ * _randbelow(i + 1) by getrandbits rejection, swap) of x[0..n) in place, on the MT19937 state of
+ * the interpreter's `random` module: mt = random.getstate()[1][:624], *pos = its index, both
+ * advanced as the interpreter would; n < 2^32.  Replaces Coach.py:149's shuffle(trainExamples)
+ * over the example history (the permutation of list(range(n)) random.shuffle gives). */
+int  azg_py_shuffle(int64_t* x, int64_t n, uint32_t* mt, int32_t* pos);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,6 +33,12 @@ Fixtures written (all small, gzip'd JSON or npz):
                          self-play episodes (Coach.learn's second-iteration network): state_dict + pairs
   mcts_trained_*.json.gz, trained_sensitivity.json.gz, trained_branches.json.gz
                          the realnet traces / certificates with that network
+  peaked_net.json        the peaked-prior network: trained_net.npz with fc3 (weight and bias) times
+                         PEAKED_FC3_SCALE, a power of two (exact in f32): the trained network's logits
+                         sharpened so that the median root's largest valid prior is >= 0.3, the regime
+                         Coach.learn reaches after a few iterations; its prior statistics
+  mcts_peaked_*.json.gz, peaked_sensitivity.json.gz, peaked_branches.json.gz
+                         the realnet traces / certificates with the peaked network
 """
 import gzip
 import hashlib
@@ -164,7 +170,7 @@ def gen_pairwise(np):
 
 
 # -------------------------------------------------------------------------- MCTS
-def gen_mcts(np, quick, othello=False, realnet=False, toy=False, trained=False):
+def gen_mcts(np, quick, othello=False, realnet=False, toy=False, trained=False, peaked=False):
     """Reference Coach.executeEpisode + MCTS traces.  With othello=True the
     reference search is driven with this repo's builder-authored OthelloGame
     plugin (the reference has no Othello): the rules are ours, the search,
@@ -216,6 +222,8 @@ def gen_mcts(np, quick, othello=False, realnet=False, toy=False, trained=False):
             return super().predict(board)
 
     real_nets = {}
+    if peaked:
+        trained = True
     if trained:
         realnet = True
 
@@ -282,6 +290,8 @@ def gen_mcts(np, quick, othello=False, realnet=False, toy=False, trained=False):
             "trained_main": dict(max_turns=343, sims=25, cpuct=1, temp_threshold=30, seeds=list(range(8))),
             "trained_sims100": dict(max_turns=40, sims=100, cpuct=1, temp_threshold=30, seeds=[10, 11]),
         }
+        if peaked:
+            sets = {k.replace("trained", "peaked"): v for k, v in sets.items()}
     if othello:
         sets = {
             "othello6": dict(n=6, sims=25, cpuct=1, temp_threshold=15, seeds=list(range(500, 516))),
@@ -313,7 +323,7 @@ def gen_mcts(np, quick, othello=False, realnet=False, toy=False, trained=False):
                     torch.manual_seed(0)  # Inflexion 7x7: the network of nnet_golden.npz (gen_nnet)
                     real_nets[key] = CountingNNet(game)
                     if trained:
-                        load_trained(np, real_nets[key].nnet)
+                        load_trained(np, real_nets[key].nnet, peaked)
                 nnet = real_nets[key]
                 nnet.calls = 0
             else:
@@ -460,7 +470,7 @@ def gen_nnet(np, InflexionGame):
 
 
 # --------------------------------------------------------------- realnet sensitivity
-def gen_realnet_sensitivity(np, othello=False, trained=False):
+def gen_realnet_sensitivity(np, othello=False, trained=False, peaked=False):
     """How far do the reference's own real-network traces survive a change of its
     network far below the north_star's 1e-5 tolerance?  The reference Coach/MCTS
     (main.py's configuration, the seeds of mcts_realnet_main) is rerun with
@@ -491,8 +501,9 @@ def gen_realnet_sensitivity(np, othello=False, trained=False):
         bases = ["realnet_othello6", "realnet_othello8", "realnet_othello8_s200"]
         kinds = ("weights",)
     else:
-        bases = ["trained_main" if trained else "realnet_main"]
+        bases = ["peaked_main" if peaked else "trained_main" if trained else "realnet_main"]
         kinds = ("weights", "outputs")
+        trained = trained or peaked
 
     class NoisyNNet(NNetWrapper):
         eps = 0.0
@@ -526,7 +537,7 @@ def gen_realnet_sensitivity(np, othello=False, trained=False):
                 torch.manual_seed(0)
                 net = NoisyNNet(game0)
                 if trained:
-                    load_trained(np, net.nnet)
+                    load_trained(np, net.nnet, peaked)
                 NoisyNNet.eps = eps if kind == "outputs" else 0.0
                 if kind == "weights":
                     g = torch.Generator().manual_seed(12345)
@@ -556,10 +567,11 @@ def gen_realnet_sensitivity(np, othello=False, trained=False):
     if not othello:
         out["config"] = cfg
     _dump("realnet_sensitivity_othello.json.gz" if othello else
-          ("trained_sensitivity.json.gz" if trained else "realnet_sensitivity.json.gz"), out)
+          ("peaked_sensitivity.json.gz" if peaked else "trained_sensitivity.json.gz" if trained
+           else "realnet_sensitivity.json.gz"), out)
 
 
-def gen_realnet_branches(np, trained=False):
+def gen_realnet_branches(np, trained=False, peaked=False):
     """The other side of each certified near-tie: for every (eps, seed) whose reference trace
     diverges under the 1e-7 / 1e-6 weight perturbation of gen_realnet_sensitivity, the
     perturbed reference's whole trace from its first divergent move on (counts, action, turn,
@@ -573,10 +585,10 @@ def gen_realnet_branches(np, trained=False):
     from inflexion.pytorch.NNet import NNetWrapper
     from utils import dotdict
 
-    bname = "trained_main" if trained else "realnet_main"
+    trained = trained or peaked
+    bname = "peaked_main" if peaked else "trained_main" if trained else "realnet_main"
     base = json.load(gzip.open(os.path.join(HERE, f"mcts_{bname}.json.gz"), "rt"))
-    sens = json.load(gzip.open(os.path.join(HERE, "trained_sensitivity.json.gz" if trained
-                                            else "realnet_sensitivity.json.gz"), "rt"))
+    sens = json.load(gzip.open(os.path.join(HERE, f"{bname.split('_')[0]}_sensitivity.json.gz"), "rt"))
     cfg = base["config"]
     game0 = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
     rec = {"actions": [], "last": None, "in_search": False}
@@ -614,7 +626,7 @@ def gen_realnet_branches(np, trained=False):
             torch.manual_seed(0)
             net = NNetWrapper(game0)
             if trained:
-                load_trained(np, net.nnet)
+                load_trained(np, net.nnet, peaked)
             g = torch.Generator().manual_seed(12345)  # the perturbation of gen_realnet_sensitivity
             with torch.no_grad():
                 for prm in net.nnet.parameters():
@@ -643,7 +655,7 @@ def gen_realnet_branches(np, trained=False):
                       f"{time.time() - t0:.1f}s", flush=True)
     finally:
         InflexionGame.to_next_state = orig_tns
-    _dump("trained_branches.json.gz" if trained else "realnet_branches.json.gz", out)
+    _dump(f"{bname.split('_')[0]}_branches.json.gz", out)
 
 
 # ------------------------------------------------------------------ trained network
@@ -652,12 +664,53 @@ TRAINED_CFG = dict(example_seeds=[1000, 1001, 1002], max_turns=343, sims=25, cpu
 TRAINED_FILE = "trained_net.npz"
 
 
-def load_trained(np, module):
-    """Load trained_net.npz's state_dict into a reference (or this repo's) InflexionNNet."""
+PEAKED_FC3_SCALE = 16.0
+
+
+def load_trained(np, module, peaked=False):
+    """Load trained_net.npz's state_dict into a reference (or this repo's) InflexionNNet
+    (peaked: fc3's weight and bias then multiplied by PEAKED_FC3_SCALE, exactly)."""
     import torch
     d = np.load(os.path.join(HERE, TRAINED_FILE))
     sd = {k[3:].replace("__", "."): torch.from_numpy(d[k].copy()) for k in d.files if k.startswith("sd_")}
+    if peaked:
+        sd["fc3.weight"] = sd["fc3.weight"] * PEAKED_FC3_SCALE
+        sd["fc3.bias"] = sd["fc3.bias"] * PEAKED_FC3_SCALE
     module.load_state_dict(sd)
+
+
+def gen_peaked_net(np, InflexionGame):
+    """The peaked-prior network's definition and prior statistics (peaked_net.json): the reference
+    NNetWrapper with trained_net.npz loaded and fc3 scaled by PEAKED_FC3_SCALE (a power of two, so
+    the scaled weights are exact) -- log_softmax(s z) sharpens the trained network's policy without
+    reordering it.  Statistics: the largest valid-action prior (MCTS.py:95-97's masked,
+    renormalised Ps) at every 4th root of the trained_main traces' games, for the trained and the
+    peaked network (median and 10th / 90th percentiles)."""
+    import torch
+    from flags import PlayerColour
+    from inflexion.pytorch.NNet import NNetWrapper
+    base = json.load(gzip.open(os.path.join(HERE, "mcts_trained_main.json.gz"), "rt"))
+    game = InflexionGame(7, max_turns=343, max_power=6)
+    stats = {}
+    for peaked in (False, True):
+        torch.manual_seed(0)
+        w = NNetWrapper(game)
+        load_trained(np, w.nnet, peaked)
+        tops = []
+        for ep in base["episodes"]:
+            for mv in ep["moves"][::4]:
+                g = game.restarted()
+                g._board = np.asarray(mv["board"]).reshape(7, 7).astype(g._board.dtype)
+                g._curr_turn = mv["turn"]
+                g._player = PlayerColour.RED if mv["turn"] % 2 == 0 else PlayerColour.BLUE
+                p, _ = w.predict(g.to_planes())
+                pv = p * g.valid_actions_mask()
+                tops.append(float(pv.max() / pv.sum()))
+        stats["peaked" if peaked else "trained"] = {
+            "roots": len(tops), "median_top_prior": float(np.median(tops)),
+            "p10_top_prior": float(np.percentile(tops, 10)), "p90_top_prior": float(np.percentile(tops, 90))}
+        print(f"  {'peaked' if peaked else 'trained'}: {stats['peaked' if peaked else 'trained']}", flush=True)
+    _dump("peaked_net.json.gz", {"base": TRAINED_FILE, "fc3_scale": PEAKED_FC3_SCALE, "root_priors": stats})
 
 
 def gen_trained_net(np, InflexionGame):
@@ -990,6 +1043,10 @@ def main():
         "trained": lambda: gen_mcts(np, quick, trained=True),
         "trained_sensitivity": lambda: gen_realnet_sensitivity(np, trained=True),
         "trained_branches": lambda: gen_realnet_branches(np, trained=True),
+        "peaked_net": lambda: gen_peaked_net(np, InflexionGame),
+        "peaked": lambda: gen_mcts(np, quick, peaked=True),
+        "peaked_sensitivity": lambda: gen_realnet_sensitivity(np, peaked=True),
+        "peaked_branches": lambda: gen_realnet_branches(np, peaked=True),
     }
     for name, fn in jobs.items():
         if only and name not in only:

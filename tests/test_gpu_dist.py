@@ -217,6 +217,52 @@ def test_overflow_on_one_rank_replays_all_ranks():
     assert (vs == ref.vs.cpu().numpy()).all()
 
 
+def _pool_worker(rank, world, port, q):
+    """Rank 1's node pool is far too small (24 nodes per game): its games fail with
+    AZG_ERR_NODE_POOL, every rank learns of it before the gather, and all replay with doubled
+    capacities until rank 1's games fit."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import azg_amd  # noqa: F401
+        from azg_amd.coach import Coach
+        from azg_amd.inflexion import InflexionGame
+        torch.cuda.set_device(0)
+        game = InflexionGame(7, max_turns=12, max_power=6)
+        args = Args(numEps=4, tempThreshold=5, maxlenOfQueue=10**6, numMCTSSims=10, cpuct=1,
+                    nodeCapacity=24 if rank == 1 else 0)
+        c = Coach(game, "stub", args)
+        ex = c._selfplay_iteration(1, None, all_ranks=True)
+        q.put((rank, {"cap": c.last_capacity, "ex": (ex.planes.cpu().numpy(), ex.pis.cpu().numpy(),
+                                                      ex.vs.cpu().numpy())}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_full_node_pool_on_one_rank_replays_all_ranks():
+    import azg_amd  # noqa: F401
+    from azg_amd.engine import SelfPlayEngine
+    from azg_amd.examples import engine_examples
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pool_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1]["cap"]["node_capacity"] >= 48 and res[0]["cap"]["node_capacity"] > 0
+    eng = SelfPlayEngine(8, sims=10, max_turns=12, temp_threshold=5)
+    eng.play()
+    ref = engine_examples(eng, 5, maxlen=10**6)
+    for r in (0, 1):
+        planes, pis, vs = res[r]["ex"]
+        assert (planes == ref.planes.cpu().numpy()).all() and (pis == ref.pis.cpu().numpy()).all()
+        assert (vs == ref.vs.cpu().numpy()).all()
+
+
 def test_bench_two_ranks_learn_iteration():
     """`bench.py --gpus 2 --learn-iteration on`, rehearsed as two ranks on
     one GPU over gloo: the launcher starts the ranks itself, rank 0 prints one JSON line whose

@@ -72,6 +72,38 @@ def test_golden_traces_bit_exact(azg, name):
     assert st["expansions"] == exp_total
 
 
+class Args(dict):
+    __getattr__ = dict.__getitem__
+
+
+@pytest.mark.parametrize("name,cap", [("deep", 0), ("short", 24), ("main", 64)])
+def test_coach_recovers_a_full_node_pool(azg, name, cap):
+    """Coach self-play whose node pool fills up (AZG_ERR_NODE_POOL) replays its games
+    with twice the nodes per game (Coach._grow) instead of aborting the iteration, and the records
+    are still the reference's, bit for bit.  `deep` (400 sims, 24 turns) at the engine's default
+    capacity (16 x 400 + 128 nodes); `short` / `main` forced to 24 / 64 nodes per game, so the
+    pool overflows in the first moves and is doubled until it fits."""
+    from azg_amd.coach import Coach
+    from azg_amd.inflexion import InflexionGame
+    data = ol.load_json(f"mcts_{name}.json.gz")
+    cfg, eps = data["config"], data["episodes"]
+    seeds = [ep["seed"] for ep in eps]
+    game = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
+    c = Coach(game, "stub", Args(numMCTSSims=cfg["sims"], cpuct=cfg["cpuct"], tempThreshold=cfg["temp_threshold"],
+                                 nodeCapacity=cap))
+    ex, rec = c.selfplay_batch(len(eps), first_game=seeds[0], return_records=True)
+    used = c.last_capacity["node_capacity"]
+    print(f"{name}: nodeCapacity {cap or 'default'} -> {used or 'default'} nodes per game")
+    if cap:
+        assert used >= 2 * cap
+    for i, ep in enumerate(eps):
+        assert rec["moves"][i] == ep["n_moves"], f"seed {ep['seed']}"
+        for m, mv in enumerate(ep["moves"]):
+            assert np.array_equal(rec["counts"][i, m], ol.golden_counts(mv)), f"seed {ep['seed']} move {m}"
+            assert rec["actions"][i, m] == mv["action"], f"seed {ep['seed']} move {m}"
+    assert len(ex) == sum(ep["n_examples"] for ep in eps)
+
+
 def test_random_seeds_vs_oracle(azg):
     cfg = dict(sims=25, cpuct=1, temp_threshold=30, max_turns=60)
     seeds = list(range(1000, 1096))

@@ -44,8 +44,8 @@ def run(label, channels_last=False, benchmark=False, batches=30, dtype="f32", fu
 
 
 if __name__ == "__main__":
-    if sys.argv[1:] == ["f32"]:  # the default trainer alone (e.g. under rocprofv3: kernel time vs wall)
-        run("nchw")
+    if sys.argv[1:2] == ["f32"]:  # the default trainer alone (e.g. under rocprofv3: kernel time vs wall)
+        run("nchw", batches=int(sys.argv[2]) if len(sys.argv) > 2 else 30)
         sys.exit(0)
     if sys.argv[1:] == ["conv"]:  # the Winograd training convolutions against the library ones, alternating
         for _ in range(3):
