@@ -128,6 +128,12 @@ SIGNATURES = [
     ("azg_wt_split2_transpose", ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _VP]),
     ("azg_wt_pow2_scale", ctypes.c_int, [_VP, ctypes.c_float, _VP, _VP]),
     ("azg_wt_dw", ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _VP, _VP]),
+    ("azg_wt_dy_stats", ctypes.c_int, [_VP, _I64, _I32, _VP, _VP, _VP, _VP]),
+    ("azg_small_mfma_layout", ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _VP]),
+    ("azg_small_conv_mfma", ctypes.c_int, [_VP, _I64, _I32, _I32, _I32, _I32, _I32, _VP, _I32, _I32, _VP, _I32, _VP,
+                                           _I32, _VP, _I64, _VP, _I32, _VP, _VP, _I32, _VP]),
+    ("azg_examples_rows", ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _I32, _I32, _I32, _I64,
+                                         _VP, _VP, _VP, ctypes.POINTER(_I64), _VP]),
     ("azg_py_shuffle", ctypes.c_int, [_VP, _I64, _VP, ctypes.POINTER(_I32)]),
     ("azg_adam_step", ctypes.c_int, [_I32, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_double, ctypes.c_double, _VP]),

@@ -525,8 +525,8 @@ def examples_from_record(template, actions, temps, counts, moves, label_mode="re
     g = template.restarted()
     planes, pis, players = [], [], []
     for m in range(moves):
-        c = counts[m].astype(np.int64)
-        if temps[m]:
+        if temps[m]:  # (only temperature-1 moves read their counts: rank-gathered records hold just those rows)
+            c = counts[m].astype(np.int64)
             pi = c / c.sum()
         else:
             pi = np.zeros(len(c), dtype=np.int8)

@@ -474,9 +474,19 @@ int azg_examples(int32_t game_kind, int32_t n, int32_t max_turns, int32_t temp_t
                  int32_t max_moves, const int32_t* moves, const int32_t* actions, const void* counts,
                  int32_t counts_bytes, int32_t label_mode, int64_t maxlen, float* planes, float* pis, float* vs,
                  int64_t* count, void* stream) {
+    return azg_examples_rows(game_kind, n, max_turns, temp_threshold, num_games, max_moves, moves, actions, counts,
+                             max_moves, counts_bytes, label_mode, maxlen, planes, pis, vs, count, stream);
+}
+
+int azg_examples_rows(int32_t game_kind, int32_t n, int32_t max_turns, int32_t temp_threshold, int32_t num_games,
+                      int32_t max_moves, const int32_t* moves, const int32_t* actions, const void* counts,
+                      int32_t count_rows, int32_t counts_bytes, int32_t label_mode, int64_t maxlen, float* planes,
+                      float* pis, float* vs, int64_t* count, void* stream) {
     azg::GameOps ops;
     if (!azg::game_ops(game_kind, n, &ops)) return fail(AZG_ERR_ARG, "unsupported game kind / size");
-    if (num_games < 0 || max_moves <= 0 || max_moves > 65535 || !moves || !actions || !counts || !count ||
+    if (count_rows < 0 || count_rows > max_moves || (count_rows < max_moves && count_rows < temp_threshold - 1))
+        return fail(AZG_ERR_ARG, "azg_examples_rows: count_rows must cover the temperature-1 moves");
+    if (num_games < 0 || max_moves <= 0 || max_moves > 65535 || !moves || !actions || (!counts && count_rows) || !count ||
         (counts_bytes != 2 && counts_bytes != 4) || (label_mode != 0 && label_mode != 1) || maxlen < 0 ||
         (maxlen > 0 && (!planes || !pis || !vs)))
         return fail(AZG_ERR_ARG, "bad azg_examples argument");
@@ -494,6 +504,7 @@ int azg_examples(int32_t game_kind, int32_t n, int32_t max_turns, int32_t temp_t
     X.actions = actions;
     X.counts16 = counts_bytes == 2 ? (const int16_t*)counts : nullptr;
     X.counts32 = counts_bytes == 4 ? (const int32_t*)counts : nullptr;
+    X.CR = count_rows;
     X.planes = planes;
     X.pis = pis;
     X.vs = vs;

@@ -1566,8 +1566,9 @@ __global__ __launch_bounds__(256) void emit_kernel(ExampleArgs X) {
     const int temp = (m + 1) < X.temp_threshold;  // episodeStep < tempThreshold (Coach.py:68)
     const int action = X.actions[row];
     long long part = 0;
+    const size_t crow = (size_t)g * X.CR + m;  // the move's count row (moves past CR: zero counts)
     for (int a = tid; a < R::A; a += 256) {
-        const int c = X.counts16 ? (int)X.counts16[row * R::A + a] : X.counts32[row * R::A + a];
+        const int c = m >= X.CR ? 0 : X.counts16 ? (int)X.counts16[crow * R::A + a] : X.counts32[crow * R::A + a];
         s_pi[a] = (float)c;  // exact: counts < 2^24
         part += c;
     }

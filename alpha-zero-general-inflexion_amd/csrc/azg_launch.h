@@ -22,8 +22,9 @@ struct ExampleArgs {
     int G, MM, max_turns, temp_threshold, label_mode, g0;
     const int32_t* moves;     // [G]
     const int32_t* actions;   // [G*MM]
-    const int16_t* counts16;  // [G*MM*A] (one of the two)
+    const int16_t* counts16;  // [G*CR*A] (one of the two)
     const int32_t* counts32;
+    int CR;                   // count rows per game (<= MM: moves from CR on are read as zero counts)
     MoveKey* keys;            // [G*MM] scratch
     int32_t* status;          // [G]
     float* zval;              // [G]

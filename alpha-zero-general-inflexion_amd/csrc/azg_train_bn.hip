@@ -106,6 +106,58 @@ __global__ __launch_bounds__(BN_T) void bn_sums_kernel(const double* __restrict_
     sums[C + c] = s2;
 }
 
+// The convolution backward's dy statistics in one read of dy [rows][C] (wino_train.WinogradConv3x3.backward):
+// per block the per-channel partial sums (f64, the second half of the part row zero) and max |dy|;
+// dy_finish_kernel sums the parts in order (db = dy.sum over batch, h, w: the conv bias's gradient)
+// and max-reduces the block maxima into *amax (the bits of max |dy|, the dM scale's input).  Replaces a
+// memset + azg_absmax's pass + torch's reduction (38.7 us per layer and step at conv2's 51 MB,
+// profiles/r06_prof_train_probe_adam.md).
+__global__ __launch_bounds__(BN_T) void dy_part_kernel(const float4* __restrict__ dy, long long rows, int C4,
+                                                       double* __restrict__ part, float* __restrict__ pmax) {
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float m = 0.f;
+    rows_of_block(rows, C4, [&](long long r, int q) {
+        const float4 v = dy[r * C4 + q];
+        a[0] += (double)v.x;
+        a[1] += (double)v.y;
+        a[2] += (double)v.z;
+        a[3] += (double)v.w;
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    });
+    block_sum_store(a, C4, part);
+    __shared__ float wm[BN_T / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float b = wm[0];
+#pragma unroll
+        for (int q = 1; q < BN_T / 64; ++q) b = fmaxf(b, wm[q]);
+        pmax[blockIdx.x] = b;
+    }
+}
+
+// one wave per channel: db[c] = the parts' sums in order (f32); the wave of channel 0 also writes
+// *amax = bits of the largest block maximum (non-negative floats order as their bits)
+__global__ __launch_bounds__(BN_T) void dy_finish_kernel(const double* __restrict__ part, const float* __restrict__ pmax,
+                                                         int nparts, int C, float* __restrict__ db,
+                                                         unsigned* __restrict__ amax) {
+    const int c = blockIdx.x * (BN_T / 64) + (int)(threadIdx.x >> 6);
+    if (c >= C) return;  // wave-uniform
+    double s, s2;
+    channel_sums(part, nparts, C, c, s, s2);
+    const int lane = threadIdx.x & 63;
+    if (lane == 0 && db) db[c] = (float)s;
+    if (c == 0) {
+        float m = 0.f;
+        for (int p = lane; p < nparts; p += 64) m = fmaxf(m, pmax[p]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        if (lane == 0) *amax = __float_as_uint(m);
+    }
+}
+
 // per channel, from (sum x, sum x^2) over n rows (every rank's, data-parallel): mean, var, scale (f32),
 // running stats
 __global__ __launch_bounds__(BN_T) void bn_finalize_kernel(const double* __restrict__ sums, int C, long long n,
@@ -284,6 +336,20 @@ extern "C" int azg_bn_relu_bwd_from_sums(const float* x, const float* dy, int64_
     const long long n4 = rows * C4;
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(n4)), dim3(BN_T), 0, st, (const float4*)x,
                        (const float4*)dy, (const float4*)sv, (const float4*)co, n4, C4, (float4*)dx);
+    return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+
+// *amax = bits of max |dy| and db [C] = dy summed over the rows (db may be null), dy [rows][C] f32;
+// work >= 2 * 512 * C doubles + 512 floats
+extern "C" int azg_wt_dy_stats(const float* dy, int64_t rows, int32_t C, uint32_t* amax, float* db, double* work,
+                               void* stream) {
+    if (!bn_args_ok(dy, rows, C) || !amax || !work) return AZG_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    float* pmax = reinterpret_cast<float*>(work + (size_t)2 * BN_PARTS * C);
+    hipLaunchKernelGGL(dy_part_kernel, dim3(BN_PARTS), dim3(BN_T), 0, st, (const float4*)dy, (long long)rows, C / 4,
+                       work, pmax);
+    hipLaunchKernelGGL(dy_finish_kernel, dim3((C + BN_T / 64 - 1) / (BN_T / 64)), dim3(BN_T), 0, st, work, pmax,
+                       BN_PARTS, C, db, amax);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 

@@ -17,6 +17,13 @@
 //    coalesced; ~100 terms a lane at B = 512), the 4 waves' partials are added in f64 in wave
 //    order into work[chunk][K][9 D + 1]; c1_wgrad_finish_kernel sums the chunks in order in f64.
 //    Fixed summation order (deterministic).
+//  * c1_fwd_row_kernel<D, N> / c1_wgrad_row_kernel<D, N> (round 6; the boards' D in {2, 4} and
+//    N in {6, 7, 8}): the same block decomposition, but a wave takes whole output rows: the row's
+//    3 x (N + 2) x D inputs are read from LDS once (D-wide vector reads of one broadcast address)
+//    into registers and feed all N outputs of the row, instead of 9 D LDS reads per output -- the
+//    per-pixel kernels were LDS-issue-bound (62 / 58 us per step at B = 512, 0.8 TB/s on y / dy;
+//    profiles/r06_prof_train_probe*.md).  The forward keeps the per-pixel kernel's summation order
+//    (taps in (c, r, s) order, then the bias): bit-identical y.
 #include <hip/hip_runtime.h>
 
 #include "../../include/azg.h"
@@ -68,6 +75,141 @@ __global__ __launch_bounds__(C1_T) void c1_fwd_kernel(const float* __restrict__ 
 #pragma unroll
                 for (int s = 0; s < 3; ++s) acc = fmaf(wr[c * 9 + r * 3 + s], xb[((oy + r) * pn + ox + s) * D + c], acc);
         y[((b0 + img) * hw + p) * K + k] = acc + bk;
+    }
+}
+
+// the padded input rows oy .. oy + 2 of one staged image into registers (uniform across lanes)
+template <int D, int N>
+__device__ __forceinline__ void c1_row_inputs(const float* xb, int oy, float (&xr)[3][N + 2][D]) {
+    constexpr int PN = N + 2;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int cx = 0; cx < PN; ++cx) {
+            const float* src = xb + ((oy + r) * PN + cx) * D;
+            if constexpr (D == 4) {
+                const float4 v = *reinterpret_cast<const float4*>(src);
+                xr[r][cx][0] = v.x, xr[r][cx][1] = v.y, xr[r][cx][2] = v.z, xr[r][cx][3] = v.w;
+            } else if constexpr (D == 2) {
+                const float2 v = *reinterpret_cast<const float2*>(src);
+                xr[r][cx][0] = v.x, xr[r][cx][1] = v.y;
+            } else {
+#pragma unroll
+                for (int c = 0; c < D; ++c) xr[r][cx][c] = src[c];
+            }
+        }
+}
+
+constexpr int C1_RIMG = 8;  // images per block of the row kernels
+
+template <int D, int N>
+__global__ __launch_bounds__(C1_T) void c1_fwd_row_kernel(const float* __restrict__ x, long long B,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ bias, int K,
+                                                          float* __restrict__ y) {
+    constexpr int PN = N + 2, HW = N * N;
+    __shared__ __attribute__((aligned(16))) float xs[C1_RIMG * PN * PN * D];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int k = blockIdx.x * 64 + lane;
+    const long long b0 = (long long)blockIdx.y * C1_RIMG;
+    const int nimg = (int)min((long long)C1_RIMG, B - b0);
+    float wr[9 * D];
+#pragma unroll
+    for (int j = 0; j < 9 * D; ++j) wr[j] = w[(long long)k * 9 * D + j];  // [c][r][s]
+    const float bk = bias ? bias[k] : 0.f;
+    c1_stage<D>(x, xs, b0, nimg, N);
+    __syncthreads();
+    for (int it = wv; it < nimg * N; it += C1_T / 64) {
+        const int img = it / N, oy = it - img * N;
+        float xr[3][PN][D];
+        c1_row_inputs<D, N>(xs + img * PN * PN * D, oy, xr);
+        float acc[N];
+#pragma unroll
+        for (int ox = 0; ox < N; ++ox) acc[ox] = 0.f;
+#pragma unroll
+        for (int c = 0; c < D; ++c)
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int s = 0; s < 3; ++s)
+#pragma unroll
+                    for (int ox = 0; ox < N; ++ox) acc[ox] = fmaf(wr[c * 9 + r * 3 + s], xr[r][ox + s][c], acc[ox]);
+        float* yr = y + ((b0 + img) * HW + (long long)oy * N) * K + k;
+#pragma unroll
+        for (int ox = 0; ox < N; ++ox) yr[(long long)ox * K] = acc[ox] + bk;
+    }
+}
+
+template <int D, int N>
+__global__ __launch_bounds__(C1_T) void c1_wgrad_row_kernel(const float* __restrict__ x,
+                                                            const float* __restrict__ dy, long long B, int K,
+                                                            long long per_chunk, double* __restrict__ work) {
+    constexpr int J = 9 * D + 1, PN = N + 2, HW = N * N;
+    __shared__ __attribute__((aligned(16))) float xs[C1_RIMG * PN * PN * D];
+    __shared__ float red[4][J][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int k = blockIdx.x * 64 + lane;
+    const long long c0 = (long long)blockIdx.y * per_chunk, c1 = min(B, c0 + per_chunk);
+    float acc[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j] = 0.f;
+    for (long long b0 = c0; b0 < c1; b0 += C1_RIMG) {
+        const int nimg = (int)min((long long)C1_RIMG, c1 - b0);
+        __syncthreads();  // (the previous group's reads of xs are done)
+        c1_stage<D>(x, xs, b0, nimg, N);
+        __syncthreads();
+        for (int it = wv; it < nimg * N; it += C1_T / 64) {
+            const int img = it / N, oy = it - img * N;
+            const float* gr = dy + ((b0 + img) * HW + (long long)oy * N) * K + k;
+            float g[N];
+#pragma unroll
+            for (int ox = 0; ox < N; ++ox) g[ox] = gr[(long long)ox * K];
+            float xr[3][PN][D];
+            c1_row_inputs<D, N>(xs + img * PN * PN * D, oy, xr);
+#pragma unroll
+            for (int c = 0; c < D; ++c)
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int s = 0; s < 3; ++s)
+#pragma unroll
+                        for (int ox = 0; ox < N; ++ox)
+                            acc[c * 9 + r * 3 + s] = fmaf(g[ox], xr[r][ox + s][c], acc[c * 9 + r * 3 + s]);
+#pragma unroll
+            for (int ox = 0; ox < N; ++ox) acc[J - 1] += g[ox];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) red[wv][j][lane] = acc[j];
+    __syncthreads();
+    for (int i = threadIdx.x; i < J * 64; i += C1_T) {
+        const int j = i / 64, l = i - j * 64;
+        const double sum = (((double)red[0][j][l] + red[1][j][l]) + red[2][j][l]) + red[3][j][l];  // wave order
+        work[((long long)blockIdx.y * K + blockIdx.x * 64 + l) * J + j] = sum;
+    }
+}
+
+// the row kernels for the boards' shapes; false: use the per-pixel kernels
+template <int D>
+bool c1_row_fwd(int n, const float* x, long long B, const float* w, const float* b, int K, float* y, hipStream_t st) {
+    const dim3 grid(K / 64, (unsigned)((B + C1_RIMG - 1) / C1_RIMG));
+    switch (n) {
+        case 6: hipLaunchKernelGGL((c1_fwd_row_kernel<D, 6>), grid, dim3(C1_T), 0, st, x, B, w, b, K, y); return true;
+        case 7: hipLaunchKernelGGL((c1_fwd_row_kernel<D, 7>), grid, dim3(C1_T), 0, st, x, B, w, b, K, y); return true;
+        case 8: hipLaunchKernelGGL((c1_fwd_row_kernel<D, 8>), grid, dim3(C1_T), 0, st, x, B, w, b, K, y); return true;
+        default: return false;
+    }
+}
+
+template <int D>
+bool c1_row_wgrad(int n, const float* x, const float* dy, long long B, int K, long long per, int chunks,
+                  double* work, hipStream_t st) {
+    const dim3 grid(K / 64, chunks);
+    switch (n) {
+        case 6: hipLaunchKernelGGL((c1_wgrad_row_kernel<D, 6>), grid, dim3(C1_T), 0, st, x, dy, B, K, per, work); return true;
+        case 7: hipLaunchKernelGGL((c1_wgrad_row_kernel<D, 7>), grid, dim3(C1_T), 0, st, x, dy, B, K, per, work); return true;
+        case 8: hipLaunchKernelGGL((c1_wgrad_row_kernel<D, 8>), grid, dim3(C1_T), 0, st, x, dy, B, K, per, work); return true;
+        default: return false;
     }
 }
 
@@ -172,8 +314,11 @@ bool c1_args_ok(const float* x, int64_t batch, int32_t depth, int32_t n, int32_t
 extern "C" int azg_conv1_train_fwd(const float* x, int64_t batch, int32_t depth, int32_t n, const float* w,
                                    const float* bias, int32_t K, float* y, void* stream) {
     if (!c1_args_ok(x, batch, depth, n, K) || !w || !y) return AZG_ERR_ARG;
-    if (!c1_dispatch<Fwd>(depth, x, (long long)batch, (int)n, w, bias, (int)K, y, (hipStream_t)stream))
-        return AZG_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const bool row = depth == 4   ? c1_row_fwd<4>(n, x, (long long)batch, w, bias, (int)K, y, st)
+                     : depth == 2 ? c1_row_fwd<2>(n, x, (long long)batch, w, bias, (int)K, y, st)
+                                  : false;
+    if (!row && !c1_dispatch<Fwd>(depth, x, (long long)batch, (int)n, w, bias, (int)K, y, st)) return AZG_ERR_ARG;
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
@@ -183,7 +328,11 @@ extern "C" int azg_conv1_train_wgrad(const float* x, const float* dy, int64_t ba
     const int chunks = (int)(batch < C1_CHUNKS ? batch : C1_CHUNKS);
     const long long per = (batch + chunks - 1) / chunks;
     const int used = (int)((batch + per - 1) / per);  // chunks with at least one image
-    if (!c1_dispatch<Wgrad>(depth, x, dy, (long long)batch, (int)n, (int)K, per, used, work, (hipStream_t)stream))
+    hipStream_t st = (hipStream_t)stream;
+    const bool row = depth == 4   ? c1_row_wgrad<4>(n, x, dy, (long long)batch, (int)K, per, used, work, st)
+                     : depth == 2 ? c1_row_wgrad<2>(n, x, dy, (long long)batch, (int)K, per, used, work, st)
+                                  : false;
+    if (!row && !c1_dispatch<Wgrad>(depth, x, dy, (long long)batch, (int)n, (int)K, per, used, work, st))
         return AZG_ERR_ARG;
     const int J = 9 * depth + 1;
     hipLaunchKernelGGL(c1_wgrad_finish_kernel, dim3((unsigned)((K * J + 255) / 256)), dim3(256), 0,

@@ -142,12 +142,13 @@ def gather_record_tensors(moves, actions, counts, dst=0, group=None, actions_per
     temperature 1 (episodeStep < tempThreshold, Coach.py:68), so only the first
     tempThreshold - 1 moves' counts are sent; the others arrive as zeros (their
     examples' pi is the one-hot of the action).  None sends every move's counts.
-    Returns ((moves [W*G], actions [W*G, m] int32, counts [W*G, m, A] int16, or
+    Returns ((moves [W*G], actions [W*G, m] int32, counts [W*G, rows, A] int16, or
     int32 if a count exceeds 32767) on dst, None elsewhere; the bytes this rank sent).
-    With temp_threshold set, the returned counts are TRUNCATED: every move from
-    tempThreshold - 1 on reads as zero counts -- exactly what
-    examples_from_records needs, but not the full records (statistics or saving records
-    need temp_threshold=None)."""
+    rows = m without temp_threshold; with it the counts are TRUNCATED to the temperature-1
+    moves, rows = min(m, tempThreshold - 1) (at 8 ranks x 4096 games
+    a dense [W*G, 344, 343] int16 buffer is 7.7 GB, the 29 rows that carry counts 0.65 GB) --
+    exactly what examples_from_records needs, but not the full records (statistics or saving
+    records need temp_threshold=None)."""
     A = counts.shape[2] if counts is not None else int(actions_per_move)
     G = moves.shape[0]
     dev = moves.device
@@ -188,12 +189,12 @@ def gather_record_tensors(moves, actions, counts, dst=0, group=None, actions_per
     W = out_mv.shape[0]
     ctype = torch.int16 if cmax <= 32767 else torch.int32
     acts = out_act.view(act16.dtype).reshape(W * G, m).to(torch.int32)
-    cnts = torch.empty((W * G, m, A), dtype=ctype, device=out_mv.device)
+    cnts = torch.empty((W * G, rows, A), dtype=ctype, device=out_mv.device)
     ptype_rows = 2 if wide else 1
     for r in range(W):
         nnz_r = int(out_hdr[r, 2])
         pr = out_pairs[r].view(torch.int32).reshape(nnz_max, ptype_rows) if wide else out_pairs[r].view(torch.int32)
-        cnts[r * G:(r + 1) * G] = dense_counts(out_rn[r].view(torch.int16), pr[:nnz_r], G, rows, m, A, ctype)
+        cnts[r * G:(r + 1) * G] = dense_counts(out_rn[r].view(torch.int16), pr[:nnz_r], G, rows, rows, A, ctype)
     return (out_mv.reshape(-1), acts, cnts), sent
 
 

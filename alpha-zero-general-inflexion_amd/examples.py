@@ -267,8 +267,9 @@ def export_reference_examples(history, filename, maxlen):
 def examples_from_records(game_name, n, max_turns, temp_threshold, moves, actions, counts,
                           label_mode="reference", maxlen=200000):
     """ExampleSet of the finished games in the records (device tensors: moves [G]
-    int32, actions [G, MM] int32, counts [G, MM, A] int16 or int32), in game order,
-    last `maxlen` kept (deque(maxlen=args.maxlenOfQueue), Coach.py:107)."""
+    int32, actions [G, MM] int32, counts [G, R, A] int16 or int32 with R = MM, or R >=
+    temp_threshold - 1: the temperature-1 moves' rows only, as the rank gather sends them), in game
+    order, last `maxlen` kept (deque(maxlen=args.maxlenOfQueue), Coach.py:107)."""
     if label_mode not in LABEL_MODES:
         raise ValueError(f"unknown label_mode {label_mode!r}")
     cells, A, nplanes, nsym = game_info(game_name, n)
@@ -276,7 +277,9 @@ def examples_from_records(game_name, n, max_turns, temp_threshold, moves, action
     if dev.type != "cuda":
         raise _lib.AzgError("examples_from_records needs device tensors (no CPU fallback)")
     G, MM = actions.shape
-    if counts.shape != (G, MM, A) or moves.shape != (G,):
+    R = counts.shape[1] if counts.dim() == 3 else -1
+    if counts.dim() != 3 or counts.shape[0] != G or counts.shape[2] != A or not (
+            R == MM or min(MM, max(int(temp_threshold) - 1, 0)) <= R < MM) or moves.shape != (G,):
         raise ValueError(f"record shapes {tuple(moves.shape)} {tuple(actions.shape)} {tuple(counts.shape)} "
                          f"do not match {game_name}({n})")
     moves = moves.to(torch.int32).contiguous()
@@ -293,9 +296,10 @@ def examples_from_records(game_name, n, max_turns, temp_threshold, moves, action
     cnt = ctypes.c_int64()
     with torch.cuda.device(dev):
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        check(_lib.lib().azg_examples(kind, int(n), int(max_turns), int(temp_threshold), G, MM,
-                                      ctypes.c_void_p(moves.data_ptr()), ctypes.c_void_p(actions.data_ptr()),
-                                      ctypes.c_void_p(counts.data_ptr()), counts.element_size(),
+        check(_lib.lib().azg_examples_rows(kind, int(n), int(max_turns), int(temp_threshold), G, MM,
+                                           ctypes.c_void_p(moves.data_ptr()), ctypes.c_void_p(actions.data_ptr()),
+                                           ctypes.c_void_p(counts.data_ptr()) if counts.numel() else None, R,
+                                           counts.element_size(),
                                       LABEL_MODES[label_mode], cap, ctypes.c_void_p(planes.data_ptr()),
                                       ctypes.c_void_p(pis.data_ptr()), ctypes.c_void_p(vs.data_ptr()),
                                       ctypes.byref(cnt), stream))

@@ -45,6 +45,10 @@ SMALL_MAX_B = 4
 # queue atomics cost more than the five kernel boundaries they replace, DESIGN.md 4.1,
 # profiles/r05_small_net_probe_loops.json -- opt in with small_fused / SMALL_FUSED)
 SMALL_FUSED = False
+# the small-batch 3x3 layers (conv1 + conv2, conv3, conv4) on the f32 MFMA (azg_small_mfma.hip): the
+# same slices of the same fmaf chains as azg_small.hip's VALU kernels (v_mfma_f32_16x16x4_f32 is a
+# k-ordered fmaf chain per output), so P and v are bit-identical, spread over 256-512 blocks
+SMALL_MFMA = True
 FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
 # NNetWrapper.train_examples on the GPU: steps run eagerly before the step is captured as a HIP graph
 _GRAPH_EAGER_STEPS = 3
@@ -261,6 +265,40 @@ ACT_BAND = (0.5, 1024.0)
 ACT_TARGET = 8.0
 
 
+def small_mfma_layout(H, pad, cin, cout, conv12):
+    """(KG, KSL, per) of azg_small_mfma_layout: the K-parts, slices per part and float4 steps per
+    slice azg_small.hip's VALU kernels use for this layer (mirrored here so the weights can be
+    packed without a library call), or None where azg_small_conv_mfma does not run (ragged slices,
+    slice lengths other than the boards' 36 / 9 float4 steps)."""
+    ho = H + 2 * pad - 2
+    n = ho * ho
+    if ho <= 0 or n > 256 or cout % 16:
+        return None
+    pxl = next(p for p in (16, 32, 64, 128, 256) if n <= p)
+    kg = 4 if conv12 else (8 if n > 16 and cin % 32 == 0 and cout % 8 == 0 else 1)
+    if cin % (4 * kg):
+        return None
+    ksl, ks = 512 // pxl, 9 * (cin // kg) // 4
+    per = -(-ks // ksl)
+    if per * ksl != ks or per not in (9, 36):
+        return None
+    return kg, ksl, per
+
+
+def pack_small_mfma(w, kg, ksl, per):
+    """A conv weight [Cout][Cin][3][3] (any memory format) -> azg_small_conv_mfma's operand
+    [KG][Cout][KSL][4][TP]: part q, channel co, slice s, slot j, step t holds the weight of
+    k = 4 (s per + t) + j of the part's tap-major K (k = tap * Cq + ci), t padded to TP = 4 ceil(per / 4)."""
+    cout, cin = w.shape[:2]
+    cq = cin // kg
+    wt = w.permute(0, 2, 3, 1).reshape(cout, 9, kg, cq).permute(2, 0, 1, 3).reshape(kg, cout, 9 * cq)
+    wt = wt.reshape(kg, cout, ksl, per, 4).permute(0, 1, 2, 4, 3)
+    tp = -(-per // 4) * 4
+    out = torch.zeros((kg, cout, ksl, 4, tp), dtype=w.dtype, device=w.device)
+    out[..., :per] = wt
+    return out.contiguous()
+
+
 def act_exponent(bn):
     """Power-of-two exponent e for the activations relu(BN(x)) of one layer: 0 if the
     BatchNorm's own estimate of their size, max over channels of beta + 3 |gamma| (on data
@@ -427,6 +465,23 @@ class InferenceNet(nn.Module):
         # It lives where the kernels run: the transforms set it with a device atomic, so a
         # host-memory flag would fault the GPU the first time an operand overflowed.
         self.register_buffer("overflow", torch.zeros(1, dtype=torch.int32, device=self.w1.device))
+        # the small-batch 3x3 layers on the f32 MFMA (SMALL_MFMA): each layer's weights packed in the
+        # slice order of its VALU kernel; layer 2 carries conv1 fused (conv12)
+        self.mfma_layout = {}
+        if net.depth <= 4 and 6 <= net.n <= 8 and self.pads[:2] == [1, 1]:
+            h = net.n
+            for i in (2, 3, 4):
+                pad = self.pads[i - 1]
+                lay = small_mfma_layout(h, pad, c, c, conv12=i == 2)
+                if lay is None:
+                    break
+                self.mfma_layout[i] = lay
+                self.register_buffer(f"wm{i}", pack_small_mfma(getattr(self, f"w{i}"), *lay))
+                h = h + 2 * pad - 2
+            if len(self.mfma_layout) < 3:  # all three or none (one launch path per forward)
+                for i in list(self.mfma_layout):
+                    delattr(self, f"wm{i}")
+                self.mfma_layout = {}
 
     @staticmethod
     def _split_k_weights(w, kp, scale):
@@ -842,7 +897,10 @@ class InferenceNet(nn.Module):
         if self._fused_ok(B):
             return self._forward_small_fused(planes, B, dev, st, wp, tp)
         first = 1
-        if self.depth <= 4 and 6 <= n <= 8 and C % 16 == 0 and self.pads[:2] == [1, 1] \
+        if getattr(self, "small_mfma", SMALL_MFMA) and self.mfma_layout:
+            x, H = self._convs_small_mfma(planes, B, dev, st)
+            first = 5
+        if first == 1 and self.depth <= 4 and 6 <= n <= 8 and C % 16 == 0 and self.pads[:2] == [1, 1] \
                 and n * n * (C // 4 + 4) * 4 + 72 * C + 16384 <= 96 * 1024:  # azg_small_conv12's LDS (4 K-parts)
             # conv1 + conv2 in one launch
             y = torch.empty((B * n * n, C), device=dev, dtype=torch.float32)
@@ -885,6 +943,39 @@ class InferenceNet(nn.Module):
                                      ctypes.c_void_p(v.data_ptr()),
                                      ctypes.c_void_p(tickets.data_ptr() + 4 * (tickets.numel() - 1)), st))
         return p, v
+
+    def _convs_small_mfma(self, planes, B, dev, st):
+        """conv1 + conv2, conv3, conv4 on azg_small_conv_mfma (bit-identical to the VALU kernels'
+        arithmetic): NHWC rows of conv4's output and its side."""
+        import ctypes
+        from . import _lib
+        L = _lib.lib()
+        n, C = self.n, self.w1.shape[0]
+        tiles = -(-B * n * n // 16) * (C // 16)
+        need = tiles * 256 * max(max(kg, ksl) for kg, ksl, _ in self.mfma_layout.values())
+        if getattr(self, "_mfma_work", None) is None or self._mfma_work.numel() < need \
+                or self._mfma_work.device != dev:
+            self._mfma_work = torch.empty(need, device=dev, dtype=torch.float32)
+            self._mfma_tickets = torch.zeros(tiles, device=dev, dtype=torch.int32)
+        work, tickets = self._mfma_work, self._mfma_tickets
+        wp, tp = ctypes.c_void_p(work.data_ptr()), ctypes.c_void_p(tickets.data_ptr())
+        x, H = planes, n
+        for i in (2, 3, 4):
+            pad = self.pads[i - 1]
+            Ho = H + 2 * pad - 2
+            y = torch.empty((B * Ho * Ho, C), device=dev, dtype=torch.float32)
+            if i == 2:  # x: the NCHW leaf planes, conv1 computed in the kernel
+                args = (ctypes.c_void_p(planes.data_ptr()), self.depth * n * n, 0, 0)
+                c1 = (ctypes.c_void_p(self.w1.data_ptr()), ctypes.c_void_p(self.b1.data_ptr()), self.depth)
+            else:
+                args = (ctypes.c_void_p(x.data_ptr()), H * H * C, H * C, C)
+                c1 = (None, None, 0)
+            _lib.check(L.azg_small_conv_mfma(*args, B, H, pad, ctypes.c_void_p(getattr(self, f"wm{i}").data_ptr()),
+                                             C, C, ctypes.c_void_p(getattr(self, f"b{i}").data_ptr()), 1,
+                                             ctypes.c_void_p(y.data_ptr()), C, wp, work.numel(), tp, tickets.numel(),
+                                             *c1, st))
+            x, H = y, Ho
+        return x, H
 
     def _fused_ok(self, B):
         """azg_small_net's preconditions (the conv1 + conv2 split-K form, pads 1, 1, 0, 0, its LDS pool)."""

@@ -52,6 +52,17 @@ class FusedAdam:
                 p.grad.zero_()
 
     def step(self, grads=None):
+        """One Adam step of every parameter (gradients: `grads` in parameter order, else each
+        parameter's .grad).  torch's global optimizer pre / post step hooks
+        (torch.optim.optimizer.register_optimizer_step_pre_hook / _post_hook) run around it."""
+        from torch.optim import optimizer as _topt
+        for hook in list(getattr(_topt, "_global_optimizer_pre_hooks", {}).values()):
+            hook(self, (), {})
+        self._step(grads)
+        for hook in list(getattr(_topt, "_global_optimizer_post_hooks", {}).values()):
+            hook(self, (), {})
+
+    def _step(self, grads):
         gs = grads if grads is not None else [p.grad for p in self.params]
         if len(gs) != self._n:
             raise ValueError(f"FusedAdam.step: {len(gs)} gradients for {self._n} parameters")

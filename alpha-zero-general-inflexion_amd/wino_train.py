@@ -28,7 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
-from .nnet import WINOGRAD_G, winograd_groups, winograd_points
+from .nnet import winograd_groups, winograd_points
 
 SPLIT2 = 2  # azg.h AZG_WINO_SPLIT2
 
@@ -119,7 +119,10 @@ class WinogradConv3x3(torch.autograd.Function):
         P = winograd_points(Ho)
         dyc = dy.contiguous(memory_format=torch.channels_last)
         dyamax = torch.empty(1, dtype=torch.int32, device=dev)
-        _lib.check(L.azg_absmax(_p(dyc), dyc.numel(), _p(dyamax), st))
+        # max |dy| (the dM scale) and db = dy summed over (batch, h, w) in one read of dy
+        db = torch.empty(K, dtype=torch.float32, device=dev) if ctx.needs_input_grad[2] else None
+        work = torch.empty(2 * 512 * K + 256, dtype=torch.float64, device=dev)
+        _lib.check(L.azg_wt_dy_stats(_p(dyc), B * Ho * Ho, K, _p(dyamax), _p(db), _p(work), st))
         dM = torch.empty(rows * 2 * K, dtype=torch.float16, device=dev)
         _lib.check(L.azg_wt_dout(_p(dyc), _p(dM), B, Ho, K, _p(dyamax), _p(ovf), st))
         dx = None
@@ -144,7 +147,6 @@ class WinogradConv3x3(torch.autograd.Function):
             # dw[k][c][r][s] = sum over the groups of G_a^T dU G_b, the dy scale undone (azg_wt_dw)
             dw = torch.empty((K, C, 3, 3), dtype=torch.float32, device=dev)
             _lib.check(L.azg_wt_dw(_p(dU), C, K, Ho, _p(dyamax), _p(dw), st))
-        db = dy.sum(dim=(0, 2, 3)) if ctx.needs_input_grad[2] else None
         return dx, dw, db, None
 
 
@@ -367,17 +369,6 @@ def take_flag(device):
 
 
 _FLAGS = {}
-_G = {}
-
-
-def _g(m, dev):
-    """nnet.WINOGRAD_G[m] as an f32 device tensor (cached: no host copy per backward)."""
-    t = _G.get((m, dev))
-    if t is None:
-        t = _G[(m, dev)] = torch.tensor(WINOGRAD_G[m], dtype=torch.float32, device=dev)
-    return t
-
-
 def _key(dev):
     dev = torch.device(dev)
     if dev.type == "cuda" and dev.index is None:

@@ -292,6 +292,24 @@ int  azg_small_net(const float* planes, int32_t batch, int32_t depth, int32_t n,
 int  azg_small_net_blocks(int32_t blocks);
 int  azg_small_heads(const float* x, int32_t ldx, int32_t batch, const float* w34, int32_t K, int32_t A,
                      const float* b34, float* logits, float* P, float* v, uint32_t* ticket, void* stream);
+/* The 3x3 layers of the small-batch forward on the f32 MFMA (azg_small_mfma.hip): the same arithmetic
+ * as azg_small_conv12 / azg_small_conv3x3 -- the same K-parts, slices and in-order sums of the same
+ * fmaf chains (v_mfma_f32_16x16x4_f32 is a k-ordered fmaf chain per output) -- so bit-identical
+ * outputs, spread over 16-channel x 16-row tiles.  azg_small_mfma_layout writes out[4] = (KG parts,
+ * KSL slices per part, float4 steps per slice, padded steps TP) for the layer (conv12 != 0: conv2 with
+ * conv1 fused); azg_small_conv_mfma takes the weights packed [KG][Cout][KSL][4][TP] (part q, channel
+ * co, slice s, slot j, step t: k = 4 (s per + t) + j of the part's tap-major K = tap * (Cin / KG) + ci;
+ * nnet.pack_small_mfma), x as azg_small_conv3x3's NHWC rows (sB, sY, sX; channels contiguous) or, with
+ * w1 / b1 / D given, the NCHW leaf planes with conv1 (w1 [Cin][3][3][D], channels_last, BN folded)
+ * computed in the kernel; y[row * ldy + co] = relu?(bias + the sums), rows = leaf x output pixel.
+ * work >= tiles x max(KG, KSL) x 256 floats, tickets >= tiles zero words (left zero), tiles = ceil(batch x
+ * Ho^2 / 16) x Cout / 16; batch <= 4, Cout % 16 == 0; slice lengths of 36 or 9 float4 steps (the boards'
+ * layers; others AZG_ERR_ARG). */
+int  azg_small_mfma_layout(int32_t H, int32_t pad, int32_t Cin, int32_t Cout, int32_t conv12, int32_t* out /*[4]*/);
+int  azg_small_conv_mfma(const float* x, int64_t sB, int32_t sY, int32_t sX, int32_t batch, int32_t H, int32_t pad,
+                         const float* wm, int32_t Cin, int32_t Cout, const float* bias, int32_t relu, float* y,
+                         int32_t ldy, float* work, int64_t work_floats, uint32_t* tickets, int32_t n_tickets,
+                         const float* w1, const float* b1, int32_t D, void* stream);
 /* The schedule azg_split_gemm picks for a launch of this shape (4, 17 or 18). */
 int  azg_split_gemm_pick(int32_t nruns, const int32_t* points, const int32_t* rows, int32_t k);
 /* Cap the persistent split GEMM's grid at `blocks` workgroups (one per CU; 0 = every CU;
@@ -387,6 +405,14 @@ int  azg_examples(int32_t game_kind, int32_t n, int32_t max_turns, int32_t temp_
                   int32_t max_moves, const int32_t* moves, const int32_t* actions, const void* counts,
                   int32_t counts_bytes, int32_t label_mode, int64_t maxlen, float* planes, float* pis,
                   float* vs, int64_t* count, void* stream);
+/* The same with counts of count_rows moves per game ([G, count_rows, A]; count_rows >= temp_threshold - 1,
+ * the moves played at temperature 1 -- the only ones whose counts an example reads): the rank gather's
+ * truncated records (dist.py) without a dense [G, max_moves, A] buffer.  azg_examples = count_rows
+ * max_moves. */
+int  azg_examples_rows(int32_t game_kind, int32_t n, int32_t max_turns, int32_t temp_threshold, int32_t num_games,
+                       int32_t max_moves, const int32_t* moves, const int32_t* actions, const void* counts,
+                       int32_t count_rows, int32_t counts_bytes, int32_t label_mode, int64_t maxlen, float* planes,
+                       float* pis, float* vs, int64_t* count, void* stream);
 
 /* ---- trainer convolutions (azg_wino_train.hip; NNetWrapper.train, NNet.py:36-76) ------------
  * conv2-4 of the training forward and backward on the Winograd transforms and the split GEMM
@@ -432,6 +458,11 @@ int  azg_bn_relu_bwd_sums(const float* x, const float* dy, int64_t rows, int32_t
 int  azg_bn_relu_bwd_from_sums(const float* x, const float* dy, int64_t rows, int32_t C, const float* sv,
                                const double* sums, int64_t n_total, float* dx, float* dgamma, float* dbeta,
                                float* co, void* stream);
+/* The convolution backward's statistics of its output gradient dy [rows][C] f32 (C % 4 == 0, C <= 1024,
+ * rows >= 2, 16-B aligned) in one read: *amax = bits of max |dy| (what azg_wt_dout / azg_wt_din scale by)
+ * and, when db is not null, db [C] = dy summed over the rows (the conv bias's gradient; f64 partials
+ * over 512 fixed row ranges, summed in order).  work >= 2 * 512 * C doubles + 512 floats. */
+int  azg_wt_dy_stats(const float* dy, int64_t rows, int32_t C, uint32_t* amax, float* db, double* work, void* stream);
 /* The trainer's conv1 (InflexionNNet.py:39: 3x3, stride 1, padding 1, on the board planes;
  * azg_train_conv1.hip): x NHWC [batch][n][n][depth] (the planes channels_last), w [K][depth][3][3],
  * depth <= 8, n <= 8, K % 64 == 0, batch <= 262140.  azg_conv1_train_fwd writes y NHWC [batch][n][n][K] = conv + bias

@@ -157,6 +157,28 @@ def golden_counts(move, A=343):
     return c
 
 
+def peaked_net(module):
+    """tests/golden/trained_net.npz with fc3's weight and bias times peaked_net.json.gz's fc3_scale (a
+    power of two: exact) -- the peaked-prior network of make_golden.py peaked_net; returns the module."""
+    import torch
+    trained_net(module)
+    scale = float(load_json("peaked_net.json.gz")["fc3_scale"])
+    with torch.no_grad():
+        module.fc3.weight.mul_(scale)
+        module.fc3.bias.mul_(scale)
+    return module
+
+
+def golden_net(module, name):
+    """The network a fixture set was recorded with: `trained*` sets trained_net, `peaked*` sets
+    peaked_net, the others the manual_seed(0) module as it is."""
+    if name.startswith("peaked"):
+        return peaked_net(module)
+    if name.startswith("trained"):
+        return trained_net(module)
+    return module
+
+
 def trained_net(module):
     """Load tests/golden/trained_net.npz (the network the reference trains on its own self-play,
     make_golden.py trained_net) into an InflexionNNet; returns the module."""

@@ -37,3 +37,22 @@ def test_errors_are_loud_without_device():
     h = ctypes.c_void_p()
     assert L.azg_create(None, None, ctypes.byref(h)) == -1
     assert b"null" in L.azg_last_error()
+
+
+def test_small_mfma_layout_matches_python_mirror():
+    """nnet.small_mfma_layout (used to pack the weights without a library call) = libazg's
+    azg_small_mfma_layout for the boards' layers (no GPU needed)."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    from azg_amd.nnet import small_mfma_layout
+    L = _lib.lib()
+    for H, pad, c12 in [(7, 1, 1), (7, 0, 0), (5, 0, 0), (6, 1, 1), (6, 0, 0), (4, 0, 0), (8, 1, 1), (8, 0, 0),
+                        (6, 0, 1)]:
+        out = (ctypes.c_int32 * 4)()
+        rc = L.azg_small_mfma_layout(H, pad, 512, 512, c12, out)
+        lay = small_mfma_layout(H, pad, 512, 512, bool(c12))
+        if rc == 0 and tuple(out)[2] in (9, 36):
+            assert lay == tuple(out)[:3], (H, pad, c12)
+        else:
+            assert lay is None, (H, pad, c12, rc, tuple(out))

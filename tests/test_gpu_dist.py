@@ -294,6 +294,35 @@ def test_bench_two_ranks_learn_iteration():
     assert li["train_rank0_s"] > 0 and li["rank0_broadcast_bytes"] > 4 * 10e6
 
 
+@pytest.mark.timeout(420)
+def test_bench_eight_ranks_learn_iteration():
+    """the 8-GPU node's rank count rehearsed on one GPU -- `bench.py --gpus 8 --dist-backend
+    gloo --learn-iteration on`: eight ranks (processes) share the device, self-play their shards, all-gather
+    the records (the count rows of the temperature-1 moves only), build the same window and train it
+    data-parallel (64 of every 512-example batch per rank, the BatchNorm sums and the gradient
+    all-reduced).  The JSON line must account for all 8 ranks' games and collectives."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--dist-backend", "gloo",
+           "--games", "16", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--learn-iteration", "on",
+           "--max-turns", "40", "--train-epochs", "1", "--train-window", "4096", "--rank0-train", "0"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=400, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["config"]["global_games"] == 128
+    li = out["learn_iteration"]
+    assert li["ranks"] == 8 and li["games"] == 128 and li["examples"] == 4096 and li["train_steps"] == 8
+    assert li["records_sent_bytes_per_rank"] > 0 and li["bn_allreduce_calls_per_step"] == 12
+    assert li["grad_allreduce_bytes_per_step"] > 4 * 10e6
+    print(json.dumps({k: li[k] for k in ("selfplay_s", "exchange_examples_s", "train_s", "records_sent_bytes_per_rank",
+                                         "grad_allreduce_ms_per_step")}))
+
+
 def _dp_train_worker(rank, world, port, q, E):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -779,6 +779,40 @@ def test_small_forward_matches_reference(n, depth, A, B):
     torch.testing.assert_close(p, p2, rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("n,depth,A", [(7, 4, 343), (6, 2, 37), (8, 2, 65)])
+@pytest.mark.parametrize("trained", [False, True])
+def test_small_mfma_bit_identical_to_valu(n, depth, A, trained):
+    """The small-batch 3x3 layers on the f32 MFMA (azg_small_conv_mfma, SMALL_MFMA) reproduce the VALU
+    kernels' P and v bit for bit at 1-4 leaves: the same slices of the same k-ordered fmaf chains
+    (v_mfma_f32_16x16x4_f32 is such a chain per output), summed in the same order.  Boards whose
+    layers the MFMA path does not cover (8x8 Othello's conv3: 18-step slices) run the VALU kernels
+    under either setting; the repeat checks the tickets are left zero between launches."""
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet, InflexionNNet
+    if trained and n != 7:
+        pytest.skip("the trained network is the 7x7 Inflexion one")
+    torch.manual_seed(0)
+    net = InflexionNNet(n=n, depth=depth, action_size=A).cuda().eval()
+    if trained:
+        ol.trained_net(net)
+    mf, va = InferenceNet(net), InferenceNet(net)
+    va.small_mfma = False
+    print("MFMA layers:", mf.mfma_layout)
+    if n in (6, 7):
+        assert set(mf.mfma_layout) == {2, 3, 4}
+    g = torch.Generator(device="cuda").manual_seed(n + 10 * depth)
+    for B in (1, 2, 3, 4, 1):
+        x = (torch.rand((B, depth, n, n), generator=g, device="cuda") < 0.3).float()
+        if depth > 2:
+            x[:, 1] *= 1 - x[:, 0]
+            x[:, 2] = float(B * 37 % 343)
+            x[:, 3] = float(B % 2)
+        with torch.no_grad():
+            p1, v1 = mf(x)
+            p2, v2 = va(x)
+        assert torch.equal(p1, p2) and torch.equal(v1, v2), (B, float((p1 - p2).abs().max()))
+
+
 def test_split_form_under_expandable_segments():
     """the range flag's device check (azg_ptr.h, hipPointerGetAttributes) must
     accept torch's expandable-segment (VMM) allocations, or the default split evaluator

@@ -27,27 +27,37 @@ def _grads(params, k):
 
 
 def test_fused_adam_matches_torch_capturable_adam():
+    """12 steps on the network's parameter shapes, gradients from 1e-9 to 1e1 and exact zeros: the
+    fused step's error against an f64 Adam on the same gradients is at most torch's own (x2, and
+    a few f32 ulps where torch is exact), per tensor."""
     from azg_amd.optim import FusedAdam
     pa, pb = _net_params(), _net_params()
+    p64 = [p.detach().double().clone() for p in pa]
+    m64 = [torch.zeros_like(p) for p in p64]
+    v64 = [torch.zeros_like(p) for p in p64]
     ta = torch.optim.Adam(pa, capturable=True)
     fb = FusedAdam(pb)
     for k in range(12):
-        for p, q, g in zip(pa, pb, _grads(pa, k)):
+        for i, (p, q, g) in enumerate(zip(pa, pb, _grads(pa, k))):
             p.grad = g.clone()
             q.grad = g.clone()
+            g64 = g.double()
+            m64[i].mul_(0.9).add_(0.1 * g64)
+            v64[i].mul_(0.999).add_(0.001 * g64 * g64)
+            bc1, bc2 = 1 - 0.9 ** (k + 1), 1 - 0.999 ** (k + 1)
+            p64[i].sub_(1e-3 / bc1 * m64[i] / (v64[i].sqrt() / bc2 ** 0.5 + 1e-8))
         ta.step()
         fb.step()
     torch.cuda.synchronize()
     assert float(fb.step_count) == 12.0
-    worst = 0.0
-    for p, q in zip(pa, pb):
-        d = (p.detach() - q.detach()).abs()
-        tol = 4 * torch.finfo(torch.float32).eps * p.detach().abs() + 1e-12
-        worst = max(worst, float((d / tol).max()))
-        assert bool((d <= tol).all()), (p.shape, float(d.max()))
-    ex_a = torch.cat([ta.state[p]["exp_avg"].reshape(-1) for p in pa])
-    assert ex_a.numel() <= fb.m.numel()
-    print(f"worst |fused - torch| in units of 4 ulp: {worst:.3f}")
+    rows = []
+    for p, q, r in zip(pa, pb, p64):
+        e_torch = float((p.detach().double() - r).abs().max())
+        e_fused = float((q.detach().double() - r).abs().max())
+        ulp = 4 * torch.finfo(torch.float32).eps * float(r.abs().max())
+        rows.append((tuple(p.shape), e_torch, e_fused))
+        assert e_fused <= 2 * e_torch + ulp, (tuple(p.shape), e_torch, e_fused)
+    print("max |p - p_f64| (torch, fused):", [(s, f"{a:.2e}", f"{b:.2e}") for s, a, b in rows])
 
 
 def test_fused_adam_graph_replay_equals_eager():

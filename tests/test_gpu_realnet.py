@@ -67,24 +67,28 @@ SETS = {"realnet_main": ("inflexion", 7, 40), "realnet_sims100": ("inflexion", 7
         "realnet_othello8_s200": ("othello", 8, 16),
         # the network the reference trains on its own self-play (make_golden.py trained_net):
         # Coach.learn's second iteration searches with it (Coach.py:110, :152)
-        "trained_main": ("inflexion", 7, 40), "trained_sims100": ("inflexion", 7, None)}
+        "trained_main": ("inflexion", 7, 40), "trained_sims100": ("inflexion", 7, None),
+        # the peaked-prior network (make_golden.py peaked_net: the trained network's fc3 x 16; median
+        # root top prior 0.66 vs 0.038): deep trees, near-ties between a few strong actions
+        "peaked_main": ("inflexion", 7, 40), "peaked_sims100": ("inflexion", 7, None)}
 
 
 def _trained(name):
-    return name.startswith("trained")
+    return name.startswith("trained") or name.startswith("peaked")
 
 
-def _ref_net(game="inflexion", n=7, trained=False):
+def _family(name):
+    return "peaked" if name.startswith("peaked") else "trained" if name.startswith("trained") else "realnet"
+
+
+def _ref_net(game="inflexion", n=7, name="realnet_main"):
     """The reference's network for the game, as NNetWrapper(game) builds it under manual_seed(0)
-    (trained: with the weights of tests/golden/trained_net.npz)."""
+    (trained / peaked sets: with the weights of tests/golden/trained_net.npz, fc3 scaled for peaked)."""
     import azg_amd  # noqa: F401
     from azg_amd.nnet import InflexionNNet
     torch.manual_seed(0)
     if game == "inflexion":
-        net = InflexionNNet()
-        if trained:
-            ol.trained_net(net)
-        return net.cuda().eval()
+        return ol.golden_net(InflexionNNet(), name).cuda().eval()
     return InflexionNNet(n=n, depth=2, action_size=n * n + 1).cuda().eval()
 
 
@@ -121,7 +125,7 @@ def _margin_report(net, evaluator, board, turn, player, template, batch=G_ENGINE
 
 def _sensitivity(name):
     fname = ("realnet_sensitivity_othello.json.gz" if "othello" in name else
-             "trained_sensitivity.json.gz" if _trained(name) else "realnet_sensitivity.json.gz")
+             f"{_family(name)}_sensitivity.json.gz")
     try:
         d = ol.load_json(fname)
     except FileNotFoundError:
@@ -133,10 +137,10 @@ def _sensitivity(name):
 def _branches(name):
     """The perturbed reference's traces past its divergent moves (make_golden.py `branches`):
     {(seed, move): [branch, ...]}."""
-    if name not in ("realnet_main", "trained_main"):
+    if name not in ("realnet_main", "trained_main", "peaked_main"):
         return {}
     try:
-        d = ol.load_json("trained_branches.json.gz" if _trained(name) else "realnet_branches.json.gz")
+        d = ol.load_json(f"{_family(name)}_branches.json.gz")
     except FileNotFoundError:
         return {}
     out = {}
@@ -219,7 +223,8 @@ def _check_episode(ep, counts, actions, n_moves, where, report, name, final=None
 
 DROPIN_CASES = ([("realnet_main", k) for k in range(8)] + [("realnet_sims100", 0)]
                 + [("realnet_othello6", i) for i in range(8)] + [("realnet_othello8", 0)]
-                + [("trained_main", k) for k in range(8)] + [("trained_sims100", 0), ("trained_sims100", 1)])
+                + [("trained_main", k) for k in range(8)] + [("trained_sims100", 0), ("trained_sims100", 1)]
+                + [("peaked_main", k) for k in range(8)] + [("peaked_sims100", 0), ("peaked_sims100", 1)])
 
 
 @pytest.mark.parametrize("form", ["module", "inference"])
@@ -243,8 +248,7 @@ def test_dropin_mcts_real_net(name, k, form):
     game = _game(name, cfg)
     torch.manual_seed(0)
     wrapper = NNetWrapper(game, device="cuda")
-    if _trained(name):
-        ol.trained_net(wrapper.nnet)
+    ol.golden_net(wrapper.nnet, name)
     ev = None
     if form == "inference":
         ev = InferenceNet(wrapper.nnet.eval(), conv="miopen", gemm="f32")
@@ -307,7 +311,7 @@ def test_engine_real_net(name, gemm, G):
     kind, n, _ = SETS[name]
     seeds = [ep["seed"] for ep in eps]
     assert seeds == list(range(seeds[0], seeds[0] + len(seeds)))
-    net = _ref_net(kind, n, _trained(name))
+    net = _ref_net(kind, n, name)
     ev = InferenceNet(net, gemm=gemm)
     game = _game(name, cfg)
     e = SelfPlayEngine(G, sims=cfg["sims"], cpuct=cfg["cpuct"], temp_threshold=cfg["temp_threshold"],

@@ -184,3 +184,32 @@ def test_batchnorm_relu_matches_torch(B, H):
         print(f"B {B} H {H}: {name} max error {err:.3g}")
         assert err < tol, (name, err)
     assert int(bn.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("rows,C", [(512 * 49, 512), (512 * 9, 512), (2, 4), (1001, 64)])
+def test_dy_statistics_and_pow2_scale(rows, C):
+    """azg_wt_dy_stats (the conv backward's one read of dy: max |dy| bits and db = dy summed over the
+    rows, f64 partials) against torch, azg_absmax on the same data, and azg_wt_pow2_scale: the power
+    of two 2^floor(log2(target / amax)) the kernels scale by."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    L = _lib.lib()
+    g = torch.Generator(device="cuda").manual_seed(rows + C)
+    dy = torch.randn((rows, C), generator=g, device="cuda") * 1e-4
+    dy[rows // 3, C // 2] = -7.5e-3  # a known largest magnitude, negative
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    amax = torch.zeros(1, dtype=torch.int32, device="cuda")
+    db = torch.empty(C, dtype=torch.float32, device="cuda")
+    work = torch.empty(2 * 512 * C + 256, dtype=torch.float64, device="cuda")
+    _lib.check(L.azg_wt_dy_stats(dy.data_ptr(), rows, C, amax.data_ptr(), db.data_ptr(), work.data_ptr(), st))
+    amax2 = torch.full((1,), 12345, dtype=torch.int32, device="cuda")
+    _lib.check(L.azg_absmax(dy.data_ptr(), dy.numel(), amax2.data_ptr(), st))
+    want = dy.abs().max()
+    assert amax.view(torch.float32).item() == want.item() == amax2.view(torch.float32).item()
+    ref = dy.double().sum(dim=0)
+    assert float((db.double() - ref).abs().max()) <= 1e-6 * float(dy.abs().sum(dim=0).max()) + 1e-30
+    out = torch.zeros(1, dtype=torch.float32, device="cuda")
+    _lib.check(L.azg_wt_pow2_scale(amax.data_ptr(), ctypes.c_float(32.0), out.data_ptr(), st))
+    s = out.item()
+    assert s == 2.0 ** np.floor(np.log2(32.0 / want.item())) and 16.0 < want.item() * s <= 32.0
