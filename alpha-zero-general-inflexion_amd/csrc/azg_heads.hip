@@ -11,7 +11,7 @@
 //    next layer's A operand, one fp16 row [hi | lo | hi] per leaf (AZG_WINO_SPLIT), so
 //    the activation never exists in f32; |y| > 65504 or NaN sets *overflow (the
 //    InferenceNet range flag).  HBM-bound: 4 values per lane, float4 loads.
-//  * policy_value: P = softmax(bias[:A] + scale * m[:, :A]) (= exp(log_softmax),
+//  * policy_value: P = exp(log_softmax(bias[:A] + scale * m[:, :A])) (the reference's exp(log_softmax),
 //    NNet.py:94) and v = tanh(bias[A] + scale * m[:, A]) from the stacked fc3 | fc4
 //    GEMM, one wave per leaf (max and sum as __shfl_xor butterflies), written in the
 //    [G, A] / [G] layout azg_sim_end reads.
@@ -181,20 +181,25 @@ __global__ __launch_bounds__(256) void policy_value_kernel(const float* __restri
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    // P = exp(log_softmax) as the reference forms it (NNet.py:94 on torch's CPU log_softmax:
+    // (x - max) - log(sum exp(x - max)), then exp): ONE rounding into the subnormal range.  The direct
+    // softmax exp(x - max) / sum rounds twice there, and a peaked network's tiny priors -- the only
+    // ones left to explore at a lost position -- then differed from the reference's by subnormal ulps
+    // or zero / nonzero, deciding PUCT ties among unvisited edges (tests/golden peaked_* traces)
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < PV_PER_LANE; ++j) {
-        x[j] = lane + 64 * j < A ? expf(x[j] - mx) : 0.f;
-        s += x[j];
+        x[j] -= mx;
+        s += lane + 64 * j < A ? expf(x[j]) : 0.f;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    const float inv = 1.f / s;
+    const float ls = logf(s);
     float* pr = P + (long long)r * A;
 #pragma unroll
     for (int j = 0; j < PV_PER_LANE; ++j) {
         const int a = lane + 64 * j;
-        if (a < A) pr[a] = x[j] * inv;
+        if (a < A) pr[a] = expf(x[j] - ls);
     }
     if (lane == 0) {
         float t = tv[0];

@@ -575,19 +575,20 @@ __device__ __forceinline__ void small_fc_body(int bid, int nblk, int tid, bool v
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            // exp(log_softmax) in the reference's order (azg_heads.hip policy_value_kernel)
             float sm = 0.f;
 #pragma unroll
             for (int j = 0; j < PL; ++j) {
-                xa[j] = lane + 64 * j < A ? expf(xa[j] - mx) : 0.f;
-                sm += xa[j];
+                xa[j] -= mx;
+                sm += lane + 64 * j < A ? expf(xa[j]) : 0.f;
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o);
-            const float inv = 1.f / sm;
+            const float ls = logf(sm);
 #pragma unroll
             for (int j = 0; j < PL; ++j) {
                 const int a = lane + 64 * j;
-                if (a < A) P[(long long)wv * A + a] = xa[j] * inv;
+                if (a < A) P[(long long)wv * A + a] = expf(xa[j] - ls);
             }
             if (lane == 0) V[wv] = tanhf(hb[A] + ld(A));
         }

@@ -125,41 +125,98 @@ __global__ __launch_bounds__(256) void wt_absmax_kernel(const float4* __restrict
     block_max_atomic<256>(m, out);
 }
 
-// U of every point in f32, uf [P][K][C] (c fastest: coalesced 4-byte stores), and max |U| (block
-// reduced, one atomic per block): one thread per (k, c), f64 arithmetic (u_points)
-__global__ __launch_bounds__(256) void wt_u_f32_kernel(const float* __restrict__ w, int C, int K, int h_out,
-                                                       float* __restrict__ uf, unsigned* __restrict__ out) {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x, CK = (long long)C * K;
+// ---- U built without an f32 intermediate (round 6) --------------------------------------------------
+// Round 5's build wrote U in f32 (P K C floats) and read it back to split it (conv2: 127 MB each way;
+// 219 us of a 2.5 ms training step, profiles/r06_prof_train_probe*.md).  Here pass 1 computes
+// every U value only for its maximum (a per-block max, no stores, no memset / atomic), and pass 2
+// recomputes U per 32 x 32 (k, c) tile from the tile's staged weights -- the same f64 expressions as
+// u_points, so the same f32 values -- scales it by the power of two of the maximum it reduces from
+// pass 1's block maxima, and writes both split layouts.
+// max |U| in f32 (it only picks the power of two 2^ku: pass 2's f64-exact U then has max |U| 2^ku within
+// one part in 10^6 of (512, 1024], far inside fp16's range); the f64 form held 2 waves per SIMD at 24 us
+template <int MA, int MB>
+__device__ __forceinline__ float u_max_type(const float (&g)[3][3]) {
+    float s[MA + 2][3];
+#pragma unroll
+    for (int a = 0; a < MA + 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            s[a][c] = (float)WinoG<MA>::G[a][0] * g[0][c] + (float)WinoG<MA>::G[a][1] * g[1][c] +
+                      (float)WinoG<MA>::G[a][2] * g[2][c];
     float m = 0.f;
-    if (i < CK)
-        u_points(w + i * 9, h_out, [&](int e, float u) {
-            uf[e * CK + i] = u;
-            m = fmaxf(m, fabsf(u));
-        });
-    block_max_atomic<256>(m, out);
+#pragma unroll
+    for (int a = 0; a < MA + 2; ++a)
+#pragma unroll
+        for (int b = 0; b < MB + 2; ++b)
+            m = fmaxf(m, fabsf(s[a][0] * (float)WinoG<MB>::G[b][0] + s[a][1] * (float)WinoG<MB>::G[b][1] +
+                               s[a][2] * (float)WinoG<MB>::G[b][2]));
+    return m;
 }
 
-// U 2^ku split into both AZG_WINO_SPLIT2 operand layouts from uf: UT [P][K][2C] (the forward GEMM's B
-// operand, U^T) and UN [P][C][2K] (the dV GEMM's, U).  One block per (point, 64 k x 64 c tile): the
-// tile in LDS, then 64 rows of 256 B in each layout (4-byte words of two channels' halves).  Replaces
-// one thread per (k, c) recomputing U in f64 per layout and storing 2-byte halves (112 us per layer
-// and layout) and a one-pass tile kernel with two barriers per point (366 us),
-// profiles/r05_prof_train_probe_wino*.md.
-__global__ __launch_bounds__(256) void wt_u_split_tile_kernel(const float* __restrict__ uf, int C, int K,
-                                                              const unsigned* __restrict__ uamax,
-                                                              unsigned* __restrict__ ut, unsigned* __restrict__ un) {
-    __shared__ float tl[64][65];  // [k][c]
-    const int t = threadIdx.x, c0 = blockIdx.x * 64, k0 = blockIdx.y * 64, e = blockIdx.z;
-    const float sc = pow2_scale(*uamax, 1024.f);
-    const float* src = uf + ((long long)e * K + k0) * C + c0;
+__global__ __launch_bounds__(256) void wt_u_max_kernel(const float* __restrict__ w, int C, int K, int h_out,
+                                                       float* __restrict__ pmax) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x, CK = (long long)C * K;
+    float m = 0.f;
+    if (i < CK) {
+        float g[3][3];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {  // 64 rows of 64 floats: 16 per thread, rows of 256 B
-        const int r = q * 4 + (t >> 6), x = t & 63;
-        tl[r][x] = src[(long long)r * C + x] * sc;  // exact (a power of two)
+        for (int j = 0; j < 9; ++j) g[j / 3][j % 3] = w[i * 9 + j];
+        const WSeq S(h_out);
+        for (int q = 0; q < 4; ++q) {
+            const int ma = q < 2 ? S.big : S.small(), mb = (q & 1) ? S.small() : S.big;
+            if (S.cnt(ma) * S.cnt(mb) == 0) continue;
+            with_types(ma, mb, [&](auto A_, auto B_) {
+                m = fmaxf(m, u_max_type<decltype(A_)::value, decltype(B_)::value>(g));
+            });
+        }
     }
+    __shared__ float wm[4];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
     __syncthreads();
-    // a row's 64 channels = two 32-channel blocks [hi 32 | lo 32] = 64 words; word wd of the row:
-    // block wd / 32, hi (wd % 32 < 16) or lo, channels 2 (wd % 16) and 2 (wd % 16) + 1 of the block
+    if (threadIdx.x == 0) pmax[blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+}
+
+// block (32-channel c tile, 32-channel k tile, tile type q): U of the type's points for the tile,
+// 2^ku-scaled and split into UT [P][K][2C] and UN [P][C][2K] (32-channel [hi | lo] blocks = one
+// 128-B row segment per row).  Thread t owns pairs (k, c) = (t / 8 + 32 i / 8 ..): 4 per thread.
+__global__ __launch_bounds__(256) void wt_u_direct_kernel(const float* __restrict__ w, int C, int K, int h_out,
+                                                          const float* __restrict__ pmax, int npm,
+                                                          unsigned* __restrict__ uamax, unsigned* __restrict__ ut,
+                                                          unsigned* __restrict__ un) {
+    __shared__ float tl[7][32][33];  // [point b of the row][k][c], scaled
+    __shared__ float red[4];
+    const int t = threadIdx.x, c0 = blockIdx.x * 32, k0 = blockIdx.y * 32, q = blockIdx.z;
+    const WSeq S(h_out);
+    const int ma = q < 2 ? S.big : S.small(), mb = (q & 1) ? S.small() : S.big;
+    if (S.cnt(ma) * S.cnt(mb) == 0) return;  // absent tile type (block-uniform)
+    // the global max |U| from pass 1's block maxima -> the scale (every block reduces the same values)
+    float m = 0.f;
+    for (int i = t; i < npm; i += 256) m = fmaxf(m, pmax[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((t & 63) == 0) red[t >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (t == 0 && blockIdx.x == 0 && blockIdx.y == 0 && q == 0) *uamax = __float_as_uint(m);  // for the consumers
+    const float sc = pow2_scale(__float_as_uint(m), 1024.f);
+    // the type's first point index (u_points' order: the groups before it)
+    int e0 = 0;
+    for (int g2 = 0; g2 < q; ++g2) {
+        const int qa = g2 < 2 ? S.big : S.small(), qb = (g2 & 1) ? S.small() : S.big;
+        if (S.cnt(qa) * S.cnt(qb)) e0 += (qa + 2) * (qb + 2);
+    }
+    // this thread's 4 pairs: (kl, cl) = (t / 32 + 8 i, t % 32), weights in f64
+    const int cl = t & 31;
+    double g[4][3][3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int kl = (t >> 5) + 8 * i;
+        const float* w9 = w + ((long long)(k0 + kl) * C + c0 + cl) * 9;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) g[i][j / 3][j % 3] = (double)w9[j];
+    }
     auto word = [&](float a, float b, bool lo) {
         const _Float16 ha = (_Float16)a, hb = (_Float16)b;
         unsigned short xa = __builtin_bit_cast(unsigned short, ha), xb = __builtin_bit_cast(unsigned short, hb);
@@ -169,14 +226,39 @@ __global__ __launch_bounds__(256) void wt_u_split_tile_kernel(const float* __res
         }
         return (unsigned)xa | ((unsigned)xb << 16);
     };
+    with_types(ma, mb, [&](auto A_, auto B_) {
+        constexpr int MA = decltype(A_)::value, MB = decltype(B_)::value;
+        for (int a = 0; a < MA + 2; ++a) {
+            double sa[4][3];  // u_points' s[a][c] for the thread's pairs
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int r = q * 4 + (t >> 6), wd = t & 63;
-        const int ch = 32 * (wd >> 5) + 2 * (wd & 15);
-        const bool lo = (wd & 31) >= 16;
-        if (ut) ut[(((long long)e * K + k0 + r) * 2 * C + 2 * c0) / 2 + wd] = word(tl[r][ch], tl[r][ch + 1], lo);
-        if (un) un[(((long long)e * C + c0 + r) * 2 * K + 2 * k0) / 2 + wd] = word(tl[ch][r], tl[ch + 1][r], lo);
-    }
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    sa[i][c] = WinoG<MA>::G[a][0] * g[i][0][c] + WinoG<MA>::G[a][1] * g[i][1][c] +
+                               WinoG<MA>::G[a][2] * g[i][2][c];
+            for (int b = 0; b < MB + 2; ++b)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float u = (float)(sa[i][0] * WinoG<MB>::G[b][0] + sa[i][1] * WinoG<MB>::G[b][1] +
+                                            sa[i][2] * WinoG<MB>::G[b][2]);
+                    tl[b][(t >> 5) + 8 * i][cl] = u * sc;  // exact (a power of two)
+                }
+            __syncthreads();
+            // per point, 32 rows x 32 words per layout: thread t writes words t % 32 of rows t / 32 + 8 i
+            const int wd = t & 31, ch = 2 * (wd & 15);
+            const bool lo = wd >= 16;
+            for (int b = 0; b < MB + 2; ++b) {
+                const int e = e0 + a * (MB + 2) + b;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = (t >> 5) + 8 * i;
+                    if (ut) ut[(((long long)e * K + k0 + r) * 2 * C + 2 * c0) / 2 + wd] = word(tl[b][r][ch], tl[b][r][ch + 1], lo);
+                    if (un) un[(((long long)e * C + c0 + r) * 2 * K + 2 * k0) / 2 + wd] = word(tl[b][ch][r], tl[b][ch + 1][r], lo);
+                }
+            }
+            __syncthreads();
+        }
+    });
 }
 
 // Forward output transform without ReLU (BatchNorm follows): y = bias + 2^-ku A^T M A,
@@ -376,16 +458,17 @@ extern "C" int azg_wt_u_build(const float* w, int32_t c, int32_t k, int32_t h_ou
         ((uintptr_t)ut & 3) || ((uintptr_t)un & 3))
         return AZG_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(uamax, 0, 4, st) != hipSuccess) return AZG_ERR_HIP;
     const WSeq S(h_out);
     int P = 0;  // transformed points: sum over the tile types of (ma + 2)(mb + 2)
     for (int i = 0; i < S.p; ++i)
         for (int j = 0; j < S.p; ++j)
             if (S.idx(i) == 0 && S.idx(j) == 0) P += (S.m(i) + 2) * (S.m(j) + 2);
-    hipLaunchKernelGGL(wt_u_f32_kernel, dim3((unsigned)(((long long)c * k + 255) / 256)), dim3(256), 0, st, w, c, k,
-                       h_out, work, uamax);
-    hipLaunchKernelGGL(wt_u_split_tile_kernel, dim3((unsigned)(c / 64), (unsigned)(k / 64), (unsigned)P), dim3(256), 0,
-                       st, work, c, k, uamax, (unsigned*)ut, (unsigned*)un);
+    (void)P;
+    // pass 1: the block maxima of |U| (work: >= ceil(c k / 256) floats); pass 2: U per tile, scaled, split
+    const int npm = (int)(((long long)c * k + 255) / 256);
+    hipLaunchKernelGGL(wt_u_max_kernel, dim3((unsigned)npm), dim3(256), 0, st, w, c, k, h_out, work);
+    hipLaunchKernelGGL(wt_u_direct_kernel, dim3((unsigned)(c / 32), (unsigned)(k / 32), 4u), dim3(256), 0, st, w, c,
+                       k, h_out, work, npm, uamax, (unsigned*)ut, (unsigned*)un);
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 

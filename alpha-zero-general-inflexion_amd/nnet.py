@@ -47,9 +47,14 @@ SMALL_MAX_B = 4
 SMALL_FUSED = False
 # the small-batch 3x3 layers (conv1 + conv2, conv3, conv4) on the f32 MFMA (azg_small_mfma.hip): the
 # same slices of the same fmaf chains as azg_small.hip's VALU kernels (v_mfma_f32_16x16x4_f32 is a
-# k-ordered fmaf chain per output), so P and v are bit-identical, spread over 256-512 blocks
-SMALL_MFMA = True
-FC1_SPLIT_MIN_BATCH = 1024  # below this the f32 fc1 GEMM is faster than the split form (C2: 256 leaves, +0.04 ms)
+# k-ordered fmaf chain per output), so P and v are bit-identical, spread over 256-512 blocks.  Opt-in
+# (InferenceNet.small_mfma): measured slower than the VALU kernels at one leaf (conv12 26.5 vs 19.2 us,
+# conv4 17.2 vs 9.3, conv3 16.9 vs 18.0; profiles/r06_small_layer_bench.json)
+SMALL_MFMA = False
+# from this many leaves the FC tail runs fc1 as the 4-part split-K GEMM (FC1_KPARTS); below it (C2's 256)
+# as the transposed small-batch form, FC1T_KPARTS / FCS_KPARTS2 / 3 (InferenceNet.fc_tail_small, the
+# default; the f32 hipBLASLt tail only when fc_tail_small is off)
+FC1_SPLIT_MIN_BATCH = 1024
 # NNetWrapper.train_examples on the GPU: steps run eagerly before the step is captured as a HIP graph
 _GRAPH_EAGER_STEPS = 3
 FC1_KPARTS = 4  # split-K parts of fc1 on libazg's split GEMM (4608 = 4 x 1152 for the 7x7 board)
@@ -1112,7 +1117,7 @@ class InferenceNet(nn.Module):
                 ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)))
             return p, v
         pv = torch.addmm(self.fb34, x, self.fw34.t())  # [B, A + 1]: fc3 logits | fc4
-        return torch.softmax(pv[:, :A], dim=1), torch.tanh(pv[:, A:])
+        return torch.exp(torch.log_softmax(pv[:, :A], dim=1)), torch.tanh(pv[:, A:])  # NNet.py:94
 
 
 def replay_form(net):

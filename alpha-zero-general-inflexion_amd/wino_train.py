@@ -52,10 +52,21 @@ def _runs(h_out, B):
     return [(P, rows) for P, rows, _ in runs]
 
 
+# measurement hook (bench.py --learn-iteration): GEMM_HOOK(what, flops) around every split GEMM launch
+# of the training convolutions, "start" / "stop" on the launching stream (eager steps only: nothing is
+# recorded inside a graph capture)
+GEMM_HOOK = None
+
+
 def _gemm(A, Bt, M, runs, c, k, dev):
     pts = (ctypes.c_int32 * len(runs))(*[P for P, _ in runs])
     rows = (ctypes.c_int32 * len(runs))(*[r for _, r in runs])
+    hook = GEMM_HOOK if not torch.cuda.is_current_stream_capturing() else None
+    if hook is not None:
+        hook("start", 0.0)
     _lib.check(_lib.lib().azg_split_gemm(_p(A), _p(Bt), _p(M), len(runs), pts, rows, c, k, _stream(dev)))
+    if hook is not None:  # executed fp16 MFMA FLOPs: 3 products per f32 multiply-add
+        hook("stop", 3.0 * 2.0 * sum(P * r for P, r in runs) * c * k)
 
 
 def applies(x, conv):
@@ -95,9 +106,8 @@ class WinogradConv3x3(torch.autograd.Function):
         uamax = torch.empty(1, dtype=torch.int32, device=dev)
         ut = torch.empty(P * K * 2 * C, dtype=torch.float16, device=dev)
         un = torch.empty(P * C * 2 * K, dtype=torch.float16, device=dev)
-        uf = torch.empty(P * K * C, dtype=torch.float32, device=dev)  # U in f32 between the build's two passes
-        _lib.check(L.azg_wt_u_build(_p(wc), C, K, Ho, _p(uamax), _p(ut), _p(un), _p(uf), st))
-        del uf
+        pm = torch.empty(-(-C * K // 256), dtype=torch.float32, device=dev)  # the build's block maxima of |U|
+        _lib.check(L.azg_wt_u_build(_p(wc), C, K, Ho, _p(uamax), _p(ut), _p(un), _p(pm), st))
         M = torch.empty(rows * K, dtype=torch.float32, device=dev)
         _gemm(V, ut, M, runs, C, K, dev)
         y = torch.empty((B, K, Ho, Ho), dtype=torch.float32, device=dev, memory_format=torch.channels_last)

@@ -319,6 +319,15 @@ def cpu_baseline(args, depth, A):
                                 f"{args.cpu_proc_moves} moves each = {exp_n} expansions; slowest process "
                                 f"{slowest:.1f}s (all {wall:.1f}s wall incl. interpreter start)",
             "sample": f"max of the two arrangements ({best}); see one_process_sample / processes_sample",
+            # the rate per core (the processes arrangement: one single-threaded search per
+            # core) and its linear extrapolation to every core this process may use
+            "per_core_value": agg / cores,
+            "all_usable_cores_extrapolated_value": agg / cores * usable,
+            "cores_note": (f"the GPU box grants one GPU's job a {CPU_BASELINE_MAX_CORES}-core share of the host "
+                           f"(os.cpu_count() there shows the whole machine's {machine}; worker pools are to be "
+                           f"sized to the share), so the baseline runs on {cores} cores; per_core_value x "
+                           f"usable_cores ({usable}) is the linear extrapolation to the whole host, not a "
+                           "measurement"),
             "tree_only_value": o2["expansions"] / dt2,
             "tree_only_sample": f"same search, hash evaluator, 1 thread: {o2['expansions']} expansions in {dt2:.2f}s"}
 
@@ -396,6 +405,11 @@ def learn_iteration(args, eng, net, rank, world, gen):
             out["grad_allreduce_ms_per_step"] = stats["grad_allreduce_ms"] / stats["grad_allreduce_timed"]
             out["grad_allreduce_note"] = ("HIP events on the compute stream around the gradient all-reduce, every "
                                           f"{stats['every']}th step, rank {rank}")
+    # the trainer's dominant kernel (libazg's split GEMM: the Winograd training convolutions' 9 GEMMs per
+    # step -- M = V U, dV = dM U^T, dU = V^T dM for conv2-4), timed with HIP events on its stream over a
+    # sample of eager steps after the timed training (a captured step records no events)
+    if game.__class__.__name__ == "InflexionGame" and bs % 64 == 0:
+        out["trainer_roofline"] = trainer_gemm_roofline(w, ex, dev)
     if world > 1 and args.rank0_train:
         # north_star's arrangement for comparison: the same training on rank 0 alone (the one-GPU
         # trainer: Winograd convolutions, NHWC BatchNorm, graph-replayed steps), then its weights
@@ -413,6 +427,53 @@ def learn_iteration(args, eng, net, rank, world, gen):
         out["train_rank0_note"] = ("the iteration's training on rank 0 alone + one broadcast of its weights "
                                    "(north_star: examples gathered, weights broadcast), same examples and draws")
     return out
+
+
+def trainer_gemm_roofline(w, ex, dev, steps=12):
+    """HIP-event durations of the training step's split-GEMM launches (wino_train.GEMM_HOOK) over `steps`
+    eager 512-example steps on a copy of the trained network: achieved executed-fp16 TFLOP/s against the
+    dense fp16 MFMA peak, per launch on average, with the per-step GEMM share."""
+    import copy
+    import azg_amd.wino_train as wt
+    from azg_amd.examples import ExampleSet
+    w2 = copy.copy(w)
+    w2.nnet = copy.deepcopy(w.nnet)
+    w2.args = dict(w.args, epochs=1, train_graph=False)
+    n = min(len(ex), steps * int(w2.args["batch_size"]))
+    sample = ExampleSet(ex.planes[:n], ex.pis[:n], ex.vs[:n])
+    pend, pairs = [], []
+
+    def hook(what, flops):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        if what == "start":
+            pend.append(e)
+        else:
+            pairs.append((pend.pop(), e, flops))
+    state = np.random.get_state()
+    wt.GEMM_HOOK = hook
+    try:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        w2.train_examples(sample)
+        torch.cuda.synchronize()
+        step_s = (time.perf_counter() - t0) / max(n // int(w2.args["batch_size"]), 1)
+    finally:
+        wt.GEMM_HOOK = None
+        np.random.set_state(state)
+    if not pairs:
+        return None
+    ms = [a.elapsed_time(b) for a, b, _ in pairs]
+    fl = sum(f for _, _, f in pairs)
+    ach = fl / (sum(ms) / 1e3) / 1e12
+    nsteps = max(n // int(w2.args["batch_size"]), 1)
+    return {"bound": "mfma", "kernel": "libazg azg_split_gemm in the training step (conv2-4: M = V U, dV = dM U^T, "
+                                       "dU = V^T dM; persistent 256-row and 128-row schedules)",
+            "achieved": ach, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TF,
+            "traffic": None, "launches": len(pairs), "avg_launch_us": sum(ms) / len(ms) * 1e3,
+            "gemm_ms_per_step": sum(ms) / nsteps, "eager_step_ms": step_s * 1e3,
+            "per_launch": f"{fl / len(pairs) / 1e9:.1f} GFLOP executed (3 fp16 products per f32 multiply-add) per "
+                          f"launch on average over {len(pairs)} launches of {nsteps} eager steps (HIP events)"}
 
 
 def rank_command(n, argv, port):
@@ -642,8 +703,10 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             gen_s = float(t.item())
         gen = {"games": G * world, "seconds": gen_s, "moves": moves}
-        if eng.stats()["error"]:
-            raise RuntimeError(f"engine error {eng.stats()['error']} in the generation pass")
+        gst = eng.stats()
+        if gst["error"]:
+            raise RuntimeError(f"engine error {gst['error']} in the generation pass")
+        gen["max_live_nodes"], gen["max_path_depth"] = gst["max_live_nodes"], gst["max_depth"]
     learn = None
     if gen is not None and args.learn_iteration != "off" and args.evaluator == "net":
         learn = learn_iteration(args, eng, net, rank, world, gen)
@@ -764,6 +827,13 @@ def main():
                            "nn_ms": nn_ms, "select_ms": sel_ms, "expand_backup_ms": exp_ms, "move_end_ms": end_ms,
                            "wall_ms": elapsed * 1e3, "graph": bool(args.graph)},
             "iteration_sync_bytes": sync_bytes,
+            # the node pool's headroom (a full pool is replayed with twice the nodes by
+            # Coach self-play, coach.Coach._grow); live nodes of the fullest game slot
+            "tree_capacity": {"node_capacity_per_game": eng.cfg.node_capacity or 16 * args.sims + 128,
+                              "max_live_nodes_timed": st1["max_live_nodes"], "max_path_depth_timed": st1["max_depth"],
+                              "max_live_nodes_generation": gen["max_live_nodes"] if gen else None,
+                              "max_path_depth_generation": gen["max_path_depth"] if gen else None,
+                              "note": "rank 0's engine; maxima over its game slots since the last reset"},
         }
         if learn is not None:
             out["learn_iteration"] = learn

@@ -319,9 +319,11 @@ int  azg_split_gemm_pick(int32_t nruns, const int32_t* points, const int32_t* ro
 int  azg_set_gemm_blocks(int32_t blocks);
 
 /* The fully connected tail of the leaf network (InflexionNNet.py:47-54, BN folded)
- * around split-fp16 GEMMs (azg_heads.hip; the GEMMs are the caller's: one fp16
- * hipBLASLt GEMM with f32 accumulation per layer, A rows [hi | lo | hi] times the
- * weights stacked [hi; hi; lo] and pre-scaled by a power of two that `scale` undoes).
+ * around split-fp16 GEMMs (azg_heads.hip; the GEMMs are the caller's -- libazg's azg_split_gemm
+ * in the default forms (split-K parts in AZG_WINO_SPLIT2 layout, azg_fc_act / azg_fc_act_t /
+ * azg_policy_value_parts below), or one fp16 GEMM per layer with f32 accumulation over A rows
+ * [hi | lo | hi] times the weights stacked [hi; hi; lo] (the AZG_WINO_SPLIT forms, split_blas),
+ * pre-scaled by a power of two that `scale` undoes).
  *   azg_fc_act_split: y = bias + scale * sum_p m[p] (parts >= 1 partial products
  *                     [rows][n] f32, part p at m + p * part_stride floats: the parts of a
  *                     split-K GEMM, summed in order), ReLU if relu != 0, written as the
@@ -424,7 +426,8 @@ int  azg_examples_rows(int32_t game_kind, int32_t n, int32_t max_turns, int32_t 
  *                         in (512, 1024], *uamax = bits of max |U|), split into AZG_WINO_SPLIT2
  *                         rows: ut [P][k][2c] (the forward GEMM's B operand) and/or un
  *                         [P][c][2k] (the input-gradient GEMM's); c % 64 == k % 64 == 0; work:
- *                         P k c floats (U in f32 between the two passes).
+ *                         ceil(c k / 256) floats (pass 1's block maxima of |U|; pass 2 recomputes U
+ *                         per 32 x 32 tile from the weights -- no f32 copy of U).
  *   azg_wt_out          : y NHWC = bias + 2^-ku A^T M A (no ReLU), h_out in {3, 5, 7}.
  *   azg_wt_dout         : dM [P][T][2k] AZG_WINO_SPLIT2 = 2^kd A dy A^T (dy NHWC; 2^kd puts
  *                         max |dy| in (16, 32]); |dM| > 65504 sets *overflow.

@@ -39,7 +39,13 @@ Fixtures written (all small, gzip'd JSON or npz):
                          Coach.learn reaches after a few iterations; its prior statistics
   mcts_peaked_*.json.gz, peaked_sensitivity.json.gz, peaked_branches.json.gz
                          the realnet traces / certificates with the peaked network
+  paths_<set>.npz        per-simulation leaf keys and closest PUCT decision gaps of the reference's
+                         traces (gen_peaked_paths): `python -O make_golden.py paths SET [SEED...]`
+  peaked_leaves_peaked_sims100_s10.npz
+                         the 800 leaves (planes, P, v) of the reference's first 8 moves of
+                         peaked_sims100 seed 10 (gen_peaked_leaves)
 """
+import glob
 import gzip
 import hashlib
 import json
@@ -658,8 +664,144 @@ def gen_realnet_branches(np, trained=False, peaked=False):
     _dump(f"{bname.split('_')[0]}_branches.json.gz", out)
 
 
+def leaf_key(np, planes):
+    """A leaf's identity in the path fixtures: the first 8 bytes of sha256 over its planes as int8."""
+    return int.from_bytes(hashlib.sha256(np.asarray(planes, np.int8).tobytes()).digest()[:8], "little", signed=True)
+
+
+def gen_peaked_paths(np, name, seeds=None, weights_eps=None):
+    """Per-simulation record of the reference's peaked traces: for every MCTS.search call from the
+    root (numMCTSSims per move, in order), the leaf it evaluated -- leaf_key of the planes
+    NNetWrapper.predict received, 0 when the simulation ended at a terminal state -- and the closest
+    PUCT decision on its way down: min over the nodes it descended through of (u1 - u2) / max(|u1|, |u2|),
+    u1 >= u2 the two best upper confidence bounds there (MCTS.py:114-129, computed as the reference
+    does).  A GPU run whose leaf sequence first leaves the reference's at simulation k took another
+    branch at one of simulation k's decisions; the gap says how close that decision was.
+    weights_eps: the same record for the branches of gen_realnet_branches (the reference with its
+    weights moved by weights_eps, for the seeds whose trace diverges): paths_<set>_w<eps>.npz."""
+    import math
+    import torch
+    import MCTS as mcts_mod
+    from Coach import Coach
+    from inflexion.InflexionGame import InflexionGame
+    from inflexion.pytorch.NNet import NNetWrapper
+    from utils import dotdict
+    from flags import GameOutcome as RefOutcome
+
+    cur = {"sims": None}
+
+    class KeyNNet(NNetWrapper):
+        def predict(self, board):
+            cur["sims"][-1][0] = leaf_key(np, board)
+            return super().predict(board)
+
+    class PathMCTS(mcts_mod.MCTS):
+        depth = 0
+        counts = None
+
+        def search(self, game):
+            if self.depth == 0:
+                cur["sims"].append([0, float("inf")])
+            s = game.to_planes().tobytes()
+            if game.outcome == RefOutcome.ONGOING and s in self.Ps:
+                valids, Ps, best = self.Vs[s], self.Ps[s], []
+                for a in range(game.max_actions):
+                    if valids[a]:
+                        if (s, a) in self.Qsa:
+                            u = self.Qsa[(s, a)] + self.args.cpuct * Ps[a] * math.sqrt(self.Ns[s]) / (1 + self.Nsa[(s, a)])
+                        else:
+                            u = self.args.cpuct * Ps[a] * math.sqrt(self.Ns[s] + mcts_mod.EPS)
+                        best.append(float(np.asarray(u, np.float64).reshape(-1)[0]))
+                if len(best) > 1:
+                    best.sort(reverse=True)
+                    rel = (best[0] - best[1]) / max(abs(best[0]), abs(best[1]), 1e-300)
+                    cur["sims"][-1][1] = min(cur["sims"][-1][1], rel)
+            self.depth += 1
+            try:
+                return super().search(game)
+            finally:
+                self.depth -= 1
+
+        def getActionProb(self, game, temp=1):
+            probs = super().getActionProb(game, temp)
+            s = game.to_planes().tobytes()
+            self.counts.append([[a, int(self.Nsa[(s, a)])] for a in range(game.max_actions) if (s, a) in self.Nsa])
+            return probs
+
+    base = json.load(gzip.open(os.path.join(HERE, f"mcts_{name}.json.gz"), "rt"))
+    cfg = base["config"]
+    game0 = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
+    torch.manual_seed(0)
+    net = KeyNNet(game0)
+    load_trained(np, net.nnet, name.startswith("peaked"))
+    branches = {}
+    if weights_eps is not None:
+        g = torch.Generator().manual_seed(12345)  # the perturbation of gen_realnet_sensitivity / _branches
+        with torch.no_grad():
+            for prm in net.nnet.parameters():
+                prm.mul_(1.0 + weights_eps * (2.0 * torch.rand(prm.shape, generator=g, dtype=torch.float64)
+                                              - 1.0).to(prm.dtype))
+        bfile = json.load(gzip.open(os.path.join(HERE, f"{name.split('_')[0]}_branches.json.gz"), "rt"))
+        branches = {b["seed"]: b for b in bfile["branches"] if b["eps"] == weights_eps}
+    args = dotdict({"numMCTSSims": cfg["sims"], "cpuct": cfg["cpuct"], "tempThreshold": cfg["temp_threshold"]})
+    out_seeds, keys, gaps, offs = [], [], [], [0]
+    for ep in base["episodes"]:
+        if seeds is not None and ep["seed"] not in seeds:
+            continue
+        if weights_eps is not None:
+            if ep["seed"] not in branches:
+                continue
+            br = branches[ep["seed"]]
+            ep = {"seed": ep["seed"], "n_moves": br["n_moves"], "moves": [None] * br["from_move"] + br["moves"]}
+        t0 = time.time()
+        cur["sims"] = []
+        mcts = PathMCTS(net, args)
+        mcts.counts = []
+        np.random.seed(ep["seed"])
+        Coach(game0, net, args).executeEpisode((game0.restarted(), mcts))
+        if len(mcts.counts) != len(ep["moves"]) or any(
+                mv is not None and c != mv["counts"] for c, mv in zip(mcts.counts, ep["moves"])):  # (-O: no asserts)
+            raise RuntimeError(f"{name} seed {ep['seed']}: the instrumented rerun left the trace")
+        if len(cur["sims"]) != cfg["sims"] * ep["n_moves"]:
+            raise RuntimeError(f"{name} seed {ep['seed']}: {len(cur['sims'])} simulations")
+        out_seeds.append(ep["seed"])
+        keys += [k for k, _ in cur["sims"]]
+        gaps += [g for _, g in cur["sims"]]
+        offs.append(len(keys))
+        g = np.array([x for _, x in cur["sims"]])
+        print(f"  {name} seed {ep['seed']}: {len(cur['sims'])} simulations, {int((g < 1e-4).sum())} with a decision "
+              f"gap < 1e-4, smallest {g.min():.3g}, {time.time() - t0:.1f}s", flush=True)
+    tag = ("" if weights_eps is None else f"_w{weights_eps:g}") + (
+        "" if seeds is None else "_part_" + "_".join(map(str, out_seeds)))
+    path = os.path.join(HERE, f"paths_{name}{tag}.npz")
+    np.savez_compressed(path, seeds=np.array(out_seeds, np.int32), offsets=np.array(offs, np.int64),
+                        leaf=np.array(keys, np.int64), gap=np.array(gaps, np.float32), sims=np.int32(cfg["sims"]))
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def merge_paths(np, name):
+    parts = sorted(glob.glob(os.path.join(HERE, f"paths_{name}_part_*.npz")))
+    ds = [np.load(p) for p in parts]
+    order = np.argsort([int(d["seeds"][0]) for d in ds])
+    seeds, keys, gaps, offs = [], [], [], [0]
+    for i in order:
+        d = ds[i]
+        for j, sd in enumerate(d["seeds"]):
+            a, b = d["offsets"][j], d["offsets"][j + 1]
+            seeds.append(int(sd))
+            keys.append(d["leaf"][a:b])
+            gaps.append(d["gap"][a:b])
+            offs.append(offs[-1] + b - a)
+    path = os.path.join(HERE, f"paths_{name}.npz")
+    np.savez_compressed(path, seeds=np.array(seeds, np.int32), offsets=np.array(offs, np.int64),
+                        leaf=np.concatenate(keys), gap=np.concatenate(gaps), sims=ds[0]["sims"])
+    for p in parts:
+        os.remove(p)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
 # ------------------------------------------------------------------ trained network
-TRAINED_CFG = dict(example_seeds=[1000, 1001, 1002], max_turns=343, sims=25, cpuct=1, temp_threshold=30,
+TRAINED_CFG =dict(example_seeds=[1000, 1001, 1002], max_turns=343, sims=25, cpuct=1, temp_threshold=30,
                    init_seed=0, batch_seed=17, torch_seed=23, pairs=64, pair_seed=5)
 TRAINED_FILE = "trained_net.npz"
 
@@ -1047,7 +1189,18 @@ def main():
         "peaked": lambda: gen_mcts(np, quick, peaked=True),
         "peaked_sensitivity": lambda: gen_realnet_sensitivity(np, peaked=True),
         "peaked_branches": lambda: gen_realnet_branches(np, peaked=True),
+        "peaked_leaves": lambda: gen_peaked_leaves(np),
     }
+    if only[:1] == ["paths"]:  # paths SET [SEED...]: gen_peaked_paths (with seeds: one process's part)
+        gen_peaked_paths(np, only[1], [int(x) for x in only[2:]] or None)
+        return
+    if only[:1] == ["paths_branches"]:  # paths_branches SET: the weight-perturbed branches' records
+        for eps in (1e-7, 1e-6):
+            gen_peaked_paths(np, only[1], None, weights_eps=eps)
+        return
+    if only[:1] == ["paths_merge"]:
+        merge_paths(np, only[1])
+        return
     for name, fn in jobs.items():
         if only and name not in only:
             continue

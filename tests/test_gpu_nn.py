@@ -796,7 +796,7 @@ def test_small_mfma_bit_identical_to_valu(n, depth, A, trained):
     if trained:
         ol.trained_net(net)
     mf, va = InferenceNet(net), InferenceNet(net)
-    va.small_mfma = False
+    mf.small_mfma, va.small_mfma = True, False
     print("MFMA layers:", mf.mfma_layout)
     if n in (6, 7):
         assert set(mf.mfma_layout) == {2, 3, 4}

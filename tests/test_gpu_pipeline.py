@@ -152,7 +152,7 @@ def test_train_examples_gpu_matches_list_trainer(monkeypatch):
     # on near-zero gradients into full-size steps, and further steps compound it):
     # the comparison is about the sampled batch and the loss, which are identical
     # bit for bit on the CPU (test_pipeline_cpu.py)
-    monkeypatch.setattr(torch.optim, "Adam", lambda params, **kw: torch.optim.SGD(params, lr=1e-3))
+    monkeypatch.setattr(NNetWrapper, "_adam", lambda self: torch.optim.SGD(self.nnet.parameters(), lr=1e-3))
     args = dict(epochs=1, batch_size=256, num_channels=16, dropout=0.0)
     nets = []
     for path in ("list", "tensor"):

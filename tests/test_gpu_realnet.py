@@ -16,7 +16,9 @@ Each is replayed by:
     realnet_main seeds;
   * SelfPlayEngine with InferenceNet(gemm="split") at 4096 concurrent games -- the
     benchmarked path (Winograd transforms, split-fp16 MFMA GEMMs, split-K fc1) -- and at
-    C2's 256 and 512 games (the split GEMM's 128 / 64-row schedules, the f32 FC tail);
+    C2's 256 and 512 games (the split GEMM's 128 / 64-row schedules; below FC1_SPLIT_MIN_BATCH
+    the small-batch libazg FC tail, fc1 transposed: InferenceNet.fc_tail_small, the default since
+    round 5);
   * the same with InferenceNet(gemm="f32") (f32 hipBLASLt GEMMs) at 1024 games.
 pi returned by getActionProb is a function of the counts (MCTS.py:48-60), so equal
 counts give pi exactly (tolerance 0, inside the north_star's 1e-5).
@@ -45,6 +47,15 @@ What is asserted, per seed, against the reference's visit counts:
     itself plays when its rounding falls the other way.  Each test prints how many of
     its moves were compared (all of them, on MI355X).
 The sims100 games (40 turns) must match entirely.
+
+The peaked-prior network (fc3 x 16: logits 16x larger, so every f32 evaluation -- the reference's own
+module on a GPU included -- moves its priors by up to ~6e-5 in log space, test_leaf_parity_peaked) is
+held to a sharper certificate: tests/golden/paths_peaked_*.npz record, for every simulation of the
+reference's traces (and of its weight-perturbed branch runs), the leaf it evaluated and the closest PUCT
+decision on its way down.  The engine's leaf sequence is recorded too; a mismatch of any shape, at any
+move, passes only when the first simulation whose leaf differs descends through a decision the reference
+itself makes by less than DECISION_TAU (2 x the leaf error bound) -- about 20 of a game's 8,600
+simulations, so it certifies the located near-tie, not the game.
 """
 import numpy as np
 import pytest
@@ -149,6 +160,61 @@ def _branches(name):
     return out
 
 
+# Decision certificate (tests/golden/paths_<set>.npz, make_golden.py gen_peaked_paths): a run whose leaf
+# sequence first leaves the reference's at simulation k took another branch at one of simulation k's
+# PUCT decisions; that is rounding, not a bug, when the reference's own closest decision on simulation
+# k's way down is nearer a tie than the evaluator's error can move it: the evaluators' priors agree with
+# the reference's to LEAF_LOG_ERR in log space on the reference's own leaves (test_leaf_parity_peaked),
+# so two upper confidence bounds can swap when they are within 2 x that of each other.
+LEAF_LOG_ERR = 6.25e-5
+DECISION_TAU = 2 * LEAF_LOG_ERR
+
+
+def _paths(name, weights_eps=None):
+    """{seed: (leaf keys, decision gaps)} of the reference's trace (or, with weights_eps, of its
+    weight-perturbed branch runs), one entry per simulation."""
+    import os
+    tag = "" if weights_eps is None else f"_w{weights_eps:g}"
+    path = os.path.join(os.path.dirname(__file__), "golden", f"paths_{name}{tag}.npz")
+    if not os.path.exists(path):
+        return None
+    d = np.load(path)
+    return {int(sd): (d["leaf"][d["offsets"][j]:d["offsets"][j + 1]], d["gap"][d["offsets"][j]:d["offsets"][j + 1]])
+            for j, sd in enumerate(d["seeds"])}
+
+
+def _leaf_keys(rows):
+    """leaf_key (make_golden.py) of each recorded planes row (int8, [4 * n * n])."""
+    import hashlib
+    return np.array([int.from_bytes(hashlib.sha256(r.tobytes()).digest()[:8], "little", signed=True) for r in rows],
+                    np.int64)
+
+
+class LeafRecorder:
+    """The evaluator with the planes of the first `slots` leaf rows of every call kept (as int8, on the
+    device) -- the engine's leaf sequence of the fixture's game slots, for the decision certificate."""
+
+    def __init__(self, ev, slots, max_calls):
+        self.ev, self.slots, self.k = ev, slots, 0
+        self.buf = None
+        self.max_calls = max_calls
+
+    def __getattr__(self, name):
+        return getattr(self.ev, name)
+
+    def __call__(self, planes):
+        if self.buf is None:
+            self.buf = torch.zeros((self.max_calls, self.slots, planes[0].numel()), dtype=torch.int8,
+                                   device=planes.device)
+        if self.k < self.max_calls:
+            self.buf[self.k].copy_(planes[:self.slots].reshape(self.slots, -1))
+        self.k += 1
+        return self.ev(planes)
+
+    def rows(self, slot, n):
+        return self.buf[:min(n, self.k), slot].cpu().numpy()
+
+
 def _first_mismatch(moves, counts, actions, n_moves, start, A):
     """First move index m >= start at which (counts, action) differ from `moves` (a list
     indexed from `start`), or None if they agree through the end of `moves`."""
@@ -160,7 +226,7 @@ def _first_mismatch(moves, counts, actions, n_moves, start, A):
     return None
 
 
-def _check_episode(ep, counts, actions, n_moves, where, report, name, final=None):
+def _check_episode(ep, counts, actions, n_moves, where, report, name, final=None, leaf_cert=None):
     """Compare one episode with the reference.  Returns (first divergent move from the
     reference's own trace or None, moves compared, branch followed or None).
 
@@ -192,13 +258,23 @@ def _check_episode(ep, counts, actions, n_moves, where, report, name, final=None
     msg, single_flip, mv = shape(m, ep["moves"], 0)
     sens = _sensitivity(name)
     certified = any(sens.get(("weights", eps, ep["seed"])) == m for eps in (1e-7, 1e-6))
-    if whole or m < min_prefix or not single_flip or not certified:
+    cert = leaf_cert(m) if leaf_cert is not None else None
+    if cert is not None and cert[2] < DECISION_TAU:
+        k, sims, gap = cert
+        print(f"DECISION-CERTIFIED FLIP {msg}; {report(mv)}; identical counts through move {m - 1}; the leaf "
+              f"sequence first leaves the reference's at simulation {k % sims} of move {k // sims}, whose closest "
+              f"PUCT decision in the reference is {gap:.3g} relative (< {DECISION_TAU:.3g} = 2 x the evaluators' "
+              f"leaf prior error bound)")
+    elif whole or m < min_prefix or not single_flip or not certified:
         raise AssertionError(msg + "; " + report(mv) + ("" if certified else "; the reference's own trace does "
-                             "not diverge at this move when its weights move by 1e-7 or 1e-6"))
-    print(f"NEAR-TIE FLIP {msg}; {report(mv)}; identical through move {m - 1}; the reference's own trace with "
-          f"its weights moved by 1e-7 / 1e-6 first diverges at move "
-          f"{sens.get(('weights', 1e-7, ep['seed']), '?')} / {sens.get(('weights', 1e-6, ep['seed']), '?')} "
-          "(None: never)")
+                             "not diverge at this move when its weights move by 1e-7 or 1e-6")
+                             + (f"; leaf sequence first differs at simulation {cert[0]}, closest decision there "
+                                f"{cert[2]:.3g} relative (not below {DECISION_TAU:.3g})" if cert is not None else ""))
+    else:
+        print(f"NEAR-TIE FLIP {msg}; {report(mv)}; identical through move {m - 1}; the reference's own trace with "
+              f"its weights moved by 1e-7 / 1e-6 first diverges at move "
+              f"{sens.get(('weights', 1e-7, ep['seed']), '?')} / {sens.get(('weights', 1e-6, ep['seed']), '?')} "
+              "(None: never)")
     for br in _branches(name).get((ep["seed"], m), []):
         if not (m < n_moves and np.array_equal(counts[m], ol.golden_counts(br["moves"][0], A))):
             continue
@@ -211,14 +287,70 @@ def _check_episode(ep, counts, actions, n_moves, where, report, name, final=None
                   f"to the end of the game ({n_moves} moves, final board / outcome / RNG position equal)")
             return m, n_moves, br
         msg2, single2, mv2 = shape(m2, br["moves"], m)
+        cert2 = leaf_cert(m2, br) if leaf_cert is not None else None
+        if cert2 is not None and cert2[2] < DECISION_TAU:
+            print(f"BRANCH {where}: seed {ep['seed']} follows the reference's eps={br['eps']:g} branch from move {m} "
+                  f"through move {m2 - 1}; at {m2}: DECISION-CERTIFIED {msg2}; {report(mv2)}; the leaf sequence "
+                  f"first leaves the branch's at simulation {cert2[0] % cert2[1]} of move {cert2[0] // cert2[1]}, "
+                  f"closest decision there {cert2[2]:.3g} relative")
+            return m, m2, br
         if not single2:
             raise AssertionError(f"on the reference's eps={br['eps']:g} branch from move {m}: " + msg2 + "; "
-                                 + report(mv2))
+                                 + report(mv2) + (f"; leaf sequence first leaves the branch's at simulation "
+                                                  f"{cert2[0]}, closest decision {cert2[2]:.3g}" if cert2 else ""))
         print(f"BRANCH {where}: seed {ep['seed']} follows the reference's eps={br['eps']:g} branch from move {m} "
               f"through move {m2 - 1}; at {m2} a second single-decision flip: {msg2}; {report(mv2)}")
         return m, m2, br
     print(f"BRANCH {where}: seed {ep['seed']}: no reference branch from move {m} matches the flipped counts")
     return m, m, None
+
+
+@pytest.mark.parametrize("form", ["split:4096", "split:256", "f32:1024", "small:1", "module:1"])
+def test_leaf_parity_peaked(form):
+    """The evaluator on the reference's own leaves (tests/golden/peaked_leaves_peaked_sims100_s10.npz:
+    the 800 leaves the reference search evaluates in its first 8 moves of peaked_sims100 seed 10, planes
+    as NNetWrapper.predict got them, with its P and v): every GPU form's priors within LEAF_LOG_ERR of the
+    reference's in log space wherever both are normal floats, v within 1e-6.  The bound the decision
+    certificate (DECISION_TAU) rests on.  Forms: the split-fp16 form at the benchmarked 4096 leaves and at
+    C2's 256, the f32-GEMM form, the drop-in's batch-1 small-batch kernels, the module itself."""
+    import os
+    import azg_amd  # noqa: F401
+    from azg_amd.nnet import InferenceNet
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "peaked_leaves_peaked_sims100_s10.npz"))
+    kind, B = form.split(":")
+    B = int(B)
+    net = _ref_net("inflexion", 7, "peaked_main")
+    ev = None if kind == "module" else InferenceNet(net, conv="miopen", gemm="f32") if kind == "small" \
+        else InferenceNet(net, gemm=kind)
+    x = torch.tensor(d["x"].astype(np.float32), device="cuda")
+    n = x.shape[0]
+    pg, vg = [], []
+    with torch.no_grad():
+        for i in range(0, n, B):
+            xb = x[i:i + B]
+            k = xb.shape[0]
+            if k < B:
+                xb = torch.cat([xb, xb[:1].expand(B - k, -1, -1, -1)])
+            if ev is None:
+                a, b = net(xb)
+                a = torch.exp(a)
+            else:
+                a, b = ev(xb)
+            pg.append(a[:k].double().cpu().numpy())
+            vg.append(b.reshape(-1)[:k].double().cpu().numpy())
+    pg, vg = np.concatenate(pg), np.concatenate(vg)
+    pr, vr = d["p"].astype(np.float64), d["v"].astype(np.float64)
+    normal = (pr >= 2.0 ** -126) & (pg >= 2.0 ** -126)
+    lerr = np.abs(np.log(np.where(normal, pg, 1.0)) - np.log(np.where(normal, pr, 1.0)))
+    # below the normal range both sides round exp() onto the subnormal grid: the forms agree there too
+    # to within a few of its steps, and the reference's zeros stay (near) zero
+    sub = ~normal & ((pr > 0) | (pg > 0))
+    print(f"{form}: {n} leaves, prior log error max {lerr.max():.3g} (normal range), {int(sub.sum())} subnormal "
+          f"entries (max |diff| {np.abs(pg - pr)[sub].max() if sub.any() else 0:.3g}), v error max "
+          f"{np.abs(vg - vr).max():.3g}")
+    assert lerr.max() <= LEAF_LOG_ERR
+    assert np.abs(vg - vr).max() <= 1e-6
+    assert (np.abs(pg - pr)[sub] <= 2.0 ** -126).all()
 
 
 DROPIN_CASES = ([("realnet_main", k) for k in range(8)] + [("realnet_sims100", 0)]
@@ -290,7 +422,8 @@ def test_dropin_mcts_real_net(name, k, form):
 
 
 ENGINE_CASES = ([(name, "split", G_ENGINE) for name in SETS] + [(name, "f32", G_ENGINE // 4) for name in SETS]
-                # C2's leaf batch (and twice it): the split GEMM's 128 / 64-row schedules and the f32 FC tail
+                # C2's leaf batch (and twice it): the split GEMM's 128 / 64-row schedules and the small-batch
+                # libazg FC tail (fc1 transposed, InferenceNet.fc_tail_small)
                 + [(name, "split", g) for g in (256, 512) for name in SETS])
 
 
@@ -301,7 +434,8 @@ def test_engine_real_net(name, gemm, G):
     games in the same leaf batches.  G = 4096 (C4 / C3 shapes, C5's 8x8 x 200 sims; the
     split form, benchmarked), 1024 (the f32-GEMM form, a fallback: same kernels, a quarter of
     the leaves keeps the suite short), and 256 / 512 (C2's batch: the split GEMM's 128- and
-    64-row tile schedules, and below FC1_SPLIT_MIN_BATCH the f32 hipBLASLt FC tail)."""
+    64-row tile schedules, and below FC1_SPLIT_MIN_BATCH the small-batch libazg FC tail, fc1
+    transposed -- InferenceNet.fc_tail_small)."""
     import azg_amd  # noqa: F401
     from azg_amd.engine import SelfPlayEngine
     from azg_amd.nnet import InferenceNet
@@ -313,9 +447,13 @@ def test_engine_real_net(name, gemm, G):
     assert seeds == list(range(seeds[0], seeds[0] + len(seeds)))
     net = _ref_net(kind, n, name)
     ev = InferenceNet(net, gemm=gemm)
+    paths = _paths(name)
+    evaluator = ev
+    if paths is not None:
+        evaluator = LeafRecorder(ev, len(seeds), max(ep["n_moves"] for ep in eps) * cfg["sims"])
     game = _game(name, cfg)
     e = SelfPlayEngine(G, sims=cfg["sims"], cpuct=cfg["cpuct"], temp_threshold=cfg["temp_threshold"],
-                       max_turns=cfg.get("max_turns", 343), seed_base=0, first_game=seeds[0], evaluator=ev,
+                       max_turns=cfg.get("max_turns", 343), seed_base=0, first_game=seeds[0], evaluator=evaluator,
                        game=kind, n=n)
     e.play()
     st = e.stats()
@@ -328,10 +466,29 @@ def test_engine_real_net(name, gemm, G):
             assert state["boards"][i].tolist() == ref["final_board"]
             assert ol.OUTCOME_VALUE[int(state["outcomes"][i])] == ref["final_outcome"]
             assert e.get_rng(i)[1] == ref["rng_pos"]
+        def leaf_cert(m, br=None, i=i, ep=ep):
+            """(first simulation whose leaf differs, sims per move, the reference's closest decision on it):
+            against the reference's trace, or -- br, a weight-perturbed branch the run has followed -- against
+            that branch's run from the run's first departure from the trace on."""
+            sims = cfg["sims"]
+            got = _leaf_keys(evaluator.rows(i, (m + 1) * sims))
+
+            def first(keys, gaps, start):
+                for k in range(start, min(len(got), len(keys))):
+                    if keys[k] != 0 and keys[k] != got[k]:
+                        return k, sims, float(gaps[k])
+                return None
+            c0 = first(*paths[ep["seed"]], 0)
+            if br is None:
+                return c0
+            bp = _paths(name, br["eps"])
+            if bp is None or ep["seed"] not in bp or c0 is None:
+                return None
+            return first(*bp[ep["seed"]], c0[0])
         flip, upto, br = _check_episode(
             ep, rec["counts"][i], rec["actions"][i], int(rec["moves"][i]), f"engine gemm={gemm} G={G}",
             lambda mv: _margin_report(net, ev, mv["board"], mv["turn"], 1 - 2 * (mv["turn"] % 2), game, batch=G),
-            name, final=final)
+            name, final=final, leaf_cert=leaf_cert if paths is not None else None)
         if flip is None:
             whole += 1
             final(ep)
@@ -349,7 +506,7 @@ def test_real_net_batch_composition_invariance(G):
     whichever GEMM schedule (persistent 256-row tiles, 128 / 64-row tiles) the size picks.
     So the games a G-game run shares with the 4096-game run -- ragged last tiles and the
     highest slots included -- have the same visit counts and actions bit for bit.  (At
-    least 1024 leaves: below FC1_SPLIT_MIN_BATCH the FC tail is the f32 one, other bits.)"""
+    least 1024 leaves: below FC1_SPLIT_MIN_BATCH the FC tail is the small-batch one, other bits.)"""
     import azg_amd  # noqa: F401
     from azg_amd.engine import SelfPlayEngine
     from azg_amd.nnet import InferenceNet
