@@ -192,12 +192,13 @@ def _leaf_keys(rows):
 
 class LeafRecorder:
     """The evaluator with the planes of the first `slots` leaf rows of every call kept (as int8, on the
-    device) -- the engine's leaf sequence of the fixture's game slots, for the decision certificate."""
+    device) -- the engine's leaf sequence of the fixture's game slots, for the decision certificate.
+    The row index is a device counter, so calls replayed from a captured HIP graph (the drop-in MCTS)
+    are recorded too."""
 
     def __init__(self, ev, slots, max_calls):
-        self.ev, self.slots, self.k = ev, slots, 0
-        self.buf = None
-        self.max_calls = max_calls
+        self.ev, self.slots, self.max_calls = ev, slots, max_calls
+        self.buf = self.idx = None
 
     def __getattr__(self, name):
         return getattr(self.ev, name)
@@ -206,13 +207,37 @@ class LeafRecorder:
         if self.buf is None:
             self.buf = torch.zeros((self.max_calls, self.slots, planes[0].numel()), dtype=torch.int8,
                                    device=planes.device)
-        if self.k < self.max_calls:
-            self.buf[self.k].copy_(planes[:self.slots].reshape(self.slots, -1))
-        self.k += 1
+            self.idx = torch.zeros(1, dtype=torch.long, device=planes.device)
+        rows = planes[:self.slots].reshape(1, self.slots, -1).to(torch.int8)
+        self.buf.index_copy_(0, self.idx.clamp(max=self.max_calls - 1), rows)
+        self.idx += 1
         return self.ev(planes)
 
     def rows(self, slot, n):
-        return self.buf[:min(n, self.k), slot].cpu().numpy()
+        k = int(self.idx.item()) if self.idx is not None else 0
+        return self.buf[:min(n, k, self.max_calls), slot].cpu().numpy() if k else np.zeros((0, 0), np.int8)
+
+
+def _leaf_certificate(paths, name, seed, rec, slot, sims):
+    """leaf_cert for _check_episode: (first simulation whose leaf differs, sims per move, the reference's
+    closest decision on it) against the reference's trace, or -- br, a weight-perturbed branch the run
+    has followed -- against that branch's run from the run's first departure from the trace on."""
+    def cert(m, br=None):
+        got = _leaf_keys(rec.rows(slot, (m + 1) * sims))
+
+        def first(keys, gaps, start):
+            for k in range(start, min(len(got), len(keys))):
+                if keys[k] != 0 and keys[k] != got[k]:
+                    return k, sims, float(gaps[k])
+            return None
+        c0 = first(*paths[seed], 0)
+        if br is None:
+            return c0
+        bp = _paths(name, br["eps"])
+        if bp is None or seed not in bp or c0 is None:
+            return None
+        return first(*bp[seed], c0[0])
+    return cert
 
 
 def _first_mismatch(moves, counts, actions, n_moves, start, A):
@@ -224,6 +249,20 @@ def _first_mismatch(moves, counts, actions, n_moves, start, A):
             continue
         return m
     return None
+
+
+def _hidden_flip(cert, where, seed):
+    """A game whose every move's counts equal the reference's may still have taken another branch inside
+    its tree (a subtree later discarded): its leaf sequence says so.  Such a departure must sit on a
+    certified near-tie like any other."""
+    if cert is None:
+        return
+    k, sims, gap = cert
+    assert gap < DECISION_TAU, (where, seed, f"leaf sequence leaves the reference's at simulation {k % sims} of "
+                                f"move {k // sims}, closest decision {gap:.3g} relative: not a near-tie")
+    print(f"HIDDEN FLIP {where}: seed {seed}: counts equal the reference's on every move; the leaf sequence leaves "
+          f"it at simulation {k % sims} of move {k // sims} (closest decision {gap:.3g} relative), inside a subtree "
+          "the game did not take")
 
 
 def _check_episode(ep, counts, actions, n_moves, where, report, name, final=None, leaf_cert=None):
@@ -385,6 +424,11 @@ def test_dropin_mcts_real_net(name, k, form):
     if form == "inference":
         ev = InferenceNet(wrapper.nnet.eval(), conv="miopen", gemm="f32")
         wrapper.azg_evaluator = ev
+    paths = _paths(name)
+    rec = None
+    if paths is not None:  # the leaf sequence, for the decision certificate
+        rec = LeafRecorder(ev if ev is not None else wrapper.nnet.eval(), 1, ep["n_moves"] * cfg["sims"] + 64)
+        wrapper.azg_evaluator = rec
     counts, actions = [], []
 
     class RecMCTS(MCTS):
@@ -416,9 +460,14 @@ def test_dropin_mcts_real_net(name, k, form):
     flip, upto, br = _check_episode(ep, counts, actions, len(counts), f"drop-in MCTS ({form})",
                                     lambda mv: _margin_report(net, ev, mv["board"], mv["turn"],
                                                               1 - 2 * (mv["turn"] % 2), game, batch=1),
-                                    name, final=final)
+                                    name, final=final,
+                                    leaf_cert=_leaf_certificate(paths, name, ep["seed"], rec, 0, cfg["sims"])
+                                    if rec is not None else None)
     if flip is None:
         final(ep)
+        if rec is not None:
+            _hidden_flip(_leaf_certificate(paths, name, ep["seed"], rec, 0, cfg["sims"])(len(counts) - 1),
+                         f"drop-in MCTS ({form})", ep["seed"])
 
 
 ENGINE_CASES = ([(name, "split", G_ENGINE) for name in SETS] + [(name, "f32", G_ENGINE // 4) for name in SETS]
@@ -466,32 +515,17 @@ def test_engine_real_net(name, gemm, G):
             assert state["boards"][i].tolist() == ref["final_board"]
             assert ol.OUTCOME_VALUE[int(state["outcomes"][i])] == ref["final_outcome"]
             assert e.get_rng(i)[1] == ref["rng_pos"]
-        def leaf_cert(m, br=None, i=i, ep=ep):
-            """(first simulation whose leaf differs, sims per move, the reference's closest decision on it):
-            against the reference's trace, or -- br, a weight-perturbed branch the run has followed -- against
-            that branch's run from the run's first departure from the trace on."""
-            sims = cfg["sims"]
-            got = _leaf_keys(evaluator.rows(i, (m + 1) * sims))
-
-            def first(keys, gaps, start):
-                for k in range(start, min(len(got), len(keys))):
-                    if keys[k] != 0 and keys[k] != got[k]:
-                        return k, sims, float(gaps[k])
-                return None
-            c0 = first(*paths[ep["seed"]], 0)
-            if br is None:
-                return c0
-            bp = _paths(name, br["eps"])
-            if bp is None or ep["seed"] not in bp or c0 is None:
-                return None
-            return first(*bp[ep["seed"]], c0[0])
         flip, upto, br = _check_episode(
             ep, rec["counts"][i], rec["actions"][i], int(rec["moves"][i]), f"engine gemm={gemm} G={G}",
             lambda mv: _margin_report(net, ev, mv["board"], mv["turn"], 1 - 2 * (mv["turn"] % 2), game, batch=G),
-            name, final=final, leaf_cert=leaf_cert if paths is not None else None)
+            name, final=final,
+            leaf_cert=_leaf_certificate(paths, name, ep["seed"], evaluator, i, cfg["sims"]) if paths else None)
         if flip is None:
             whole += 1
             final(ep)
+            if paths:
+                _hidden_flip(_leaf_certificate(paths, name, ep["seed"], evaluator, i, cfg["sims"])(
+                    int(rec["moves"][i]) - 1), f"engine gemm={gemm} G={G}", ep["seed"])
         compared += upto
         total += int(rec["moves"][i])
     print(f"{name} gemm={gemm} G={G}: {whole} of {len(eps)} games identical to the reference move for move; "
