@@ -106,9 +106,6 @@ SIGNATURES = [
     ("azg_arena_follow", ctypes.c_int, [_VP, _VP, _VP]),
     ("azg_examples", ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _I32, _I32, _I64, _VP, _VP,
                                     _VP, ctypes.POINTER(_I64), _VP]),
-    ("azg_small_net", ctypes.c_int, [_VP, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _VP,
-                                     _I64, _VP, _I32, _VP, _VP, _VP]),
-    ("azg_small_net_blocks", ctypes.c_int, [_I32]),
     ("azg_fc_act_t", ctypes.c_int, [_VP, _I32, _I64, _VP, ctypes.c_float, _VP, _I32, _I32, _I32, _I32, _VP, _VP]),
     ("azg_absmax", ctypes.c_int, [_VP, _I64, _VP, _VP]),
     ("azg_bn_relu_fwd", ctypes.c_int, [_VP, _I64, _I32, _VP, _VP, ctypes.c_float, ctypes.c_float, _VP, _VP, _VP,
@@ -129,9 +126,6 @@ SIGNATURES = [
     ("azg_wt_pow2_scale", ctypes.c_int, [_VP, ctypes.c_float, _VP, _VP]),
     ("azg_wt_dw", ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _VP, _VP]),
     ("azg_wt_dy_stats", ctypes.c_int, [_VP, _I64, _I32, _VP, _VP, _VP, _VP]),
-    ("azg_small_mfma_layout", ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _VP]),
-    ("azg_small_conv_mfma", ctypes.c_int, [_VP, _I64, _I32, _I32, _I32, _I32, _I32, _VP, _I32, _I32, _VP, _I32, _VP,
-                                           _I32, _VP, _I64, _VP, _I32, _VP, _VP, _I32, _VP]),
     ("azg_examples_rows", ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _I32, _I32, _I32, _I64,
                                          _VP, _VP, _VP, ctypes.POINTER(_I64), _VP]),
     ("azg_py_shuffle", ctypes.c_int, [_VP, _I64, _VP, ctypes.POINTER(_I32)]),

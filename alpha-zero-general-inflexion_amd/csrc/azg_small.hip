@@ -37,6 +37,9 @@
 
 #include "../../include/azg.h"
 #include "azg_conv1.h"
+#ifdef AZG_SMALL_PROBES
+#include "../../tools/azg_small_probes.h"
+#endif
 
 // The split-K hand-off below (partials stored with relaxed agent-scope atomic stores, every
 // wave draining them with `s_waitcnt vmcnt(0)`, one relaxed ticket per block, the last block
@@ -72,7 +75,7 @@ __host__ __device__ constexpr int sc_pitch(int cin) { return ((cin + 3) & ~3) + 
 // profiles/r05_small_net_probe_*.json.)
 constexpr int BUF_SC1 = 16;  // cache-policy bit of sc1 in the buffer intrinsics' aux operand (gfx940+)
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t coh_rsrc(const float* base) {
+[[maybe_unused]] __device__ __forceinline__ __amdgpu_buffer_rsrc_t coh_rsrc(const float* base) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
 }
 
@@ -609,6 +612,7 @@ __global__ __launch_bounds__(SF_T) void small_fc_kernel(const float* __restrict_
                                     relu, y, ldy, hb, P, V, ticket);
 }
 
+#ifdef AZG_SMALL_PROBES  // the one-launch form: probe build only (tools/Makefile libazg_small_probes.so)
 // ---- the whole forward in one launch (small_net_kernel) ---------------------------------------
 // conv1 + conv2 (split-K, 4 K-parts), conv3 (split-K, 8 K-parts), conv4 (2-channel blocks), fc1, fc2,
 // [fc3 | fc4] + heads: the same block bodies as the per-layer kernels above (same arithmetic, same
@@ -763,6 +767,8 @@ __global__ __launch_bounds__(SC_T) void small_net_kernel(SmallNetArgs a) {
         for (int w = 0; w < SN_SCHED_WORDS; ++w) __hip_atomic_store(q + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#endif  // AZG_SMALL_PROBES
+
 template <int PXL, bool VEC>
 int launch_conv(dim3 grid, hipStream_t st, const float* x, long long sB, int sY, int sX, int sC, int B, int H,
                 int pad, const float* w, int Cin, int Cout, const float* bias, int relu, float* y, int ldy) {
@@ -903,6 +909,7 @@ extern "C" int azg_small_heads(const float* x, int32_t ldx, int32_t batch, const
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 
+#ifdef AZG_SMALL_PROBES
 // grid of azg_small_net (azg_small_net_blocks; 0: one block per CU)
 static int g_small_net_blocks = 0;
 
@@ -985,3 +992,4 @@ extern "C" int azg_small_net(const float* planes, int32_t batch, int32_t depth, 
     }
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
+#endif  // AZG_SMALL_PROBES

@@ -38,19 +38,8 @@ WINOGRAD_MIN_BATCH = 64  # below this many leaves the Winograd path is slower (C
 # launch per layer, no library) instead of MIOpen / hipBLASLt
 SMALL_PATH = True
 SMALL_MAX_B = 4
-# the small-batch forward as ONE launch (azg_small_net: the per-layer kernels' block bodies as items of
-# an in-order work queue, an item waiting for the previous layer's done count; bit-identical results),
-# else one launch per layer (the default: the one-launch form measured 130 us per one-leaf forward
-# against the per-layer kernels' 68.9 us in one HIP graph -- cross-XCD activation reads and per-item
-# queue atomics cost more than the five kernel boundaries they replace, DESIGN.md 4.1,
-# profiles/r05_small_net_probe_loops.json -- opt in with small_fused / SMALL_FUSED)
-SMALL_FUSED = False
-# the small-batch 3x3 layers (conv1 + conv2, conv3, conv4) on the f32 MFMA (azg_small_mfma.hip): the
-# same slices of the same fmaf chains as azg_small.hip's VALU kernels (v_mfma_f32_16x16x4_f32 is a
-# k-ordered fmaf chain per output), so P and v are bit-identical, spread over 256-512 blocks.  Opt-in
-# (InferenceNet.small_mfma): measured slower than the VALU kernels at one leaf (conv12 26.5 vs 19.2 us,
-# conv4 17.2 vs 9.3, conv3 16.9 vs 18.0; profiles/r06_small_layer_bench.json)
-SMALL_MFMA = False
+# (the one-launch small-batch forward and the f32-MFMA small-batch 3x3 layers measured slower than the
+# per-layer VALU kernels below; they live in the probe library, tools/small_probes.py)
 # from this many leaves the FC tail runs fc1 as the 4-part split-K GEMM (FC1_KPARTS); below it (C2's 256)
 # as the transposed small-batch form, FC1T_KPARTS / FCS_KPARTS2 / 3 (InferenceNet.fc_tail_small, the
 # default; the f32 hipBLASLt tail only when fc_tail_small is off)
@@ -270,40 +259,6 @@ ACT_BAND = (0.5, 1024.0)
 ACT_TARGET = 8.0
 
 
-def small_mfma_layout(H, pad, cin, cout, conv12):
-    """(KG, KSL, per) of azg_small_mfma_layout: the K-parts, slices per part and float4 steps per
-    slice azg_small.hip's VALU kernels use for this layer (mirrored here so the weights can be
-    packed without a library call), or None where azg_small_conv_mfma does not run (ragged slices,
-    slice lengths other than the boards' 36 / 9 float4 steps)."""
-    ho = H + 2 * pad - 2
-    n = ho * ho
-    if ho <= 0 or n > 256 or cout % 16:
-        return None
-    pxl = next(p for p in (16, 32, 64, 128, 256) if n <= p)
-    kg = 4 if conv12 else (8 if n > 16 and cin % 32 == 0 and cout % 8 == 0 else 1)
-    if cin % (4 * kg):
-        return None
-    ksl, ks = 512 // pxl, 9 * (cin // kg) // 4
-    per = -(-ks // ksl)
-    if per * ksl != ks or per not in (9, 36):
-        return None
-    return kg, ksl, per
-
-
-def pack_small_mfma(w, kg, ksl, per):
-    """A conv weight [Cout][Cin][3][3] (any memory format) -> azg_small_conv_mfma's operand
-    [KG][Cout][KSL][4][TP]: part q, channel co, slice s, slot j, step t holds the weight of
-    k = 4 (s per + t) + j of the part's tap-major K (k = tap * Cq + ci), t padded to TP = 4 ceil(per / 4)."""
-    cout, cin = w.shape[:2]
-    cq = cin // kg
-    wt = w.permute(0, 2, 3, 1).reshape(cout, 9, kg, cq).permute(2, 0, 1, 3).reshape(kg, cout, 9 * cq)
-    wt = wt.reshape(kg, cout, ksl, per, 4).permute(0, 1, 2, 4, 3)
-    tp = -(-per // 4) * 4
-    out = torch.zeros((kg, cout, ksl, 4, tp), dtype=w.dtype, device=w.device)
-    out[..., :per] = wt
-    return out.contiguous()
-
-
 def act_exponent(bn):
     """Power-of-two exponent e for the activations relu(BN(x)) of one layer: 0 if the
     BatchNorm's own estimate of their size, max over channels of beta + 3 |gamma| (on data
@@ -470,23 +425,6 @@ class InferenceNet(nn.Module):
         # It lives where the kernels run: the transforms set it with a device atomic, so a
         # host-memory flag would fault the GPU the first time an operand overflowed.
         self.register_buffer("overflow", torch.zeros(1, dtype=torch.int32, device=self.w1.device))
-        # the small-batch 3x3 layers on the f32 MFMA (SMALL_MFMA): each layer's weights packed in the
-        # slice order of its VALU kernel; layer 2 carries conv1 fused (conv12)
-        self.mfma_layout = {}
-        if net.depth <= 4 and 6 <= net.n <= 8 and self.pads[:2] == [1, 1]:
-            h = net.n
-            for i in (2, 3, 4):
-                pad = self.pads[i - 1]
-                lay = small_mfma_layout(h, pad, c, c, conv12=i == 2)
-                if lay is None:
-                    break
-                self.mfma_layout[i] = lay
-                self.register_buffer(f"wm{i}", pack_small_mfma(getattr(self, f"w{i}"), *lay))
-                h = h + 2 * pad - 2
-            if len(self.mfma_layout) < 3:  # all three or none (one launch path per forward)
-                for i in list(self.mfma_layout):
-                    delattr(self, f"wm{i}")
-                self.mfma_layout = {}
 
     @staticmethod
     def _split_k_weights(w, kp, scale):
@@ -898,35 +836,7 @@ class InferenceNet(nn.Module):
             self._small_work = torch.empty(need, device=dev, dtype=torch.float32)
             self._small_tickets = torch.zeros(max(C // 8, 1) + 1, device=dev, dtype=torch.int32)
         work, tickets = self._small_work, self._small_tickets
-        wp, tp = ctypes.c_void_p(work.data_ptr()), ctypes.c_void_p(tickets.data_ptr())
-        if self._fused_ok(B):
-            return self._forward_small_fused(planes, B, dev, st, wp, tp)
-        first = 1
-        if getattr(self, "small_mfma", SMALL_MFMA) and self.mfma_layout:
-            x, H = self._convs_small_mfma(planes, B, dev, st)
-            first = 5
-        if first == 1 and self.depth <= 4 and 6 <= n <= 8 and C % 16 == 0 and self.pads[:2] == [1, 1] \
-                and n * n * (C // 4 + 4) * 4 + 72 * C + 16384 <= 96 * 1024:  # azg_small_conv12's LDS (4 K-parts)
-            # conv1 + conv2 in one launch
-            y = torch.empty((B * n * n, C), device=dev, dtype=torch.float32)
-            _lib.check(L.azg_small_conv12(ctypes.c_void_p(planes.data_ptr()), B, self.depth, n,
-                                          ctypes.c_void_p(self.w1.data_ptr()), ctypes.c_void_p(self.b1.data_ptr()),
-                                          ctypes.c_void_p(self.w2.data_ptr()), ctypes.c_void_p(self.b2.data_ptr()),
-                                          C, ctypes.c_void_p(y.data_ptr()), C, wp, work.numel(), tp,
-                                          tickets.numel() - 1, st))
-            x, strides, H, cin, first = y, (n * n * C, n * C, C, 1), n, C, 3
-        for i, pad in enumerate(self.pads, start=1):
-            if i < first:
-                continue
-            Ho = H + 2 * pad - 2
-            y = torch.empty((B * Ho * Ho, C), device=dev, dtype=torch.float32)
-            _lib.check(L.azg_small_conv3x3(ctypes.c_void_p(x.data_ptr()), *strides, B, H, pad,
-                                           ctypes.c_void_p(getattr(self, f"w{i}").data_ptr()), cin, C,
-                                           ctypes.c_void_p(getattr(self, f"b{i}").data_ptr()), 1,
-                                           ctypes.c_void_p(y.data_ptr()), C, wp, work.numel(), tp,
-                                           tickets.numel() - 1, st))
-            x, H, cin = y, Ho, C
-            strides = (H * H * C, H * C, C, 1)
+        x, H = self._convs_small(planes, B, dev, st, work, tickets)
         feat = H * H * C  # NHWC flatten (fw1's column order)
 
         def fc(x, ldx, w, b, relu):
@@ -949,81 +859,38 @@ class InferenceNet(nn.Module):
                                      ctypes.c_void_p(tickets.data_ptr() + 4 * (tickets.numel() - 1)), st))
         return p, v
 
-    def _convs_small_mfma(self, planes, B, dev, st):
-        """conv1 + conv2, conv3, conv4 on azg_small_conv_mfma (bit-identical to the VALU kernels'
-        arithmetic): NHWC rows of conv4's output and its side."""
+    def _convs_small(self, planes, B, dev, st, work, tickets):
+        """conv1-4 at up to SMALL_MAX_B leaves (azg_small_conv12 + azg_small_conv3x3): NHWC rows of
+        conv4's output and its side."""
         import ctypes
         from . import _lib
         L = _lib.lib()
         n, C = self.n, self.w1.shape[0]
-        tiles = -(-B * n * n // 16) * (C // 16)
-        need = tiles * 256 * max(max(kg, ksl) for kg, ksl, _ in self.mfma_layout.values())
-        if getattr(self, "_mfma_work", None) is None or self._mfma_work.numel() < need \
-                or self._mfma_work.device != dev:
-            self._mfma_work = torch.empty(need, device=dev, dtype=torch.float32)
-            self._mfma_tickets = torch.zeros(tiles, device=dev, dtype=torch.int32)
-        work, tickets = self._mfma_work, self._mfma_tickets
         wp, tp = ctypes.c_void_p(work.data_ptr()), ctypes.c_void_p(tickets.data_ptr())
-        x, H = planes, n
-        for i in (2, 3, 4):
-            pad = self.pads[i - 1]
+        x, strides, H, cin, first = planes, (self.depth * n * n, n, 1, n * n), n, self.depth, 1
+        if self.depth <= 4 and 6 <= n <= 8 and C % 16 == 0 and self.pads[:2] == [1, 1] \
+                and n * n * (C // 4 + 4) * 4 + 72 * C + 16384 <= 96 * 1024:  # azg_small_conv12's LDS (4 K-parts)
+            # conv1 + conv2 in one launch
+            y = torch.empty((B * n * n, C), device=dev, dtype=torch.float32)
+            _lib.check(L.azg_small_conv12(ctypes.c_void_p(planes.data_ptr()), B, self.depth, n,
+                                          ctypes.c_void_p(self.w1.data_ptr()), ctypes.c_void_p(self.b1.data_ptr()),
+                                          ctypes.c_void_p(self.w2.data_ptr()), ctypes.c_void_p(self.b2.data_ptr()),
+                                          C, ctypes.c_void_p(y.data_ptr()), C, wp, work.numel(), tp,
+                                          tickets.numel() - 1, st))
+            x, strides, H, cin, first = y, (n * n * C, n * C, C, 1), n, C, 3
+        for i, pad in enumerate(self.pads, start=1):
+            if i < first:
+                continue
             Ho = H + 2 * pad - 2
             y = torch.empty((B * Ho * Ho, C), device=dev, dtype=torch.float32)
-            if i == 2:  # x: the NCHW leaf planes, conv1 computed in the kernel
-                args = (ctypes.c_void_p(planes.data_ptr()), self.depth * n * n, 0, 0)
-                c1 = (ctypes.c_void_p(self.w1.data_ptr()), ctypes.c_void_p(self.b1.data_ptr()), self.depth)
-            else:
-                args = (ctypes.c_void_p(x.data_ptr()), H * H * C, H * C, C)
-                c1 = (None, None, 0)
-            _lib.check(L.azg_small_conv_mfma(*args, B, H, pad, ctypes.c_void_p(getattr(self, f"wm{i}").data_ptr()),
-                                             C, C, ctypes.c_void_p(getattr(self, f"b{i}").data_ptr()), 1,
-                                             ctypes.c_void_p(y.data_ptr()), C, wp, work.numel(), tp, tickets.numel(),
-                                             *c1, st))
-            x, H = y, Ho
+            _lib.check(L.azg_small_conv3x3(ctypes.c_void_p(x.data_ptr()), *strides, B, H, pad,
+                                           ctypes.c_void_p(getattr(self, f"w{i}").data_ptr()), cin, C,
+                                           ctypes.c_void_p(getattr(self, f"b{i}").data_ptr()), 1,
+                                           ctypes.c_void_p(y.data_ptr()), C, wp, work.numel(), tp,
+                                           tickets.numel() - 1, st))
+            x, H, cin = y, Ho, C
+            strides = (H * H * C, H * C, C, 1)
         return x, H
-
-    def _fused_ok(self, B):
-        """azg_small_net's preconditions (the conv1 + conv2 split-K form, pads 1, 1, 0, 0, its LDS pool)."""
-        n, C = self.n, self.w1.shape[0]
-        return (getattr(self, "small_fused", SMALL_FUSED) and self.depth <= 4 and 6 <= n <= 8 and C % 16 == 0
-                and self.pads == [1, 1, 0, 0] and n * n * (C // 4 + 4) * 4 + 72 * C + 16384 <= 96 * 1024
-                and (n - 2) ** 2 * (C + 4) * 4 + 4096 <= 96 * 1024 and B <= SMALL_MAX_B
-                # conv3 split-K in 8 K-parts where it has > 16 output pixels (7x7, 8x8 boards)
-                and ((n - 2) ** 2 <= 16 or (C % 32 == 0 and n * n * (C // 8 + 4) * 4 + 36 * C + 16384 <= 96 * 1024)))
-
-    def _forward_small_fused(self, planes, B, dev, st, wp, tp):
-        """The small-batch forward in one launch (azg_small_net): conv1 + conv2, conv3, conv4, fc1,
-        fc2, [fc3 | fc4] + softmax / tanh, the layers' blocks as items of one in-order work queue."""
-        import ctypes
-        from . import _lib
-        n, C, A = self.n, self.w1.shape[0], self.fw3.shape[0]
-        n1, n2 = self.fw1.shape[0], self.fw2.shape[0]
-        need = SMALL_MAX_B * (n * n * C + (n - 2) ** 2 * C + (n - 4) ** 2 * C + n1 + n2 + A + 1)
-        if getattr(self, "_fused_acts", None) is None or self._fused_acts.device != dev:
-            self._fused_acts = torch.empty(need, device=dev, dtype=torch.float32)
-            # [0:8] the work queue's counters (azg_small_net: zero, and left zero by every launch), [8] error flag
-            self._fused_bar = torch.zeros(16, device=dev, dtype=torch.int32)
-            ptrs = [self.w1, self.b1, self.w2, self.b2, self.w3, self.b3, self.w4, self.b4, self.fw1, self.fb1,
-                    self.fw2, self.fb2, self.fw34, self.fb34]
-            self._fused_ptrs = (ctypes.c_void_p * 14)(*[t.data_ptr() for t in ptrs])
-        # (the 14 weight pointers stay valid: refresh_from copies new weights into the same storage)
-        p = torch.empty((B, A), device=dev, dtype=torch.float32)
-        v = torch.empty((B, 1), device=dev, dtype=torch.float32)
-        bar = self._fused_bar
-        _lib.check(_lib.lib().azg_small_net(
-            ctypes.c_void_p(planes.data_ptr()), B, self.depth, n, C, A, n1, n2, self._fused_ptrs,
-            ctypes.c_void_p(self._fused_acts.data_ptr()), self._fused_acts.numel(), ctypes.c_void_p(p.data_ptr()),
-            ctypes.c_void_p(v.data_ptr()), wp, self._small_work.numel(), tp, self._small_tickets.numel(),
-            ctypes.c_void_p(bar.data_ptr()), ctypes.c_void_p(bar.data_ptr() + 32), st))
-        return p, v
-
-    def check_fused(self):
-        """Raise if a wait of the fused small-batch forward gave up (a layer's items never all
-        finished: the results of that launch are void), and reset its work queue."""
-        bar = getattr(self, "_fused_bar", None)
-        if bar is not None and int(bar[8].item()) != 0:
-            bar.zero_()
-            raise RuntimeError("azg_small_net: a layer wait timed out")
 
     def _small_ok(self, planes):
         """Whether the small-batch kernels take this forward: at most SMALL_MAX_B leaves and

@@ -40,13 +40,15 @@ def test_errors_are_loud_without_device():
 
 
 def test_small_mfma_layout_matches_python_mirror():
-    """nnet.small_mfma_layout (used to pack the weights without a library call) = libazg's
-    azg_small_mfma_layout for the boards' layers (no GPU needed)."""
+    """tools/small_probes.small_mfma_layout (used to pack the weights without a library call) = the
+    probe library's azg_small_mfma_layout for the boards' layers (no GPU needed)."""
     import ctypes
-    import azg_amd  # noqa: F401
-    from azg_amd import _lib
-    from azg_amd.nnet import small_mfma_layout
-    L = _lib.lib()
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import small_probes as sp
+    from small_probes import small_mfma_layout
+    L = sp.lib()
     for H, pad, c12 in [(7, 1, 1), (7, 0, 0), (5, 0, 0), (6, 1, 1), (6, 0, 0), (4, 0, 0), (8, 1, 1), (8, 0, 0),
                         (6, 0, 1)]:
         out = (ctypes.c_int32 * 4)()

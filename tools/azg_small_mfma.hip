@@ -31,8 +31,9 @@
 
 #include <cstdint>
 
-#include "../../include/azg.h"
-#include "azg_conv1.h"
+#include "../include/azg.h"
+#include "../alpha-zero-general-inflexion_amd/csrc/azg_conv1.h"
+#include "azg_small_probes.h"
 
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "azg_small_mfma.hip's hand-off assumes the gfx950 memory model (see azg_small.hip)"

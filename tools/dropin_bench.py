@@ -59,10 +59,9 @@ def main():
             ev, graph = InferenceNet(w.nnet.eval(), conv="miopen", gemm="f32", small=False), True
         elif form == "layers":  # azg_small.hip one launch per layer (the default)
             ev, graph = InferenceNet(w.nnet.eval(), conv="miopen", gemm="f32", small=True), True
-            ev.small_fused = False
-        else:  # "small": azg_small.hip explicitly (the fused one-launch forward, azg_small_net)
-            ev, graph = InferenceNet(w.nnet.eval(), conv="miopen", gemm="f32", small=True), True
-            ev.small_fused = True
+        else:  # "small": the probe library's one-launch forward (azg_small_net, tools/small_probes.py)
+            import small_probes as sp
+            ev, graph = sp.ProbeInferenceNet(w.nnet.eval(), conv="miopen", gemm="f32", small=True, mode="fused"), True
         t = run(ev, game, a.sims, graph, a.moves, fast)
         print(json.dumps({"game": a.game, "form": form, "sims": a.sims, "ms_per_call": t * 1e3,
                           "sims_per_s": a.sims / t}), flush=True)

@@ -76,7 +76,8 @@ def main():
         arms = [("azg", azg), ("lib", lib)]
         if taps == 9:  # the one-block-per-2-channels form (no split-K combine)
             arms.append(("azg_nosk", lambda: azg(False)))
-        from azg_amd.nnet import pack_small_mfma, small_mfma_layout
+        import small_probes as sp
+        from small_probes import pack_small_mfma, small_mfma_layout
         lay = small_mfma_layout(H, pad, cin, cout, False) if taps == 9 and layout == "nhwc" else None
         if lay is not None:  # the f32-MFMA form (azg_small_mfma.hip), bit-identical to "azg"
             wm = pack_small_mfma(wk, *lay)
@@ -87,11 +88,12 @@ def main():
             y2 = torch.empty_like(y)
 
             def mfma():
-                _lib.check(L.azg_small_conv_mfma(ctypes.c_void_p(xin.data_ptr()), *strides[:3], B, H, pad,
+                sp.check(sp.lib().azg_small_conv_mfma(ctypes.c_void_p(xin.data_ptr()), *strides[:3], B, H, pad,
                                                  ctypes.c_void_p(wm.data_ptr()), cin, cout,
                                                  ctypes.c_void_p(b.data_ptr()), 1, ctypes.c_void_p(y2.data_ptr()),
                                                  cout, ctypes.c_void_p(mwork.data_ptr()), mwork.numel(),
-                                                 ctypes.c_void_p(mtk.data_ptr()), mtk.numel(), None, None, 0, st))
+                                                 ctypes.c_void_p(mtk.data_ptr()), mtk.numel(), None, None, 0, st),
+                         "azg_small_conv_mfma")
             arms.append(("azg_mfma", mfma))
         for _, f in arms:
             for _ in range(5):
@@ -132,7 +134,8 @@ def fused(L, st):
         _lib.check(L.azg_small_conv12(V(planes), B, depth, n, V(w1), V(b1), V(w2), V(b2), C, V(y), C, V(work),
                                       work.numel(), V(tickets), C // 8, st))
 
-    from azg_amd.nnet import pack_small_mfma, small_mfma_layout
+    import small_probes as sp
+    from small_probes import pack_small_mfma, small_mfma_layout
     lay = small_mfma_layout(n, 1, C, C, True)
     wm = pack_small_mfma(w2, *lay)
     tiles = -(-B * n * n // 16) * (C // 16)
@@ -141,16 +144,16 @@ def fused(L, st):
     y2 = torch.empty_like(y)
 
     def conv12_mfma():
-        _lib.check(L.azg_small_conv_mfma(V(planes), depth * n * n, 0, 0, B, n, 1, V(wm), C, C, V(b2), 1, V(y2), C,
-                                         V(mwork), mwork.numel(), V(mtk), mtk.numel(), V(w1), V(b1), depth, st))
+        sp.check(sp.lib().azg_small_conv_mfma(V(planes), depth * n * n, 0, 0, B, n, 1, V(wm), C, C, V(b2), 1, V(y2),
+                                              C, V(mwork), mwork.numel(), V(mtk), mtk.numel(), V(w1), V(b1), depth,
+                                              st), "azg_small_conv_mfma")
 
     def heads():
         _lib.check(L.azg_small_heads(V(x), 512, B, V(w34), 512, 343, V(b34), V(lg), V(P), V(v), tk, st))
     torch.manual_seed(0)
     net = InflexionNNet().cuda().eval()
-    small, lib_form = InferenceNet(net), InferenceNet(net, conv="miopen", small=False)
+    small, lib_form = sp.ProbeInferenceNet(net, mode="mfma"), InferenceNet(net, conv="miopen", small=False)
     valu = InferenceNet(net)
-    valu.small_mfma = False
     s = (torch.rand(B, depth, n, n, device="cuda") < 0.3).float()
 
     def fwd_small():

@@ -15,6 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import azg_amd  # noqa: E402,F401
 from azg_amd import _lib  # noqa: E402
 from azg_amd.nnet import InferenceNet, InflexionNNet  # noqa: E402
+import small_probes as sp  # noqa: E402  (tools/, the script's own directory)
 
 
 def graph_time(fn, x, n=20, reps=10):
@@ -46,18 +47,18 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
     torch.manual_seed(0)
     net = InflexionNNet(n=7, depth=4, action_size=343).cuda().eval()
-    ev = InferenceNet(net, conv="miopen", gemm="f32").cuda()
+    layers = InferenceNet(net, conv="miopen", gemm="f32").cuda()
+    fused_ev = sp.ProbeInferenceNet(net, conv="miopen", gemm="f32", mode="fused").cuda()
     x = (torch.rand(B, 4, 7, 7, device="cuda") < 0.3).float()
-    L = _lib.lib()
+    L = sp.lib()
     with torch.no_grad():
         for form, fused, blocks in [("layers", False, 0), ("fused", True, 0), ("fused", True, 128),
                                     ("fused", True, 64), ("layers", False, 0), ("fused", True, 0)]:
-            ev.small_fused = fused
-            _lib.check(L.azg_small_net_blocks(blocks))
-            t = graph_time(ev, x)
+            sp.check(L.azg_small_net_blocks(blocks), "azg_small_net_blocks")
+            t = graph_time(fused_ev if fused else layers, x)
             print(json.dumps({"form": form, "blocks": blocks, "B": B, "us_per_forward": t}), flush=True)
-        _lib.check(L.azg_small_net_blocks(0))
-        ev.check_fused()
+        sp.check(L.azg_small_net_blocks(0), "azg_small_net_blocks")
+        fused_ev.check_fused()
 
 
 if __name__ == "__main__":
