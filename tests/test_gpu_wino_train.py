@@ -213,3 +213,27 @@ def test_dy_statistics_and_pow2_scale(rows, C):
     _lib.check(L.azg_wt_pow2_scale(amax.data_ptr(), ctypes.c_float(32.0), out.data_ptr(), st))
     s = out.item()
     assert s == 2.0 ** np.floor(np.log2(32.0 / want.item())) and 16.0 < want.item() * s <= 32.0
+
+
+@pytest.mark.parametrize("P,T,C", [(121, 512, 512), (3, 64, 128), (2, 192, 64)])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_split2_transpose_matches_torch(P, T, C, offset):
+    """azg_wt_split2_transpose (the dU GEMM's operand transposes): AZG_WINO_SPLIT2 [P][T][2C] ->
+    [P][C][2T] bit for bit against the same permutation in torch -- the 16-B-access kernel for
+    aligned operands (offset 0), the element-wise one otherwise (offset 1 half)."""
+    import ctypes
+    import azg_amd  # noqa: F401
+    from azg_amd import _lib
+    g = torch.Generator(device="cuda").manual_seed(P + T + C)
+    base = torch.randint(-32768, 32767, (P * T * 2 * C + 8,), generator=g, device="cuda", dtype=torch.int32)
+    base = base.to(torch.int16)
+    src = base[offset:offset + P * T * 2 * C]
+    out = torch.zeros(P * C * 2 * T + 8, dtype=torch.int16, device="cuda")
+    dst = out[offset:offset + P * C * 2 * T]
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(_lib.lib().azg_wt_split2_transpose(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
+                                                  P, T, C, st))
+    logical = src.view(P, T, C // 32, 2, 32).permute(0, 3, 1, 2, 4).reshape(P, 2, T, C)  # (hi|lo, t, c)
+    want = logical.transpose(2, 3).reshape(P, 2, C, T // 32, 32).permute(0, 2, 3, 1, 4).reshape(-1)
+    assert torch.equal(dst, want)
+    assert torch.count_nonzero(out[:offset]) == 0 and torch.count_nonzero(out[offset + dst.numel():]) == 0
