@@ -429,47 +429,68 @@ __global__ __launch_bounds__(256) void wt_split2_transpose_kernel(const unsigned
     }
 }
 
-// The same transpose with 16-B global accesses (8 halves per lane: 256 B per row = 16 lanes, one
-// 64-row x 64-channel tile = 4 passes of a 256-thread block each way).  The read scatters each lane's
-// 8 channels into the LDS tile transposed (hs[c][t]), so the write reads 8 consecutive t of one channel
-// as one 16-B LDS load; the row pitch (72 halves) keeps those loads aligned and spreads the scatter's
-// banks.  The scalar-access kernel above moved ~3.7 TB/s over the trainer's 408 MB per step.
+// The same transpose with 16-B global accesses and a conflict-free LDS tile.  A (t, c) element's hi and lo
+// halves (64 B apart in both layouts) are paired into one dword, so the tile is a 64 x 64 dword transpose
+// (word (c, t) at c * 65 + t: bank (c + t) mod 64).  Read: lane (channel group cg of 8, row tl) loads the
+// hi and the lo 16 B of its 8 channels of row t (a wave covers 8 whole 256-B rows) and writes 8 dwords
+// whose banks (8 cg + t + k) are distinct across the wave; write: lane (channel, t-group of 8) reads 8
+// consecutive t of one channel (banks c + 8 tg + k, distinct) and stores their hi and lo 16 B (64-B runs
+// per row).  The element-wise kernel above moved ~3.7 TB/s over the trainer's 408 MB per step.
 __global__ __launch_bounds__(256) void wt_split2_transpose_v_kernel(const uint4* __restrict__ src,
                                                                     uint4* __restrict__ dst, int T, int C) {
-    constexpr int PITCH = 72;  // halves per LDS row (64 + 8): 144 B, 16-B aligned rows
-    __shared__ __attribute__((aligned(16))) unsigned short hs[64 * PITCH], ls[64 * PITCH];
+    __shared__ unsigned tile[64 * 65];
     const int tt = blockIdx.x, ct = blockIdx.y, e = blockIdx.z, tid = threadIdx.x;
     const int t0 = tt * 64, c0 = ct * 64;
-    const int rl = tid >> 4, j = tid & 15;  // row within a pass, 16-B chunk within the 256-B row
-    const int x0 = j * 8, blk = x0 >> 6, o = x0 & 63;  // 64-half block [hi(32) | lo(32)], offset in it
-    const bool is_lo = o >= 32;
-    const int cl = blk * 32 + (o & 31);  // the chunk's first channel (read) / first t (write) in the tile
-    const uint4* s = src + ((long long)e * T * 2 * C) / 8;
-    uint4* d = dst + ((long long)e * C * 2 * T) / 8;
-    uint4 v[4];
+    const unsigned short* s = reinterpret_cast<const unsigned short*>(src) + (long long)e * T * 2 * C;
+    unsigned short* d = reinterpret_cast<unsigned short*>(dst) + (long long)e * C * 2 * T;
+    const int lane = tid & 63, wv = tid >> 6;
+    {
+        const int cg = lane & 7, tl = lane >> 3;   // 8 channel groups x 8 rows per wave
+        const int cb = cg * 8;                     // the group's first channel in the tile
+        const int hoff = 64 * (cb >> 5) + (cb & 31);  // its hi halves within the row's two 32-channel blocks
+        uint4 hv[2], lv[2];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {  // all four loads in flight before the scatter
-        const int r = p * 16 + rl;  // t within the tile
-        v[p] = s[((long long)(t0 + r) * 2 * C + 2 * c0 + x0) / 8];
-    }
+        for (int p = 0; p < 2; ++p) {  // rows wv * 8 + tl and 32 further: all loads in flight first
+            const int t = p * 32 + wv * 8 + tl;
+            const unsigned short* row = s + (long long)(t0 + t) * 2 * C + 2 * c0;
+            hv[p] = *reinterpret_cast<const uint4*>(row + hoff);
+            lv[p] = *reinterpret_cast<const uint4*>(row + hoff + 32);
+        }
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const int r = p * 16 + rl;
-        unsigned short* dstl = is_lo ? ls : hs;
-        const unsigned w[4] = {v[p].x, v[p].y, v[p].z, v[p].w};
+        for (int p = 0; p < 2; ++p) {
+            const int t = p * 32 + wv * 8 + tl;
+            const unsigned h[4] = {hv[p].x, hv[p].y, hv[p].z, hv[p].w}, l[4] = {lv[p].x, lv[p].y, lv[p].z, lv[p].w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            dstl[(cl + 2 * i) * PITCH + r] = (unsigned short)(w[i] & 0xffffu);
-            dstl[(cl + 2 * i + 1) * PITCH + r] = (unsigned short)(w[i] >> 16);
+            for (int k = 0; k < 8; ++k) {
+                const unsigned hk = (h[k >> 1] >> (16 * (k & 1))) & 0xffffu, lk = (l[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                tile[(cb + k) * 65 + t] = hk | (lk << 16);
+            }
         }
     }
     __syncthreads();
+    {
+        const int tg = lane & 7, cl = lane >> 3;  // 8 t-groups x 8 channels per wave
+        const int tb = tg * 8;                    // the group's first t in the tile
+        const int toff = 64 * (tb >> 5) + (tb & 31);
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const int c = p * 16 + rl;  // channel within the tile: output row
-        const unsigned short* srcl = (is_lo ? ls : hs) + c * PITCH + cl;  // 8 consecutive t
-        const uint4 w = *reinterpret_cast<const uint4*>(srcl);
-        d[((long long)(c0 + c) * 2 * T + 2 * t0 + x0) / 8] = w;
+        for (int p = 0; p < 2; ++p) {
+            const int c = p * 32 + wv * 8 + cl;
+            unsigned w[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w[k] = tile[c * 65 + tb + k];
+            uint4 hv, lv;
+            hv.x = (w[0] & 0xffffu) | (w[1] << 16);
+            hv.y = (w[2] & 0xffffu) | (w[3] << 16);
+            hv.z = (w[4] & 0xffffu) | (w[5] << 16);
+            hv.w = (w[6] & 0xffffu) | (w[7] << 16);
+            lv.x = (w[0] >> 16) | (w[1] & 0xffff0000u);
+            lv.y = (w[2] >> 16) | (w[3] & 0xffff0000u);
+            lv.z = (w[4] >> 16) | (w[5] & 0xffff0000u);
+            lv.w = (w[6] >> 16) | (w[7] & 0xffff0000u);
+            unsigned short* row = d + (long long)(c0 + c) * 2 * T + 2 * t0;
+            *reinterpret_cast<uint4*>(row + toff) = hv;
+            *reinterpret_cast<uint4*>(row + toff + 32) = lv;
+        }
     }
 }
 
