@@ -628,7 +628,8 @@ class InferenceNet(nn.Module):
         if split_out:
             # the flattened NHWC activation as fc1's A operand: [parts][B][chunk] split2 blocks
             # for libazg's split-K GEMM, else one [hi | lo | hi] fp16 row per image (hipBLASLt)
-            kp = self.fc1_kparts if B >= FC1_SPLIT_MIN_BATCH else FC1T_KPARTS  # (the small tail: _fc_split_small)
+            # (the small tail's part count from its own buffer: the one it was split with)
+            kp = self.fc1_kparts if B >= FC1_SPLIT_MIN_BATCH else self.fw1_skT.shape[0]
             y = torch.empty((B, (2 if kp else 3) * Ho * Ho * K), device=dev, dtype=torch.float16)
             self._khook("transform", i, "start")
             _lib.check(L.azg_winograd_out_split(M, bias, ctypes.c_void_p(y.data_ptr()), B, Ho, K, 1, mscale,
@@ -764,7 +765,9 @@ class InferenceNet(nn.Module):
         import ctypes
         from . import _lib
         L = _lib.lib()
-        kp1, kp2, kp3 = FC1T_KPARTS, FCS_KPARTS2, FCS_KPARTS3
+        # the part counts the buffers were split with (not the module globals, which a bench or test may
+        # have changed since this form was built)
+        kp1, kp2, kp3 = self.fw1_skT.shape[0], self.fw2_skS.shape[0], self.fw34_skS.shape[0]
         n1, c1 = self.fw1_skT.shape[1], self.fw1_skT.shape[2] // 2
         m1 = torch.empty((kp1, n1, B), device=dev, dtype=torch.float32)
         pts, rows = (ctypes.c_int32 * 1)(kp1), (ctypes.c_int32 * 1)(n1)
