@@ -46,6 +46,8 @@ SMALL_MAX_B = 4
 FC1_SPLIT_MIN_BATCH = 1024
 # NNetWrapper.train_examples on the GPU: steps run eagerly before the step is captured as a HIP graph
 _GRAPH_EAGER_STEPS = 3
+# training steps per captured HIP graph (args["train_graph_steps"] overrides)
+TRAIN_GRAPH_STEPS = 1
 FC1_KPARTS = 4  # split-K parts of fc1 on libazg's split GEMM (4608 = 4 x 1152 for the 7x7 board)
 # split-K parts of fc2 (1024 -> 512) and [fc3 | fc4] (512 -> 344, padded to 512 columns) when the whole
 # FC tail runs on libazg's split GEMM (InferenceNet.fc_tail_azg): 4 x 256 and 2 x 256 channels, the
@@ -1216,19 +1218,30 @@ class NNetWrapper:
         dev = self.device
         E = planes.shape[0]
         opt = self._adam()
-        ids_buf = torch.zeros(bs, dtype=torch.int64, device=dev)
-        loss_buf = torch.zeros(2, dtype=torch.float32, device=dev)
+        # steps per captured graph: one replay runs gs whole steps (each with its own batch, forward,
+        # backward and Adam update; gradients zeroed in between), so the host issues one launch per
+        # gs steps; an epoch's last nb % gs steps run eagerly
+        gs = max(1, int(self.args.get("train_graph_steps", TRAIN_GRAPH_STEPS)))
+        gs = min(gs, max(1, nb))
+        ids_buf = torch.zeros((gs, bs), dtype=torch.int64, device=dev)
+        loss_buf = torch.zeros((gs, 2), dtype=torch.float32, device=dev)
 
-        def step():
-            tp, tv = pis[ids_buf], vs[ids_buf]
+        def step(i):
+            tp, tv = pis[ids_buf[i]], vs[ids_buf[i]]
             with self._autocast(cache=False):
-                out_pi, out_v = self._train_forward(planes[ids_buf])
+                out_pi, out_v = self._train_forward(planes[ids_buf[i]])
                 l_pi = -torch.sum(tp * out_pi) / tp.size()[0]
                 l_v = torch.sum((tv - out_v.view(-1)) ** 2) / tv.size()[0]
             (l_pi + l_v).backward()
             opt.step()
-            loss_buf[0].copy_(l_pi.detach())
-            loss_buf[1].copy_(l_v.detach())
+            loss_buf[i, 0].copy_(l_pi.detach())
+            loss_buf[i, 1].copy_(l_v.detach())
+
+        def steps():
+            for i in range(gs):
+                if i:
+                    opt.zero_grad(set_to_none=False)  # (the captured grads exist: zero, then accumulate)
+                step(i)
 
         cur = torch.cuda.current_stream(dev)
         side = torch.cuda.Stream(dev)
@@ -1239,15 +1252,16 @@ class NNetWrapper:
         try:
             for _ in range(self.args["epochs"]):
                 ids_all = torch.from_numpy(np.random.randint(E, size=(nb, bs))).to(dev) if nb else None
-                for j in range(nb):
-                    if graph is None and not eager and k >= _GRAPH_EAGER_STEPS:
-                        # capture the step (nothing executes during a capture; a failed one leaves the
+                j = 0
+                while j < nb:
+                    if graph is None and not eager and k >= _GRAPH_EAGER_STEPS and j + gs <= nb:
+                        # capture gs steps (nothing executes during a capture; a failed one leaves the
                         # weights, the optimizer's device state and the RNG where they were)
                         try:
                             g = torch.cuda.CUDAGraph()
                             opt.zero_grad(set_to_none=True)
                             with torch.cuda.graph(g):
-                                step()
+                                steps()
                             graph = g
                         except RuntimeError as err:
                             from ._lib import AzgError
@@ -1258,19 +1272,22 @@ class NNetWrapper:
                                           f"graph ({err}); the remaining steps run eagerly")
                             eager = True
                             torch.cuda.synchronize(dev)
-                    if graph is None:
-                        side.wait_stream(cur)
-                        with torch.cuda.stream(side):
-                            ids_buf.copy_(ids_all[j])
-                            opt.zero_grad(set_to_none=True)
-                            step()
-                            losses[k].copy_(loss_buf)
-                        cur.wait_stream(side)
-                    else:
-                        ids_buf.copy_(ids_all[j])
+                    if graph is not None and j + gs <= nb:
+                        ids_buf.copy_(ids_all[j:j + gs])
                         graph.replay()
-                        losses[k].copy_(loss_buf)
+                        losses[k:k + gs].copy_(loss_buf)
+                        k += gs
+                        j += gs
+                        continue
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        ids_buf[0].copy_(ids_all[j])
+                        opt.zero_grad(set_to_none=graph is None)
+                        step(0)
+                        losses[k].copy_(loss_buf[0])
+                    cur.wait_stream(side)
                     k += 1
+                    j += 1
         finally:
             if graph is not None:
                 torch.cuda.current_stream(dev).synchronize()

@@ -45,11 +45,13 @@ class FusedAdam:
         self._counts = (ctypes.c_int64 * n)(*counts)
 
     def zero_grad(self, set_to_none=True):
-        for p in self.params:
-            if set_to_none:
+        if set_to_none:
+            for p in self.params:
                 p.grad = None
-            elif p.grad is not None:
-                p.grad.zero_()
+            return
+        grads = [p.grad for p in self.params if p.grad is not None]
+        if grads:
+            torch._foreach_zero_(grads)  # one multi-tensor launch, not one per parameter
 
     def step(self, grads=None):
         """One Adam step of every parameter (gradients: `grads` in parameter order, else each

@@ -18,10 +18,13 @@ from azg_amd.inflexion import InflexionGame  # noqa: E402
 from azg_amd.nnet import NNetWrapper  # noqa: E402
 
 
-def run(label, channels_last=False, benchmark=False, batches=30, dtype="f32", fused=False, conv="winograd"):
+def run(label, channels_last=False, benchmark=False, batches=30, dtype="f32", fused=False, conv="winograd",
+        graph_steps=None):
     torch.backends.cudnn.benchmark = benchmark
     torch.manual_seed(0)
-    w = NNetWrapper(InflexionGame(7), dict(epochs=1, batch_size=512, fused_adam=fused, train_dtype=dtype, train_conv=conv), device="cuda")
+    extra = {} if graph_steps is None else {"train_graph_steps": graph_steps}
+    w = NNetWrapper(InflexionGame(7), dict(epochs=1, batch_size=512, fused_adam=fused, train_dtype=dtype,
+                                           train_conv=conv, **extra), device="cuda")
     if channels_last:
         w.nnet.to(memory_format=torch.channels_last)
     E = 512 * batches
@@ -46,6 +49,11 @@ def run(label, channels_last=False, benchmark=False, batches=30, dtype="f32", fu
 if __name__ == "__main__":
     if sys.argv[1:2] == ["f32"]:  # the default trainer alone (e.g. under rocprofv3: kernel time vs wall)
         run("nchw", batches=int(sys.argv[2]) if len(sys.argv) > 2 else 30)
+        sys.exit(0)
+    if sys.argv[1:2] == ["gsteps"]:  # training steps per captured graph, alternating
+        for _ in range(2):
+            for gsn in (1, 2, 4, 8):
+                run(f"graph_steps={gsn}", batches=96, graph_steps=gsn)
         sys.exit(0)
     if sys.argv[1:] == ["conv"]:  # the Winograd training convolutions against the library ones, alternating
         for _ in range(3):
