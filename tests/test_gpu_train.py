@@ -271,6 +271,51 @@ def test_graph_capture_failure_runs_eagerly(monkeypatch):
     torch.testing.assert_close(out[1][2], out[0][2], rtol=1e-6, atol=1e-8)
 
 
+def test_graph_capture_failure_inside_step(monkeypatch):
+    """a capture that fails HALFWAY through the step (an op refusing capture after the
+    forward -- dropout's philox offsets already registered -- before the backward and Adam) falls
+    back to eager steps with the weights, Adam's device state and the RNG streams untouched: the
+    same losses and weights as the eager loop with dropout on, numpy's stream at the same position."""
+    import azg_amd  # noqa: F401
+    from azg_amd.examples import ExampleSet
+    from azg_amd.inflexion import InflexionGame
+    from azg_amd.nnet import NNetWrapper
+
+    gen = torch.Generator().manual_seed(11)
+    E = 512 * 6
+    ex = ExampleSet((torch.rand((E, 4, 7, 7), generator=gen) < 0.3).float().cuda(),
+                    torch.softmax(torch.randn((E, 343), generator=gen), 1).cuda(),
+                    (torch.randint(0, 2, (E,), generator=gen).float() * 2 - 1).cuda())
+    orig = NNetWrapper._train_forward
+
+    def refusing(self, x):
+        out = orig(self, x)
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("op refused capture halfway (test)")
+        return out
+
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    out = []
+    try:
+        for refuse in (False, True):
+            if refuse:
+                monkeypatch.setattr(NNetWrapper, "_train_forward", refusing)
+            torch.manual_seed(0)
+            w = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.3, train_graph=refuse), device="cuda")
+            np.random.seed(4)
+            with pytest.warns(UserWarning, match="could not be captured") if refuse else _nullcontext():
+                losses = w.train_examples(ex).cpu().numpy()
+            out.append((losses, np.random.get_state()[2], w.nnet.state_dict()["fc1.weight"].cpu(),
+                        torch.cuda.get_rng_state().clone()))
+    finally:
+        torch.backends.cudnn.deterministic = det
+    np.testing.assert_allclose(out[1][0], out[0][0], rtol=1e-6)
+    assert out[1][1] == out[0][1]
+    torch.testing.assert_close(out[1][2], out[0][2], rtol=1e-6, atol=1e-8)
+    assert torch.equal(out[1][3], out[0][3])  # torch's CUDA generator where the eager run left it
+
+
 class _nullcontext:
     def __enter__(self):
         return self
