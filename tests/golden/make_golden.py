@@ -733,7 +733,8 @@ def gen_peaked_paths(np, name, seeds=None, weights_eps=None):
     game0 = InflexionGame(7, max_turns=cfg["max_turns"], max_power=6)
     torch.manual_seed(0)
     net = KeyNNet(game0)
-    load_trained(np, net.nnet, name.startswith("peaked"))
+    if name.startswith("trained") or name.startswith("peaked"):  # (realnet_*: the manual_seed(0) network)
+        load_trained(np, net.nnet, name.startswith("peaked"))
     branches = {}
     if weights_eps is not None:
         g = torch.Generator().manual_seed(12345)  # the perturbation of gen_realnet_sensitivity / _branches
