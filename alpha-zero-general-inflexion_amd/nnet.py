@@ -15,6 +15,7 @@ on the CPU with the reference's arithmetic (bit-identical), on the GPU with
 conv2-4 in the Winograd domain and bn1-4 + ReLU on libazg's kernels
 (wino_train.py), each step after the third replayed from a captured HIP graph.
 """
+import contextlib
 import os
 
 import numpy as np
@@ -1122,10 +1123,37 @@ class NNetWrapper:
                 return train_examples_dp(self, ex, group, stats=stats)
             return self._train_single(ex, stats)
 
-        losses = self._overflow_replay(run, group if dp is not None else None)
+        with self._tuned_gemms():
+            losses = self._overflow_replay(run, group if dp is not None else None)
         if stats is not None and self.last_replayed_library:
             stats["replayed_library"] = True
         return losses
+
+    @contextlib.contextmanager
+    def _tuned_gemms(self):
+        """The trainer's library GEMMs (the FC layers on hipBLASLt, f32) under torch's TunableOp for the
+        call: each GEMM shape's fastest hipBLASLt / rocBLAS solution is measured once per process, in
+        the eager steps before the step is captured (+3% examples/s at batch 512,
+        profiles/r06_train_tunableop.json; args["tunable_gemm"] False keeps the heuristic's choice).
+        The process-wide TunableOp switches are restored afterwards."""
+        on = (self.device.type == "cuda" and self.args.get("tunable_gemm", True)
+              and hasattr(torch.cuda, "tunable"))
+        if not on:
+            yield
+            return
+        tun = torch.cuda.tunable
+        prev = (tun.is_enabled(), tun.tuning_is_enabled())
+        if not prev[0]:  # (a user's own TunableOp settings are left as they are)
+            import tempfile
+            tun.set_filename(os.path.join(tempfile.gettempdir(), f"azg_tunableop_{os.getpid()}.csv"))
+        tun.enable(True)
+        tun.tuning_enable(True)
+        tun.set_max_tuning_duration(30)  # ms per GEMM shape
+        try:
+            yield
+        finally:
+            tun.tuning_enable(prev[1])
+            tun.enable(prev[0])
 
     def _overflow_replay(self, run, group=None):
         """run() (a training call); if the Winograd training convolutions met an operand fp16

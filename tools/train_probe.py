@@ -50,6 +50,16 @@ if __name__ == "__main__":
     if sys.argv[1:2] == ["f32"]:  # the default trainer alone (e.g. under rocprofv3: kernel time vs wall)
         run("nchw", batches=int(sys.argv[2]) if len(sys.argv) > 2 else 30)
         sys.exit(0)
+    if sys.argv[1:2] == ["tunable"]:  # the FC layers' hipBLASLt GEMMs with torch's TunableOp, alternating
+        import tempfile
+        for rep in range(2):
+            for on in (False, True):
+                torch.cuda.tunable.enable(on)
+                if on:
+                    torch.cuda.tunable.set_filename(os.path.join(tempfile.gettempdir(), "azg_tunableop.csv"))
+                    torch.cuda.tunable.set_max_tuning_duration(30)
+                run(f"tunableop={on}", batches=96)
+        sys.exit(0)
     if sys.argv[1:2] == ["gsteps"]:  # training steps per captured graph, alternating
         for _ in range(2):
             for gsn in (1, 2, 4, 8):
