@@ -131,6 +131,9 @@ SIGNATURES = [
     ("azg_py_shuffle", ctypes.c_int, [_VP, _I64, _VP, ctypes.POINTER(_I32)]),
     ("azg_adam_step", ctypes.c_int, [_I32, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_double, ctypes.c_double, _VP]),
+    ("azg_train_loss_fwd", ctypes.c_int, [_VP, _I32, _VP, _I32, _VP, _I32, _VP, _I32, _I32, _VP, _VP, _VP]),
+    ("azg_train_loss_bwd", ctypes.c_int, [_VP, _I32, _VP, _I32, _VP, _I32, _VP, _VP, _I32, _I32, _VP, _VP, _I32, _VP,
+                                          _I32, _VP]),
 ]
 
 _lib = None

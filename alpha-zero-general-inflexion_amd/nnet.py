@@ -1046,6 +1046,20 @@ class NNetWrapper:
                 return train_forward(self.nnet, x)
         return self.nnet(x)
 
+    def _train_losses(self, x, tp, tv):
+        """(l_pi, l_v) of a training step (NNet.py:57-61, 96-100).  On the Winograd training path the
+        heads and both losses run on libazg (wino_train.train_losses: 3 launches, args["fused_loss"],
+        default on); otherwise the reference's torch expressions on _train_forward's outputs."""
+        if (self.args.get("fused_loss", True) and x.is_cuda and self.args.get("train_conv", "winograd") == "winograd"
+                and self.args["train_dtype"] == "f32"):
+            from .wino_train import applies_net, train_losses
+            if applies_net(self.nnet, x):
+                return train_losses(self.nnet, x, tp, tv)
+        out_pi, out_v = self._train_forward(x)
+        l_pi = -torch.sum(tp * out_pi) / tp.size()[0]
+        l_v = torch.sum((tv - out_v.view(-1)) ** 2) / tv.size()[0]
+        return l_pi, l_v
+
     def _adam(self):
         """torch.optim.Adam() as NNet.py:37 builds it.  On the GPU: args["optimizer"] "azg" (default)
         is optim.FusedAdam, the capturable foreach form's arithmetic in one libazg launch per step;
@@ -1221,9 +1235,7 @@ class NNetWrapper:
                 ids = ids_all[j]
                 tp, tv = pis[ids], vs[ids]
                 with self._autocast():
-                    out_pi, out_v = self._train_forward(planes[ids])
-                    l_pi = -torch.sum(tp * out_pi) / tp.size()[0]
-                    l_v = torch.sum((tv - out_v.view(-1)) ** 2) / tv.size()[0]
+                    l_pi, l_v = self._train_losses(planes[ids], tp, tv)
                 opt.zero_grad()
                 (l_pi + l_v).backward()
                 opt.step()
@@ -1257,9 +1269,7 @@ class NNetWrapper:
         def step(i):
             tp, tv = pis[ids_buf[i]], vs[ids_buf[i]]
             with self._autocast(cache=False):
-                out_pi, out_v = self._train_forward(planes[ids_buf[i]])
-                l_pi = -torch.sum(tp * out_pi) / tp.size()[0]
-                l_v = torch.sum((tv - out_v.view(-1)) ** 2) / tv.size()[0]
+                l_pi, l_v = self._train_losses(planes[ids_buf[i]], tp, tv)
             (l_pi + l_v).backward()
             opt.step()
             loss_buf[i, 0].copy_(l_pi.detach())

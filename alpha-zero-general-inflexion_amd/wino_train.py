@@ -339,9 +339,9 @@ def conv3x3(x, conv):
     return conv(x)
 
 
-def train_forward(net, s):
-    """InflexionNNet.forward (InflexionNNet.py:39-54) in training, conv2-4 on the Winograd
-    kernels (conv3x3).  Returns (log_softmax(fc3), tanh(fc4)) as the module does."""
+def train_trunk(net, s):
+    """InflexionNNet.forward (InflexionNNet.py:39-53) in training up to fc2's dropout, conv2-4 on the
+    Winograd kernels (conv3x3): the input of fc3 and fc4."""
     x = s.view(-1, net.depth, net.n, net.n)
     if x.is_cuda:
         x = x.contiguous(memory_format=torch.channels_last)
@@ -350,8 +350,51 @@ def train_forward(net, s):
         x = bn_relu(getattr(net, f"bn{i}"), conv3x3(x, getattr(net, f"conv{i}")))
     x = x.reshape(x.shape[0], -1)
     x = F.dropout(F.relu(net.fc_bn1(net.fc1(x))), p=net.dropout, training=net.training)
-    x = F.dropout(F.relu(net.fc_bn2(net.fc2(x))), p=net.dropout, training=net.training)
+    return F.dropout(F.relu(net.fc_bn2(net.fc2(x))), p=net.dropout, training=net.training)
+
+
+def train_forward(net, s):
+    """InflexionNNet.forward (InflexionNNet.py:39-54) in training, conv2-4 on the Winograd
+    kernels (conv3x3).  Returns (log_softmax(fc3), tanh(fc4)) as the module does."""
+    x = train_trunk(net, s)
     return F.log_softmax(net.fc3(x), dim=1), torch.tanh(net.fc4(x))
+
+
+class HeadsLoss(torch.autograd.Function):
+    """(l_pi, l_v) of the training step (NNet.py:57-61, 96-100: -sum(t_pi * log_softmax(x3)) / B and
+    sum((t_v - tanh(z4))^2) / B) and their gradients w.r.t. the fc3 / fc4 outputs on libazg
+    (azg_train_loss.hip): 3 launches per step instead of torch's ~16 (log_softmax, tanh, products, sums,
+    negation, divisions and their adjoints).  Returns two 0-dim tensors."""
+
+    @staticmethod
+    def forward(ctx, x3, z4, tpi, tv):
+        B, A = x3.shape
+        x3c, z4c, tpc, tvc = x3.contiguous(), z4.contiguous(), tpi.contiguous(), tv.contiguous()
+        rows = torch.empty((B, 4), dtype=torch.float32, device=x3.device)
+        out = torch.empty(2, dtype=torch.float32, device=x3.device)
+        _lib.check(_lib.lib().azg_train_loss_fwd(_p(x3c), A, _p(z4c), z4c.stride(0), _p(tpc), A, _p(tvc), B, A,
+                                                 _p(rows), _p(out), _stream(x3.device)))
+        ctx.save_for_backward(x3c, z4c, tpc, tvc, rows)
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, g_pi, g_v):
+        x3, z4, tpi, tv, rows = ctx.saved_tensors
+        B, A = x3.shape
+        dev = x3.device
+        g = torch.stack([g_pi if g_pi is not None else torch.zeros((), device=dev),
+                         g_v if g_v is not None else torch.zeros((), device=dev)]).float().contiguous()
+        dx3 = torch.empty_like(x3)
+        dz4 = torch.empty_like(z4)
+        _lib.check(_lib.lib().azg_train_loss_bwd(_p(x3), A, _p(z4), z4.stride(0), _p(tpi), A, _p(tv), _p(rows), B, A,
+                                                 _p(g), _p(dx3), A, _p(dz4), dz4.stride(0), _stream(dev)))
+        return dx3, dz4, None, None
+
+
+def train_losses(net, s, tpi, tv):
+    """(l_pi, l_v) of a training step: train_trunk, fc3 / fc4, then HeadsLoss."""
+    x = train_trunk(net, s)
+    return HeadsLoss.apply(net.fc3(x), net.fc4(x), tpi, tv)
 
 
 def check_range(device=None):

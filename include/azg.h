@@ -455,6 +455,19 @@ int  azg_wt_pow2_scale(const uint32_t* amax, float target, float* out, void* str
 /* dw [k][c][3][3] = 2^-kd sum_e G_a^T dU_e G_b from dU [P][c][k] (the weights' adjoint transform). */
 int  azg_wt_dw(const float* dU, int32_t c, int32_t k, int32_t h_out, const uint32_t* dyamax, float* dw, void* stream);
 
+/* ---- the training step's heads and losses (azg_train_loss.hip; NNet.py:57-61, 96-100) ---------------
+ * azg_train_loss_fwd: out[0] = l_pi = -sum_b sum_a t_pi[b][a] log_softmax(x3[b])[a] / B, out[1] = l_v =
+ *   sum_b (t_v[b] - tanh(z4[b]))^2 / B (rows summed in a fixed order); rows [B][4] receives each row's two
+ *   terms and its softmax statistics (max, log sum exp) for the backward.
+ * azg_train_loss_bwd: dx3 = g[0] (softmax(x3) sum_a t_pi - t_pi) / B and dz4 = g[1] (-2 (t_v - v)) (1 - v^2) / B
+ *   (the adjoints of log_softmax and tanh as torch forms them), g: the losses' gradients (device, 2 floats).
+ * x3 / t_pi / dx3 rows of A floats at strides ld3 / ldt / lddx; z4 / dz4 at strides ld4 / lddz. */
+int  azg_train_loss_fwd(const float* x3, int32_t ld3, const float* z4, int32_t ld4, const float* tpi, int32_t ldt,
+                        const float* tv, int32_t B, int32_t A, float* rows, float* out, void* stream);
+int  azg_train_loss_bwd(const float* x3, int32_t ld3, const float* z4, int32_t ld4, const float* tpi, int32_t ldt,
+                        const float* tv, const float* rows, int32_t B, int32_t A, const float* g, float* dx3,
+                        int32_t lddx, float* dz4, int32_t lddz, void* stream);
+
 /* ---- the trainer's optimizer (azg_adam.hip) -------------------------------------------------
  * azg_adam_step: torch.optim.Adam's step (NNet.py:37; the capturable foreach arithmetic of
  * torch/optim/adam.py in f32, no weight decay / amsgrad) over nseg parameter tensors in one launch:

@@ -286,10 +286,10 @@ def test_graph_capture_failure_inside_step(monkeypatch):
     ex = ExampleSet((torch.rand((E, 4, 7, 7), generator=gen) < 0.3).float().cuda(),
                     torch.softmax(torch.randn((E, 343), generator=gen), 1).cuda(),
                     (torch.randint(0, 2, (E,), generator=gen).float() * 2 - 1).cuda())
-    orig = NNetWrapper._train_forward
+    orig = NNetWrapper._train_losses
 
-    def refusing(self, x):
-        out = orig(self, x)
+    def refusing(self, x, tp, tv):
+        out = orig(self, x, tp, tv)
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("op refused capture halfway (test)")
         return out
@@ -300,7 +300,7 @@ def test_graph_capture_failure_inside_step(monkeypatch):
     try:
         for refuse in (False, True):
             if refuse:
-                monkeypatch.setattr(NNetWrapper, "_train_forward", refusing)
+                monkeypatch.setattr(NNetWrapper, "_train_losses", refusing)
             torch.manual_seed(0)
             w = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.3, train_graph=refuse), device="cuda")
             np.random.seed(4)

@@ -237,3 +237,27 @@ def test_split2_transpose_matches_torch(P, T, C, offset):
     want = logical.transpose(2, 3).reshape(P, 2, C, T // 32, 32).permute(0, 2, 3, 1, 4).reshape(-1)
     assert torch.equal(dst, want)
     assert torch.count_nonzero(out[:offset]) == 0 and torch.count_nonzero(out[offset + dst.numel():]) == 0
+
+
+@pytest.mark.parametrize("B,A", [(512, 343), (64, 37), (8, 65)])
+def test_heads_loss_matches_torch(B, A):
+    """wino_train.HeadsLoss (azg_train_loss.hip: log_softmax + tanh + both losses and their adjoints in 3
+    launches) against the reference's torch expressions (NNet.py:57-61, 96-100) in f64: losses within
+    2e-6 relative, the gradients w.r.t. the fc3 / fc4 outputs within 1e-6 of their size."""
+    import azg_amd  # noqa: F401
+    from azg_amd.wino_train import HeadsLoss
+    g = torch.Generator(device="cuda").manual_seed(B + A)
+    x3 = (torch.randn((B, A), generator=g, device="cuda") * 3).requires_grad_()
+    z4 = torch.randn((B, 1), generator=g, device="cuda").requires_grad_()
+    tp = torch.softmax(torch.randn((B, A), generator=g, device="cuda"), 1)
+    tv = torch.randint(0, 2, (B,), generator=g, device="cuda").float() * 2 - 1
+    l_pi, l_v = HeadsLoss.apply(x3, z4, tp, tv)
+    (l_pi + 0.5 * l_v).backward()
+    x64, z64 = x3.detach().double().requires_grad_(), z4.detach().double().requires_grad_()
+    r_pi = -torch.sum(tp.double() * torch.log_softmax(x64, dim=1)) / B
+    r_v = torch.sum((tv.double() - torch.tanh(z64).view(-1)) ** 2) / B
+    (r_pi + 0.5 * r_v).backward()
+    assert abs(l_pi.item() - r_pi.item()) <= 2e-6 * abs(r_pi.item())
+    assert abs(l_v.item() - r_v.item()) <= 2e-6 * abs(r_v.item())
+    assert ((x3.grad.double() - x64.grad).norm() / x64.grad.norm()).item() < 1e-6
+    assert ((z4.grad.double() - z64.grad).norm() / z64.grad.norm()).item() < 1e-6

@@ -19,10 +19,10 @@ from azg_amd.nnet import NNetWrapper  # noqa: E402
 
 
 def run(label, channels_last=False, benchmark=False, batches=30, dtype="f32", fused=False, conv="winograd",
-        graph_steps=None):
+        graph_steps=None, **more):
     torch.backends.cudnn.benchmark = benchmark
     torch.manual_seed(0)
-    extra = {} if graph_steps is None else {"train_graph_steps": graph_steps}
+    extra = dict(more) if graph_steps is None else {"train_graph_steps": graph_steps, **more}
     w = NNetWrapper(InflexionGame(7), dict(epochs=1, batch_size=512, fused_adam=fused, train_dtype=dtype,
                                            train_conv=conv, **extra), device="cuda")
     if channels_last:
@@ -49,6 +49,11 @@ def run(label, channels_last=False, benchmark=False, batches=30, dtype="f32", fu
 if __name__ == "__main__":
     if sys.argv[1:2] == ["f32"]:  # the default trainer alone (e.g. under rocprofv3: kernel time vs wall)
         run("nchw", batches=int(sys.argv[2]) if len(sys.argv) > 2 else 30)
+        sys.exit(0)
+    if sys.argv[1:2] == ["ab"]:  # one trainer option on / off, alternating: ab <option>
+        for _ in range(3):
+            for on in (False, True):
+                run(f"{sys.argv[2]}={on}", batches=96, **{sys.argv[2]: on})
         sys.exit(0)
     if sys.argv[1:2] == ["tunable"]:  # the FC layers' hipBLASLt GEMMs with torch's TunableOp, alternating
         import tempfile
