@@ -709,7 +709,14 @@ def main():
         gen["max_live_nodes"], gen["max_path_depth"] = gst["max_live_nodes"], gst["max_depth"]
     learn = None
     if gen is not None and args.learn_iteration != "off" and args.evaluator == "net":
-        learn = learn_iteration(args, eng, net, rank, world, gen)
+        # (after the timed region: a failure here is reported in the line, not allowed to lose the
+        # measured value -- every rank runs the same code, so an error raises on all of them)
+        try:
+            learn = learn_iteration(args, eng, net, rank, world, gen)
+        except Exception as e:  # noqa: BLE001
+            import traceback
+            traceback.print_exc(file=sys.stderr)
+            learn = {"error": f"{type(e).__name__}: {e}"[:500]}
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
