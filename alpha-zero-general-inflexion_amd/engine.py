@@ -232,12 +232,44 @@ class SelfPlayEngine:
         check(self.L.azg_active_games(self.h, ctypes.byref(n), self._stream()))
         return n.value
 
-    def play(self, max_moves=None):
+    # leaf batches up to this many games replay each move from a captured HIP graph in play() /
+    # play_games() (graph="auto"): with few games a move's ~50 launches per simulation cost host time the
+    # GPU waits for -- 64 games x 25 sims, whole games: 0.30-0.34M -> 0.39-0.40M node expansions/s; at 256
+    # and 1024 the two loops measured equal (1.10-1.11M, 1.80-1.81M; profiles/r06_play_graph_ab.json)
+    GRAPH_MAX_GAMES = 256
+
+    def _auto_graph(self, graph, moved):
+        """Capture the move as a HIP graph after the first eager move when graph is True, or "auto" and
+        the batch is small (GRAPH_MAX_GAMES) with an InferenceNet evaluator; a refused capture keeps the
+        eager loop (the same kernels: the same records)."""
+        if getattr(self, "_graph", None) is not None or moved < 1:
+            return
+        if graph == "auto":  # (only this repo's network forms: a user's callable may run host code per call,
+            from .nnet import InferenceNet  # which a replayed graph would skip)
+            graph = self.G <= self.GRAPH_MAX_GAMES and isinstance(self.evaluator, InferenceNet)
+        if not graph:
+            return
+        try:
+            self.capture_move()
+        except _lib.AzgError:
+            raise  # an engine error is an error, not a capture limitation
+        except RuntimeError as e:
+            import warnings
+            warnings.warn(f"SelfPlayEngine: the move could not be captured ({e}); playing eagerly")
+            self._graph = None
+            torch.cuda.synchronize(self.device)
+
+    def play(self, max_moves=None, graph="auto"):
         """Play every slot's game to the end (or max_moves moves). Returns moves made."""
         m = 0
-        while self.active() > 0 and (max_moves is None or m < max_moves):
-            self.move()
-            m += 1
+        try:
+            while self.active() > 0 and (max_moves is None or m < max_moves):
+                self._auto_graph(graph, m)
+                self.move()
+                m += 1
+        finally:
+            if graph == "auto":
+                self.drop_graph()
         self.check_evaluator()
         return m
 
@@ -250,7 +282,7 @@ class SelfPlayEngine:
         if chk is not None:
             chk()
 
-    def play_games(self, num_games, first_game=None, check_every=1):
+    def play_games(self, num_games, first_game=None, check_every=1, graph="auto"):
         """Continuous batching (azg_refill): play the num_games games
         with global indices first_game .. first_game + num_games - 1 through the G
         slots.  A slot whose game ends hands its record off and starts the next index
@@ -276,12 +308,17 @@ class SelfPlayEngine:
         args = (_ptr(nxt), fg + n, self.cfg.seed_base, _ptr(cnt), n, _ptr(ids), _ptr(moves), _ptr(actions),
                 _ptr(temps), _ptr(counts) if counts is not None else None)
         k = 0
-        while True:
-            self.move()
-            check(self.L.azg_refill(self.h, *args, self._stream()))
-            k += 1
-            if k % check_every == 0 and self.active() == 0:
-                break
+        try:
+            while True:
+                self._auto_graph(graph, k)
+                self.move()
+                check(self.L.azg_refill(self.h, *args, self._stream()))
+                k += 1
+                if k % check_every == 0 and self.active() == 0:
+                    break
+        finally:
+            if graph == "auto":
+                self.drop_graph()
         self.check_evaluator()
         done = int(cnt.item())
         if done != n:
