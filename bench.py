@@ -41,7 +41,7 @@ EXPANSIONS_PER_GAME_REF = 8555   # reference random-init Inflexion episodes (BAS
 GEMM_PMC_FILE = os.path.join(ROOT, "profiles", "r05_split_gemm_pmc_v4.json")  # the azg_split_gemm default (round 5 tree)
 # PMC passes of the current Winograd tiling (F(4,3)+F(3,3) / F(5,3) / F(3,3)); the r01 files
 # were measured on the earlier F(3,3)/F(2,3) tiling and are kept for the record only
-PMC_FILE_WINOGRAD = {"split": os.path.join(ROOT, "profiles", "r05_pmc_G4096_winograd_split.json")}
+PMC_FILE_WINOGRAD = {"split": os.path.join(ROOT, "profiles", "r06_pmc_C4.json")}  # (round 6 pass; r05 agrees to 1e-4)
 
 PRESETS = {
     "C1": dict(game="othello", n=6, games=1, sims=25),
