@@ -454,8 +454,6 @@ class InferenceNet(nn.Module):
     def check_range(self):
         """Raise if any split-GEMM operand since the last call was out of fp16 range
         (|v| > 65504 or NaN): the GEMM would have been wrong, not just inexact."""
-        if getattr(self, "_fused_bar", None) is not None:
-            self.check_fused()
         if self.gemm != "f32" and int(self.overflow.item()) != 0:
             self.overflow.zero_()
             raise FloatingPointError("Winograd split-GEMM operand out of fp16 range; use InferenceNet(gemm='f32')")

@@ -178,6 +178,10 @@ def _probe_class():
                 st), "azg_small_net")
             return p, v
 
+        def check_range(self):
+            self.check_fused()
+            super().check_range()
+
         def check_fused(self):
             """Raise if a wait of the fused forward gave up (a layer's items never all finished: the
             results of that launch are void), and reset its work queue."""
