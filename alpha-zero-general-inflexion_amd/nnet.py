@@ -49,6 +49,9 @@ FC1_SPLIT_MIN_BATCH = 1024
 _GRAPH_EAGER_STEPS = 3
 # training steps per captured HIP graph (args["train_graph_steps"] overrides)
 TRAIN_GRAPH_STEPS = 1
+# the trainer's FC GEMMs tuned once on an MI355X by torch's TunableOp (tools/tune_gemms.py): read at the
+# start of train_examples so that no process spends its first call tuning (NNetWrapper._tuned_gemms)
+TUNABLEOP_RESULTS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_results.csv")
 FC1_KPARTS = 4  # split-K parts of fc1 on libazg's split GEMM (4608 = 4 x 1152 for the 7x7 board)
 # split-K parts of fc2 (1024 -> 512) and [fc3 | fc4] (512 -> 344, padded to 512 columns) when the whole
 # FC tail runs on libazg's split GEMM (InferenceNet.fc_tail_azg): 4 x 256 and 2 x 256 channels, the
@@ -1004,6 +1007,8 @@ def replay_form(net):
 class NNetWrapper:
     """Reference NNetWrapper surface (NNet.py:27-120) over InflexionNNet."""
 
+    _tuned_read = None  # whether TunableOp accepted TUNABLEOP_RESULTS (read once per process)
+
     def __init__(self, game=None, args=None, device=None):
         a = dict(DEFAULT_ARGS)
         a.update(args or {})
@@ -1144,12 +1149,15 @@ class NNetWrapper:
     @contextlib.contextmanager
     def _tuned_gemms(self):
         """The trainer's library GEMMs (the FC layers on hipBLASLt, f32) under torch's TunableOp for the
-        call: each GEMM shape's fastest hipBLASLt / rocBLAS solution is measured once per process, in
-        the eager steps before the step is captured (+3% examples/s at batch 512,
-        profiles/r06_train_tunableop.json; args["tunable_gemm"] False keeps the heuristic's choice).
-        The process-wide TunableOp switches are restored afterwards."""
-        on = (self.device.type == "cuda" and self.args.get("tunable_gemm", True)
-              and hasattr(torch.cuda, "tunable"))
+        call, each GEMM shape on its fastest hipBLASLt / rocBLAS solution (+3% examples/s at batch 512,
+        profiles/r06_train_tunableop.json).  The solutions come from TUNABLEOP_RESULTS (tuned once by
+        tools/tune_gemms.py); when that file is absent or TunableOp rejects it (another torch, ROCm or
+        GPU), or args["tunable_gemm"] is "tune", each shape is measured once per process instead, in the
+        eager steps before the step is captured (a few seconds on a process's first call).
+        args["tunable_gemm"] False keeps the heuristic's choice.  The process-wide TunableOp switches are
+        restored afterwards."""
+        mode = self.args.get("tunable_gemm", True)
+        on = self.device.type == "cuda" and bool(mode) and hasattr(torch.cuda, "tunable")
         if not on:
             yield
             return
@@ -1159,7 +1167,12 @@ class NNetWrapper:
             import tempfile
             tun.set_filename(os.path.join(tempfile.gettempdir(), f"azg_tunableop_{os.getpid()}.csv"))
         tun.enable(True)
-        tun.tuning_enable(True)
+        tuned = False
+        if mode != "tune" and os.path.exists(TUNABLEOP_RESULTS):
+            if NNetWrapper._tuned_read is None:
+                NNetWrapper._tuned_read = bool(tun.read_file(TUNABLEOP_RESULTS))
+            tuned = NNetWrapper._tuned_read
+        tun.tuning_enable(not tuned)
         tun.set_max_tuning_duration(30)  # ms per GEMM shape
         try:
             yield
