@@ -353,8 +353,9 @@ def test_data_parallel_trainer_on_the_training_kernels():
     """The data-parallel trainer at the real network's size (512 channels: conv2-4 on the Winograd
     training kernels, bn1-4 + ReLU on BatchNormReLUDP -- the NHWC kernels with the ranks' f64 sums
     all-reduced), two gloo ranks on one GPU, against the one-process GPU trainer on the same
-    examples and draws (dropout 0, MIOpen deterministic): per-batch losses within the GPU trainer's
-    2e-3, the weights' update (in norm) within 5e-2 of its size, the running variance within 1e-3 (three
+    examples and draws (dropout 0, MIOpen deterministic): per-batch losses within 2e-3 and the weights'
+    update (in norm) within 5e-2 of its size -- or within 1.25x the one-process trainer's own spread when
+    rerun from initial weights moved by one ulp, where that is larger (Adam's sign steps) -- the running variance within 1e-3 (three
     steps: the second and third batches' variances are taken under weights that already differ by the
     two trainers' rounding; measured 1.1e-4) -- and 12 BatchNorm all-reduces per step (4 conv BatchNorms + 2 FC ones, forward and backward)."""
     import azg_amd  # noqa: F401
@@ -388,15 +389,43 @@ def test_data_parallel_trainer_on_the_training_kernels():
         np.random.seed(4)
         ref = w0.train_examples(ex).cpu().numpy()
         sd = {k: v.detach().cpu().numpy() for k, v in w0.nnet.state_dict().items()}
+        # the one-process trainer's own spread: rerun from the initial weights moved by one ulp each
+        # (random directions, two seeds) -- how far rounding alone moves its three steps
+        spread_sd, spread_loss = [], []
+        for s in (1, 2):
+            torch.manual_seed(0)
+            w1 = NNetWrapper(InflexionGame(7), dict(epochs=1, dropout=0.0, train_graph=False), device="cuda")
+            gs = torch.Generator().manual_seed(s)
+            with torch.no_grad():
+                for prm in w1.nnet.parameters():
+                    up = torch.rand(prm.shape, generator=gs) < 0.5
+                    inf = torch.where(up, torch.tensor(float("inf")), torch.tensor(float("-inf"))).to(prm.device)
+                    prm.copy_(torch.nextafter(prm, inf))
+            np.random.seed(4)
+            spread_loss.append(np.abs(w1.train_examples(ex).cpu().numpy() - ref))
+            spread_sd.append({k: v.detach().cpu().numpy() for k, v in w1.nnet.state_dict().items()})
     finally:
         torch.backends.cudnn.deterministic = det
+    # Adam's early steps are lr x sign(g): an element whose gradient sits in the rounding noise takes
+    # either step, so the data-parallel trainer (other reduction orders, 256-example FC GEMMs) is held to
+    # the one-process trainer's own ulp spread (x 1.25) where that exceeds 2e-3 (losses) / 5e-2 (updates)
+    tol_w = {k: max(5e-2, 1.25 * max(np.linalg.norm(q[k] - sd[k]) / np.linalg.norm(sd[k] - init[k])
+                                     for q in spread_sd))
+             for k in ("conv2.weight", "conv4.weight", "fc1.weight")}
+    # batch k's losses are taken under the weights after k updates: on top of 2e-3 they may differ by the
+    # updates' tolerated fraction of how far the losses moved from batch 0's
+    tol_loss = np.maximum(2e-3 * np.abs(ref) + max(tol_w.values()) * np.abs(ref - ref[0]),
+                          1.25 * np.max(spread_loss, axis=0))
+    print("ulp spread: losses", np.max(spread_loss, axis=0).tolist(), "updates", tol_w)
     for r in (0, 1):
         losses, w, calls = res[r]
-        np.testing.assert_allclose(losses, ref, rtol=2e-3)
+        np.testing.assert_allclose(losses[0], ref[0], rtol=2e-3)
+        assert (np.abs(losses - ref) <= tol_loss).all(), (r, losses, ref, tol_loss)
         assert calls == 12, calls
-        for k in ("conv2.weight", "conv4.weight", "fc1.weight"):
+        for k in tol_w:
             d = np.linalg.norm(w[k] - sd[k]) / np.linalg.norm(sd[k] - init[k])
-            assert d < 5e-2, (r, k, d)
+            print(f"rank {r} {k}: update {d:.2e} apart (tolerance {tol_w[k]:.2e})")
+            assert d < tol_w[k], (r, k, d, tol_w[k])
         np.testing.assert_allclose(w["bn2.running_var"], sd["bn2.running_var"], rtol=1e-3, atol=1e-6)
     for k in res[0][1]:  # the ranks' weights stay bitwise equal
         assert np.array_equal(res[0][1][k], res[1][1][k]), k
