@@ -347,3 +347,30 @@ def test_out_of_range_train_list_replays():
     np.random.seed(1)
     w2.train(ex)
     assert not w2.last_replayed_library
+
+
+def test_tuned_gemm_file_is_used():
+    """train_examples reads the packaged TunableOp solutions (nnet.TUNABLEOP_RESULTS) instead of tuning:
+    TunableOp accepts the file on this image's MI355X, tunes nothing during the call (its results are
+    exactly the file's), and leaves the process-wide switches as it found them."""
+    import azg_amd  # noqa: F401
+    from azg_amd import nnet
+    from azg_amd.examples import ExampleSet
+    from azg_amd.inflexion import InflexionGame
+    tun = torch.cuda.tunable
+    before = (tun.is_enabled(), tun.tuning_is_enabled())
+    g = torch.Generator().manual_seed(3)
+    E = 512 * 2
+    ex = ExampleSet((torch.rand((E, 4, 7, 7), generator=g) < 0.3).float().cuda(),
+                    torch.softmax(torch.randn((E, 343), generator=g), 1).cuda(),
+                    (torch.randint(0, 2, (E,), generator=g).float() * 2 - 1).cuda())
+    torch.manual_seed(0)
+    w = nnet.NNetWrapper(InflexionGame(7), dict(epochs=1), device="cuda")
+    np.random.seed(0)
+    w.train_examples(ex)
+    assert nnet.NNetWrapper._tuned_read is True
+    with open(nnet.TUNABLEOP_RESULTS) as f:
+        filed = {tuple(line.strip().split(",")[:3]) for line in f if not line.startswith("Validator")}
+    got = {tuple(map(str, r[:3])) for r in tun.get_results()}
+    assert got <= filed, got - filed
+    assert (tun.is_enabled(), tun.tuning_is_enabled()) == before
