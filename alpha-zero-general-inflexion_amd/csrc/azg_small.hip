@@ -52,6 +52,20 @@
 #error "azg_small.hip's split-K hand-off assumes the gfx950 memory model (see the comment above)"
 #endif
 
+#ifdef AZG_SMALL_TIMING  // probe build only (tools/Makefile libazg_small_timing.so, tools/sk_stamps.py)
+// per-block wall-clock stamps of the split-K conv's phases: [block][8] (vector stores from lane 0)
+__device__ unsigned long long azg_sk_stamps[1024 * 8];
+#define SK_STAMP(i)                                                                                     \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && bid < 1024)                                                             \
+            __builtin_nontemporal_store(wall_clock64(), azg_sk_stamps + bid * 8 + (i) + threadIdx.x); \
+    } while (0)
+#else
+#define SK_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
+
 namespace {
 
 constexpr int SC_T = 512;  // small_conv threads
@@ -259,7 +273,7 @@ __global__ __launch_bounds__(SC_T) void small_conv_kernel(const float* __restric
 // block waits on another.
 // KG = SK_KG = 8 K-parts for conv3 / conv4 (staged input eighth + weights + slice partials, n <= 8,
 // Cin = 512: <= 52 KB, two blocks per CU) and SK_KG1 = 4 for conv12, whose conv1 registers
-// allow one 512-thread block per CU (<= 87 KB)
+// allow one 512-thread block per CU (<= 87 KB; 8 parts at two blocks per CU spill 258 VGPRs)
 // (4 / 8 / 16 K-parts for conv3 at one leaf: 16.2 / 14.3 / 19.0 us; 16 fit two blocks per CU for 1024
 // blocks, two rounds; tools/small_layer_bench.py)
 constexpr int SK_CO = 8, SK_KG = 8, SK_KG1 = 4;
@@ -285,6 +299,7 @@ __device__ __forceinline__ void small_conv_sk_body(int bid, int nblk, float* __r
                                                    const float* __restrict__ w1, const float* __restrict__ b1, int D) {
     constexpr int KSL = SC_T / PXL;
     constexpr int SC_WPF = sk_wpf(KG);
+    SK_STAMP(0);
     const int tid = threadIdx.x;
     const int p = tid % PXL, s = tid / PXL;
     const int cg = bid / KG, kg = bid % KG;
@@ -294,21 +309,41 @@ __device__ __forceinline__ void small_conv_sk_body(int bid, int nblk, float* __r
     const int P = Cq + 4;                       // LDS pitch of a staged pixel
     const int Kq = 9 * Cq;                      // this quarter's products per output
     float* xs = lds;                            // [H * H][P]
-    float* ws = xs + H * H * P;                 // [Kq][SK_CO]: k-major, the 8 channels of a k adjacent
+    // the quarter's weights w[co0 + c][tap][ci_base + ci], k = tap * Cq + ci:
+    //  * CM (conv3 / conv4): channel-major, ws[c * Kq + k] -- float4 i of the slice at ws[4 i], one
+    //    conflict-free ds_write_b128 each (the k-major layout's four strided ds_write_b32 per float4
+    //    conflict 32 ways: staging 8.6 -> 2.6 us per block at one leaf, tools/sk_stamps.py);
+    //  * conv12 (F1 > 0): k-major, ws[k * 8 + c], the 8 channels of a k adjacent (its weights are staged
+    //    under conv1's arithmetic; channel-major measured slower there, 7.0 -> 9.0 us of products)
+    constexpr bool CM = F1 == 0;
+    float* ws = xs + H * H * P;                 // [SK_CO][Kq] (CM) or [Kq][SK_CO]
     float* red = ws + Kq * SK_CO;               // [KSL][PXL][SK_CO]
-    // the quarter's weights: w[co0 + c][tap][ci_base + ci] -> ws[(tap * Cq + ci) * 8 + c]
     const int q4 = Cq / 4, nw4 = SK_CO * 9 * q4;
+    // float4 i of the slice: channel c = i / (9 q4), then (tap, ci), so that (CM) ws[4 i] is its place
+    // (conv12's staging is bound by conv1's arithmetic, not by its strided stores: c fastest, 4-way
+    // instead of 32-way conflicts, left its 8.0 us unchanged, tools/sk_stamps.py)
+    auto wcoord = [&](int i, int& c, int& tap, int& ci) {
+        c = i / (9 * q4);
+        const int r = i - c * 9 * q4;
+        tap = r / q4, ci = (r - tap * q4) * 4;
+    };
     auto wload = [&](int i) {
-        const int c = i / (9 * q4), r = i - c * 9 * q4, tap = r / q4, ci = (r - tap * q4) * 4;
+        int c, tap, ci;
+        wcoord(i, c, tap, ci);
         return *(const float4*)(w + ((long long)(co0 + c) * 9 + tap) * Cin + ci_base + ci);
     };
     auto wstore = [&](int i, float4 v) {
-        const int c = i / (9 * q4), r = i - c * 9 * q4, tap = r / q4, ci = (r - tap * q4) * 4;
-        float* d = ws + (tap * Cq + ci) * SK_CO + c;
-        d[0] = v.x;
-        d[SK_CO] = v.y;
-        d[2 * SK_CO] = v.z;
-        d[3 * SK_CO] = v.w;
+        if constexpr (CM) {
+            *(float4*)(ws + 4 * i) = v;
+        } else {
+            int c, tap, ci;
+            wcoord(i, c, tap, ci);
+            float* d = ws + (tap * Cq + ci) * SK_CO + c;
+            d[0] = v.x;
+            d[SK_CO] = v.y;
+            d[2 * SK_CO] = v.z;
+            d[3 * SK_CO] = v.w;
+        }
     };
     float4 wpf[F1 > 0 ? 1 : SC_WPF];  // (conv12: the waves that compute no conv1 stage the weights)
     if constexpr (F1 == 0) {
@@ -364,17 +399,22 @@ __device__ __forceinline__ void small_conv_sk_body(int bid, int nblk, float* __r
         }
         const float* __restrict__ xb = x + b * sB + ci_base;
         const int c4 = Cq / 4, n4 = F1 > 0 ? 0 : H * H * c4;
-        for (int base = tid; base < n4; base += SC_T * SC_UNR) {
-            float4 r[SC_UNR];
+        // input loads in flight per thread: 4 (a one-leaf eighth of conv3's input is 784 float4, two per
+        // thread; 16 in flight cost 64 VGPRs and spilled under the two-blocks-per-CU bound)
+        constexpr int UNR = 4;
+        for (int base = tid; base < n4; base += SC_T * UNR) {
+            const int rem = n4 - (base - tid);  // (block-uniform: no load past the block's last float4)
+            float4 r[UNR];
 #pragma unroll
-            for (int u = 0; u < SC_UNR; ++u) {
+            for (int u = 0; u < UNR; ++u) {
+                if (u * SC_T >= rem) break;
                 const int i = min(base + u * SC_T, n4 - 1);
                 const int pix = i / c4, c = (i - pix * c4) * 4, iy = pix / H, ix = pix - iy * H;
                 r[u] = ld4<COH>(xb, (long long)iy * sY + (long long)ix * sX + c);
             }
             stage_w();  // the weights' stores once the first input loads are in flight
 #pragma unroll
-            for (int u = 0; u < SC_UNR; ++u) {
+            for (int u = 0; u < UNR; ++u) {
                 const int i = base + u * SC_T;
                 if (i < n4) {
                     const int pix = i / c4, c = (i - pix * c4) * 4;
@@ -384,6 +424,7 @@ __device__ __forceinline__ void small_conv_sk_body(int bid, int nblk, float* __r
         }
         stage_w();
         __syncthreads();
+        SK_STAMP(1);
         float acc[SK_CO];
 #pragma unroll
         for (int c = 0; c < SK_CO; ++c) acc[c] = 0.f;
@@ -396,23 +437,39 @@ __device__ __forceinline__ void small_conv_sk_body(int bid, int nblk, float* __r
                 const int iy = oy + tap / 3 - pad, ix = ox + tap % 3 - pad;
                 if (iy >= 0 && iy < H && ix >= 0 && ix < H) {
                     const float* xp = xs + (iy * H + ix) * P + ci0;
-                    const float* wp = ws + k * SK_CO;
+                    if constexpr (CM) {
+                        const float* wp = ws + k;
 #pragma unroll 2
-                    for (int j = 0; j < run; ++j) {
-                        const float4 xv = *(const float4*)(xp + 4 * j);
-                        const float xs4[4] = {xv.x, xv.y, xv.z, xv.w};
+                        for (int j = 0; j < run; ++j) {
+                            const float4 xv = *(const float4*)(xp + 4 * j);
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const float4 wa = *(const float4*)(wp + (4 * j + e) * SK_CO);
-                            const float4 wb = *(const float4*)(wp + (4 * j + e) * SK_CO + 4);
-                            acc[0] = fmaf(wa.x, xs4[e], acc[0]);
-                            acc[1] = fmaf(wa.y, xs4[e], acc[1]);
-                            acc[2] = fmaf(wa.z, xs4[e], acc[2]);
-                            acc[3] = fmaf(wa.w, xs4[e], acc[3]);
-                            acc[4] = fmaf(wb.x, xs4[e], acc[4]);
-                            acc[5] = fmaf(wb.y, xs4[e], acc[5]);
-                            acc[6] = fmaf(wb.z, xs4[e], acc[6]);
-                            acc[7] = fmaf(wb.w, xs4[e], acc[7]);
+                            for (int c = 0; c < SK_CO; ++c) {  // per channel its four k in order
+                                const float4 wv = *(const float4*)(wp + c * Kq + 4 * j);
+                                acc[c] = fmaf(wv.x, xv.x, acc[c]);
+                                acc[c] = fmaf(wv.y, xv.y, acc[c]);
+                                acc[c] = fmaf(wv.z, xv.z, acc[c]);
+                                acc[c] = fmaf(wv.w, xv.w, acc[c]);
+                            }
+                        }
+                    } else {
+                        const float* wp = ws + k * SK_CO;
+#pragma unroll 2
+                        for (int j = 0; j < run; ++j) {
+                            const float4 xv = *(const float4*)(xp + 4 * j);
+                            const float xs4[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const float4 wa = *(const float4*)(wp + (4 * j + e) * SK_CO);
+                                const float4 wb = *(const float4*)(wp + (4 * j + e) * SK_CO + 4);
+                                acc[0] = fmaf(wa.x, xs4[e], acc[0]);
+                                acc[1] = fmaf(wa.y, xs4[e], acc[1]);
+                                acc[2] = fmaf(wa.z, xs4[e], acc[2]);
+                                acc[3] = fmaf(wa.w, xs4[e], acc[3]);
+                                acc[4] = fmaf(wb.x, xs4[e], acc[4]);
+                                acc[5] = fmaf(wb.y, xs4[e], acc[5]);
+                                acc[6] = fmaf(wb.z, xs4[e], acc[6]);
+                                acc[7] = fmaf(wb.w, xs4[e], acc[7]);
+                            }
                         }
                     }
                 }
@@ -423,6 +480,7 @@ __device__ __forceinline__ void small_conv_sk_body(int bid, int nblk, float* __r
         r4[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
         r4[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
         __syncthreads();
+        SK_STAMP(2);
         // the block's partial for leaf b, slices summed in order -> part[kg][b][pixel][8]
         for (int t = tid; t < hw * SK_CO; t += SC_T) {
             const int pp = t / SK_CO, c = t - pp * SK_CO;
@@ -441,9 +499,11 @@ __device__ __forceinline__ void small_conv_sk_body(int bid, int nblk, float* __r
     // held these kernels at 64-91 us per leaf, the drop-in call at 6.7 ms instead of 2.7)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    SK_STAMP(3);
     if (tid == 0)
         s_last = __hip_atomic_fetch_add(ticket + cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KG - 1;
     __syncthreads();
+    SK_STAMP(4);
     if (!s_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler order only: every load below is sc1)
     const int G = nblk / KG;
@@ -462,10 +522,15 @@ __device__ __forceinline__ void small_conv_sk_body(int bid, int nblk, float* __r
     }
     // every block of the group has arrived: ready for the next launch (or the fused forward's next layer)
     if (tid == 0) __hip_atomic_store(ticket + cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    SK_STAMP(5);
 }
 
+// conv3 / conv4 (F1 == 0): two 512-thread blocks per CU (4 waves per SIMD, <= 128 VGPRs) so that all
+// 512 blocks of a layer are resident at once -- at 167 VGPRs the second half started only as the first
+// finished (11 us of start spread, tools/sk_stamps.py); conv12 (F1 > 0, 96 KB of LDS) is one block per CU
 template <int PXL, int F1, int KG>
-__global__ __launch_bounds__(SC_T) void small_conv_sk_kernel(const float* __restrict__ x, long long sB, int sY,
+__global__ __launch_bounds__(SC_T) __attribute__((amdgpu_waves_per_eu(F1 > 0 ? 1 : 4)))
+void small_conv_sk_kernel(const float* __restrict__ x, long long sB, int sY,
                                                              int sX, int B, int H, int pad,
                                                              const float* __restrict__ w, int Cin,
                                                              const float* __restrict__ bias, int relu,
@@ -993,3 +1058,16 @@ extern "C" int azg_small_net(const float* planes, int32_t batch, int32_t depth, 
     return hipGetLastError() == hipSuccess ? 0 : AZG_ERR_HIP;
 }
 #endif  // AZG_SMALL_PROBES
+
+#ifdef AZG_SMALL_TIMING
+// the stamps of the last launch(es) and the wall clock's rate (kHz)
+extern "C" int azg_sk_stamps_read(unsigned long long* out, int32_t n, int32_t* khz) {
+    if (!out || n <= 0 || n > 1024 * 8 || !khz) return AZG_ERR_ARG;
+    int dev = 0, rate = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&rate, hipDeviceAttributeWallClockRate, dev) != hipSuccess)
+        return AZG_ERR_HIP;
+    *khz = rate;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(azg_sk_stamps), (size_t)n * 8) == hipSuccess ? 0 : AZG_ERR_HIP;
+}
+#endif
